@@ -1,0 +1,314 @@
+"""Forward / backward kernel programs of the Speech-Transformer sublayers.
+
+Every function here issues native kernels only (asrx.kernels -> libasrx.so).  Activations are row-major
+token-major matrices [B*T, features]; the residual stream is kept in fp32, GEMM operands in the compute dtype
+(bf16 on the training path, fp32 on the parity path).  Forward functions stash what their backward needs in a
+plain dict `S`.
+
+Reference call sites (modules/Transformer): pre-LN sublayers model.py:18-25 / 65-75; MHA layers.py:15-40;
+FeedForward layers.py:53-58; front-end model.py:168-171 + 41-47; decoder embedding model.py:117.
+"""
+import math
+
+import torch
+
+from . import kernels as K
+from .kernels import MaskSpec
+
+
+class Ctx:
+    """Per-call configuration shared by the programs."""
+
+    def __init__(self, store, cd, train, p_drop, seeds, attn_impl="fused"):
+        self.store = store
+        self.cd = cd                    # compute dtype of GEMM operands: torch.bfloat16 | torch.float32
+        self.train = train
+        self.p = p_drop if train else 0.0
+        self.seeds = seeds
+        self.attn_impl = attn_impl
+
+    def W(self, p):
+        return self.store.w16(p) if self.cd == torch.bfloat16 else self.store.w32(p)
+
+    def G(self, p):
+        return self.store.g(p)
+
+    def seed(self):
+        return self.seeds.next() if self.p > 0 else 0
+
+
+class Seeds:
+    def __init__(self, base):
+        self.base = base
+        self.i = 0
+
+    def next(self):
+        self.i += 1
+        x = (self.base * 0x9E3779B97F4A7C15 + self.i * 0xBF58476D1CE4E5B9) & ((1 << 64) - 1)
+        return x ^ (x >> 31)
+
+
+def _empty(shape, dtype, like):
+    return torch.empty(shape, dtype=dtype, device=like.device)
+
+
+# ------------------------------------------------------------------------------------------------ LayerNorm
+
+def ln_fwd(C, x, ln, out_dtype=None):
+    y = _empty(x.shape, out_dtype or C.cd, x)
+    mean, rstd = K.layernorm_fwd(x, ln.weight.data, ln.bias.data, y)
+    return y, mean, rstd
+
+
+def ln_grad_buf(C, ln):
+    gw, gb = C.G(ln.weight), C.G(ln.bias)
+    if gb.data_ptr() == gw.data_ptr() + 4 * gw.numel():
+        return C.store.grad[C.store.offset(ln.weight):C.store.offset(ln.weight) + 2 * gw.numel()], None
+    tmp = torch.zeros(2 * gw.numel(), device=gw.device, dtype=torch.float32)
+    return tmp, (gw, gb)
+
+
+def ln_bwd(C, x, dy, ln, mean, rstd, dres=None, drop_out=None, drop_seed=0, drop_p=0.0):
+    """dx (fp32) = LN^T dy + dres; optional drop_out (compute dtype) = dropout_bwd(dx)."""
+    buf, split = ln_grad_buf(C, ln)
+    dx = K.layernorm_bwd(x, dy, ln.weight.data, mean, rstd, buf, dres=dres, dx_drop=drop_out, dropout_p=drop_p,
+                         seed=drop_seed)
+    if split is not None:
+        d = split[0].numel()
+        split[0].add_(buf[:d].view_as(split[0]))
+        split[1].add_(buf[d:].view_as(split[1]))
+    return dx
+
+
+# ------------------------------------------------------------------------------------------------ attention
+
+def attn_fwd(C, q, k, v, o, B, H, Lq, Lk, dh, strides, scale, spec):
+    """Fused LDS-tiled kernel on the bf16 path; materialised scores + row softmax otherwise."""
+    seed = C.seed()
+    S = {"seed": seed, "spec": spec, "dims": (B, H, Lq, Lk, dh), "strides": strides, "scale": scale}
+    if C.cd == torch.bfloat16 and C.attn_impl == "fused" and dh in (32, 64):
+        S["lse"] = K.attention_fwd(q, k, v, o, B, H, Lq, Lk, dh, strides, scale, spec, C.p, seed)
+        S["impl"] = "fused"
+        return S
+    S["impl"] = "unfused"
+    (qr, qb), (kr, kb), (vr, vb), (orr, ob) = strides
+    ld = (Lk + 7) // 8 * 8
+    nbh = B * H
+    sc = _empty((nbh, Lq, ld), C.cd, q)
+    K.gemm(q, k, sc, Lq, Lk, dh, lda=qr, ldb=kr, ldc=ld, batch=nbh, batch_inner=H, sa=(qb, dh), sb=(kb, dh),
+           sc=(H * Lq * ld, Lq * ld))
+    p = _empty((nbh, Lq, ld), C.cd, q)
+    pd = _empty((nbh, Lq, ld), C.cd, q) if C.p > 0 else None
+    K.softmax_fwd(sc, p, pd, nbh, H, Lq, Lk, ld, scale, spec, C.p, seed)
+    pv = pd if pd is not None else p
+    K.gemm(pv, v, o, Lq, dh, Lk, lda=ld, ldb=vr, ldc=orr, b_trans=True, batch=nbh, batch_inner=H,
+           sa=(H * Lq * ld, Lq * ld), sb=(vb, dh), sc=(ob, dh))
+    S["p"], S["pd"], S["ld"] = p, pd, ld
+    return S
+
+
+def attn_bwd(C, S, q, k, v, o, do, dq, dk, dv, gstrides):
+    B, H, Lq, Lk, dh = S["dims"]
+    strides, scale, spec, seed = S["strides"], S["scale"], S["spec"], S["seed"]
+    if S["impl"] == "fused":
+        K.attention_bwd(q, k, v, o, S["lse"], do, dq, dk, dv, B, H, Lq, Lk, dh, strides, gstrides, scale, spec,
+                        C.p, seed)
+        return
+    (qr, qb), (kr, kb), (vr, vb), _ = strides
+    (dor, dob), (dqr, dqb), (dkr, dkb), (dvr, dvb) = gstrides
+    p, pd, ld = S["p"], S["pd"], S["ld"]
+    nbh = B * H
+    so = (H * Lq * ld, Lq * ld)
+    dpd = _empty((nbh, Lq, ld), C.cd, q)
+    K.gemm(do, v, dpd, Lq, Lk, dh, lda=dor, ldb=vr, ldc=ld, batch=nbh, batch_inner=H, sa=(dob, dh), sb=(vb, dh),
+           sc=so)
+    ds = _empty((nbh, Lq, ld), C.cd, q)
+    K.softmax_bwd(p, dpd, ds, nbh, Lq, Lk, ld, scale, C.p, seed)
+    pv = pd if pd is not None else p
+    # dV = Pd^T dO ; dQ = dS K ; dK = dS^T Q
+    K.gemm(pv, do, dv, Lk, dh, Lq, lda=ld, ldb=dor, ldc=dvr, a_trans=True, b_trans=True, batch=nbh, batch_inner=H,
+           sa=so, sb=(dob, dh), sc=(dvb, dh))
+    K.gemm(ds, k, dq, Lq, dh, Lk, lda=ld, ldb=kr, ldc=dqr, b_trans=True, batch=nbh, batch_inner=H, sa=so,
+           sb=(kb, dh), sc=(dqb, dh))
+    K.gemm(ds, q, dk, Lk, dh, Lq, lda=ld, ldb=qr, ldc=dkr, a_trans=True, b_trans=True, batch=nbh, batch_inner=H,
+           sa=so, sb=(qb, dh), sc=(dkb, dh))
+
+
+# ------------------------------------------------------------------------------------------------ sublayers
+
+def self_attn_fwd(C, x, ln, mha, B, T, H, spec):
+    """x + Drop(MHA(LN(x))) with fused per-head projections (layers.py:10-12 -> one N=3d GEMM)."""
+    M, d = x.shape
+    dh = d // H
+    h, mean, rstd = ln_fwd(C, x, ln)
+    qkv = _empty((M, 3 * d), C.cd, x)
+    K.linear(h, C.W(mha.wqkv), qkv, bias=mha.bqkv.data)
+    o = _empty((M, d), C.cd, x)
+    st = ((3 * d, T * 3 * d),) * 3 + ((d, T * d),)
+    A = attn_fwd(C, qkv, qkv[:, d:], qkv[:, 2 * d:], o, B, H, T, T, dh, st, d ** -0.5, spec)
+    y = _empty((M, d), torch.float32, x)
+    sd = C.seed()
+    K.linear(o, C.W(mha._out_linear.weight), y, bias=mha._out_linear.bias.data, dropout_p=C.p, seed=sd, resid=x,
+             ld_resid=d)
+    return y, dict(x=x, h=h, mean=mean, rstd=rstd, qkv=qkv, o=o, A=A, sd=sd, ln=ln, mha=mha, H=H, T=T, B=B)
+
+
+def self_attn_bwd(C, S, dy, dy_c, dx_c_out=None, dx_c_p=0.0, dx_c_seed=0):
+    """dy: fp32 grad of the sublayer output; dy_c: dropout_bwd(dy) in the compute dtype (out-proj dY).
+    Returns dx (fp32) and fills dx_c_out (compute dtype) = dropout_bwd of dx for the sublayer below."""
+    x, h, qkv, o, mha = S["x"], S["h"], S["qkv"], S["o"], S["mha"]
+    M, d = x.shape
+    T, B = S["T"], S["B"]
+    W, G = C.W, C.G
+    do = _empty((M, d), C.cd, x)
+    K.linear_dgrad(dy_c, W(mha._out_linear.weight), do)
+    K.linear_wgrad(dy_c, o, G(mha._out_linear.weight))
+    K.colsum(dy_c, G(mha._out_linear.bias))
+    dqkv = _empty((M, 3 * d), C.cd, x)
+    gst = ((d, T * d),) + ((3 * d, T * 3 * d),) * 3
+    attn_bwd(C, S["A"], qkv, qkv[:, d:], qkv[:, 2 * d:], o, do, dqkv, dqkv[:, d:], dqkv[:, 2 * d:], gst)
+    dh = _empty((M, d), C.cd, x)
+    K.linear_dgrad(dqkv, W(mha.wqkv), dh)
+    K.linear_wgrad(dqkv, h, G(mha.wqkv))
+    K.colsum(dqkv, G(mha.bqkv))
+    return ln_bwd(C, x, dh, S["ln"], S["mean"], S["rstd"], dres=dy, drop_out=dx_c_out, drop_seed=dx_c_seed,
+                  drop_p=dx_c_p)
+
+
+def cross_attn_fwd(C, x, ln, mha, kv, kv_ld, B, L, Te, H):
+    """x + Drop(MHA(LN(x), enc)) — no mask (model.py:71); K/V come from the precomputed all-layer projection."""
+    M, d = x.shape
+    dh = d // H
+    h, mean, rstd = ln_fwd(C, x, ln)
+    q = _empty((M, d), C.cd, x)
+    K.linear(h, C.W(mha.wq), q, bias=mha.bq.data)
+    o = _empty((M, d), C.cd, x)
+    st = ((d, L * d), (kv_ld, Te * kv_ld), (kv_ld, Te * kv_ld), (d, L * d))
+    A = attn_fwd(C, q, kv, kv[:, d:], o, B, H, L, Te, dh, st, d ** -0.5, MaskSpec())
+    y = _empty((M, d), torch.float32, x)
+    sd = C.seed()
+    K.linear(o, C.W(mha._out_linear.weight), y, bias=mha._out_linear.bias.data, dropout_p=C.p, seed=sd, resid=x,
+             ld_resid=d)
+    return y, dict(x=x, h=h, mean=mean, rstd=rstd, q=q, o=o, A=A, sd=sd, ln=ln, mha=mha, L=L, Te=Te, kv=kv,
+                   kv_ld=kv_ld)
+
+
+def cross_attn_bwd(C, S, dy, dy_c, dkv, dx_c_out=None, dx_c_p=0.0, dx_c_seed=0):
+    x, h, q, o, mha, kv, kv_ld = S["x"], S["h"], S["q"], S["o"], S["mha"], S["kv"], S["kv_ld"]
+    M, d = x.shape
+    L, Te = S["L"], S["Te"]
+    W, G = C.W, C.G
+    do = _empty((M, d), C.cd, x)
+    K.linear_dgrad(dy_c, W(mha._out_linear.weight), do)
+    K.linear_wgrad(dy_c, o, G(mha._out_linear.weight))
+    K.colsum(dy_c, G(mha._out_linear.bias))
+    dq = _empty((M, d), C.cd, x)
+    gst = ((d, L * d), (d, L * d), (kv_ld, Te * kv_ld), (kv_ld, Te * kv_ld))
+    attn_bwd(C, S["A"], q, kv, kv[:, d:], o, do, dq, dkv, dkv[:, d:], gst)
+    dh = _empty((M, d), C.cd, x)
+    K.linear_dgrad(dq, W(mha.wq), dh)
+    K.linear_wgrad(dq, h, G(mha.wq))
+    K.colsum(dq, G(mha.bq))
+    return ln_bwd(C, x, dh, S["ln"], S["mean"], S["rstd"], dres=dy, drop_out=dx_c_out, drop_seed=dx_c_seed,
+                  drop_p=dx_c_p)
+
+
+def ffn_fwd(C, x, ln, ff):
+    """x + W2 Drop(ReLU(W1 LN(x) + b1)) + b2 (layers.py:53-58; residual model.py:24,74)."""
+    M, d = x.shape
+    h, mean, rstd = ln_fwd(C, x, ln)
+    nf = ff.squeeze.weight.shape[0]
+    f = _empty((M, nf), C.cd, x)
+    sf = C.seed()
+    K.linear(h, C.W(ff.squeeze.weight), f, bias=ff.squeeze.bias.data, relu=True, dropout_p=C.p, seed=sf)
+    y = _empty((M, d), torch.float32, x)
+    K.linear(f, C.W(ff.unsqueeze.weight), y, bias=ff.unsqueeze.bias.data, resid=x, ld_resid=d)
+    return y, dict(x=x, h=h, mean=mean, rstd=rstd, f=f, ln=ln, ff=ff)
+
+
+def ffn_bwd(C, S, dy, dy_c, dx_c_out=None, dx_c_p=0.0, dx_c_seed=0):
+    x, h, f, ff = S["x"], S["h"], S["f"], S["ff"]
+    M, d = x.shape
+    nf = f.shape[1]
+    W, G = C.W, C.G
+    dpre = _empty((M, nf), C.cd, x)
+    keep_scale = 1.0 / (1.0 - C.p) if C.p > 0 else 1.0
+    # f = Drop(ReLU(pre)) -> dpre = df * [f > 0] / (1-p)   (f > 0 <=> pre > 0 and kept)
+    K.linear_dgrad(dy_c, W(ff.unsqueeze.weight), dpre, alpha=keep_scale, gate=f, ld_gate=nf)
+    K.linear_wgrad(dy_c, f, G(ff.unsqueeze.weight))
+    K.colsum(dy, G(ff.unsqueeze.bias))
+    dh = _empty((M, d), C.cd, x)
+    K.linear_dgrad(dpre, W(ff.squeeze.weight), dh)
+    K.linear_wgrad(dpre, h, G(ff.squeeze.weight))
+    K.colsum(dpre, G(ff.squeeze.bias))
+    return ln_bwd(C, x, dh, S["ln"], S["mean"], S["rstd"], dres=dy, drop_out=dx_c_out, drop_seed=dx_c_seed,
+                  drop_p=dx_c_p)
+
+
+# ------------------------------------------------------------------------------------------------ layers
+
+def enc_layer_fwd(C, x, layer, B, T, H):
+    """EncoderLayer.forward (model.py:18-25): no attention mask."""
+    x1, Sa = self_attn_fwd(C, x, layer._norm1, layer._attention, B, T, H, MaskSpec())
+    x2, Sf = ffn_fwd(C, x1, layer._norm2, layer._feedforward)
+    return x2, (Sa, Sf)
+
+
+def enc_layer_bwd(C, S, dy, dy_c, dx_c_out, dx_c_p=0.0, dx_c_seed=0):
+    Sa, Sf = S
+    d = dy.shape[1]
+    dmid_c = _empty(dy.shape, C.cd, dy)
+    dmid = ffn_bwd(C, Sf, dy, dy_c, dx_c_out=dmid_c, dx_c_p=C.p, dx_c_seed=Sa["sd"])
+    return self_attn_bwd(C, Sa, dmid, dmid_c, dx_c_out=dx_c_out, dx_c_p=dx_c_p, dx_c_seed=dx_c_seed)
+
+
+def dec_layer_fwd(C, x, layer, B, L, H, spec, kv, kv_ld, Te):
+    """DecoderLayer.forward (model.py:65-75)."""
+    x1, Sa = self_attn_fwd(C, x, layer._norm1, layer._mask_attention, B, L, H, spec)
+    x2, Sc = cross_attn_fwd(C, x1, layer._norm2, layer._cross_attention, kv, kv_ld, B, L, Te, H)
+    x3, Sf = ffn_fwd(C, x2, layer._norm3, layer._feedforward)
+    return x3, (Sa, Sc, Sf)
+
+
+def dec_layer_bwd(C, S, dy, dy_c, dkv, dx_c_out, dx_c_p=0.0, dx_c_seed=0):
+    Sa, Sc, Sf = S
+    d2_c = _empty(dy.shape, C.cd, dy)
+    d2 = ffn_bwd(C, Sf, dy, dy_c, dx_c_out=d2_c, dx_c_p=C.p, dx_c_seed=Sc["sd"])
+    d1_c = _empty(dy.shape, C.cd, dy)
+    d1 = cross_attn_bwd(C, Sc, d2, d2_c, dkv, dx_c_out=d1_c, dx_c_p=C.p, dx_c_seed=Sa["sd"])
+    return self_attn_bwd(C, Sa, d1, d1_c, dx_c_out=dx_c_out, dx_c_p=dx_c_p, dx_c_seed=dx_c_seed)
+
+
+# ------------------------------------------------------------------------------------------------ front-end
+
+def frontend_fwd(C, spectrum, conv1, conv2):
+    """input_layer (model.py:168-171) -> (B*T2, F2*64) features, column order f*64 + c (the conv2 GEMM output
+    rows are (b, t2, f2), so the reference's view/transpose/contiguous of model.py:43-45 costs nothing)."""
+    B, _, F, T = spectrum.shape
+    F1, T1 = (F - 3) // 2 + 1, (T - 3) // 2 + 1
+    F2, T2 = (F1 - 3) // 2 + 1, (T1 - 3) // 2 + 1
+    x = spectrum.contiguous().float()
+    y1 = _empty((B, F1, T1, 64), C.cd, x)
+    K.conv1_fwd(x, conv1.weight.data.reshape(64, 9).contiguous(), conv1.bias.data, y1)
+    cols = _empty((B * T2 * F2, 576), C.cd, x)
+    K.im2col_conv2(y1, cols)
+    feats = _empty((B * T2, F2 * 64), C.cd, x)
+    K.gemm(cols, C.W(conv2.weight), feats, B * T2 * F2, 64, 576, lda=576, ldb=576, ldc=64, bias=conv2.bias.data,
+           relu=True)
+    return feats, dict(x=x, y1=y1, cols=cols, feats=feats, dims=(B, F, T, F1, T1, F2, T2))
+
+
+def frontend_bwd(C, S, dfeats_c, conv1, conv2):
+    """dfeats_c: gradient of the features (compute dtype, already gated by the conv2 ReLU)."""
+    B, F, T, F1, T1, F2, T2 = S["dims"]
+    M2 = B * T2 * F2
+    dy2 = dfeats_c.view(M2, 64)
+    cols = S["cols"]
+    G = C.G
+    K.linear_wgrad(dy2, cols, G(conv2.weight))
+    dcols = _empty((M2, 576), C.cd, dy2)
+    K.linear_dgrad(dy2, C.W(conv2.weight), dcols)
+    K.colsum(dy2, G(conv2.bias))
+    dy1 = _empty((B, F1, T1, 64), torch.float32, dy2)
+    K.col2im_conv2(dcols, S["y1"], dy1)
+    K.conv1_bwd_w(S["x"], dy1, G(conv1.weight).view(64, 9), G(conv1.bias))

@@ -1,0 +1,595 @@
+"""Autograd glue: each drop-in module's forward is one torch.autograd.Function whose forward and backward run
+the explicit native programs of asrx.blocks.  Weight gradients are written by the kernels straight into the
+flat gradient buffer that `p.grad` views (asrx.params); the Functions return None for parameters.
+
+`model_forward` / `model_backward` are also used directly (no autograd) by the fused trainer (asrx.train).
+"""
+import random
+
+import torch
+
+from . import blocks as Bk
+from . import kernels as K
+from .kernels import MaskSpec
+from .params import FlatParams
+
+_SEED_BASE = random.SystemRandom().randrange(1 << 62)
+
+
+# ------------------------------------------------------------------------------------------- store / context
+
+def root_of(m):
+    r = m.__dict__.get("_asrx_root")
+    r = r() if r is not None else None
+    return r if r is not None else m
+
+
+def param_order(root):
+    """Module order, except that the decoder's per-layer cross-attention K/V projections are grouped into one
+    contiguous [n_layers*2d, d] block (+ bias block): the all-layer K/V GEMM reads them as one matrix."""
+    from .model import Decoder
+    ps = list(root.parameters())
+    decs = [m for m in root.modules() if isinstance(m, Decoder)]
+    for dec in decs:
+        wkv = [l._cross_attention.wkv for l in dec._layers]
+        bkv = [l._cross_attention.bkv for l in dec._layers]
+        if not wkv:
+            continue
+        ids = {id(p) for p in wkv + bkv}
+        pos = min(i for i, p in enumerate(ps) if id(p) in ids)
+        rest = [p for p in ps if id(p) not in ids]
+        ps = rest[:pos] + wkv + bkv + rest[pos:]
+    return ps
+
+
+def get_store(m):
+    root = root_of(m)
+    st = root.__dict__.get("_asrx_store")
+    try:
+        dev = next(root.parameters()).device
+    except StopIteration:
+        raise RuntimeError("asrx: module has no parameters")
+    if dev.type != "cuda":
+        raise RuntimeError("asrx modules compute on the GPU only (libasrx.so, gfx950); move the model with .cuda()")
+    if st is None or st.device != dev or not st.valid():
+        st = FlatParams(param_order(root), dev)
+        root.__dict__["_asrx_store"] = st
+    return st
+
+
+def make_ctx(m, p_drop):
+    root = root_of(m)
+    st = get_store(m)
+    prec = getattr(root, "precision", "bf16")
+    cd = torch.bfloat16 if prec == "bf16" else torch.float32
+    if cd == torch.bfloat16:
+        st.refresh_shadow()
+    train = m.training
+    n = root.__dict__.get("_asrx_calls", 0) + 1
+    root.__dict__["_asrx_calls"] = n
+    seeds = Bk.Seeds(_SEED_BASE + n * 1000003)
+    return Bk.Ctx(st, cd, train, p_drop, seeds, getattr(root, "attention", "fused"))
+
+
+def _prepare_grads(C):
+    st = C.store
+    unbound = [p for p in st.params if p.grad is None or p.grad.data_ptr() != st._view(st.grad, p).data_ptr()]
+    if not unbound:
+        return
+    if len(unbound) == len(st.params):
+        st.zero_grad()
+        for p in st.params:
+            p.grad = st._view(st.grad, p)
+    else:
+        for p in unbound:
+            st.ensure_grad(p)
+
+
+def _params(m):
+    return tuple(p for p in m.parameters())
+
+
+# ------------------------------------------------------------------------------------------- programs
+
+def encoder_input(C, x):
+    """Accepts the FrontEnd's logical (B, 64, F'', T'') tensor (ideally the permuted view of its (B, T'', F'', 64)
+    buffer) and returns (feats [B*T'', F''*64] compute dtype, B, T'')."""
+    if x.dim() != 4:
+        raise ValueError("Encoder expects the input_layer output (B, 64, F'', T'')")
+    B, Cc, F2, T2 = x.shape
+    buf = x.permute(0, 3, 2, 1)
+    if not buf.is_contiguous() or buf.dtype != C.cd:
+        buf = buf.to(C.cd).contiguous()
+    return buf.reshape(B * T2, F2 * Cc), B, T2
+
+
+def encoder_fwd(C, enc, feats, B, T):
+    d = enc.emb_dim
+    H = enc.num_heads
+    x = torch.empty(B * T, d, dtype=torch.float32, device=feats.device)
+    pe = enc._pe.pe[0]
+    if T > pe.shape[0]:
+        raise ValueError(f"encoder length {T} exceeds the PE table ({pe.shape[0]}) as in layers.py:73")
+    K.linear(feats, C.W(enc._lin_in.weight), x, bias=enc._lin_in.bias.data, rowadd=pe, rowadd_mod=T, ld_rowadd=d)
+    Ss = []
+    for layer in enc._layers:
+        x, S = Bk.enc_layer_fwd(C, x, layer, B, T, H)
+        Ss.append(S)
+    y, mean, rstd = Bk.ln_fwd(C, x, enc._norm_out)
+    return y, dict(feats=feats, x=x, mean=mean, rstd=rstd, layers=Ss)
+
+
+def encoder_bwd(C, enc, S, dy, gate_feats):
+    """dy: grad of the encoder output (fp32 or compute dtype). Returns dfeats (compute dtype)."""
+    x = S["x"]
+    dx_c = torch.empty(x.shape, dtype=C.cd, device=x.device)
+    dx = Bk.ln_bwd(C, x, dy, enc._norm_out, S["mean"], S["rstd"], drop_out=dx_c)
+    for layer_S in reversed(S["layers"]):
+        nxt = torch.empty(x.shape, dtype=C.cd, device=x.device)
+        dx = Bk.enc_layer_bwd(C, layer_S, dx, dx_c, nxt)
+        dx_c = nxt
+    feats = S["feats"]
+    dfeats = torch.empty(feats.shape, dtype=C.cd, device=x.device)
+    w = enc._lin_in.weight
+    if gate_feats:
+        K.linear_dgrad(dx_c, C.W(w), dfeats, gate=feats, ld_gate=feats.shape[1])
+    else:
+        K.linear_dgrad(dx_c, C.W(w), dfeats)
+    K.linear_wgrad(dx_c, feats, C.G(w))
+    K.colsum(dx, C.G(enc._lin_in.bias))
+    return dfeats
+
+
+def _kv_block(C, dec):
+    st = C.store
+    n = len(dec._layers)
+    first_w = dec._layers[0]._cross_attention.wkv
+    first_b = dec._layers[0]._cross_attention.bkv
+    d = dec.emb_dim
+    buf = st.shadow if C.cd == torch.bfloat16 else st.flat
+    W = st.span(first_w, n, buf)
+    bias = st.span(first_b, n, st.flat)
+    gW = st.span(first_w, n, st.grad)
+    gb = st.span(first_b, n, st.grad)
+    if W is None or bias is None:
+        raise RuntimeError("asrx: cross-attention K/V parameters are not contiguous in the flat store")
+    return W.view(n * 2 * d, d), bias, gW.view(n * 2 * d, d), gb
+
+
+def decoder_fwd(C, dec, text, mask, enc_c, B, L, Te, final_norm=True, spec=None):
+    d, H, n = dec.emb_dim, dec.num_heads, len(dec._layers)
+    dev = enc_c.device
+    Md = B * L
+    text = text.to(device=dev, dtype=torch.int64).contiguous()
+    if spec is None:
+        spec = MaskSpec.decoder(mask.to(dev))
+    pe = dec._pe.pe[0]
+    if L > pe.shape[0]:
+        raise ValueError(f"decoder length {L} exceeds the PE table ({pe.shape[0]})")
+    x = torch.empty(Md, d, dtype=torch.float32, device=dev)
+    s_emb = C.seed()
+    K.embed_fwd(text, dec._embedding.weight.data, pe, x, L, C.p, s_emb)
+    Wkv, bkv, _, _ = _kv_block(C, dec)
+    kv = torch.empty(B * Te, n * 2 * d, dtype=C.cd, device=dev)
+    K.linear(enc_c, Wkv, kv, bias=bkv)
+    Ss = []
+    for l, layer in enumerate(dec._layers):
+        x, S = Bk.dec_layer_fwd(C, x, layer, B, L, H, spec, kv[:, l * 2 * d:], n * 2 * d, Te)
+        Ss.append(S)
+    cls = dec._classifier
+    if final_norm:
+        h, mean, rstd = Bk.ln_fwd(C, x, dec._norm_layer)
+    else:
+        h, mean, rstd = x.to(C.cd), None, None
+    logits = torch.empty(Md, cls.Vp, dtype=torch.float32, device=dev)
+    K.linear(h, C.W(cls.weight), logits)
+    return logits, dict(text=text, x=x, h=h, mean=mean, rstd=rstd, kv=kv, enc=enc_c, layers=Ss, s_emb=s_emb,
+                        dims=(B, L, Te))
+
+
+def decoder_bwd(C, dec, S, dlogits_c):
+    """dlogits_c: [B*L, Vp] compute dtype (padded columns zero). Returns d(encoder output) fp32 [B*Te, d]."""
+    B, L, Te = S["dims"]
+    d, n = dec.emb_dim, len(dec._layers)
+    x, h = S["x"], S["h"]
+    dev = x.device
+    cls = dec._classifier
+    dh = torch.empty(B * L, d, dtype=C.cd, device=dev)
+    K.linear_dgrad(dlogits_c, C.W(cls.weight), dh)
+    K.linear_wgrad(dlogits_c, h, C.G(cls.weight))
+    dx_c = torch.empty(B * L, d, dtype=C.cd, device=dev)
+    dx = Bk.ln_bwd(C, x, dh, dec._norm_layer, S["mean"], S["rstd"], drop_out=dx_c)
+    dkv = torch.empty(B * Te, n * 2 * d, dtype=C.cd, device=dev)
+    for l in reversed(range(n)):
+        nxt = torch.empty(B * L, d, dtype=C.cd, device=dev)
+        dx = Bk.dec_layer_bwd(C, S["layers"][l], dx, dx_c, dkv[:, l * 2 * d:], nxt)
+        dx_c = nxt
+    K.embed_bwd(S["text"], dx, C.G(dec._embedding.weight), L, dec.pad_token_id if dec.pad_token_id is not None else -1,
+                C.p, S["s_emb"])
+    Wkv, _, gW, gb = _kv_block(C, dec)
+    denc = torch.empty(B * Te, d, dtype=torch.float32, device=dev)
+    K.linear_dgrad(dkv, Wkv, denc)
+    K.linear_wgrad(dkv, S["enc"], gW)
+    K.colsum(dkv, gb)
+    return denc
+
+
+def model_forward(C, model, spectrum, text, mask):
+    """Transformer.forward (model.py:194-198) as one native program. Returns (logits [B*L, Vp] fp32, S)."""
+    dev = C.store.device
+    spectrum = spectrum.to(dev)
+    feats, Sf = Bk.frontend_fwd(C, spectrum, model.input_layer[0], model.input_layer[2])
+    B = spectrum.shape[0]
+    T2 = Sf["dims"][-1]
+    enc, Se = encoder_fwd(C, model.encoder, feats, B, T2)
+    L = text.shape[1]
+    logits, Sd = decoder_fwd(C, model.decoder, text, mask, enc, B, L, T2)
+    return logits, dict(f=Sf, e=Se, d=Sd)
+
+
+def model_backward(C, model, S, dlogits_c):
+    _prepare_grads(C)
+    denc = decoder_bwd(C, model.decoder, S["d"], dlogits_c)
+    dfeats = encoder_bwd(C, model.encoder, S["e"], denc, gate_feats=True)
+    Bk.frontend_bwd(C, S["f"], dfeats, model.input_layer[0], model.input_layer[2])
+
+
+def _dlogits_padded(C, dlogits, rows, V, Vp):
+    g = torch.zeros(rows, Vp, dtype=C.cd, device=dlogits.device)
+    g[:, :V].copy_(dlogits.reshape(rows, V))
+    return g
+
+
+# ------------------------------------------------------------------------------------------- Functions
+
+class _TransformerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, model, C, spectrum, text, mask, *params):
+        logits, S = model_forward(C, model, spectrum, text, mask)
+        ctx.model, ctx.C, ctx.S = model, C, S
+        B, L = text.shape
+        V = model.decoder._classifier.V
+        ctx.shape = (B, L, V, logits.shape[1])
+        out = logits.view(B, L, -1)
+        return out[:, :, :V] if V != logits.shape[1] else out
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        B, L, V, Vp = ctx.shape
+        C = ctx.C
+        model_backward(C, ctx.model, ctx.S, _dlogits_padded(C, dlogits, B * L, V, Vp))
+        ctx.S = None
+        return (None,) * (5 + len(_params(ctx.model)))
+
+
+def transformer(model, spectrum, text, mask):
+    C = make_ctx(model, model.decoder.p)
+    return _TransformerFn.apply(model, C, spectrum, text, mask, *_params(model))
+
+
+class _FrontEndFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, fe, C, spectrum, *params):
+        feats, S = Bk.frontend_fwd(C, spectrum, fe[0], fe[2])
+        ctx.fe, ctx.C, ctx.S = fe, C, S
+        B, F, T, F1, T1, F2, T2 = S["dims"]
+        return feats.view(B, T2, F2, 64).permute(0, 3, 2, 1)
+
+    @staticmethod
+    def backward(ctx, g):
+        C, S = ctx.C, ctx.S
+        _prepare_grads(C)
+        buf = g.permute(0, 3, 2, 1).to(C.cd).contiguous()
+        B, F, T, F1, T1, F2, T2 = S["dims"]
+        dy2 = buf.view(B * T2, F2 * 64)
+        dy2 = torch.where(S["feats"] > 0, dy2, torch.zeros((), dtype=dy2.dtype, device=dy2.device))
+        Bk.frontend_bwd(C, S, dy2, ctx.fe[0], ctx.fe[2])
+        return (None,) * (3 + len(_params(ctx.fe)))
+
+
+def frontend(fe, spectrum):
+    C = make_ctx(fe, 0.0)
+    return _FrontEndFn.apply(fe, C, spectrum, *_params(fe))
+
+
+class _EncoderFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, enc, C, x, *params):
+        feats, B, T = encoder_input(C, x)
+        y, S = encoder_fwd(C, enc, feats, B, T)
+        ctx.enc, ctx.C, ctx.S, ctx.xshape = enc, C, S, (B, T, x.shape[1], x.shape[2])
+        return y.view(B, T, -1)
+
+    @staticmethod
+    def backward(ctx, g):
+        C, S = ctx.C, ctx.S
+        _prepare_grads(C)
+        B, T, Cc, F2 = ctx.xshape
+        dfeats = encoder_bwd(C, ctx.enc, S, g.reshape(B * T, -1).contiguous(), gate_feats=False)
+        dx = dfeats.view(B, T, F2, Cc).permute(0, 3, 2, 1)
+        return (None, None, dx) + (None,) * len(_params(ctx.enc))
+
+
+def encoder(enc, x):
+    C = make_ctx(enc, enc.p)
+    return _EncoderFn.apply(enc, C, x, *_params(enc))
+
+
+class _DecoderFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, dec, C, text, mask, enc_x, *params):
+        B, Te, d = enc_x.shape
+        enc_c = enc_x.reshape(B * Te, d).to(C.cd).contiguous()
+        L = text.shape[1]
+        logits, S = decoder_fwd(C, dec, text, mask, enc_c, B, L, Te)
+        ctx.dec, ctx.C, ctx.S = dec, C, S
+        V = dec._classifier.V
+        ctx.shape = (B, L, V, logits.shape[1], Te, d)
+        out = logits.view(B, L, -1)
+        return out[:, :, :V] if V != logits.shape[1] else out
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        B, L, V, Vp, Te, d = ctx.shape
+        C = ctx.C
+        _prepare_grads(C)
+        denc = decoder_bwd(C, ctx.dec, ctx.S, _dlogits_padded(C, dlogits, B * L, V, Vp))
+        return (None, None, None, None, denc.view(B, Te, d)) + (None,) * len(_params(ctx.dec))
+
+
+def decoder(dec, x, mask, enc_x):
+    C = make_ctx(dec, dec.p)
+    return _DecoderFn.apply(dec, C, x, mask, enc_x, *_params(dec))
+
+
+@torch.no_grad()
+def decoder_evaluate(dec, x, enc_x):
+    """Decoder.evaluate (model.py:125-151) with its quirks: per-sample loop, whole prefix recomputed each
+    step, causal-only mask, NO final LayerNorm before the classifier, no break on EOS; returns the last
+    sample's token row and the list of logits snapshots (one per EOS hit or final step)."""
+    C = make_ctx(dec, 0.0)
+    C.train, C.p = False, 0.0
+    B, Te, d = enc_x.shape
+    V = dec._classifier.V
+    probs = []
+    decoder_input = None
+    for s in range(x.shape[0]):
+        decoder_input = x[s].unsqueeze(0).to(enc_x.device)
+        e = enc_x[s].reshape(Te, d).to(C.cd).contiguous()
+        for i in range(1, dec._seq_len + 1):
+            L = decoder_input.shape[1]
+            spec = MaskSpec(1, True)
+            logits, _ = decoder_fwd(C, dec, decoder_input, None, e, 1, L, Te, final_norm=False, spec=spec)
+            prob = logits[:, :V].view(1, L, V)
+            next_word = prob.argmax(dim=-1)[:, -1].unsqueeze(1)
+            decoder_input = torch.cat([decoder_input, next_word.to(decoder_input.dtype)], dim=-1)
+            if next_word.item() == dec._eos_token_id or i == dec._seq_len:
+                probs.append(prob[:, :-1].squeeze())
+    return decoder_input, probs
+
+
+@torch.no_grad()
+def transformer_evaluate(model, spectrum, text):
+    """Transformer.evaluate (model.py:201-206)."""
+    feats = model.input_layer(spectrum)
+    enc = model.encoder(feats)
+    return model.decoder.evaluate(text, enc)
+
+
+# ------------------------------------------------------------------------------------------- sub-modules
+
+def _cd_input(C, x):
+    return x.reshape(-1, x.shape[-1]).to(C.cd).contiguous()
+
+
+class _LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ln, C, x, *params):
+        x2 = x.reshape(-1, x.shape[-1]).float().contiguous()
+        y, mean, rstd = Bk.ln_fwd(C, x2, ln, out_dtype=torch.float32)
+        ctx.ln, ctx.C, ctx.S, ctx.shape = ln, C, (x2, mean, rstd), x.shape
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, g):
+        C = ctx.C
+        _prepare_grads(C)
+        x2, mean, rstd = ctx.S
+        dx = Bk.ln_bwd(C, x2, g.reshape(x2.shape).float().contiguous(), ctx.ln, mean, rstd)
+        return (None, None, dx.view(ctx.shape)) + (None,) * len(_params(ctx.ln))
+
+
+def layernorm(ln, x):
+    C = make_ctx(ln, 0.0)
+    return _LayerNormFn.apply(ln, C, x, *_params(ln))
+
+
+class _MHAFn(torch.autograd.Function):
+    """Standalone MHA: y = Drop(W_o . attn(x W_q, kv W_k, kv W_v) + b_o) — no LayerNorm, no residual."""
+
+    @staticmethod
+    def forward(ctx, m, C, x, enc_x, attention_mask, *params):
+        B, Lq, d = x.shape
+        kv_in = x if enc_x is None else enc_x
+        Lk = kv_in.shape[1]
+        H = m.num_heads
+        dh = d // H
+        xc = _cd_input(C, x)
+        kc = xc if enc_x is None else _cd_input(C, enc_x)
+        if m.cross:
+            Wq, bq, Wkv, bkv = C.W(m.wq), m.bq.data, C.W(m.wkv), m.bkv.data
+        else:
+            Wq = C.W(m.wqkv)[:d]
+            bq = m.bqkv.data[:d]
+            Wkv, bkv = C.W(m.wqkv)[d:], m.bqkv.data[d:]
+        q = torch.empty(B * Lq, d, dtype=C.cd, device=xc.device)
+        K.linear(xc, Wq, q, bias=bq)
+        kv = torch.empty(B * Lk, 2 * d, dtype=C.cd, device=xc.device)
+        K.linear(kc, Wkv, kv, bias=bkv)
+        spec = MaskSpec.from_attention_mask(attention_mask.to(xc.device) if attention_mask is not None else None,
+                                            B, Lq, Lk)
+        o = torch.empty(B * Lq, d, dtype=C.cd, device=xc.device)
+        st = ((d, Lq * d), (2 * d, Lk * 2 * d), (2 * d, Lk * 2 * d), (d, Lq * d))
+        A = Bk.attn_fwd(C, q, kv, kv[:, d:], o, B, H, Lq, Lk, dh, st, d ** -0.5, spec)
+        y = torch.empty(B * Lq, d, dtype=torch.float32, device=xc.device)
+        sd = C.seed()
+        K.linear(o, C.W(m._out_linear.weight), y, bias=m._out_linear.bias.data, dropout_p=C.p, seed=sd)
+        ctx.m, ctx.C = m, C
+        ctx.S = dict(xc=xc, kc=kc, q=q, kv=kv, o=o, A=A, sd=sd, dims=(B, Lq, Lk, d), self_attn=enc_x is None,
+                     xdtype=x.dtype, kdtype=kv_in.dtype)
+        return y.view(B, Lq, d).to(x.dtype) if x.dtype != torch.float32 else y.view(B, Lq, d)
+
+    @staticmethod
+    def backward(ctx, g):
+        C, S, m = ctx.C, ctx.S, ctx.m
+        _prepare_grads(C)
+        B, Lq, Lk, d = S["dims"]
+        dev = S["xc"].device
+        # dropout bwd of the output (same RNG stream as the forward epilogue)
+        g2 = g.reshape(B * Lq, d).float().contiguous()
+        dy_c = torch.empty(B * Lq, d, dtype=C.cd, device=dev)
+        if C.p > 0:
+            keep = K.dropout_mask(B * Lq * d, C.p, S["sd"], dev).view(B * Lq, d)
+            dy_c.copy_(g2 * keep / (1.0 - C.p))
+        else:
+            dy_c.copy_(g2)
+        do = torch.empty(B * Lq, d, dtype=C.cd, device=dev)
+        K.linear_dgrad(dy_c, C.W(m._out_linear.weight), do)
+        K.linear_wgrad(dy_c, S["o"], C.G(m._out_linear.weight))
+        K.colsum(dy_c, C.G(m._out_linear.bias))
+        dq = torch.empty(B * Lq, d, dtype=C.cd, device=dev)
+        dkv = torch.empty(B * Lk, 2 * d, dtype=C.cd, device=dev)
+        q, kv = S["q"], S["kv"]
+        gst = ((d, Lq * d), (d, Lq * d), (2 * d, Lk * 2 * d), (2 * d, Lk * 2 * d))
+        Bk.attn_bwd(C, S["A"], q, kv, kv[:, d:], S["o"], do, dq, dkv, dkv[:, d:], gst)
+        if m.cross:
+            Wq, Wkv, gWq, gbq, gWkv, gbkv = C.W(m.wq), C.W(m.wkv), C.G(m.wq), C.G(m.bq), C.G(m.wkv), C.G(m.bkv)
+        else:
+            Wq, Wkv = C.W(m.wqkv)[:d], C.W(m.wqkv)[d:]
+            gw, gb = C.G(m.wqkv), C.G(m.bqkv)
+            gWq, gbq, gWkv, gbkv = gw[:d], gb[:d], gw[d:], gb[d:]
+        dx = torch.empty(B * Lq, d, dtype=torch.float32, device=dev)
+        K.linear_dgrad(dq, Wq, dx)
+        K.linear_wgrad(dq, S["xc"], gWq)
+        K.colsum(dq, gbq)
+        dk_in = torch.empty(B * Lk, d, dtype=torch.float32, device=dev)
+        K.linear_dgrad(dkv, Wkv, dk_in)
+        K.linear_wgrad(dkv, S["kc"], gWkv)
+        K.colsum(dkv, gbkv)
+        if S["self_attn"]:
+            dx.add_(dk_in)
+            return (None, None, dx.view(B, Lq, d).to(S["xdtype"]), None, None) + (None,) * len(_params(m))
+        return (None, None, dx.view(B, Lq, d).to(S["xdtype"]), dk_in.view(B, Lk, d).to(S["kdtype"]), None) + \
+            (None,) * len(_params(m))
+
+
+def mha(m, x, enc_x=None, attention_mask=None):
+    C = make_ctx(m, m.p)
+    return _MHAFn.apply(m, C, x, enc_x, attention_mask, *_params(m))
+
+
+class _FFNFn(torch.autograd.Function):
+    """Standalone FeedForward (layers.py:53-58), no residual."""
+
+    @staticmethod
+    def forward(ctx, ff, C, x, *params):
+        shape = x.shape
+        xc = _cd_input(C, x)
+        M = xc.shape[0]
+        nf = ff.ff_dim
+        f = torch.empty(M, nf, dtype=C.cd, device=xc.device)
+        sf = C.seed()
+        K.linear(xc, C.W(ff.squeeze.weight), f, bias=ff.squeeze.bias.data, relu=True, dropout_p=C.p, seed=sf)
+        y = torch.empty(M, ff.emb_dim, dtype=torch.float32, device=xc.device)
+        K.linear(f, C.W(ff.unsqueeze.weight), y, bias=ff.unsqueeze.bias.data)
+        ctx.ff, ctx.C, ctx.S = ff, C, (xc, f, shape, x.dtype)
+        return y.view(shape).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        C, ff = ctx.C, ctx.ff
+        _prepare_grads(C)
+        xc, f, shape, xdt = ctx.S
+        M = xc.shape[0]
+        g2 = g.reshape(M, -1).float().contiguous()
+        g_c = g2.to(C.cd)
+        dpre = torch.empty(M, ff.ff_dim, dtype=C.cd, device=xc.device)
+        K.linear_dgrad(g_c, C.W(ff.unsqueeze.weight), dpre, alpha=1.0 / (1.0 - C.p) if C.p > 0 else 1.0, gate=f,
+                       ld_gate=ff.ff_dim)
+        K.linear_wgrad(g_c, f, C.G(ff.unsqueeze.weight))
+        K.colsum(g2, C.G(ff.unsqueeze.bias))
+        dx = torch.empty(M, ff.emb_dim, dtype=torch.float32, device=xc.device)
+        K.linear_dgrad(dpre, C.W(ff.squeeze.weight), dx)
+        K.linear_wgrad(dpre, xc, C.G(ff.squeeze.weight))
+        K.colsum(dpre, C.G(ff.squeeze.bias))
+        return (None, None, dx.view(shape).to(xdt)) + (None,) * len(_params(ff))
+
+
+def feed_forward(ff, x):
+    C = make_ctx(ff, ff.p)
+    return _FFNFn.apply(ff, C, x, *_params(ff))
+
+
+class _EncLayerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, layer, C, x, *params):
+        B, T, d = x.shape
+        x32 = x.reshape(B * T, d).float().contiguous()
+        y, S = Bk.enc_layer_fwd(C, x32, layer, B, T, layer.num_heads)
+        ctx.layer, ctx.C, ctx.S, ctx.xdt = layer, C, S, x.dtype
+        return y.view(B, T, d).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        C = ctx.C
+        _prepare_grads(C)
+        B, T, d = g.shape
+        g32 = g.reshape(B * T, d).float().contiguous()
+        dx = Bk.enc_layer_bwd(C, ctx.S, g32, g32.to(C.cd), None)
+        return (None, None, dx.view(B, T, d).to(ctx.xdt)) + (None,) * len(_params(ctx.layer))
+
+
+def encoder_layer(layer, x):
+    C = make_ctx(layer, layer.p)
+    return _EncLayerFn.apply(layer, C, x, *_params(layer))
+
+
+class _DecLayerFn(torch.autograd.Function):
+    """Standalone DecoderLayer(x, mask, enc_x): `mask` is the attention mask as the reference passes it to
+    the layer (bool/uint8 broadcastable to (B, L, L), >0 = masked), cross-attention K/V from enc_x."""
+
+    @staticmethod
+    def forward(ctx, layer, C, x, mask, enc_x, *params):
+        B, L, d = x.shape
+        Te = enc_x.shape[1]
+        x32 = x.reshape(B * L, d).float().contiguous()
+        enc_c = _cd_input(C, enc_x)
+        ca = layer._cross_attention
+        kv = torch.empty(B * Te, 2 * d, dtype=C.cd, device=x32.device)
+        K.linear(enc_c, C.W(ca.wkv), kv, bias=ca.bkv.data)
+        spec = MaskSpec.from_attention_mask(mask.to(x32.device) if mask is not None else None, B, L, L)
+        y, S = Bk.dec_layer_fwd(C, x32, layer, B, L, layer.num_heads, spec, kv, 2 * d, Te)
+        ctx.layer, ctx.C, ctx.S, ctx.extra = layer, C, S, (enc_c, kv, x.dtype, enc_x.dtype, Te)
+        return y.view(B, L, d).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        C, layer = ctx.C, ctx.layer
+        _prepare_grads(C)
+        enc_c, kv, xdt, edt, Te = ctx.extra
+        B, L, d = g.shape
+        g32 = g.reshape(B * L, d).float().contiguous()
+        dkv = torch.empty(B * Te, 2 * d, dtype=C.cd, device=g32.device)
+        dx = Bk.dec_layer_bwd(C, ctx.S, g32, g32.to(C.cd), dkv, None)
+        ca = layer._cross_attention
+        denc = torch.empty(B * Te, d, dtype=torch.float32, device=g32.device)
+        K.linear_dgrad(dkv, C.W(ca.wkv), denc)
+        K.linear_wgrad(dkv, enc_c, C.G(ca.wkv))
+        K.colsum(dkv, C.G(ca.bkv))
+        return (None, None, dx.view(B, L, d).to(xdt), None, denc.view(B, Te, d).to(edt)) + \
+            (None,) * len(_params(layer))
+
+
+def decoder_layer(layer, x, mask, enc_x):
+    C = make_ctx(layer, layer.p)
+    return _DecLayerFn.apply(layer, C, x, mask, enc_x, *_params(layer))

@@ -1,0 +1,315 @@
+"""Tensor-level wrappers around the C-ABI (include/asrx.h). All calls are asynchronous on torch's current
+HIP stream; every call goes to the native library (no CPU / PyTorch fallback)."""
+import ctypes
+import math
+
+import torch
+
+from ._lib import AttnDesc, BF16, F32, GemmDesc, call
+
+_U64 = (1 << 64) - 1
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def code(t):
+    if t.dtype == torch.bfloat16:
+        return BF16
+    if t.dtype == torch.float32:
+        return F32
+    raise TypeError(f"asrx: unsupported dtype {t.dtype}")
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("asrx: tensors must live on the GPU (no CPU fallback)")
+
+
+# ------------------------------------------------------------------------------------------- GEMM
+
+def auto_splitk(m, n, k, batch=1, tile=64):
+    """Split the reduction when the output grid alone cannot fill the 256 CUs (dW GEMMs: K = B*T)."""
+    if batch != 1:
+        return 1
+    tiles = math.ceil(m / tile) * math.ceil(n / tile)
+    if tiles >= 256 or k < 1024:
+        return 1
+    s = min(math.ceil(512 / tiles), max(1, k // 512), 256)
+    return max(1, s)
+
+
+def gemm(a, b, c, m, n, k, *, lda, ldb, ldc, a_trans=False, b_trans=False, alpha=1.0, beta=0.0, bias=None,
+         rowadd=None, rowadd_mod=1, ld_rowadd=0, relu=False, dropout_p=0.0, seed=0, gate=None, ld_gate=0,
+         resid=None, ld_resid=0, batch=1, batch_inner=1, sa=(0, 0), sb=(0, 0), sc=(0, 0), splitk=1, tile=0):
+    """C = epi(alpha * op(A) op(B)^T) — see asrx_gemm in include/asrx.h."""
+    _cuda(a, b, c)
+    if a.dtype != b.dtype:
+        raise TypeError("asrx.gemm: A and B must share a dtype")
+    if splitk == "auto":
+        splitk = auto_splitk(m, n, k, batch)
+    d = GemmDesc()
+    d.m, d.n, d.k = m, n, k
+    d.in_dtype = code(a)
+    d.a, d.lda, d.a_trans = a.data_ptr(), lda, int(a_trans)
+    d.b, d.ldb, d.b_trans = b.data_ptr(), ldb, int(b_trans)
+    d.c, d.ldc, d.c_dtype = c.data_ptr(), ldc, code(c)
+    d.batch, d.batch_inner = batch, batch_inner
+    d.sa_outer, d.sa_inner = sa
+    d.sb_outer, d.sb_inner = sb
+    d.sc_outer, d.sc_inner = sc
+    d.alpha, d.beta = alpha, beta
+    d.bias = _p(bias)
+    if rowadd is not None:
+        d.rowadd, d.ld_rowadd, d.rowadd_mod = rowadd.data_ptr(), ld_rowadd, rowadd_mod
+    d.relu = int(relu)
+    d.dropout_p, d.seed = dropout_p, seed & _U64
+    if gate is not None:
+        d.gate, d.ld_gate, d.gate_dtype = gate.data_ptr(), ld_gate, code(gate)
+    if resid is not None:
+        d.resid, d.ld_resid, d.resid_dtype = resid.data_ptr(), ld_resid, code(resid)
+    ws = None
+    if splitk > 1:
+        ws = torch.empty(splitk * m * n, device=c.device, dtype=torch.float32)
+        d.splitk, d.workspace, d.workspace_elems = splitk, ws.data_ptr(), ws.numel()
+    else:
+        d.splitk = 1
+    d.tile = tile
+    call("asrx_gemm", ctypes.byref(d), stream())
+    return ws
+
+
+def linear(x, w, out, *, bias=None, **kw):
+    """out[M,N] = x[M,K] . w[N,K]^T (+ epilogue). x, out 2-D row-major (unit inner stride)."""
+    m, k = x.shape
+    n = w.shape[0]
+    return gemm(x, w, out, m, n, k, lda=x.stride(0), ldb=w.stride(0), ldc=out.stride(0), bias=bias, **kw)
+
+
+def linear_dgrad(dy, w, out, **kw):
+    """out[M,K] = dy[M,N] . w[N,K]"""
+    m, n = dy.shape
+    k = w.shape[1]
+    return gemm(dy, w, out, m, k, n, lda=dy.stride(0), ldb=w.stride(0), ldc=out.stride(0), b_trans=True, **kw)
+
+
+def linear_wgrad(dy, x, wgrad, *, beta=1.0, **kw):
+    """wgrad[N,K] (+)= dy[M,N]^T . x[M,K]  (fp32 gradient buffer)."""
+    m, n = dy.shape
+    k = x.shape[1]
+    return gemm(dy, x, wgrad, n, k, m, lda=dy.stride(0), ldb=x.stride(0), ldc=wgrad.stride(0), a_trans=True,
+                b_trans=True, beta=beta, splitk=kw.pop("splitk", "auto"), **kw)
+
+
+def colsum(x, out, *, accumulate=True, rows=None, cols=None, ld=None):
+    """out[c] (+)= sum_r x[r, c]"""
+    _cuda(x, out)
+    rows = x.shape[0] if rows is None else rows
+    cols = x.shape[1] if cols is None else cols
+    ld = x.stride(0) if ld is None else ld
+    nblocks = max(1, min(512, (rows + 63) // 64))
+    part = torch.empty(nblocks * cols, device=x.device, dtype=torch.float32)
+    call("asrx_reduce_rows", code(x), x.data_ptr(), rows, cols, ld, out.data_ptr(), int(accumulate),
+         part.data_ptr(), nblocks, stream())
+
+
+# ------------------------------------------------------------------------------------------- LayerNorm
+
+def layernorm_fwd(x, gamma, beta, y, eps=1e-5):
+    _cuda(x, gamma, beta, y)
+    rows, d = x.shape
+    mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+    rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
+    call("asrx_layernorm_fwd", code(x), x.data_ptr(), code(y), y.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+         mean.data_ptr(), rstd.data_ptr(), rows, d, eps, stream())
+    return mean, rstd
+
+
+def layernorm_bwd(x, dy, gamma, mean, rstd, dgb, *, dres=None, dx_drop=None, dropout_p=0.0, seed=0):
+    """Returns dx (fp32). dgb: fp32 [2*d] grad buffer (gamma grads then beta grads), accumulated.
+    If dx_drop (bf16 or fp32) is given it receives dropout_bwd(dx) for the upstream sublayer."""
+    _cuda(x, dy, gamma, mean, rstd, dgb)
+    rows, d = x.shape
+    dx = torch.empty(rows, d, device=x.device, dtype=torch.float32)
+    nblocks = max(1, min(512, (rows + 15) // 16))
+    part = torch.empty(nblocks * 2 * d, device=x.device, dtype=torch.float32)
+    call("asrx_layernorm_bwd", code(x), x.data_ptr(), code(dy), dy.data_ptr(), gamma.data_ptr(), mean.data_ptr(),
+         rstd.data_ptr(), _p(dres), dx.data_ptr(), _p(dx_drop), code(dx_drop) if dx_drop is not None else 0,
+         dropout_p, seed & _U64, part.data_ptr(), nblocks, rows, d, stream())
+    part2 = torch.empty(max(1, (nblocks + 63) // 64) * 2 * d, device=x.device, dtype=torch.float32)
+    call("asrx_reduce_rows", F32, part.data_ptr(), nblocks, 2 * d, 2 * d, dgb.data_ptr(), 1, part2.data_ptr(),
+         max(1, (nblocks + 63) // 64), stream())
+    return dx
+
+
+# ------------------------------------------------------------------------------------------- attention
+
+class MaskSpec:
+    """How a score (b, q, key) is masked (True = -inf). mode 0: none; 1: causal/key-valid/query-valid vectors;
+    2: dense bytes with broadcast strides."""
+
+    def __init__(self, mode=0, causal=False, kvalid=None, qvalid=None, valid_bstride=0, dense=None,
+                 strides=(0, 0, 0)):
+        self.mode, self.causal = mode, causal
+        self.kvalid, self.qvalid, self.valid_bstride = kvalid, qvalid, valid_bstride
+        self.dense, self.strides = dense, strides
+
+    @staticmethod
+    def decoder(mask):
+        """model.py:108-115: pad = mask < 1; masked = causal | key pad | query pad."""
+        valid = (mask >= 1).to(torch.uint8).contiguous()
+        return MaskSpec(1, True, valid, valid, valid.stride(0))
+
+    @staticmethod
+    def from_attention_mask(m, B, Lq, Lk):
+        """Any-dtype mask broadcastable to (B, Lq, Lk); nonzero (>0) means masked (layers.py:22-23)."""
+        if m is None:
+            return MaskSpec()
+        mb = m.gt(0).to(torch.uint8)
+        while mb.dim() < 3:
+            mb = mb.unsqueeze(0)
+        mb = mb.expand(B, Lq, Lk)
+        return MaskSpec(2, dense=mb, strides=tuple(mb.stride()))
+
+
+def _attn_desc(q, k, v, o, B, H, Lq, Lk, dh, strides, scale, spec, dropout_p, seed):
+    d = AttnDesc()
+    d.batch, d.heads, d.lq, d.lk, d.dh = B, H, Lq, Lk, dh
+    (qr, qb), (kr, kb), (vr, vb), (orr, ob) = strides
+    d.q, d.q_rstride, d.q_bstride = q.data_ptr(), qr, qb
+    d.k, d.k_rstride, d.k_bstride = k.data_ptr(), kr, kb
+    d.v, d.v_rstride, d.v_bstride = v.data_ptr(), vr, vb
+    d.o, d.o_rstride, d.o_bstride = o.data_ptr(), orr, ob
+    d.scale = scale
+    d.mask_mode, d.causal = spec.mode, int(spec.causal)
+    d.kvalid, d.qvalid, d.valid_bstride = _p(spec.kvalid), _p(spec.qvalid), spec.valid_bstride
+    if spec.mode == 2:
+        d.mask = spec.dense.data_ptr()
+        d.mask_sb, d.mask_sq, d.mask_sk = spec.strides
+    d.dropout_p, d.seed = dropout_p, seed & _U64
+    return d
+
+
+def attention_fwd(q, k, v, o, B, H, Lq, Lk, dh, strides, scale, spec, dropout_p=0.0, seed=0):
+    """Fused attention (bf16). Returns lse [B*H*Lq] (log2 domain)."""
+    _cuda(q, k, v, o)
+    lse = torch.empty(B * H * Lq, device=q.device, dtype=torch.float32)
+    d = _attn_desc(q, k, v, o, B, H, Lq, Lk, dh, strides, scale, spec, dropout_p, seed)
+    d.lse = lse.data_ptr()
+    call("asrx_attention_fwd", ctypes.byref(d), stream())
+    return lse
+
+
+def attention_bwd(q, k, v, o, lse, do, dq, dk, dv, B, H, Lq, Lk, dh, strides, gstrides, scale, spec,
+                  dropout_p=0.0, seed=0):
+    _cuda(q, k, v, o, lse, do, dq, dk, dv)
+    d = _attn_desc(q, k, v, o, B, H, Lq, Lk, dh, strides, scale, spec, dropout_p, seed)
+    d.lse = lse.data_ptr()
+    (dor, dob), (dqr, dqb), (dkr, dkb), (dvr, dvb) = gstrides
+    d.dout, d.do_rstride, d.do_bstride = do.data_ptr(), dor, dob
+    d.dq, d.dq_rstride, d.dq_bstride = dq.data_ptr(), dqr, dqb
+    d.dk, d.dk_rstride, d.dk_bstride = dk.data_ptr(), dkr, dkb
+    d.dv, d.dv_rstride, d.dv_bstride = dv.data_ptr(), dvr, dvb
+    delta = torch.empty(B * H * Lq, device=q.device, dtype=torch.float32)
+    d.delta = delta.data_ptr()
+    acc = None
+    if Lk > 256:
+        acc = torch.empty(B * Lq * H * dh, device=q.device, dtype=torch.float32)
+        d.dq_acc = acc.data_ptr()
+    call("asrx_attention_bwd", ctypes.byref(d), stream())
+
+
+def softmax_fwd(s, p, pd, nbh, H, Lq, Lk, ld, scale, spec, dropout_p=0.0, seed=0):
+    _cuda(s, p, pd)
+    sb, sq, sk = spec.strides if spec.mode == 2 else (0, 0, 0)
+    call("asrx_softmax_fwd", code(s), s.data_ptr(), p.data_ptr(), _p(pd), nbh, H, Lq, Lk, ld, scale, spec.mode,
+         int(spec.causal), _p(spec.kvalid), _p(spec.qvalid), spec.valid_bstride,
+         _p(spec.dense) if spec.mode == 2 else None, sb, sq, sk, dropout_p, seed & _U64, stream())
+
+
+def softmax_bwd(p, dpd, ds, nbh, Lq, Lk, ld, scale, dropout_p=0.0, seed=0):
+    _cuda(p, dpd, ds)
+    call("asrx_softmax_bwd", code(p), p.data_ptr(), dpd.data_ptr(), ds.data_ptr(), nbh, Lq, Lk, ld, scale,
+         dropout_p, seed & _U64, stream())
+
+
+# ------------------------------------------------------------------------------------------- misc
+
+def cast(src, dst):
+    _cuda(src, dst)
+    assert src.numel() == dst.numel()
+    call("asrx_cast", code(src), src.data_ptr(), code(dst), dst.data_ptr(), src.numel(), stream())
+
+
+def dropout_mask(n, p, seed, device):
+    keep = torch.empty(n, dtype=torch.uint8, device=device)
+    call("asrx_dropout_mask", keep.data_ptr(), n, p, seed & _U64, stream())
+    return keep
+
+
+def conv1_fwd(x, w, b, y1):
+    _cuda(x, w, b, y1)
+    B, _, F, T = x.shape
+    call("asrx_conv1_fwd", x.data_ptr(), B, F, T, w.data_ptr(), b.data_ptr(), y1.data_ptr(), code(y1), stream())
+
+
+def im2col_conv2(y1, cols):
+    _cuda(y1, cols)
+    B, F1, T1, _ = y1.shape
+    assert y1.dtype == cols.dtype
+    call("asrx_im2col_conv2", code(y1), y1.data_ptr(), B, F1, T1, cols.data_ptr(), stream())
+
+
+def col2im_conv2(dcols, y1, dy1):
+    _cuda(dcols, y1, dy1)
+    B, F1, T1, _ = y1.shape
+    call("asrx_col2im_conv2", code(dcols), dcols.data_ptr(), code(y1), y1.data_ptr(), B, F1, T1, dy1.data_ptr(),
+         stream())
+
+
+def conv1_bwd_w(x, dy1, dw, db):
+    _cuda(x, dy1, dw, db)
+    B, _, F, T = x.shape
+    nblocks = 512
+    part = torch.empty(nblocks * 640, device=x.device, dtype=torch.float32)
+    call("asrx_conv1_bwd_w", x.data_ptr(), dy1.data_ptr(), B, F, T, part.data_ptr(), nblocks, dw.data_ptr(),
+         db.data_ptr(), stream())
+
+
+def embed_fwd(tok, table, pe, out, L, dropout_p=0.0, seed=0):
+    _cuda(tok, table, pe, out)
+    call("asrx_embed_fwd", tok.data_ptr(), tok.numel(), L, table.data_ptr(), table.shape[1], pe.data_ptr(),
+         dropout_p, seed & _U64, out.data_ptr(), stream())
+
+
+def embed_bwd(tok, dout, dtable, L, pad_id, dropout_p=0.0, seed=0):
+    _cuda(tok, dout, dtable)
+    call("asrx_embed_bwd", tok.data_ptr(), tok.numel(), L, dout.data_ptr(), dtable.shape[1], dtable.shape[0],
+         pad_id, dropout_p, seed & _U64, dtable.data_ptr(), stream())
+
+
+def cross_entropy(logits, V, target, ignore_index=-100, grad_scale=1.0, want_grad=True, want_argmax=False):
+    """logits fp32 [rows, ld]; returns (loss[1], dlogits bf16 [rows, ld] or None, argmax or None)."""
+    _cuda(logits, target)
+    rows, ld = logits.shape
+    loss = torch.empty(1, device=logits.device, dtype=torch.float32)
+    dl = torch.empty(rows, ld, device=logits.device, dtype=torch.bfloat16) if want_grad else None
+    am = torch.empty(rows, device=logits.device, dtype=torch.int64) if want_argmax else None
+    ws = torch.empty(rows + 2, device=logits.device, dtype=torch.float32)
+    call("asrx_cross_entropy", logits.data_ptr(), rows, V, logits.stride(0), target.data_ptr(), ignore_index,
+         grad_scale, loss.data_ptr(), _p(dl), _p(am), ws.data_ptr(), stream())
+    return loss, dl, am
+
+
+def adam(p, g, m, v, p_bf16, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0, decoupled=False):
+    _cuda(p, g, m, v, p_bf16)
+    bc1 = 1.0 - beta1 ** step
+    bc2 = 1.0 - beta2 ** step
+    call("asrx_adam", p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), _p(p_bf16), p.numel(), lr, beta1,
+         beta2, eps, weight_decay, bc1, bc2, grad_scale, int(decoupled), stream())

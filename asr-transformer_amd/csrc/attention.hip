@@ -1,0 +1,515 @@
+// Fused multi-head attention for gfx950 (bf16 operands, fp32 softmax state).
+//
+// Reference semantics (layers.py:15-28): S = (q k^T) * d_model**-0.5; masked_fill(mask > 0, -inf);
+// P = nan_to_num(softmax(S)) (a fully-masked row gives P = 0 and a zero head output); dropout(P); P v.
+//
+// Forward: grid (ceil(Lq/64), B*H), 4 waves x 16 queries.  K/V tiles of 64 keys are staged global->regs->LDS
+// (prefetch of tile t+1 overlaps the MFMAs of tile t).  v_mfma_f32_16x16x16_bf16 throughout, oriented so that
+// the score accumulator S^T[key][q] holds one query per lane: the row max / row sum are in-lane folds plus two
+// cross-lane xor-shuffles (16, 32), and the exponentiated accumulator feeds the P.V product directly as the
+// MFMA B operand (no LDS round trip for P); V^T fragments come from ds_read_b64_tr_b16.  Online softmax in the
+// log2 domain; lse (log2 domain, +inf for fully-masked rows) is saved for the backward pass.
+//
+// Backward: grid (ceil(Lk/(32*NW)), B*H), NW waves x 32 keys, sweeping query chunks of 16 staged in LDS.
+// S and dP are recomputed with the query on the accumulator row, so P and dS feed dV^T and dK^T as B operands
+// directly; dS crosses LDS once (bf16) for dQ^T = K^T dS^T, reduced over the waves in LDS and stored (or
+// accumulated with fp32 atomics when several workgroups share a (b, h)).
+#include "common.h"
+
+namespace {
+
+typedef __attribute__((address_space(3))) s4_t lds_s4_t;
+
+ASRX_DEV s4_t lds_tr(const bf16_t* p) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)p); }
+ASRX_DEV s4_t lds_b64(const bf16_t* p) { return *(const s4_t*)p; }
+ASRX_DEV f4_t mfma16(s4_t a, s4_t b, f4_t c) { return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0); }
+
+ASRX_DEV s4_t to_bf4(f4_t v) {
+  s4_t r;
+  r[0] = (short)f2bf(v[0]); r[1] = (short)f2bf(v[1]); r[2] = (short)f2bf(v[2]); r[3] = (short)f2bf(v[3]);
+  return r;
+}
+
+struct AttnArgs {
+  int B, H, Lq, Lk;
+  const bf16_t* q; int64_t qr, qb;
+  const bf16_t* k; int64_t kr, kb;
+  const bf16_t* v; int64_t vr, vb;
+  bf16_t* o; int64_t orr, ob;
+  float* lse;
+  float scale, scale2;
+  int mode, causal;
+  const uint8_t* kvalid; const uint8_t* qvalid; int64_t validb;
+  const uint8_t* mask; int64_t msb, msq, msk;
+  uint32_t thr; float dscale; uint64_t seed;
+  const bf16_t* dout; int64_t dor, dob;
+  bf16_t* dq; int64_t dqr, dqb;
+  bf16_t* dk; int64_t dkr, dkb;
+  bf16_t* dv; int64_t dvr, dvb;
+  float* delta; float* dq_acc;
+};
+
+ASRX_DEV bool masked(const AttnArgs& a, int b, int q, int key) {
+  if (key >= a.Lk) return true;
+  if (a.mode == 1) {
+    if (a.causal && key > q) return true;
+    if (a.kvalid && !a.kvalid[b * a.validb + key]) return true;
+    if (a.qvalid && !a.qvalid[b * a.validb + q]) return true;
+    return false;
+  }
+  if (a.mode == 2) return a.mask[b * a.msb + (int64_t)q * a.msq + (int64_t)key * a.msk] != 0;
+  return false;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// forward
+// ---------------------------------------------------------------------------------------------------------
+template <int DH>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
+  constexpr int KS = DH + 4;   // K image row stride (elements): conflict-free ds_read_b64 row reads
+  constexpr int VS = DH + 16;  // V image row stride: conflict-free ds_read_b64_tr_b16
+  constexpr int NU = DH / 16;
+  constexpr int CPR = DH / 8;  // 16-B chunks per row
+  constexpr int CH = 64 * CPR / 256;
+  __shared__ __attribute__((aligned(16))) bf16_t sk[64 * KS];
+  __shared__ __attribute__((aligned(16))) bf16_t sv[64 * VS];
+
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, li = l & 15;
+  const int qblk = blockIdx.x * 64;
+  const int q = qblk + 16 * w + li;
+  const bool qlive = q < a.Lq;
+
+  const bf16_t* Kb = a.k + b * a.kb + h * DH;
+  const bf16_t* Vb = a.v + b * a.vb + h * DH;
+
+  s4_t qf[NU];
+  {
+    const bf16_t* qp = a.q + b * a.qb + (int64_t)(qlive ? q : 0) * a.qr + h * DH + 4 * g;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) qf[u] = qlive ? *(const s4_t*)(qp + 16 * u) : s4_t{0, 0, 0, 0};
+  }
+
+  int ntiles = (a.Lk + 63) / 64;
+  if (a.mode == 1 && a.causal) ntiles = min(ntiles, (min(a.Lq, qblk + 64) - 1) / 64 + 1);
+
+  uint4 rk[CH], rv[CH];
+  auto gload = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      const int key = kt * 64 + c / CPR, dc = (c % CPR) * 8;
+      if (key < a.Lk) {
+        rk[i] = *(const uint4*)(Kb + (int64_t)key * a.kr + dc);
+        rv[i] = *(const uint4*)(Vb + (int64_t)key * a.vr + dc);
+      } else {
+        rk[i] = make_uint4(0, 0, 0, 0);
+        rv[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      const int key = c / CPR, dc = (c % CPR) * 8;
+      uint2* kp = (uint2*)(sk + key * KS + dc);
+      kp[0] = make_uint2(rk[i].x, rk[i].y);
+      kp[1] = make_uint2(rk[i].z, rk[i].w);
+      *(uint4*)(sv + key * VS + dc) = rv[i];
+    }
+  };
+
+  f4_t oacc[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) oacc[u] = f4_t{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+  const uint32_t drow = (uint32_t)(((int64_t)bh * a.Lq + q) * a.Lk);
+
+  if (ntiles > 0) gload(0);
+  for (int kt = 0; kt < ntiles; ++kt) {
+    __syncthreads();
+    lstore();
+    __syncthreads();
+    if (kt + 1 < ntiles) gload(kt + 1);
+
+    f4_t s[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s[t] = f4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < NU; ++u) s[t] = mfma16(lds_b64(sk + (16 * t + li) * KS + 16 * u + 4 * g), qf[u], s[t]);
+    }
+    float mt = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kt * 64 + 16 * t + 4 * g + r;
+        const float x = (!qlive || masked(a, b, q, key)) ? -INFINITY : s[t][r] * a.scale2;
+        s[t][r] = x;
+        mt = fmaxf(mt, x);
+      }
+    mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float m_new = fmaxf(m_run, mt);
+    const float m_use = m_new == -INFINITY ? 0.f : m_new;
+    const float alpha = exp2f(m_run - m_use);
+    float rs = 0.f;
+    s4_t pf[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = exp2f(s[t][r] - m_use);
+        rs += p;
+        float pd = p;
+        if (a.thr) pd = rng_keep(a.seed, drow + (uint32_t)(kt * 64 + 16 * t + 4 * g + r), a.thr) ? p * a.dscale : 0.f;
+        s[t][r] = pd;
+      }
+      pf[t] = to_bf4(s[t]);
+    }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    l_run = l_run * alpha + rs;
+    m_run = m_new;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      oacc[u] *= alpha;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const s4_t vt = lds_tr(sv + (16 * t + 4 * g + (li >> 2)) * VS + 16 * u + 4 * (li & 3));
+        oacc[u] = mfma16(vt, pf[t], oacc[u]);
+      }
+    }
+  }
+
+  if (!qlive) return;
+  const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+  bf16_t* op = a.o + b * a.ob + (int64_t)q * a.orr + h * DH + 4 * g;
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    uint2 st;
+    st.x = pack2bf(oacc[u][0] * inv, oacc[u][1] * inv);
+    st.y = pack2bf(oacc[u][2] * inv, oacc[u][3] * inv);
+    *(uint2*)(op + 16 * u) = st;
+  }
+  if (g == 0 && a.lse) {
+    const float mu = m_run == -INFINITY ? 0.f : m_run;
+    a.lse[(int64_t)bh * a.Lq + q] = l_run > 0.f ? mu + log2f(l_run) : INFINITY;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// backward prologue: delta = rowsum(dO * O)
+// ---------------------------------------------------------------------------------------------------------
+template <int DH>
+__global__ __launch_bounds__(256) void attn_delta_kernel(AttnArgs a) {
+  constexpr int PER = DH / 16;  // elements per lane, 16 lanes per row
+  const int64_t rows = (int64_t)a.B * a.H * a.Lq;
+  const int64_t row = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int li = threadIdx.x & 15;
+  float s = 0.f;
+  if (row < rows) {
+    const int q = (int)(row % a.Lq);
+    const int64_t bh = row / a.Lq;
+    const int b = (int)(bh / a.H), h = (int)(bh % a.H);
+    const bf16_t* op = a.o + b * a.ob + (int64_t)q * a.orr + h * DH + li * PER;
+    const bf16_t* dp = a.dout + b * a.dob + (int64_t)q * a.dor + h * DH + li * PER;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) s += bf2f(op[i]) * bf2f(dp[i]);
+  }
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (row < rows && li == 0) a.delta[row] = s;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// backward
+// ---------------------------------------------------------------------------------------------------------
+template <int DH>
+__global__ __launch_bounds__(512) void attn_bwd_kernel(AttnArgs a, int nw, int single) {
+  constexpr int NU = DH / 16;
+  constexpr int KST = DH + 16;   // K image (tr reads for dQ)
+  constexpr int CS = DH + 16;    // Q / dO chunk images (row reads + tr reads)
+  constexpr int DSS = 32 + 4;    // per-wave dS image [16 q][32 keys]
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* sk = (bf16_t*)smem;                              // [32*nw][KST]
+  bf16_t* sq = sk + 32 * nw * KST;                         // [16][CS]
+  bf16_t* sdo = sq + 16 * CS;                              // [16][CS]
+  bf16_t* sds = sdo + 16 * CS;                             // [nw][16][DSS]
+  float* red = (float*)(sds + nw * 16 * DSS);              // [nw][16][DH]
+  float* slse = red + nw * 16 * DH;                        // [16]
+  float* sdel = slse + 16;                                 // [16]
+
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, li = l & 15;
+  const int nthr = nw * 64;
+  const int kwg = blockIdx.x * 32 * nw;
+  const int kw0 = kwg + 32 * w;
+
+  // stage this workgroup's K rows in LDS, keep K/V B-operand fragments in registers
+  const bf16_t* Kb = a.k + b * a.kb + h * DH;
+  const bf16_t* Vb = a.v + b * a.vb + h * DH;
+  for (int c = threadIdx.x; c < 32 * nw * (DH / 8); c += nthr) {
+    const int kr = c / (DH / 8), dc = (c % (DH / 8)) * 8;
+    const int key = kwg + kr;
+    uint4 val = make_uint4(0, 0, 0, 0);
+    if (key < a.Lk) val = *(const uint4*)(Kb + (int64_t)key * a.kr + dc);
+    *(uint4*)(sk + kr * KST + dc) = val;
+  }
+  s4_t kf[2][NU], vf[2][NU];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int key = kw0 + 16 * t + li;
+    const bool ok = key < a.Lk;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      kf[t][u] = ok ? *(const s4_t*)(Kb + (int64_t)key * a.kr + 16 * u + 4 * g) : s4_t{0, 0, 0, 0};
+      vf[t][u] = ok ? *(const s4_t*)(Vb + (int64_t)key * a.vr + 16 * u + 4 * g) : s4_t{0, 0, 0, 0};
+    }
+  }
+
+  f4_t dva[NU][2], dka[NU][2];
+#pragma unroll
+  for (int u = 0; u < NU; ++u)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) { dva[u][t] = f4_t{0.f, 0.f, 0.f, 0.f}; dka[u][t] = f4_t{0.f, 0.f, 0.f, 0.f}; }
+
+  const bf16_t* Qb = a.q + b * a.qb + h * DH;
+  const bf16_t* Db = a.dout + b * a.dob + h * DH;
+  const float* lseb = a.lse + (int64_t)bh * a.Lq;
+  const float* delb = a.delta + (int64_t)bh * a.Lq;
+  bf16_t* myds = sds + w * 16 * DSS;
+  float* myred = red + w * 16 * DH;
+
+  int qstart = 0;
+  if (a.mode == 1 && a.causal) qstart = (kwg / 16) * 16;  // queries below the first key are fully masked
+  for (int q0 = qstart; q0 < a.Lq; q0 += 16) {
+    __syncthreads();  // previous chunk's LDS reads complete
+    for (int c = threadIdx.x; c < 2 * 16 * (DH / 8); c += nthr) {
+      const int which = c / (16 * (DH / 8));
+      const int cc = c % (16 * (DH / 8));
+      const int qr = cc / (DH / 8), dc = (cc % (DH / 8)) * 8;
+      const int qq = q0 + qr;
+      uint4 val = make_uint4(0, 0, 0, 0);
+      if (qq < a.Lq) val = *(const uint4*)((which ? Db + (int64_t)qq * a.dor : Qb + (int64_t)qq * a.qr) + dc);
+      *(uint4*)((which ? sdo : sq) + qr * CS + dc) = val;
+    }
+    if (threadIdx.x < 16) {
+      const int qq = q0 + threadIdx.x;
+      slse[threadIdx.x] = qq < a.Lq ? lseb[qq] : INFINITY;
+      sdel[threadIdx.x] = qq < a.Lq ? delb[qq] : 0.f;
+    }
+    __syncthreads();
+
+    // S[q][key] and dP[q][key]: A = Q / dO rows (lane = query), B = K^T / V^T fragments in registers
+    f4_t s[2], dp[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) { s[t] = f4_t{0.f, 0.f, 0.f, 0.f}; dp[t] = f4_t{0.f, 0.f, 0.f, 0.f}; }
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const s4_t qa = lds_b64(sq + li * CS + 16 * u + 4 * g);
+      const s4_t da = lds_b64(sdo + li * CS + 16 * u + 4 * g);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        s[t] = mfma16(qa, kf[t][u], s[t]);
+        dp[t] = mfma16(da, vf[t][u], dp[t]);
+      }
+    }
+    s4_t pb[2], dsb[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f4_t pd, dsv;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qq = q0 + 4 * g + r;
+        const int key = kw0 + 16 * t + li;
+        const bool live = qq < a.Lq && !masked(a, b, qq, key);
+        const float p = live ? exp2f(s[t][r] * a.scale2 - slse[4 * g + r]) : 0.f;
+        float dpe = dp[t][r];
+        float pdv = p;
+        if (a.thr) {
+          const bool keep = rng_keep(a.seed, (uint32_t)(((int64_t)bh * a.Lq + qq) * a.Lk + key), a.thr);
+          dpe = keep ? dpe * a.dscale : 0.f;
+          pdv = keep ? p * a.dscale : 0.f;
+        }
+        pd[r] = pdv;
+        dsv[r] = p * (dpe - sdel[4 * g + r]);
+      }
+      pb[t] = to_bf4(pd);
+      dsb[t] = to_bf4(dsv);
+      // dS -> LDS as [q][key] (bf16) for the dQ product
+#pragma unroll
+      for (int r = 0; r < 4; ++r) myds[(4 * g + r) * DSS + 16 * t + li] = (bf16_t)dsb[t][r];
+    }
+    // dV^T += dO^T Pd ; dK^T += Q^T dS    (A = transposed chunk reads, B = accumulators)
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const s4_t doT = lds_tr(sdo + (4 * g + (li >> 2)) * CS + 16 * u + 4 * (li & 3));
+      const s4_t qT = lds_tr(sq + (4 * g + (li >> 2)) * CS + 16 * u + 4 * (li & 3));
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        dva[u][t] = mfma16(doT, pb[t], dva[u][t]);
+        dka[u][t] = mfma16(qT, dsb[t], dka[u][t]);
+      }
+    }
+    // dQ^T[d][q] = sum_key K^T[d][key] dS^T[key][q]
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      f4_t dq = f4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const s4_t kT = lds_tr(sk + (32 * w + 16 * t + 4 * g + (li >> 2)) * KST + 16 * u + 4 * (li & 3));
+        const s4_t dsT = lds_b64(myds + li * DSS + 16 * t + 4 * g);
+        dq = mfma16(kT, dsT, dq);
+      }
+      // dq element r: d = 16u + 4g + r, q = li
+      *(f4_t*)(myred + li * DH + 16 * u + 4 * g) = dq;
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < 16 * DH; c += nthr) {
+      const int qr = c / DH, d = c % DH;
+      const int qq = q0 + qr;
+      float sum = 0.f;
+      for (int ww = 0; ww < nw; ++ww) sum += red[ww * 16 * DH + c];
+      if (qq < a.Lq) {
+        if (single) a.dq[b * a.dqb + (int64_t)qq * a.dqr + h * DH + d] = f2bf(sum * a.scale);
+        else atomicAdd(a.dq_acc + (((int64_t)b * a.Lq + qq) * a.H + h) * DH + d, sum);
+      }
+    }
+  }
+
+  // dK = scale * dK^T, dV = dV^T; accumulator element r: d = 16u + 4g + r, key = kw0 + 16t + li
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int key = kw0 + 16 * t + li;
+    if (key >= a.Lk) continue;
+    bf16_t* dkp = a.dk + b * a.dkb + (int64_t)key * a.dkr + h * DH + 4 * g;
+    bf16_t* dvp = a.dv + b * a.dvb + (int64_t)key * a.dvr + h * DH + 4 * g;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      uint2 x;
+      x.x = pack2bf(dka[u][t][0] * a.scale, dka[u][t][1] * a.scale);
+      x.y = pack2bf(dka[u][t][2] * a.scale, dka[u][t][3] * a.scale);
+      *(uint2*)(dkp + 16 * u) = x;
+      x.x = pack2bf(dva[u][t][0], dva[u][t][1]);
+      x.y = pack2bf(dva[u][t][2], dva[u][t][3]);
+      *(uint2*)(dvp + 16 * u) = x;
+    }
+  }
+}
+
+// dq (bf16, strided) = scale * dq_acc (fp32 [B][Lq][H][DH])
+__global__ __launch_bounds__(256) void dq_finish_kernel(AttnArgs a, int dh) {
+  const int64_t total = (int64_t)a.B * a.Lq * a.H * dh;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int d = (int)(i % dh);
+    const int64_t r = i / dh;
+    const int h = (int)(r % a.H);
+    const int64_t r2 = r / a.H;
+    const int q = (int)(r2 % a.Lq);
+    const int b = (int)(r2 / a.Lq);
+    a.dq[b * a.dqb + (int64_t)q * a.dqr + h * dh + d] = f2bf(a.dq_acc[i] * a.scale);
+  }
+}
+
+int fill_args(const asrx_attn_desc* d, AttnArgs& a) {
+  if (!d || d->batch <= 0 || d->heads <= 0 || d->lq <= 0 || d->lk <= 0) return ASRX_ERR_ARG;
+  if (d->dh != 32 && d->dh != 64) return ASRX_ERR_UNSUPPORTED;
+  if (!d->q || !d->k || !d->v) return ASRX_ERR_ARG;
+  if (d->mask_mode == 2 && !d->mask) return ASRX_ERR_ARG;
+  // 16-byte row chunks for the staged loads, 8-byte fragment loads
+  const int64_t strides[] = {d->q_rstride, d->q_bstride, d->k_rstride, d->k_bstride, d->v_rstride, d->v_bstride};
+  for (int64_t s : strides) if (s % 8) return ASRX_ERR_UNSUPPORTED;
+  if (((uintptr_t)d->q | (uintptr_t)d->k | (uintptr_t)d->v) % 16) return ASRX_ERR_UNSUPPORTED;
+  a.B = d->batch; a.H = d->heads; a.Lq = d->lq; a.Lk = d->lk;
+  a.q = (const bf16_t*)d->q; a.qr = d->q_rstride; a.qb = d->q_bstride;
+  a.k = (const bf16_t*)d->k; a.kr = d->k_rstride; a.kb = d->k_bstride;
+  a.v = (const bf16_t*)d->v; a.vr = d->v_rstride; a.vb = d->v_bstride;
+  a.o = (bf16_t*)d->o; a.orr = d->o_rstride; a.ob = d->o_bstride;
+  a.lse = d->lse;
+  a.scale = d->scale; a.scale2 = d->scale * 1.4426950408889634f;
+  a.mode = d->mask_mode; a.causal = d->causal;
+  a.kvalid = d->kvalid; a.qvalid = d->qvalid; a.validb = d->valid_bstride;
+  a.mask = d->mask; a.msb = d->mask_sb; a.msq = d->mask_sq; a.msk = d->mask_sk;
+  a.thr = drop_threshold(d->dropout_p);
+  a.dscale = (d->dropout_p > 0.f && d->dropout_p < 1.f) ? 1.f / (1.f - d->dropout_p) : 1.f;
+  a.seed = d->seed;
+  a.dout = (const bf16_t*)d->dout; a.dor = d->do_rstride; a.dob = d->do_bstride;
+  a.dq = (bf16_t*)d->dq; a.dqr = d->dq_rstride; a.dqb = d->dq_bstride;
+  a.dk = (bf16_t*)d->dk; a.dkr = d->dk_rstride; a.dkb = d->dk_bstride;
+  a.dv = (bf16_t*)d->dv; a.dvr = d->dv_rstride; a.dvb = d->dv_bstride;
+  a.delta = d->delta; a.dq_acc = d->dq_acc;
+  return ASRX_OK;
+}
+
+size_t bwd_smem(int nw, int dh) {
+  const int kst = dh + 16, cs = dh + 16, dss = 36;
+  return (size_t)(32 * nw * kst + 2 * 16 * cs + nw * 16 * dss) * 2 + (size_t)nw * 16 * dh * 4 + 32 * 4;
+}
+
+}  // namespace
+
+extern "C" int asrx_attention_fwd(const asrx_attn_desc* d, void* stream) {
+  AttnArgs a;
+  int rc = fill_args(d, a);
+  if (rc) return rc;
+  if (!a.o || (a.orr % 4) || (a.ob % 4) || ((uintptr_t)a.o % 8)) return ASRX_ERR_UNSUPPORTED;
+  dim3 grid((a.Lq + 63) / 64, a.B * a.H);
+  if (grid.y > 65535u * 1024u) return ASRX_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  if (d->dh == 64) hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(attn_fwd_kernel<32>, grid, dim3(256), 0, st, a);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
+extern "C" int asrx_attn_delta(const asrx_attn_desc* d, void* stream) {
+  AttnArgs a;
+  int rc = fill_args(d, a);
+  if (rc) return rc;
+  if (!a.o || !a.dout || !a.delta) return ASRX_ERR_ARG;
+  const int64_t rows = (int64_t)a.B * a.H * a.Lq;
+  dim3 grid((unsigned)((rows + 15) / 16));
+  hipStream_t st = (hipStream_t)stream;
+  if (d->dh == 64) hipLaunchKernelGGL(attn_delta_kernel<64>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(attn_delta_kernel<32>, grid, dim3(256), 0, st, a);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
+extern "C" int asrx_attention_bwd(const asrx_attn_desc* d, void* stream) {
+  AttnArgs a;
+  int rc = fill_args(d, a);
+  if (rc) return rc;
+  if (!a.o || !a.dout || !a.dq || !a.dk || !a.dv || !a.lse || !a.delta) return ASRX_ERR_ARG;
+  const int64_t ostr[] = {a.orr, a.ob, a.dor, a.dob, a.dkr, a.dkb, a.dvr, a.dvb};
+  for (int64_t s : ostr) if (s % 8) return ASRX_ERR_UNSUPPORTED;
+  hipStream_t st = (hipStream_t)stream;
+  rc = asrx_attn_delta(d, stream);
+  if (rc) return rc;
+  int nw = (a.Lk + 31) / 32;
+  if (nw > 8) nw = 8;
+  const int nblk = (a.Lk + 32 * nw - 1) / (32 * nw);
+  const int single = nblk == 1;
+  if (!single) {
+    if (!a.dq_acc) return ASRX_ERR_ARG;
+    hipMemsetAsync(a.dq_acc, 0, sizeof(float) * (size_t)a.B * a.Lq * a.H * d->dh, st);
+  }
+  const size_t smem = bwd_smem(nw, d->dh);
+  dim3 grid(nblk, a.B * a.H);
+  if (d->dh == 64) hipLaunchKernelGGL(attn_bwd_kernel<64>, grid, dim3(64 * nw), smem, st, a, nw, single);
+  else hipLaunchKernelGGL(attn_bwd_kernel<32>, grid, dim3(64 * nw), smem, st, a, nw, single);
+  ASRX_CHECK_LAUNCH();
+  if (!single) {
+    const int64_t total = (int64_t)a.B * a.Lq * a.H * d->dh;
+    unsigned blocks = (unsigned)std::min<int64_t>((total + 255) / 256, 8192);
+    hipLaunchKernelGGL(dq_finish_kernel, dim3(blocks), dim3(256), 0, st, a, d->dh);
+    ASRX_CHECK_LAUNCH();
+  }
+  return ASRX_OK;
+}

@@ -1,0 +1,478 @@
+// Conv2d subsampling front-end, decoder embedding, cross-entropy, fused Adam, casts.
+//   conv front-end  : model.py:168-171 (Conv2d(1,64,3,s2)+ReLU, Conv2d(64,64,3,s2)+ReLU) and the flatten of
+//                     model.py:43-45.  conv1 is a direct 9-tap kernel writing channels-last bf16; conv2 is a GEMM
+//                     over an im2col image whose rows are (b, t2, f2) and columns (kh, kw, c), so the GEMM output
+//                     IS the encoder input (B*T', F''*64) — the reference's transpose+contiguous disappears (the
+//                     channel-major feature order c*F''+f is absorbed by permuting _lin_in's columns host-side).
+//   embedding       : model.py:94-96,117 (nn.Embedding(padding_idx) + PE + dropout).
+//   cross-entropy   : train.py:32 (caller-supplied CE, mean reduction).
+//   Adam            : train.py:35 (caller-supplied optimizer; fused over the flat parameter buffer).
+#include "common.h"
+
+namespace {
+
+constexpr int C1 = 64;
+
+template <typename OT>
+__global__ __launch_bounds__(256) void conv1_fwd_kernel(const float* __restrict__ x, int B, int F, int T, int F1,
+                                                        int T1, const float* __restrict__ w,
+                                                        const float* __restrict__ bias, OT* __restrict__ y) {
+  __shared__ float sw[C1 * 9 + C1];
+  for (int i = threadIdx.x; i < C1 * 10; i += 256) sw[i] = i < C1 * 9 ? w[i] : bias[i - C1 * 9];
+  __syncthreads();
+  const int64_t total = (int64_t)B * F1 * T1 * 8;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    const int cg = (int)(t & 7);
+    const int64_t pos = t >> 3;
+    const int t1 = (int)(pos % T1);
+    const int64_t r = pos / T1;
+    const int f1 = (int)(r % F1);
+    const int b = (int)(r / F1);
+    const float* xp = x + ((int64_t)b * F + 2 * f1) * T + 2 * t1;
+    float in[9];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) in[kh * 3 + kw] = xp[(int64_t)kh * T + kw];
+    float o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = cg * 8 + i;
+      float s = sw[C1 * 9 + c];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) s += sw[c * 9 + k] * in[k];
+      o[i] = fmaxf(s, 0.f);
+    }
+    if constexpr (sizeof(OT) == 2) {
+      uint4 u;
+      u.x = pack2bf(o[0], o[1]); u.y = pack2bf(o[2], o[3]); u.z = pack2bf(o[4], o[5]); u.w = pack2bf(o[6], o[7]);
+      *(uint4*)(y + pos * C1 + cg * 8) = u;
+    } else {
+      *(f4_t*)(y + pos * C1 + cg * 8) = f4_t{o[0], o[1], o[2], o[3]};
+      *(f4_t*)(y + pos * C1 + cg * 8 + 4) = f4_t{o[4], o[5], o[6], o[7]};
+    }
+  }
+}
+
+template <typename ET>
+__global__ __launch_bounds__(256) void im2col_kernel(const ET* __restrict__ y1, int B, int F1, int T1, int F2,
+                                                     int T2, ET* __restrict__ cols) {
+  constexpr int EPC = 16 / sizeof(ET);   // elements per 16-byte chunk
+  constexpr int CPR = 576 / EPC;         // chunks per im2col row
+  constexpr int CPT = C1 / EPC;          // chunks per (kh, kw) tap
+  const int64_t total = (int64_t)B * T2 * F2 * CPR;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    const int ch = (int)(t % CPR);
+    const int64_t row = t / CPR;
+    const int f2 = (int)(row % F2);
+    const int64_t r = row / F2;
+    const int t2 = (int)(r % T2);
+    const int b = (int)(r / T2);
+    const int kk = ch / CPT, c0 = (ch % CPT) * EPC;
+    const int kh = kk / 3, kw = kk % 3;
+    const uint4 v = *(const uint4*)(y1 + (((int64_t)b * F1 + 2 * f2 + kh) * T1 + 2 * t2 + kw) * C1 + c0);
+    *(uint4*)(cols + row * 576 + ch * EPC) = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void col2im_kernel(int dtype, const void* __restrict__ dcols, int ydtype,
+                                                     const void* __restrict__ y1, int B, int F1, int T1, int F2,
+                                                     int T2, float* __restrict__ dy1) {
+  const int64_t total = (int64_t)B * F1 * T1 * 16;  // 4 channels per thread
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    const int cq = (int)(t & 15);
+    const int64_t pos = t >> 4;
+    const int t1 = (int)(pos % T1);
+    const int64_t r = pos / T1;
+    const int f1 = (int)(r % F1);
+    const int b = (int)(r / F1);
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int fd = f1 - kh;
+      if (fd < 0 || (fd & 1) || (fd >> 1) >= F2) continue;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int td = t1 - kw;
+        if (td < 0 || (td & 1) || (td >> 1) >= T2) continue;
+        const int64_t row = ((int64_t)b * T2 + (td >> 1)) * F2 + (fd >> 1);
+        const int64_t off = row * 576 + (kh * 3 + kw) * C1 + cq * 4;
+        if (dtype == ASRX_F32) {
+          const f4_t v = *(const f4_t*)((const float*)dcols + off);
+          s[0] += v[0]; s[1] += v[1]; s[2] += v[2]; s[3] += v[3];
+        } else {
+          const uint2 u = *(const uint2*)((const bf16_t*)dcols + off);
+          s[0] += bf2f(u.x & 0xffff); s[1] += bf2f(u.x >> 16); s[2] += bf2f(u.y & 0xffff); s[3] += bf2f(u.y >> 16);
+        }
+      }
+    }
+    float gv[4];
+    if (ydtype == ASRX_F32) {
+      const f4_t g = *(const f4_t*)((const float*)y1 + pos * C1 + cq * 4);
+      gv[0] = g[0]; gv[1] = g[1]; gv[2] = g[2]; gv[3] = g[3];
+    } else {
+      const uint2 g = *(const uint2*)((const bf16_t*)y1 + pos * C1 + cq * 4);
+      gv[0] = bf2f(g.x & 0xffff); gv[1] = bf2f(g.x >> 16); gv[2] = bf2f(g.y & 0xffff); gv[3] = bf2f(g.y >> 16);
+    }
+    f4_t o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = gv[i] > 0.f ? s[i] : 0.f;
+    *(f4_t*)(dy1 + pos * C1 + cq * 4) = o;
+  }
+}
+
+// dW1/db1 partials: thread = (channel c, stream sub); positions of the block strided by 4 subs.
+__global__ __launch_bounds__(256) void conv1_bwd_w_kernel(const float* __restrict__ x, const float* __restrict__ dy1,
+                                                          int B, int F, int T, int F1, int T1, float* __restrict__ part,
+                                                          int64_t per_block) {
+  const int c = threadIdx.x & 63, sub = threadIdx.x >> 6;
+  const int64_t npos = (int64_t)B * F1 * T1;
+  const int64_t p0 = (int64_t)blockIdx.x * per_block;
+  const int64_t p1 = min(npos, p0 + per_block);
+  float acc[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) acc[k] = 0.f;
+  for (int64_t pos = p0 + sub; pos < p1; pos += 4) {
+    const int t1 = (int)(pos % T1);
+    const int64_t r = pos / T1;
+    const int f1 = (int)(r % F1);
+    const int b = (int)(r / F1);
+    const float g = dy1[pos * C1 + c];
+    const float* xp = x + ((int64_t)b * F + 2 * f1) * T + 2 * t1;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) acc[kh * 3 + kw] += g * xp[(int64_t)kh * T + kw];
+    acc[9] += g;
+  }
+  __shared__ float red[4][640];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) red[sub][c * 10 + k] = acc[k];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 640; i += 256)
+    part[(int64_t)blockIdx.x * 640 + i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+}
+
+__global__ __launch_bounds__(256) void conv1_bwd_finish(const float* part, int nblocks, float* dw, float* db) {
+  for (int i = threadIdx.x + blockIdx.x * 256; i < 640; i += gridDim.x * 256) {
+    float s = 0.f;
+    for (int p = 0; p < nblocks; ++p) s += part[(int64_t)p * 640 + i];
+    const int c = i / 10, k = i % 10;
+    if (k < 9) dw[c * 9 + k] += s;
+    else db[c] += s;
+  }
+}
+
+__global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restrict__ tok, int64_t ntok, int L,
+                                                        const float* __restrict__ table, int d,
+                                                        const float* __restrict__ pe, uint32_t thr, float sc,
+                                                        uint64_t seed, float* __restrict__ out) {
+  const int dq = d / 4;
+  const int64_t total = ntok * dq;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    const int64_t row = t / dq;
+    const int c = (int)(t % dq) * 4;
+    const int64_t v = tok[row];
+    const f4_t e = *(const f4_t*)(table + v * d + c);
+    const f4_t p = *(const f4_t*)(pe + (int64_t)(row % L) * d + c);
+    f4_t o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      o[i] = e[i] + p[i];
+      if (thr) o[i] = rng_keep(seed, (uint32_t)(row * d + c + i), thr) ? o[i] * sc : 0.f;
+    }
+    *(f4_t*)(out + row * d + c) = o;
+  }
+}
+
+__global__ __launch_bounds__(256) void embed_bwd_kernel(const int64_t* __restrict__ tok, int64_t ntok, int d,
+                                                        const float* __restrict__ dout, int pad_id, uint32_t thr,
+                                                        float sc, uint64_t seed, float* __restrict__ dtable) {
+  const int v = blockIdx.x;
+  if (v == pad_id) return;
+  for (int c = threadIdx.x; c < d; c += 256) {
+    float s = 0.f;
+    for (int64_t r = 0; r < ntok; ++r) {
+      if (tok[r] != v) continue;
+      float g = dout[r * d + c];
+      if (thr) g = rng_keep(seed, (uint32_t)(r * d + c), thr) ? g * sc : 0.f;
+      s += g;
+    }
+    dtable[(int64_t)v * d + c] += s;
+  }
+}
+
+__global__ __launch_bounds__(256) void ce_count_kernel(const int64_t* tgt, int64_t rows, int64_t ignore, float* ws) {
+  __shared__ float red[256];
+  float c = 0.f;
+  for (int64_t r = threadIdx.x; r < rows; r += 256) c += tgt[r] != ignore ? 1.f : 0.f;
+  red[threadIdx.x] = c;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) ws[rows] = red[0];
+}
+
+template <int NJ>
+__global__ __launch_bounds__(256) void ce_rows_kernel(const float* __restrict__ logits, int64_t rows, int V,
+                                                      int64_t ld, const int64_t* __restrict__ tgt, int64_t ignore,
+                                                      float gscale, bf16_t* __restrict__ dlog, int64_t* argmax,
+                                                      float* ws) {
+  const int l = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const float* x = logits + r * ld;
+  float v[NJ];
+  float mx = -INFINITY;
+  int am = 0;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = j * 64 + l;
+    v[j] = c < V ? x[c] : -INFINITY;
+    if (v[j] > mx) { mx = v[j]; am = c; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(mx, o, 64);
+    const int oa = __shfl_xor(am, o, 64);
+    if (om > mx || (om == mx && oa < am)) { mx = om; am = oa; }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) s += __expf(v[j] - mx);
+  s = wave_sum(s);
+  const float lse = mx + __logf(s);
+  const int64_t t = tgt[r];
+  const bool valid = t != ignore;
+  const float cnt = ws[rows];
+  const float k = valid && cnt > 0.f ? gscale / cnt : 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = j * 64 + l;
+    if (c < ld) {
+      float gr = 0.f;
+      if (c < V) gr = (__expf(v[j] - lse) - (c == t ? 1.f : 0.f)) * k;
+      if (dlog) dlog[r * ld + c] = f2bf(gr);
+    }
+  }
+  if (l == 0) {
+    ws[r] = valid ? lse - x[t] : 0.f;
+    if (argmax) argmax[r] = am;
+  }
+}
+
+__global__ __launch_bounds__(256) void ce_final_kernel(const float* ws, int64_t rows, float* loss) {
+  __shared__ float red[256];
+  float s = 0.f;
+  for (int64_t r = threadIdx.x; r < rows; r += 256) s += ws[r];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss[0] = ws[rows] > 0.f ? red[0] / ws[rows] : 0.f;
+}
+
+__global__ __launch_bounds__(256) void cast_kernel(int sd, const void* __restrict__ src, int dd, void* __restrict__ dst,
+                                                   int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float v = sd == ASRX_F32 ? ((const float*)src)[i] : bf2f(((const bf16_t*)src)[i]);
+    if (dd == ASRX_F32) ((float*)dst)[i] = v;
+    else ((bf16_t*)dst)[i] = f2bf(v);
+  }
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v,
+                                                   bf16_t* __restrict__ pb, int64_t n, float lr, float b1, float b2,
+                                                   float eps, float wd, float bc1, float rbc2, float gs,
+                                                   int decoupled) {
+  const int64_t n4 = n / 4;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    f4_t pp = ((f4_t*)p)[i], gg = ((const f4_t*)g)[i], mm = ((f4_t*)m)[i], vv = ((f4_t*)v)[i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float gr = gg[k] * gs;
+      float pv = pp[k];
+      if (decoupled) pv *= (1.f - lr * wd);
+      else gr += wd * pv;
+      mm[k] = b1 * mm[k] + (1.f - b1) * gr;
+      vv[k] = b2 * vv[k] + (1.f - b2) * gr * gr;
+      const float denom = sqrtf(vv[k]) * rbc2 + eps;
+      pv -= (lr / bc1) * mm[k] / denom;
+      pp[k] = pv;
+    }
+    ((f4_t*)p)[i] = pp;
+    ((f4_t*)m)[i] = mm;
+    ((f4_t*)v)[i] = vv;
+    if (pb) {
+      uint2 u;
+      u.x = pack2bf(pp[0], pp[1]);
+      u.y = pack2bf(pp[2], pp[3]);
+      ((uint2*)pb)[i] = u;
+    }
+  }
+  // tail
+  if (blockIdx.x == 0) {
+    for (int64_t i = n4 * 4 + threadIdx.x; i < n; i += 256) {
+      float gr = g[i] * gs, pv = p[i];
+      if (decoupled) pv *= (1.f - lr * wd);
+      else gr += wd * pv;
+      m[i] = b1 * m[i] + (1.f - b1) * gr;
+      v[i] = b2 * v[i] + (1.f - b2) * gr * gr;
+      pv -= (lr / bc1) * m[i] / (sqrtf(v[i]) * rbc2 + eps);
+      p[i] = pv;
+      if (pb) pb[i] = f2bf(pv);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void dropout_mask_kernel(uint8_t* keep, int64_t n, uint32_t thr, uint64_t seed) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    keep[i] = rng_keep(seed, (uint32_t)i, thr) ? 1 : 0;
+}
+
+inline unsigned grid_for(int64_t work, int cap = 8192) {
+  int64_t b = (work + 255) / 256;
+  if (b < 1) b = 1;
+  if (b > cap) b = cap;
+  return (unsigned)b;
+}
+
+}  // namespace
+
+extern "C" int asrx_version(void) { return 1; }
+
+extern "C" int asrx_conv1_fwd(const float* x, int32_t B, int32_t F, int32_t T, const float* w, const float* b,
+                              void* y1, int32_t y_dtype, void* stream) {
+  if (!x || !w || !b || !y1 || B <= 0 || F < 3 || T < 3) return ASRX_ERR_ARG;
+  const int F1 = (F - 3) / 2 + 1, T1 = (T - 3) / 2 + 1;
+  const dim3 grid(grid_for((int64_t)B * F1 * T1 * 8));
+  if (y_dtype == ASRX_F32)
+    hipLaunchKernelGGL(conv1_fwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, x, B, F, T, F1, T1, w, b,
+                       (float*)y1);
+  else
+    hipLaunchKernelGGL(conv1_fwd_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, x, B, F, T, F1, T1, w, b,
+                       (bf16_t*)y1);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
+extern "C" int asrx_im2col_conv2(int32_t dtype, const void* y1, int32_t B, int32_t F1, int32_t T1, void* cols,
+                                 void* stream) {
+  if (!y1 || !cols || B <= 0 || F1 < 3 || T1 < 3) return ASRX_ERR_ARG;
+  const int F2 = (F1 - 3) / 2 + 1, T2 = (T1 - 3) / 2 + 1;
+  if (dtype == ASRX_F32)
+    hipLaunchKernelGGL(im2col_kernel<float>, dim3(grid_for((int64_t)B * T2 * F2 * 144)), dim3(256), 0,
+                       (hipStream_t)stream, (const float*)y1, B, F1, T1, F2, T2, (float*)cols);
+  else
+    hipLaunchKernelGGL(im2col_kernel<bf16_t>, dim3(grid_for((int64_t)B * T2 * F2 * 72)), dim3(256), 0,
+                       (hipStream_t)stream, (const bf16_t*)y1, B, F1, T1, F2, T2, (bf16_t*)cols);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
+extern "C" int asrx_col2im_conv2(int32_t dtype, const void* dcols, int32_t y1_dtype, const void* y1, int32_t B,
+                                 int32_t F1, int32_t T1, float* dy1, void* stream) {
+  if (!dcols || !y1 || !dy1 || B <= 0 || F1 < 3 || T1 < 3) return ASRX_ERR_ARG;
+  const int F2 = (F1 - 3) / 2 + 1, T2 = (T1 - 3) / 2 + 1;
+  hipLaunchKernelGGL(col2im_kernel, dim3(grid_for((int64_t)B * F1 * T1 * 16)), dim3(256), 0, (hipStream_t)stream,
+                     dtype, dcols, y1_dtype, y1, B, F1, T1, F2, T2, dy1);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
+extern "C" int asrx_conv1_bwd_w(const float* x, const float* dy1, int32_t B, int32_t F, int32_t T, float* part,
+                                int32_t nblocks, float* dw, float* db, void* stream) {
+  if (!x || !dy1 || !part || !dw || !db || nblocks <= 0) return ASRX_ERR_ARG;
+  const int F1 = (F - 3) / 2 + 1, T1 = (T - 3) / 2 + 1;
+  const int64_t npos = (int64_t)B * F1 * T1;
+  const int64_t per = (npos + nblocks - 1) / nblocks;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(conv1_bwd_w_kernel, dim3(nblocks), dim3(256), 0, st, x, dy1, B, F, T, F1, T1, part, per);
+  ASRX_CHECK_LAUNCH();
+  hipLaunchKernelGGL(conv1_bwd_finish, dim3(3), dim3(256), 0, st, part, nblocks, dw, db);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
+extern "C" int asrx_embed_fwd(const int64_t* tok, int64_t ntok, int32_t L, const float* table, int32_t d,
+                              const float* pe, float dropout_p, uint64_t seed, float* out, void* stream) {
+  if (!tok || !table || !pe || !out || d % 4 || L <= 0) return ASRX_ERR_ARG;
+  if (ntok == 0) return ASRX_OK;
+  const uint32_t thr = drop_threshold(dropout_p);
+  const float sc = (dropout_p > 0.f && dropout_p < 1.f) ? 1.f / (1.f - dropout_p) : 1.f;
+  hipLaunchKernelGGL(embed_fwd_kernel, dim3(grid_for(ntok * (d / 4))), dim3(256), 0, (hipStream_t)stream, tok, ntok, L,
+                     table, d, pe, thr, sc, seed, out);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
+extern "C" int asrx_embed_bwd(const int64_t* tok, int64_t ntok, int32_t L, const float* dout, int32_t d,
+                              int32_t vocab, int32_t pad_id, float dropout_p, uint64_t seed, float* dtable,
+                              void* stream) {
+  (void)L;
+  if (!tok || !dout || !dtable || vocab <= 0) return ASRX_ERR_ARG;
+  const uint32_t thr = drop_threshold(dropout_p);
+  const float sc = (dropout_p > 0.f && dropout_p < 1.f) ? 1.f / (1.f - dropout_p) : 1.f;
+  hipLaunchKernelGGL(embed_bwd_kernel, dim3(vocab), dim3(256), 0, (hipStream_t)stream, tok, ntok, d, dout, pad_id, thr,
+                     sc, seed, dtable);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
+extern "C" int asrx_cross_entropy(const float* logits, int64_t rows, int32_t V, int64_t ld, const int64_t* target,
+                                  int64_t ignore_index, float grad_scale, float* loss, void* dlogits,
+                                  int64_t* argmax, float* ws, void* stream) {
+  if (!logits || !target || !loss || !ws || V <= 0 || ld < V || rows < 0) return ASRX_ERR_ARG;
+  if (ld > 1024) return ASRX_ERR_UNSUPPORTED;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(ce_count_kernel, dim3(1), dim3(256), 0, st, target, rows, ignore_index, ws);
+  ASRX_CHECK_LAUNCH();
+  if (rows > 0) {
+    const dim3 grid((unsigned)((rows + 3) / 4));
+    const int nj = (int)((ld + 63) / 64);
+    if (nj <= 4) hipLaunchKernelGGL((ce_rows_kernel<4>), grid, dim3(256), 0, st, logits, rows, V, ld, target, ignore_index, grad_scale, (bf16_t*)dlogits, argmax, ws);
+    else if (nj <= 8) hipLaunchKernelGGL((ce_rows_kernel<8>), grid, dim3(256), 0, st, logits, rows, V, ld, target, ignore_index, grad_scale, (bf16_t*)dlogits, argmax, ws);
+    else hipLaunchKernelGGL((ce_rows_kernel<16>), grid, dim3(256), 0, st, logits, rows, V, ld, target, ignore_index, grad_scale, (bf16_t*)dlogits, argmax, ws);
+    ASRX_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(ce_final_kernel, dim3(1), dim3(256), 0, st, ws, rows, loss);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
+extern "C" int asrx_cast(int32_t src_dtype, const void* src, int32_t dst_dtype, void* dst, int64_t n, void* stream) {
+  if (!src || !dst || n < 0) return ASRX_ERR_ARG;
+  if (n == 0) return ASRX_OK;
+  hipLaunchKernelGGL(cast_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, src_dtype, src, dst_dtype, dst,
+                     n);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
+extern "C" int asrx_adam(float* p, const float* g, float* m, float* v, void* p_bf16, int64_t n, float lr, float beta1,
+                         float beta2, float eps, float weight_decay, float bias_corr1, float bias_corr2,
+                         float grad_scale, int32_t decoupled, void* stream) {
+  if (!p || !g || !m || !v || n < 0 || bias_corr1 <= 0.f || bias_corr2 <= 0.f) return ASRX_ERR_ARG;
+  if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16) return ASRX_ERR_ARG;
+  if (p_bf16 && (uintptr_t)p_bf16 % 8) return ASRX_ERR_ARG;
+  if (n == 0) return ASRX_OK;
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1)), dim3(256), 0, (hipStream_t)stream, p, g, m, v,
+                     (bf16_t*)p_bf16, n, lr, beta1, beta2, eps, weight_decay, bias_corr1, 1.f / sqrtf(bias_corr2),
+                     grad_scale, decoupled);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
+extern "C" int asrx_dropout_mask(uint8_t* keep, int64_t n, float p, uint64_t seed, void* stream) {
+  if (!keep || n < 0) return ASRX_ERR_ARG;
+  if (n == 0) return ASRX_OK;
+  hipLaunchKernelGGL(dropout_mask_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, keep, n,
+                     drop_threshold(p), seed);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}

@@ -1,0 +1,510 @@
+// MFMA GEMMs with fused epilogues for gfx950.
+//
+//   bf16 path: v_mfma_f32_16x16x32_bf16, 256-thread workgroups (2x2 waves), BMxBN in {64,128}^2, BK=64,
+//              register-staged double-buffered LDS (one barrier per K-step).
+//              k-contiguous operands: LDS image [R][BK+8] read with ds_read_b128;
+//              k-strided operands (A^T / B^T storage, used by the dX and dW GEMMs of the backward pass):
+//              LDS image [BK][R] with a 32-byte XOR swizzle, read with ds_read_b64_tr_b16 (hardware transpose).
+//   f32 path:  v_mfma_f32_16x16x4_f32 (exact fp32 fma chain) for the fp32 parity configuration (c2).
+//
+// Operand roles are swapped inside the MFMA (weights in the A slot, activations in the B slot) so that each
+// lane ends up holding 4 CONSECUTIVE output columns of one row: epilogue stores are 8 B (bf16) / 16 B (f32).
+//
+// Replaces the reference's nn.Linear / aten::addmm and aten::bmm calls (layers.py:10-12,16-18,20,27,36,48,51;
+// model.py:32,102) and, through im2col, the conv2 of the front-end (model.py:168-171).
+#include "common.h"
+
+namespace {
+
+struct GemmArgs {
+  int M, N, K;
+  const void* a; int64_t lda;
+  const void* b; int64_t ldb;
+  void* c; int64_t ldc; int c_dtype;
+  int batch_inner;
+  int64_t sa_o, sa_i, sb_o, sb_i, sc_o, sc_i;
+  float alpha, beta;
+  const float* bias;
+  const float* rowadd; int64_t ld_rowadd; int rowadd_mod;
+  int relu;
+  uint32_t drop_thr; float drop_scale; uint64_t seed;
+  const void* gate; int64_t ld_gate; int gate_dtype;
+  const void* resid; int64_t ld_resid; int resid_dtype;
+  int splitk; int k_per_split;    // k_per_split multiple of BK
+  float* ws;                       // split-K partials [split][M][N]
+  int cvec;                        // C row starts 4-element aligned
+};
+
+ASRX_DEV float ld_any(const void* p, int dtype, int64_t i) {
+  return dtype == ASRX_BF16 ? bf2f(((const bf16_t*)p)[i]) : ((const float*)p)[i];
+}
+
+// Full epilogue for 4 consecutive columns n0..n0+3 of row m (batch z).
+ASRX_DEV void epilogue4(const GemmArgs& g, int z, int m, int n0, const float* acc) {
+  if (m >= g.M || n0 >= g.N) return;
+  const int zo = z / g.batch_inner, zi = z % g.batch_inner;
+  const int64_t coff = zo * g.sc_o + zi * g.sc_i;
+  float r[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = acc[i] * g.alpha;
+  const int nv = min(4, g.N - n0);
+  if (g.bias) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) if (i < nv) r[i] += g.bias[n0 + i];
+  }
+  if (g.rowadd) {
+    const float* ra = g.rowadd + (int64_t)(m % g.rowadd_mod) * g.ld_rowadd + n0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) if (i < nv) r[i] += ra[i];
+  }
+  if (g.relu) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = fmaxf(r[i], 0.f);
+  }
+  if (g.drop_thr) {
+    const uint32_t base = (uint32_t)(((int64_t)z * g.M + m) * g.N + n0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = rng_keep(g.seed, base + i, g.drop_thr) ? r[i] * g.drop_scale : 0.f;
+  }
+  if (g.gate) {
+    const int64_t o = (int64_t)m * g.ld_gate + n0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) if (i < nv && !(ld_any(g.gate, g.gate_dtype, o + i) > 0.f)) r[i] = 0.f;
+  }
+  if (g.resid) {
+    const int64_t o = (int64_t)m * g.ld_resid + n0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) if (i < nv) r[i] += ld_any(g.resid, g.resid_dtype, o + i);
+  }
+  const int64_t co = coff + (int64_t)m * g.ldc + n0;
+  if (g.c_dtype == ASRX_F32) {
+    float* c = (float*)g.c + co;
+    if (g.beta != 0.f) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) if (i < nv) r[i] += g.beta * c[i];
+    }
+    if (nv == 4 && g.cvec) {
+      *(f4_t*)c = f4_t{r[0], r[1], r[2], r[3]};
+    } else {
+      for (int i = 0; i < nv; ++i) c[i] = r[i];
+    }
+  } else {
+    bf16_t* c = (bf16_t*)g.c + co;
+    if (g.beta != 0.f) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) if (i < nv) r[i] += g.beta * bf2f(c[i]);
+    }
+    if (nv == 4 && g.cvec) {
+      uint2 u;
+      u.x = pack2bf(r[0], r[1]);
+      u.y = pack2bf(r[2], r[3]);
+      *(uint2*)c = u;
+    } else {
+      for (int i = 0; i < nv; ++i) c[i] = f2bf(r[i]);
+    }
+  }
+}
+
+// Raw split-K partial store (no epilogue).
+ASRX_DEV void store_partial4(const GemmArgs& g, int split, int m, int n0, const float* acc) {
+  if (m >= g.M || n0 >= g.N) return;
+  float* w = g.ws + ((int64_t)split * g.M + m) * g.N + n0;
+  const int nv = min(4, g.N - n0);
+  if (nv == 4 && (g.N & 3) == 0) {
+    *(f4_t*)w = f4_t{acc[0], acc[1], acc[2], acc[3]};
+  } else {
+    for (int i = 0; i < nv; ++i) w[i] = acc[i];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// bf16 kernel
+// ------------------------------------------------------------------------------------------------
+constexpr int BK = 64;
+constexpr int KC_STRIDE = BK + 8;  // elements; 144 B rows for k-contiguous images
+
+template <int R>
+ASRX_DEV int ks_swz(int krow) {  // 32-byte-chunk XOR for the [BK][R] k-strided image
+  if constexpr (R == 128) return (krow & 3) | (((krow >> 3) & 1) << 2);
+  else return ((krow >> 1) & 1) | (((krow >> 3) & 1) << 1);
+}
+
+template <int R, bool KSTRIDED>
+struct TileBF16 {
+  static constexpr int ELEMS = KSTRIDED ? BK * R : R * KC_STRIDE;
+  static constexpr int CHUNKS = R * BK / 8;           // 16-byte chunks per tile
+  static constexpr int PER_THREAD = CHUNKS / 256;
+
+  // global -> registers.  rows of the logical operand are [r0, r0+R) (limited by rmax), k in [k0, k0+BK).
+  template <bool VEC>
+  ASRX_DEV static void load(s8_t* regs, const bf16_t* base, int64_t ld, int r0, int rmax, int k0, int kmax) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < PER_THREAD; ++i) {
+      const int c = t + 256 * i;
+      int row, kk;
+      if constexpr (!KSTRIDED) { row = c >> 3; kk = (c & 7) * 8; }
+      else { kk = c / (R / 8); row = (c % (R / 8)) * 8; }
+      const int gr = r0 + row, gk = k0 + kk;
+      s8_t v = {0, 0, 0, 0, 0, 0, 0, 0};
+      if constexpr (!KSTRIDED) {
+        if (gr < rmax) {
+          const bf16_t* p = base + (int64_t)gr * ld + gk;
+          if (VEC && gk + 8 <= kmax) {
+            v = *(const s8_t*)p;
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) if (gk + j < kmax) v[j] = (short)p[j];
+          }
+        }
+      } else {
+        if (gk < kmax) {
+          const bf16_t* p = base + (int64_t)gk * ld + gr;
+          if (VEC && gr + 8 <= rmax) {
+            v = *(const s8_t*)p;
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) if (gr + j < rmax) v[j] = (short)p[j];
+          }
+        }
+      }
+      regs[i] = v;
+    }
+  }
+
+  ASRX_DEV static void store(bf16_t* lds, const s8_t* regs) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < PER_THREAD; ++i) {
+      const int c = t + 256 * i;
+      if constexpr (!KSTRIDED) {
+        const int row = c >> 3, kk = (c & 7) * 8;
+        *(s8_t*)(lds + row * KC_STRIDE + kk) = regs[i];
+      } else {
+        const int krow = c / (R / 8), cc = c % (R / 8);
+        const int phys = (((cc >> 1) ^ ks_swz<R>(krow)) << 1) | (cc & 1);
+        *(s8_t*)(lds + krow * R + phys * 8) = regs[i];
+      }
+    }
+  }
+
+  // Fragment for MFMA 16x16x32: lane holds operand(row = i0 + (lane&15), k = ks*32 + 8*(lane>>4) + j), j<8.
+  ASRX_DEV static s8_t frag(const bf16_t* lds, int i0, int ks) {
+    const int l = threadIdx.x & 63;
+    const int g = l >> 4;
+    if constexpr (!KSTRIDED) {
+      return *(const s8_t*)(lds + (i0 + (l & 15)) * KC_STRIDE + ks * 32 + 8 * g);
+    } else {
+      const int i = l & 15, q = i >> 2, p = i & 3;
+      const int k1 = ks * 32 + 8 * g + q;
+      const int k2 = k1 + 4;
+      const bf16_t* a1 = lds + k1 * R + (((i0 >> 4) ^ ks_swz<R>(k1)) << 4) + 4 * p;
+      const bf16_t* a2 = lds + k2 * R + (((i0 >> 4) ^ ks_swz<R>(k2)) << 4) + 4 * p;
+      s4_t r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4_t*)a1);
+      s4_t r2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4_t*)a2);
+      return s8_t{r1[0], r1[1], r1[2], r1[3], r2[0], r2[1], r2[2], r2[3]};
+    }
+  }
+};
+
+template <int BM, int BN, bool AT, bool BT, bool VEC>
+__global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs g) {
+  using TA = TileBF16<BM, AT>;
+  using TB = TileBF16<BN, BT>;
+  constexpr int TM = BM / 32, TN = BN / 32;  // 16x16 subtiles per wave (2x2 waves)
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * (TA::ELEMS + TB::ELEMS)];
+  constexpr int STAGE = TA::ELEMS + TB::ELEMS;
+
+  const int ntn = (g.N + BN - 1) / BN;
+  const int tile = blockIdx.x;
+  const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
+  const int split = blockIdx.y;
+  const int z = blockIdx.z;
+  const int zo = z / g.batch_inner, zi = z % g.batch_inner;
+  const bf16_t* A = (const bf16_t*)g.a + zo * g.sa_o + zi * g.sa_i;
+  const bf16_t* B = (const bf16_t*)g.b + zo * g.sb_o + zi * g.sb_i;
+  const int kbeg = split * g.k_per_split;
+  const int kend = min(g.K, kbeg + g.k_per_split);
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+
+  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int wm = (wave >> 1) * (BM / 2), wn = (wave & 1) * (BN / 2);
+
+  f4_t acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+
+  s8_t ra[TA::PER_THREAD], rb[TB::PER_THREAD];
+  if (nk > 0) {
+    TA::template load<VEC>(ra, A, g.lda, m0, g.M, kbeg, kend);
+    TB::template load<VEC>(rb, B, g.ldb, n0, g.N, kbeg, kend);
+    TA::store(lds, ra);
+    TB::store(lds + TA::ELEMS, rb);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      TA::template load<VEC>(ra, A, g.lda, m0, g.M, kbeg + (kt + 1) * BK, kend);
+      TB::template load<VEC>(rb, B, g.ldb, n0, g.N, kbeg + (kt + 1) * BK, kend);
+    }
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      s8_t fa[TM], fb[TN];
+#pragma unroll
+      for (int j = 0; j < TM; ++j) fa[j] = TA::frag(lds + cur * STAGE, wm + 16 * j, ks);
+#pragma unroll
+      for (int i = 0; i < TN; ++i) fb[i] = TB::frag(lds + cur * STAGE + TA::ELEMS, wn + 16 * i, ks);
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) {
+      TA::store(lds + (cur ^ 1) * STAGE, ra);
+      TB::store(lds + (cur ^ 1) * STAGE + TA::ELEMS, rb);
+    }
+    __syncthreads();
+  }
+
+  const int gq = l >> 4;
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int m = m0 + wm + 16 * j + (l & 15);
+      const int n = n0 + wn + 16 * i + 4 * gq;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (g.splitk > 1) store_partial4(g, split, m, n, v);
+      else epilogue4(g, z, m, n, v);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// fp32 kernel (exact fp32 MFMA; parity path)
+// ------------------------------------------------------------------------------------------------
+constexpr int FBM = 64, FBN = 64, FBK = 16, FSTRIDE = 64 + 16;
+
+template <bool KSTRIDED>
+ASRX_DEV void f32_load(float* regs, const float* base, int64_t ld, int r0, int rmax, int k0, int kmax, bool vec) {
+  const int t = threadIdx.x;
+  int row, kk;
+  if (!KSTRIDED) { row = t >> 2; kk = (t & 3) * 4; }
+  else { kk = t >> 4; row = (t & 15) * 4; }
+  const int gr = r0 + row, gk = k0 + kk;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) regs[j] = 0.f;
+  if (!KSTRIDED) {
+    if (gr < rmax) {
+      const float* p = base + (int64_t)gr * ld + gk;
+      if (vec && gk + 4 <= kmax) {
+        f4_t v = *(const f4_t*)p;
+        regs[0] = v[0]; regs[1] = v[1]; regs[2] = v[2]; regs[3] = v[3];
+      } else {
+        for (int j = 0; j < 4; ++j) if (gk + j < kmax) regs[j] = p[j];
+      }
+    }
+  } else {
+    if (gk < kmax) {
+      const float* p = base + (int64_t)gk * ld + gr;
+      if (vec && gr + 4 <= rmax) {
+        f4_t v = *(const f4_t*)p;
+        regs[0] = v[0]; regs[1] = v[1]; regs[2] = v[2]; regs[3] = v[3];
+      } else {
+        for (int j = 0; j < 4; ++j) if (gr + j < rmax) regs[j] = p[j];
+      }
+    }
+  }
+}
+
+template <bool KSTRIDED>
+ASRX_DEV void f32_store(float* lds, const float* regs) {
+  const int t = threadIdx.x;
+  if (!KSTRIDED) {
+    const int row = t >> 2, kk = (t & 3) * 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) lds[(kk + j) * FSTRIDE + row] = regs[j];
+  } else {
+    const int kk = t >> 4, row = (t & 15) * 4;
+    *(f4_t*)(lds + kk * FSTRIDE + row) = f4_t{regs[0], regs[1], regs[2], regs[3]};
+  }
+}
+
+template <bool AT, bool BT>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g, int vec) {
+  __shared__ __attribute__((aligned(16))) float lds[2][2][FBK * FSTRIDE];
+  const int ntn = (g.N + FBN - 1) / FBN;
+  const int tile = blockIdx.x;
+  const int m0 = (tile / ntn) * FBM, n0 = (tile % ntn) * FBN;
+  const int split = blockIdx.y;
+  const int z = blockIdx.z;
+  const int zo = z / g.batch_inner, zi = z % g.batch_inner;
+  const float* A = (const float*)g.a + zo * g.sa_o + zi * g.sa_i;
+  const float* B = (const float*)g.b + zo * g.sb_o + zi * g.sb_i;
+  const int kbeg = split * g.k_per_split;
+  const int kend = min(g.K, kbeg + g.k_per_split);
+  const int nk = kend > kbeg ? (kend - kbeg + FBK - 1) / FBK : 0;
+  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  f4_t acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+  float ra[4], rb[4];
+  if (nk > 0) {
+    f32_load<AT>(ra, A, g.lda, m0, g.M, kbeg, kend, vec);
+    f32_load<BT>(rb, B, g.ldb, n0, g.N, kbeg, kend, vec);
+    f32_store<AT>(lds[0][0], ra);
+    f32_store<BT>(lds[0][1], rb);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      f32_load<AT>(ra, A, g.lda, m0, g.M, kbeg + (kt + 1) * FBK, kend, vec);
+      f32_load<BT>(rb, B, g.ldb, n0, g.N, kbeg + (kt + 1) * FBK, kend, vec);
+    }
+    const float* sa = lds[cur][0];
+    const float* sb = lds[cur][1];
+#pragma unroll
+    for (int ks = 0; ks < FBK / 4; ++ks) {
+      const int kr = (ks * 4 + (l >> 4)) * FSTRIDE + (l & 15);
+      float fa[2], fb[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fa[j] = sa[kr + wm + 16 * j];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fb[i] = sb[kr + wn + 16 * i];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fb[i], fa[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) {
+      f32_store<AT>(lds[cur ^ 1][0], ra);
+      f32_store<BT>(lds[cur ^ 1][1], rb);
+    }
+    __syncthreads();
+  }
+  const int gq = l >> 4;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int m = m0 + wm + 16 * j + (l & 15);
+      const int n = n0 + wn + 16 * i + 4 * gq;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (g.splitk > 1) store_partial4(g, split, m, n, v);
+      else epilogue4(g, z, m, n, v);
+    }
+}
+
+// Split-K finish: sum partial slabs in fixed order, then the full epilogue.
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g) {
+  const int64_t quads = (int64_t)g.M * ((g.N + 3) / 4);
+  const int nq = (g.N + 3) / 4;
+  for (int64_t t = blockIdx.x * 256 + threadIdx.x; t < quads; t += (int64_t)gridDim.x * 256) {
+    const int m = (int)(t / nq), n0 = (int)(t % nq) * 4;
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    const int nv = min(4, g.N - n0);
+    for (int sp = 0; sp < g.splitk; ++sp) {
+      const float* w = g.ws + ((int64_t)sp * g.M + m) * g.N + n0;
+      for (int i = 0; i < nv; ++i) s[i] += w[i];
+    }
+    epilogue4(g, 0, m, n0, s);
+  }
+}
+
+template <int BM, int BN, bool AT, bool BT, bool VEC>
+void launch_bf16(const GemmArgs& g, int ntiles, int batch, hipStream_t st) {
+  dim3 grid(ntiles, g.splitk, batch);
+  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, AT, BT, VEC>), grid, dim3(256), 0, st, g);
+}
+
+template <int BM, int BN>
+void dispatch_bf16(const GemmArgs& g, bool at, bool bt, bool vec, int batch, hipStream_t st) {
+  const int ntiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
+#define ASRX_L(AT_, BT_)                                                   \
+  if (vec) launch_bf16<BM, BN, AT_, BT_, true>(g, ntiles, batch, st);      \
+  else launch_bf16<BM, BN, AT_, BT_, false>(g, ntiles, batch, st);
+  if (!at && !bt) { ASRX_L(false, false) }
+  else if (!at && bt) { ASRX_L(false, true) }
+  else if (at && !bt) { ASRX_L(true, false) }
+  else { ASRX_L(true, true) }
+#undef ASRX_L
+}
+
+}  // namespace
+
+extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
+  if (!d || d->m < 0 || d->n < 0 || d->k < 0 || !d->a || !d->b || !d->c) return ASRX_ERR_ARG;
+  if (d->in_dtype != ASRX_BF16 && d->in_dtype != ASRX_F32) return ASRX_ERR_ARG;
+  if (d->c_dtype != ASRX_BF16 && d->c_dtype != ASRX_F32) return ASRX_ERR_ARG;
+  if (d->m == 0 || d->n == 0) return ASRX_OK;
+  const int batch = d->batch > 0 ? d->batch : 1;
+  const int binner = d->batch_inner > 0 ? d->batch_inner : 1;
+  int splitk = d->splitk > 1 ? d->splitk : 1;
+  if (splitk > 1 && (batch != 1 || !d->workspace || d->workspace_elems < (int64_t)splitk * d->m * d->n))
+    return ASRX_ERR_ARG;
+  if (batch > 65535 || splitk > 65535) return ASRX_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+
+  GemmArgs g;
+  g.M = d->m; g.N = d->n; g.K = d->k;
+  g.a = d->a; g.lda = d->lda; g.b = d->b; g.ldb = d->ldb;
+  g.c = d->c; g.ldc = d->ldc; g.c_dtype = d->c_dtype;
+  g.batch_inner = binner;
+  g.sa_o = d->sa_outer; g.sa_i = d->sa_inner; g.sb_o = d->sb_outer; g.sb_i = d->sb_inner;
+  g.sc_o = d->sc_outer; g.sc_i = d->sc_inner;
+  g.alpha = d->alpha; g.beta = d->beta;
+  g.bias = d->bias;
+  g.rowadd = d->rowadd; g.ld_rowadd = d->ld_rowadd; g.rowadd_mod = d->rowadd_mod > 0 ? d->rowadd_mod : 1;
+  g.relu = d->relu;
+  g.drop_thr = drop_threshold(d->dropout_p);
+  g.drop_scale = d->dropout_p > 0.f && d->dropout_p < 1.f ? 1.f / (1.f - d->dropout_p) : 0.f;
+  g.seed = d->seed;
+  g.gate = d->gate; g.ld_gate = d->ld_gate; g.gate_dtype = d->gate_dtype;
+  g.resid = d->resid; g.ld_resid = d->ld_resid; g.resid_dtype = d->resid_dtype;
+  g.ws = d->workspace;
+  const int esz = d->c_dtype == ASRX_F32 ? 16 : 8;
+  g.cvec = (d->ldc % 4 == 0) && ((uintptr_t)d->c % esz == 0) && (d->sc_outer % 4 == 0) && (d->sc_inner % 4 == 0);
+
+  if (d->in_dtype == ASRX_BF16) {
+    const bool vec = (d->lda % 8 == 0) && (d->ldb % 8 == 0) && ((uintptr_t)d->a % 16 == 0) &&
+                     ((uintptr_t)d->b % 16 == 0) && (d->sa_outer % 8 == 0) && (d->sa_inner % 8 == 0) &&
+                     (d->sb_outer % 8 == 0) && (d->sb_inner % 8 == 0);
+    int tile = d->tile;
+    if (tile != 64 && tile != 128) {
+      const long t128 = (long)((d->m + 127) / 128) * ((d->n + 127) / 128) * batch * splitk;
+      tile = t128 >= 400 ? 128 : 64;
+    }
+    const int kb = (d->k + BK - 1) / BK;
+    g.splitk = splitk;
+    g.k_per_split = ((kb + splitk - 1) / splitk) * BK;
+    if (tile == 128) dispatch_bf16<128, 128>(g, d->a_trans, d->b_trans, vec, batch, st);
+    else dispatch_bf16<64, 64>(g, d->a_trans, d->b_trans, vec, batch, st);
+  } else {
+    const int vec = (d->lda % 4 == 0) && (d->ldb % 4 == 0) && ((uintptr_t)d->a % 16 == 0) &&
+                    ((uintptr_t)d->b % 16 == 0) && (d->sa_outer % 4 == 0) && (d->sa_inner % 4 == 0) &&
+                    (d->sb_outer % 4 == 0) && (d->sb_inner % 4 == 0);
+    const int kb = (d->k + FBK - 1) / FBK;
+    g.splitk = splitk;
+    g.k_per_split = ((kb + splitk - 1) / splitk) * FBK;
+    const int ntiles = ((d->m + FBM - 1) / FBM) * ((d->n + FBN - 1) / FBN);
+    dim3 grid(ntiles, splitk, batch);
+    if (!d->a_trans && !d->b_trans) hipLaunchKernelGGL((gemm_f32_kernel<false, false>), grid, dim3(256), 0, st, g, vec);
+    else if (!d->a_trans && d->b_trans) hipLaunchKernelGGL((gemm_f32_kernel<false, true>), grid, dim3(256), 0, st, g, vec);
+    else if (d->a_trans && !d->b_trans) hipLaunchKernelGGL((gemm_f32_kernel<true, false>), grid, dim3(256), 0, st, g, vec);
+    else hipLaunchKernelGGL((gemm_f32_kernel<true, true>), grid, dim3(256), 0, st, g, vec);
+  }
+  ASRX_CHECK_LAUNCH();
+  if (splitk > 1) {
+    const int64_t quads = (int64_t)d->m * ((d->n + 3) / 4);
+    const int blocks = (int)std::min<int64_t>((quads + 255) / 256, 4096);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, g);
+    ASRX_CHECK_LAUNCH();
+  }
+  return ASRX_OK;
+}

@@ -1,0 +1,245 @@
+// LayerNorm forward/backward and deterministic row reductions (HBM-bound kernels).
+// Replaces nn.LayerNorm (model.py:14,16,33,59,61,63,101) = aten::native_layer_norm(+_backward).
+// One wave per row, CH contiguous elements per lane per step (16-B fp32 / 8-B bf16 accesses), NJ steps.
+#include "common.h"
+
+namespace {
+
+template <int CH>
+ASRX_DEV void load_ch(const void* p, int dtype, int64_t off, float* v) {
+  if (dtype == ASRX_F32) {
+    const float* f = (const float*)p + off;
+    if constexpr (CH == 4) { f4_t x = *(const f4_t*)f; v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3]; }
+    else if constexpr (CH == 2) { float2 x = *(const float2*)f; v[0] = x.x; v[1] = x.y; }
+    else v[0] = f[0];
+  } else {
+    const bf16_t* b = (const bf16_t*)p + off;
+    if constexpr (CH == 4) { uint2 u = *(const uint2*)b; v[0] = bf2f(u.x & 0xffff); v[1] = bf2f(u.x >> 16); v[2] = bf2f(u.y & 0xffff); v[3] = bf2f(u.y >> 16); }
+    else if constexpr (CH == 2) { uint32_t u = *(const uint32_t*)b; v[0] = bf2f(u & 0xffff); v[1] = bf2f(u >> 16); }
+    else v[0] = bf2f(b[0]);
+  }
+}
+
+template <int CH>
+ASRX_DEV void store_ch(void* p, int dtype, int64_t off, const float* v) {
+  if (dtype == ASRX_F32) {
+    float* f = (float*)p + off;
+    if constexpr (CH == 4) *(f4_t*)f = f4_t{v[0], v[1], v[2], v[3]};
+    else if constexpr (CH == 2) *(float2*)f = make_float2(v[0], v[1]);
+    else f[0] = v[0];
+  } else {
+    bf16_t* b = (bf16_t*)p + off;
+    if constexpr (CH == 4) { uint2 u; u.x = pack2bf(v[0], v[1]); u.y = pack2bf(v[2], v[3]); *(uint2*)b = u; }
+    else if constexpr (CH == 2) *(uint32_t*)b = pack2bf(v[0], v[1]);
+    else b[0] = f2bf(v[0]);
+  }
+}
+
+template <int CH, int NJ>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(int x_dtype, const void* x, int y_dtype, void* y,
+                                                     const float* gamma, const float* beta, float* mean,
+                                                     float* rstd, int64_t rows, float eps) {
+  constexpr int D = CH * NJ * 64;
+  const int l = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float v[NJ][CH];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    load_ch<CH>(x, x_dtype, row * D + (j * 64 + l) * CH, v[j]);
+#pragma unroll
+    for (int i = 0; i < CH; ++i) s += v[j][i];
+  }
+  const float mu = wave_sum(s) * (1.f / D);
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int i = 0; i < CH; ++i) { const float t = v[j][i] - mu; q += t * t; }
+  const float rs = rsqrtf(wave_sum(q) * (1.f / D) + eps);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c0 = (j * 64 + l) * CH;
+    float o[CH];
+#pragma unroll
+    for (int i = 0; i < CH; ++i) o[i] = (v[j][i] - mu) * rs * gamma[c0 + i] + beta[c0 + i];
+    store_ch<CH>(y, y_dtype, row * D + c0, o);
+  }
+  if (l == 0) { mean[row] = mu; rstd[row] = rs; }
+}
+
+// Backward. Each block: 4 waves, grid-stride over rows; per-column dgamma/dbeta partials kept in registers
+// and reduced across the block's waves into part[block][2*D].
+template <int CH, int NJ>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(int x_dtype, const void* x, int dy_dtype, const void* dy,
+                                                     const float* gamma, const float* mean, const float* rstd,
+                                                     const float* dres, float* dx_out, void* dx_drop,
+                                                     int drop_dtype, uint32_t thr, float dscale, uint64_t seed, float* part,
+                                                     int64_t rows) {
+  constexpr int D = CH * NJ * 64;
+  __shared__ float red[4][2 * D];
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float pg[NJ][CH], pb[NJ][CH], ga[NJ][CH];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int i = 0; i < CH; ++i) { pg[j][i] = 0.f; pb[j][i] = 0.f; ga[j][i] = gamma[(j * 64 + l) * CH + i]; }
+  for (int64_t row = (int64_t)blockIdx.x * 4 + w; row < rows; row += (int64_t)gridDim.x * 4) {
+    const float mu = mean[row], rs = rstd[row];
+    float xh[NJ][CH], g[NJ][CH];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int64_t off = row * D + (j * 64 + l) * CH;
+      float xv[CH], dv[CH];
+      load_ch<CH>(x, x_dtype, off, xv);
+      load_ch<CH>(dy, dy_dtype, off, dv);
+#pragma unroll
+      for (int i = 0; i < CH; ++i) {
+        xh[j][i] = (xv[i] - mu) * rs;
+        g[j][i] = dv[i] * ga[j][i];
+        sg += g[j][i];
+        sgx += g[j][i] * xh[j][i];
+        pg[j][i] += dv[i] * xh[j][i];
+        pb[j][i] += dv[i];
+      }
+    }
+    sg = wave_sum(sg) * (1.f / D);
+    sgx = wave_sum(sgx) * (1.f / D);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int64_t off = row * D + (j * 64 + l) * CH;
+      float o[CH];
+#pragma unroll
+      for (int i = 0; i < CH; ++i) o[i] = rs * (g[j][i] - sg - xh[j][i] * sgx);
+      if (dres) {
+        float r[CH];
+        load_ch<CH>(dres, ASRX_F32, off, r);
+#pragma unroll
+        for (int i = 0; i < CH; ++i) o[i] += r[i];
+      }
+      store_ch<CH>(dx_out, ASRX_F32, off, o);
+      if (dx_drop) {
+        float od[CH];
+#pragma unroll
+        for (int i = 0; i < CH; ++i)
+          od[i] = (thr == 0u || rng_keep(seed, (uint32_t)(off + i), thr)) ? o[i] * dscale : 0.f;
+        store_ch<CH>(dx_drop, drop_dtype, off, od);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      red[w][(j * 64 + l) * CH + i] = pg[j][i];
+      red[w][D + (j * 64 + l) * CH + i] = pb[j][i];
+    }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 2 * D; c += 256)
+    part[(int64_t)blockIdx.x * 2 * D + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+}
+
+// Column sums: stage 1 (per block partial over a row range), stage 2 (sum of partials in block order).
+__global__ __launch_bounds__(256) void colsum_stage1(int dtype, const void* in, int64_t rows, int cols, int64_t ld,
+                                                     float* part, int64_t rows_per_block) {
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
+  const int64_t r1 = min(rows, r0 + rows_per_block);
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int sub = threadIdx.x >> 6;
+  __shared__ float red[4][64];
+  float s = 0.f;
+  if (c < cols) {
+    for (int64_t r = r0 + sub; r < r1; r += 4) {
+      const int64_t o = r * ld + c;
+      s += dtype == ASRX_F32 ? ((const float*)in)[o] : bf2f(((const bf16_t*)in)[o]);
+    }
+  }
+  red[sub][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (sub == 0 && c < cols)
+    part[(int64_t)blockIdx.y * cols + c] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+
+__global__ __launch_bounds__(256) void colsum_stage2(const float* part, int nparts, int cols, float* out, int acc) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int p = 0; p < nparts; ++p) s += part[(int64_t)p * cols + c];
+  out[c] = acc ? out[c] + s : s;
+}
+
+template <int CH, int NJ>
+bool ln_fwd_launch(int x_dtype, const void* x, int y_dtype, void* y, const float* gamma, const float* beta,
+                   float* mean, float* rstd, int64_t rows, int d, float eps, hipStream_t st) {
+  if (d != CH * NJ * 64) return false;
+  hipLaunchKernelGGL((ln_fwd_kernel<CH, NJ>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, x_dtype, x,
+                     y_dtype, y, gamma, beta, mean, rstd, rows, eps);
+  return true;
+}
+
+template <int CH, int NJ>
+bool ln_bwd_launch(int x_dtype, const void* x, int dy_dtype, const void* dy, const float* gamma, const float* mean,
+                   const float* rstd, const float* dres, float* dx_out, void* dx_drop, int drop_dtype, float p,
+                   uint64_t seed, float* part, int nblocks, int64_t rows, int d, hipStream_t st) {
+  if (d != CH * NJ * 64) return false;
+  const uint32_t thr = drop_threshold(p);
+  const float sc = (p > 0.f && p < 1.f) ? 1.f / (1.f - p) : 1.f;
+  hipLaunchKernelGGL((ln_bwd_kernel<CH, NJ>), dim3(nblocks), dim3(256), 0, st, x_dtype, x, dy_dtype, dy, gamma, mean,
+                     rstd, dres, dx_out, dx_drop, drop_dtype, thr, sc, seed, part, rows);
+  return true;
+}
+
+}  // namespace
+
+extern "C" int asrx_layernorm_fwd(int32_t x_dtype, const void* x, int32_t y_dtype, void* y, const float* gamma,
+                                  const float* beta, float* mean, float* rstd, int64_t rows, int32_t d, float eps,
+                                  void* stream) {
+  if (!x || !y || !gamma || !beta || !mean || !rstd || rows < 0) return ASRX_ERR_ARG;
+  if (rows == 0) return ASRX_OK;
+  hipStream_t st = (hipStream_t)stream;
+  bool ok = ln_fwd_launch<1, 1>(x_dtype, x, y_dtype, y, gamma, beta, mean, rstd, rows, d, eps, st) ||
+            ln_fwd_launch<2, 1>(x_dtype, x, y_dtype, y, gamma, beta, mean, rstd, rows, d, eps, st) ||
+            ln_fwd_launch<4, 1>(x_dtype, x, y_dtype, y, gamma, beta, mean, rstd, rows, d, eps, st) ||
+            ln_fwd_launch<4, 2>(x_dtype, x, y_dtype, y, gamma, beta, mean, rstd, rows, d, eps, st) ||
+            ln_fwd_launch<4, 3>(x_dtype, x, y_dtype, y, gamma, beta, mean, rstd, rows, d, eps, st) ||
+            ln_fwd_launch<4, 4>(x_dtype, x, y_dtype, y, gamma, beta, mean, rstd, rows, d, eps, st) ||
+            ln_fwd_launch<4, 8>(x_dtype, x, y_dtype, y, gamma, beta, mean, rstd, rows, d, eps, st);
+  if (!ok) return ASRX_ERR_UNSUPPORTED;
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
+extern "C" int asrx_layernorm_bwd(int32_t x_dtype, const void* x, int32_t dy_dtype, const void* dy,
+                                  const float* gamma, const float* mean, const float* rstd, const float* dres,
+                                  float* dx_out, void* dx_drop, int32_t drop_dtype, float dropout_p, uint64_t seed,
+                                  float* part, int32_t nblocks, int64_t rows, int32_t d, void* stream) {
+  if (!x || !dy || !gamma || !mean || !rstd || !dx_out || !part || nblocks <= 0 || rows < 0) return ASRX_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  bool ok = ln_bwd_launch<1, 1>(x_dtype, x, dy_dtype, dy, gamma, mean, rstd, dres, dx_out, dx_drop, drop_dtype, dropout_p, seed, part, nblocks, rows, d, st) ||
+            ln_bwd_launch<2, 1>(x_dtype, x, dy_dtype, dy, gamma, mean, rstd, dres, dx_out, dx_drop, drop_dtype, dropout_p, seed, part, nblocks, rows, d, st) ||
+            ln_bwd_launch<4, 1>(x_dtype, x, dy_dtype, dy, gamma, mean, rstd, dres, dx_out, dx_drop, drop_dtype, dropout_p, seed, part, nblocks, rows, d, st) ||
+            ln_bwd_launch<4, 2>(x_dtype, x, dy_dtype, dy, gamma, mean, rstd, dres, dx_out, dx_drop, drop_dtype, dropout_p, seed, part, nblocks, rows, d, st) ||
+            ln_bwd_launch<4, 3>(x_dtype, x, dy_dtype, dy, gamma, mean, rstd, dres, dx_out, dx_drop, drop_dtype, dropout_p, seed, part, nblocks, rows, d, st) ||
+            ln_bwd_launch<4, 4>(x_dtype, x, dy_dtype, dy, gamma, mean, rstd, dres, dx_out, dx_drop, drop_dtype, dropout_p, seed, part, nblocks, rows, d, st);
+  if (!ok) return ASRX_ERR_UNSUPPORTED;
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
+extern "C" int asrx_reduce_rows(int32_t dtype, const void* in, int64_t rows, int32_t cols, int64_t ld, float* out,
+                                int32_t accumulate, float* part, int32_t nblocks, void* stream) {
+  if (!in || !out || !part || cols <= 0 || rows < 0 || nblocks <= 0) return ASRX_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t rpb = (rows + nblocks - 1) / nblocks;
+  const int nparts = rows > 0 ? (int)((rows + rpb - 1) / rpb) : 0;
+  if (nparts > 0) {
+    hipLaunchKernelGGL(colsum_stage1, dim3((cols + 63) / 64, nparts), dim3(256), 0, st, dtype, in, rows, cols, ld,
+                       part, rpb);
+    ASRX_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(colsum_stage2, dim3((cols + 255) / 256), dim3(256), 0, st, part, nparts, cols, out, accumulate);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}

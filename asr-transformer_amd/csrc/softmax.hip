@@ -1,0 +1,231 @@
+// Masked row softmax over materialised attention scores (unfused attention path; fp32 parity path).
+// Replaces layers.py:20 (scale), :22-23 (masked_fill(mask>0,-inf)), :25 (softmax + nan_to_num), :26 dropout,
+// and their autograd backward.  HBM-bound: one read + one (or two) writes of the score matrix.
+// LPR lanes per row (rows/wave = 64/LPR), V contiguous elements per lane per step (16-B accesses), NJ steps.
+#include "common.h"
+
+namespace {
+
+struct SmArgs {
+  int dtype;
+  const void* s; void* p; void* pd;
+  int64_t rows; int heads, lq, lk; int64_t ld;
+  float scale2;  // scale * log2(e)
+  int mode, causal;
+  const uint8_t* kvalid; const uint8_t* qvalid; int64_t vb;
+  const uint8_t* mask; int64_t msb, msq, msk;
+  uint32_t thr; float dscale; uint64_t seed;
+};
+
+template <int V>
+ASRX_DEV void ld_vec(const void* p, int dtype, int64_t off, float* v, int nvalid) {
+  if (nvalid >= V && V > 1) {
+    if (dtype == ASRX_F32) {
+      if constexpr (V == 4) { f4_t x = *(const f4_t*)((const float*)p + off); v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3]; return; }
+    } else {
+      if constexpr (V == 8) {
+        uint4 u = *(const uint4*)((const bf16_t*)p + off);
+        uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { v[2 * i] = bf2f(w[i] & 0xffff); v[2 * i + 1] = bf2f(w[i] >> 16); }
+        return;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < V; ++i)
+    v[i] = i < nvalid ? (dtype == ASRX_F32 ? ((const float*)p)[off + i] : bf2f(((const bf16_t*)p)[off + i])) : 0.f;
+}
+
+template <int V>
+ASRX_DEV void st_vec(void* p, int dtype, int64_t off, const float* v, int nvalid) {
+  if (nvalid >= V && V > 1) {
+    if (dtype == ASRX_F32) {
+      if constexpr (V == 4) { *(f4_t*)((float*)p + off) = f4_t{v[0], v[1], v[2], v[3]}; return; }
+    } else {
+      if constexpr (V == 8) {
+        uint4 u;
+        u.x = pack2bf(v[0], v[1]); u.y = pack2bf(v[2], v[3]); u.z = pack2bf(v[4], v[5]); u.w = pack2bf(v[6], v[7]);
+        *(uint4*)((bf16_t*)p + off) = u;
+        return;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < V; ++i)
+    if (i < nvalid) {
+      if (dtype == ASRX_F32) ((float*)p)[off + i] = v[i];
+      else ((bf16_t*)p)[off + i] = f2bf(v[i]);
+    }
+}
+
+ASRX_DEV bool is_masked(const SmArgs& a, int b, int q, int key) {
+  if (a.mode == 1) {
+    if (a.causal && key > q) return true;
+    if (a.kvalid && !a.kvalid[b * a.vb + key]) return true;
+    if (a.qvalid && !a.qvalid[b * a.vb + q]) return true;
+    return false;
+  }
+  if (a.mode == 2) return a.mask[b * a.msb + (int64_t)q * a.msq + (int64_t)key * a.msk] != 0;
+  return false;
+}
+
+template <int V, int LPR, int NJ>
+__global__ __launch_bounds__(256) void softmax_fwd_kernel(SmArgs a) {
+  constexpr int RPW = 64 / LPR;
+  const int l = threadIdx.x & 63;
+  const int sub = l / LPR, ll = l % LPR;
+  const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + sub;
+  const bool live = row < a.rows;
+  const int64_t rr = live ? row : 0;
+  const int64_t bh = rr / a.lq;
+  const int q = (int)(rr % a.lq);
+  const int b = (int)(bh / a.heads);
+  float v[NJ][V];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int k0 = (j * LPR + ll) * V;
+    const int nv = max(0, min(V, a.lk - k0));
+    ld_vec<V>(a.s, a.dtype, rr * a.ld + k0, v[j], nv);
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      const int key = k0 + i;
+      const bool m = key >= a.lk || is_masked(a, b, q, key);
+      v[j][i] = m ? -INFINITY : v[j][i] * a.scale2;
+      mx = fmaxf(mx, v[j][i]);
+    }
+  }
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  const float mref = mx == -INFINITY ? 0.f : mx;
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int i = 0; i < V; ++i) { v[j][i] = exp2f(v[j][i] - mref); sum += v[j][i]; }
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+  const float inv = sum > 0.f ? 1.f / sum : 0.f;  // all-masked row -> 0 (nan_to_num, layers.py:25)
+  if (!live) return;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int k0 = (j * LPR + ll) * V;
+    const int nv = max(0, min(V, a.lk - k0));
+    if (nv <= 0) continue;
+    float o[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) o[i] = v[j][i] * inv;
+    st_vec<V>(a.p, a.dtype, rr * a.ld + k0, o, nv);
+    if (a.pd) {
+      const uint32_t base = (uint32_t)(rr * a.lk + k0);
+#pragma unroll
+      for (int i = 0; i < V; ++i) o[i] = (a.thr == 0u || rng_keep(a.seed, base + i, a.thr)) ? o[i] * a.dscale : 0.f;
+      st_vec<V>(a.pd, a.dtype, rr * a.ld + k0, o, nv);
+    }
+  }
+}
+
+template <int V, int LPR, int NJ>
+__global__ __launch_bounds__(256) void softmax_bwd_kernel(SmArgs a, void* ds) {
+  constexpr int RPW = 64 / LPR;
+  const int l = threadIdx.x & 63;
+  const int sub = l / LPR, ll = l % LPR;
+  const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + sub;
+  const bool live = row < a.rows;
+  const int64_t rr = live ? row : 0;
+  float pv[NJ][V], gv[NJ][V];
+  float dot = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int k0 = (j * LPR + ll) * V;
+    const int nv = max(0, min(V, a.lk - k0));
+    ld_vec<V>(a.p, a.dtype, rr * a.ld + k0, pv[j], nv);
+    ld_vec<V>(a.pd, a.dtype, rr * a.ld + k0, gv[j], nv);
+    const uint32_t base = (uint32_t)(rr * a.lk + k0);
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      if (a.thr) gv[j][i] = rng_keep(a.seed, base + i, a.thr) ? gv[j][i] * a.dscale : 0.f;
+      dot += pv[j][i] * gv[j][i];
+    }
+  }
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) dot += __shfl_xor(dot, o, 64);
+  if (!live) return;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int k0 = (j * LPR + ll) * V;
+    const int nv = max(0, min(V, a.lk - k0));
+    if (nv <= 0) continue;
+    float o[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) o[i] = pv[j][i] * (gv[j][i] - dot) * a.scale2;
+    st_vec<V>(ds, a.dtype, rr * a.ld + k0, o, nv);
+  }
+}
+
+template <int V, int LPR, int NJ>
+bool try_launch(const SmArgs& a, bool bwd, void* ds, hipStream_t st) {
+  if ((int64_t)a.lk > (int64_t)NJ * LPR * V) return false;
+  constexpr int RPW = 64 / LPR;
+  const int64_t waves = (a.rows + RPW - 1) / RPW;
+  const unsigned blocks = (unsigned)((waves + 3) / 4);
+  if (bwd) hipLaunchKernelGGL((softmax_bwd_kernel<V, LPR, NJ>), dim3(blocks), dim3(256), 0, st, a, ds);
+  else hipLaunchKernelGGL((softmax_fwd_kernel<V, LPR, NJ>), dim3(blocks), dim3(256), 0, st, a);
+  return true;
+}
+
+template <int V>
+bool dispatch(const SmArgs& a, bool bwd, void* ds, hipStream_t st) {
+  return try_launch<V, 16, 1>(a, bwd, ds, st) || try_launch<V, 32, 1>(a, bwd, ds, st) ||
+         try_launch<V, 64, 1>(a, bwd, ds, st) || try_launch<V, 64, 2>(a, bwd, ds, st) ||
+         try_launch<V, 64, 4>(a, bwd, ds, st) || try_launch<V, 64, 8>(a, bwd, ds, st) ||
+         try_launch<V, 64, 16>(a, bwd, ds, st);
+}
+
+int run(const SmArgs& a, bool bwd, void* ds, hipStream_t st) {
+  bool ok;
+  const bool al = a.dtype == ASRX_F32 ? (a.ld % 4 == 0) : (a.ld % 8 == 0);
+  if (al && a.dtype == ASRX_F32) ok = dispatch<4>(a, bwd, ds, st);
+  else if (al) ok = dispatch<8>(a, bwd, ds, st);
+  else ok = dispatch<1>(a, bwd, ds, st);
+  if (!ok) return ASRX_ERR_UNSUPPORTED;
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
+}  // namespace
+
+extern "C" int asrx_softmax_fwd(int32_t dtype, const void* s, void* p, void* pd, int64_t nbh, int32_t heads,
+                                int32_t lq, int32_t lk, int64_t ld, float scale, int32_t mask_mode, int32_t causal,
+                                const uint8_t* kvalid, const uint8_t* qvalid, int64_t valid_bstride,
+                                const uint8_t* mask, int64_t mask_sb, int64_t mask_sq, int64_t mask_sk,
+                                float dropout_p, uint64_t seed, void* stream) {
+  if (!s || !p || nbh < 0 || lq <= 0 || lk <= 0 || ld < lk || heads <= 0) return ASRX_ERR_ARG;
+  if (mask_mode == 2 && !mask) return ASRX_ERR_ARG;
+  SmArgs a;
+  a.dtype = dtype; a.s = s; a.p = p; a.pd = pd;
+  a.rows = nbh * lq; a.heads = heads; a.lq = lq; a.lk = lk; a.ld = ld;
+  a.scale2 = scale * 1.4426950408889634f;
+  a.mode = mask_mode; a.causal = causal; a.kvalid = kvalid; a.qvalid = qvalid; a.vb = valid_bstride;
+  a.mask = mask; a.msb = mask_sb; a.msq = mask_sq; a.msk = mask_sk;
+  a.thr = drop_threshold(dropout_p);
+  a.dscale = (dropout_p > 0.f && dropout_p < 1.f) ? 1.f / (1.f - dropout_p) : 1.f;
+  a.seed = seed;
+  if (a.rows == 0) return ASRX_OK;
+  return run(a, false, nullptr, (hipStream_t)stream);
+}
+
+extern "C" int asrx_softmax_bwd(int32_t dtype, const void* p, const void* dpd, void* ds, int64_t nbh, int32_t lq,
+                                int32_t lk, int64_t ld, float scale, float dropout_p, uint64_t seed, void* stream) {
+  if (!p || !dpd || !ds || nbh < 0 || lq <= 0 || lk <= 0 || ld < lk) return ASRX_ERR_ARG;
+  SmArgs a = {};
+  a.dtype = dtype; a.p = (void*)p; a.pd = (void*)dpd;
+  a.rows = nbh * lq; a.heads = 1; a.lq = lq; a.lk = lk; a.ld = ld;
+  a.scale2 = scale;
+  a.thr = drop_threshold(dropout_p);
+  a.dscale = (dropout_p > 0.f && dropout_p < 1.f) ? 1.f / (1.f - dropout_p) : 1.f;
+  a.seed = seed;
+  if (a.rows == 0) return ASRX_OK;
+  return run(a, true, ds, (hipStream_t)stream);
+}

@@ -1,0 +1,190 @@
+/*
+ * asrx — C-ABI of the MI355X (gfx950) Speech-Transformer attention path.
+ *
+ * The reference (shockless/asr-transformer) has no FFI: every hot-path op is an ATen call made from the
+ * Python modules in modules/Transformer/{layers,model}.py.  Each entry point below replaces the ATen
+ * call sequence cited next to it; the drop-in nn.Modules in asr-transformer_amd/asrx bind these symbols
+ * through ctypes (INTEGRATION.md shows the binding).
+ *
+ * Conventions (all entry points):
+ *   - plain device pointers, element counts/strides in ELEMENTS (not bytes), int64 sizes;
+ *   - `stream` is a hipStream_t (torch.cuda.current_stream().cuda_stream); every call is asynchronous
+ *     on that stream; the library never allocates, frees or synchronises (graph-capturable);
+ *   - return 0 on success, a negative ASRX_ERR_* code on bad arguments or launch failure;
+ *   - dtype codes: ASRX_BF16 (bfloat16 storage) or ASRX_F32.
+ */
+#ifndef ASRX_H
+#define ASRX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ASRX_OK 0
+#define ASRX_ERR_ARG (-1)
+#define ASRX_ERR_LAUNCH (-2)
+#define ASRX_ERR_UNSUPPORTED (-3)
+
+#define ASRX_BF16 0
+#define ASRX_F32 1
+
+/* Library version / build identification. */
+int asrx_version(void);
+
+/* ---------------------------------------------------------------------------------------------------
+ * GEMM with fused epilogue:   C[z][m][n] = epi( alpha * sum_k A(z,m,k) * B(z,n,k) )
+ *   A(m,k) = a_trans ? A[k*lda + m] : A[m*lda + k]
+ *   B(n,k) = b_trans ? B[k*ldb + n] : B[n*ldb + k]          (b_trans=0 is the nn.Linear weight layout)
+ *   batch index z in [0, batch): element offsets (z / batch_inner)*s?_outer + (z % batch_inner)*s?_inner
+ *   epi order: +bias[n] -> +rowadd[(m % rowadd_mod)*ld_rowadd + n] -> relu -> dropout(p, seed, idx =
+ *              (z*M + m)*N + n) -> *gate (keep where gate[m][n] > 0) -> +resid[m][n] -> +beta*C_old -> store
+ * Replaces: nn.Linear (layers.py:10-12,36,48,51; model.py:32,102) = aten::addmm/linear, the per-head
+ * q@k^T and attn@v aten::bmm (layers.py:20,27), and the conv2 implicit GEMM (model.py:168-171).
+ * Split-K (splitk > 1, batch == 1) needs workspace of splitk*M*N floats.
+ * ------------------------------------------------------------------------------------------------- */
+typedef struct asrx_gemm_desc {
+  int32_t m, n, k;
+  int32_t in_dtype;             /* dtype of A and B */
+  const void* a; int64_t lda; int32_t a_trans;
+  const void* b; int64_t ldb; int32_t b_trans;
+  void* c; int64_t ldc; int32_t c_dtype;
+  int32_t batch, batch_inner;
+  int64_t sa_outer, sa_inner, sb_outer, sb_inner, sc_outer, sc_inner;
+  float alpha, beta;
+  const float* bias;
+  const float* rowadd; int64_t ld_rowadd; int32_t rowadd_mod;
+  int32_t relu;
+  float dropout_p; uint64_t seed;
+  const void* gate; int64_t ld_gate; int32_t gate_dtype;
+  const void* resid; int64_t ld_resid; int32_t resid_dtype;
+  int32_t splitk; float* workspace; int64_t workspace_elems;
+  int32_t tile;                 /* 0 = auto, 64 or 128 = forced square tile (bf16 path) */
+} asrx_gemm_desc;
+
+int asrx_gemm(const asrx_gemm_desc* d, void* stream);
+
+/* ---------------------------------------------------------------------------------------------------
+ * Fused multi-head attention (bf16 in/out, fp32 softmax): per (batch b, head h)
+ *   S = scale * Q K^T ; masked -> -inf ; P = nan_to_num(softmax(S)) ; O = dropout(P) V
+ * Tensors are token-major: row r of batch b of X starts at X + b*x_bstride + r*x_rstride; head h's dh
+ * columns start at +h*dh.  lse[(b*heads+h)*lq + q] receives the log2-domain log-sum-exp (+inf for a
+ * fully-masked row, whose output is 0 exactly as layers.py:25 nan_to_num gives).
+ * mask_mode: 0 none (encoder self / cross, model.py:21,71);
+ *            1 structured: causal (if causal) OR key invalid (kvalid[b*valid_bstride+key]==0) OR query
+ *              invalid (qvalid[...]==0) — the decoder mask of model.py:108-115 without materialising it;
+ *            2 dense bytes: masked where mask[b*mask_sb + q*mask_sq + key*mask_sk] != 0 (layers.py:22-23).
+ * Replaces MHAHead.forward's bmm/mul/masked_fill/softmax/nan_to_num/dropout/bmm (layers.py:20-27).
+ * Supported dh: 32, 64.
+ * ------------------------------------------------------------------------------------------------- */
+typedef struct asrx_attn_desc {
+  int32_t batch, heads, lq, lk, dh;
+  const void* q; int64_t q_rstride, q_bstride;
+  const void* k; int64_t k_rstride, k_bstride;
+  const void* v; int64_t v_rstride, v_bstride;
+  void* o; int64_t o_rstride, o_bstride;
+  float* lse;
+  float scale;
+  int32_t mask_mode, causal;
+  const uint8_t* kvalid; const uint8_t* qvalid; int64_t valid_bstride;
+  const uint8_t* mask; int64_t mask_sb, mask_sq, mask_sk;
+  float dropout_p; uint64_t seed;
+  /* backward only */
+  const void* dout; int64_t do_rstride, do_bstride;
+  void* dq; int64_t dq_rstride, dq_bstride;
+  void* dk; int64_t dk_rstride, dk_bstride;
+  void* dv; int64_t dv_rstride, dv_bstride;
+  float* delta;                 /* [batch*heads*lq] workspace */
+  float* dq_acc;                /* [batch*lq*heads*dh] fp32 workspace, used when lk > 256 */
+} asrx_attn_desc;
+
+int asrx_attention_fwd(const asrx_attn_desc* d, void* stream);
+int asrx_attention_bwd(const asrx_attn_desc* d, void* stream);
+
+/* ---------------------------------------------------------------------------------------------------
+ * Row softmax over materialised scores (the unfused path; HBM-roofline kernel of BASELINE.md §3):
+ *   rows = nbh*lq rows of length lk (row stride ld); row r -> (bh = r / lq, q = r % lq, b = bh / heads)
+ *   p = nan_to_num(softmax(scale * s  masked -> -inf)); if pd != NULL also pd = dropout(p)
+ * Replaces layers.py:20 (scale), :22-23 masked_fill, :25 softmax+nan_to_num, :26 dropout.
+ * bwd: ds = p * (dpd*keep/(1-p_drop) - sum_k p*dpd*keep/(1-p_drop)) * scale
+ * ------------------------------------------------------------------------------------------------- */
+int asrx_softmax_fwd(int32_t dtype, const void* s, void* p, void* pd, int64_t nbh, int32_t heads, int32_t lq,
+                     int32_t lk, int64_t ld, float scale, int32_t mask_mode, int32_t causal,
+                     const uint8_t* kvalid, const uint8_t* qvalid, int64_t valid_bstride, const uint8_t* mask,
+                     int64_t mask_sb, int64_t mask_sq, int64_t mask_sk, float dropout_p, uint64_t seed,
+                     void* stream);
+int asrx_softmax_bwd(int32_t dtype, const void* p, const void* dpd, void* ds, int64_t nbh, int32_t lq, int32_t lk,
+                     int64_t ld, float scale, float dropout_p, uint64_t seed, void* stream);
+
+/* ---------------------------------------------------------------------------------------------------
+ * LayerNorm over the last dim d (nn.LayerNorm, eps, affine: model.py:14,16,33,59,61,63,101).
+ * fwd: y = (x - mean) * rstd * gamma + beta; saves mean/rstd (fp32, one per row).
+ * bwd: dx = rstd*(g - mean(g) - xhat*mean(g*xhat)), g = dy*gamma;  dx_out = dx + dres (dres nullable)
+ *      if dx_drop != NULL also dx_drop = (drop_dtype)(dx_out * keep/(1-p))  (upstream sublayer's dropout bwd)
+ *      per-block partial dgamma/dbeta go to part[nblocks][2][d]; finish with asrx_reduce_rows.
+ * ------------------------------------------------------------------------------------------------- */
+int asrx_layernorm_fwd(int32_t x_dtype, const void* x, int32_t y_dtype, void* y, const float* gamma,
+                       const float* beta, float* mean, float* rstd, int64_t rows, int32_t d, float eps,
+                       void* stream);
+int asrx_layernorm_bwd(int32_t x_dtype, const void* x, int32_t dy_dtype, const void* dy, const float* gamma,
+                       const float* mean, const float* rstd, const float* dres, float* dx_out, void* dx_drop,
+                       int32_t drop_dtype, float dropout_p, uint64_t seed, float* part, int32_t nblocks,
+                       int64_t rows, int32_t d, void* stream);
+
+/* out[c] (+)= sum_r in[r*ld + c] for r < rows (fp32 or bf16 in, fp32 out). Deterministic two-level sum.
+ * Used for bias gradients (column sums of dY) and to finish LayerNorm/conv partials. */
+int asrx_reduce_rows(int32_t dtype, const void* in, int64_t rows, int32_t cols, int64_t ld, float* out,
+                     int32_t accumulate, float* part, int32_t nblocks, void* stream);
+
+/* ---------------------------------------------------------------------------------------------------
+ * Conv2d front-end (model.py:168-171): conv(1->64,3x3,s2)+ReLU -> conv(64->64,3x3,s2)+ReLU, no padding.
+ * conv1_fwd: x (B,1,F,T) fp32 -> y1 channels-last (B,F1,T1,64) in y_dtype (bf16 or fp32)
+ * im2col_conv2: y1 -> cols [(b,t2,f2)][(kh,kw,c)] (B*T2*F2, 576), same dtype: conv2 = GEMM(cols, W2p^T)
+ * col2im_conv2: dcols -> dy1 (B,F1,T1,64) fp32, gated by y1 > 0 (ReLU backward)
+ * conv1_bwd_w: dW1[c][kh*3+kw] += sum dy1*x, db1[c] += sum dy1 (partials in part[nblocks][64*10])
+ * ------------------------------------------------------------------------------------------------- */
+int asrx_conv1_fwd(const float* x, int32_t B, int32_t F, int32_t T, const float* w, const float* b, void* y1,
+                   int32_t y_dtype, void* stream);
+int asrx_im2col_conv2(int32_t dtype, const void* y1, int32_t B, int32_t F1, int32_t T1, void* cols, void* stream);
+int asrx_col2im_conv2(int32_t dcols_dtype, const void* dcols, int32_t y1_dtype, const void* y1, int32_t B,
+                      int32_t F1, int32_t T1, float* dy1, void* stream);
+int asrx_conv1_bwd_w(const float* x, const float* dy1, int32_t B, int32_t F, int32_t T, float* part,
+                     int32_t nblocks, float* dw, float* db, void* stream);
+
+/* ---------------------------------------------------------------------------------------------------
+ * Decoder embedding (model.py:94-96,117): out[t] = dropout(E[tok[t]] + pe[t % L]) (fp32 residual stream);
+ * bwd: dE[v] += sum over tokens == v (v != pad_id) of dropout_bwd(dout)   (padding_idx row gets none).
+ * ------------------------------------------------------------------------------------------------- */
+int asrx_embed_fwd(const int64_t* tok, int64_t ntok, int32_t L, const float* table, int32_t d, const float* pe,
+                   float dropout_p, uint64_t seed, float* out, void* stream);
+int asrx_embed_bwd(const int64_t* tok, int64_t ntok, int32_t L, const float* dout, int32_t d, int32_t vocab,
+                   int32_t pad_id, float dropout_p, uint64_t seed, float* dtable, void* stream);
+
+/* ---------------------------------------------------------------------------------------------------
+ * Cross-entropy over V classes (train.py:32, caller-supplied CE): logits fp32 rows (stride ld);
+ * loss = mean over rows with target != ignore_index of (lse - logit[target]);
+ * dlogits (bf16, stride ld, padded columns zeroed) = grad_scale*(softmax - onehot)/count; argmax (nullable).
+ * ws: >= rows + 2 floats.
+ * ------------------------------------------------------------------------------------------------- */
+int asrx_cross_entropy(const float* logits, int64_t rows, int32_t V, int64_t ld, const int64_t* target,
+                       int64_t ignore_index, float grad_scale, float* loss, void* dlogits, int64_t* argmax,
+                       float* ws, void* stream);
+
+/* ---------------------------------------------------------------------------------------------------
+ * Elementwise utilities.
+ * ------------------------------------------------------------------------------------------------- */
+int asrx_cast(int32_t src_dtype, const void* src, int32_t dst_dtype, void* dst, int64_t n, void* stream);
+/* Fused Adam/AdamW over flat fp32 buffers; optionally refreshes the bf16 shadow copy of the params. */
+int asrx_adam(float* p, const float* g, float* m, float* v, void* p_bf16, int64_t n, float lr, float beta1,
+              float beta2, float eps, float weight_decay, float bias_corr1, float bias_corr2, float grad_scale,
+              int32_t decoupled, void* stream);
+/* delta[(b*heads+h)*lq+q] = sum_d dO*O (attention backward prologue). */
+int asrx_attn_delta(const asrx_attn_desc* d, void* stream);
+/* y = dropout(x) with the library RNG (idx = element index); used for tests of the RNG stream. */
+int asrx_dropout_mask(uint8_t* keep, int64_t n, float p, uint64_t seed, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ASRX_H */

@@ -1,0 +1,382 @@
+"""Per-kernel numerics of libasrx.so on the GPU vs plain PyTorch fp32/fp64 references."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import asrx
+    asrx.native()
+
+
+def K():
+    from asrx import kernels
+    return kernels
+
+
+def relerr(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def bf(x):
+    return x.to(torch.bfloat16)
+
+
+# ------------------------------------------------------------------------------------------------ GEMM
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("at,bt", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("m,n,k", [(200, 136, 96), (1000, 250, 64), (129, 64, 576), (64, 1536, 512), (33, 17, 40)])
+def test_gemm_layouts(dtype, at, bt, m, n, k):
+    g = torch.Generator(device="cpu").manual_seed(m * 7 + n * 3 + k)
+    A = torch.randn(m, k, generator=g)
+    B = torch.randn(n, k, generator=g)
+    Ad = (A.t().contiguous() if at else A).to(dev, dtype)
+    Bd = (B.t().contiguous() if bt else B).to(dev, dtype)
+    C = torch.empty(m, n, device=dev, dtype=torch.float32)
+    K().gemm(Ad, Bd, C, m, n, k, lda=Ad.stride(0), ldb=Bd.stride(0), ldc=n, a_trans=at, b_trans=bt)
+    ref = A.to(dtype).double() @ B.to(dtype).double().t()
+    tol = 1e-5 if dtype == torch.float32 else 2e-3
+    assert relerr(C.cpu(), ref) < tol
+
+
+@pytest.mark.parametrize("tile", [64, 128])
+def test_gemm_epilogue(tile):
+    m, n, k = 300, 192, 128
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(m, k, generator=g)
+    w = torch.randn(n, k, generator=g) * 0.1
+    bias = torch.randn(n, generator=g)
+    pe = torch.randn(50, n, generator=g)
+    res = torch.randn(m, n, generator=g)
+    gate = torch.randn(m, n, generator=g)
+    out = torch.empty(m, n, device=dev)
+    K().gemm(bf(x).to(dev), bf(w).to(dev), out, m, n, k, lda=k, ldb=k, ldc=n, alpha=0.5, bias=bias.to(dev),
+             rowadd=pe.to(dev), rowadd_mod=50, ld_rowadd=n, relu=True, gate=gate.to(dev), ld_gate=n,
+             resid=res.to(dev), ld_resid=n, tile=tile)
+    acc = 0.5 * (bf(x).double() @ bf(w).double().t()) + bias.double() + pe.double()[torch.arange(m) % 50]
+    ref = torch.where(gate > 0, acc.clamp_min(0), torch.zeros(())) + res.double()
+    assert relerr(out.cpu(), ref) < 2e-3
+
+
+def test_gemm_beta_splitk_and_bf16_out():
+    m, n, k = 64, 96, 5000
+    g = torch.Generator().manual_seed(2)
+    A = torch.randn(k, m, generator=g)            # stored [K][M] -> a_trans
+    B = torch.randn(k, n, generator=g)            # stored [K][N] -> b_trans
+    C0 = torch.randn(m, n, generator=g)
+    C = C0.clone().to(dev)
+    K().gemm(bf(A).to(dev), bf(B).to(dev), C, m, n, k, lda=m, ldb=n, ldc=n, a_trans=True, b_trans=True, beta=1.0,
+             splitk=7)
+    ref = C0.double() + bf(A).double().t() @ bf(B).double()
+    assert relerr(C.cpu(), ref) < 2e-3
+    Cb = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
+    K().gemm(bf(A).to(dev), bf(B).to(dev), Cb, m, n, k, lda=m, ldb=n, ldc=n, a_trans=True, b_trans=True)
+    assert relerr(Cb.float().cpu(), ref - C0.double()) < 1e-2
+
+
+def test_gemm_batched_heads():
+    """Two-level batch strides as used by the unfused attention: z = b*H + h."""
+    Bn, H, L, dh = 3, 4, 37, 32
+    d = H * dh
+    g = torch.Generator().manual_seed(3)
+    qkv = torch.randn(Bn, L, 3 * d, generator=g)
+    q = qkv[..., :d].reshape(Bn, L, H, dh).permute(0, 2, 1, 3)
+    k = qkv[..., d:2 * d].reshape(Bn, L, H, dh).permute(0, 2, 1, 3)
+    ld = 40
+    S = torch.zeros(Bn * H, L, ld, device=dev)
+    x = qkv.to(dev)
+    K().gemm(x, x[..., d:], S, L, L, dh, lda=3 * d, ldb=3 * d, ldc=ld, batch=Bn * H, batch_inner=H,
+             sa=(L * 3 * d, dh), sb=(L * 3 * d, dh), sc=(H * L * ld, L * ld))
+    ref = (q.double() @ k.double().transpose(-1, -2)).reshape(Bn * H, L, L)
+    assert relerr(S[:, :, :L].cpu(), ref) < 1e-5
+
+
+# ------------------------------------------------------------------------------------------------ LayerNorm
+
+@pytest.mark.parametrize("d", [64, 128, 256, 512])
+@pytest.mark.parametrize("ydt", [torch.bfloat16, torch.float32])
+def test_layernorm(d, ydt):
+    rows = 333
+    g = torch.Generator().manual_seed(d)
+    x = torch.randn(rows, d, generator=g) * 2 + 0.5
+    gam = 1 + 0.1 * torch.randn(d, generator=g)
+    bet = 0.1 * torch.randn(d, generator=g)
+    dy = torch.randn(rows, d, generator=g)
+    dres = torch.randn(rows, d, generator=g)
+    y = torch.empty(rows, d, device=dev, dtype=ydt)
+    mean, rstd = K().layernorm_fwd(x.to(dev), gam.to(dev), bet.to(dev), y)
+    xr = x.double().requires_grad_(True)
+    gr = gam.double().requires_grad_(True)
+    br = bet.double().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(xr, (d,), gr, br, 1e-5)
+    assert relerr(y.float().cpu(), yr.detach()) < (1e-5 if ydt == torch.float32 else 1e-2)
+    yr.backward(dy.double())
+    dgb = torch.zeros(2 * d, device=dev)
+    drop = torch.empty(rows, d, device=dev, dtype=torch.bfloat16)
+    dx = K().layernorm_bwd(x.to(dev), dy.to(dev), gam.to(dev), mean, rstd, dgb, dres=dres.to(dev), dx_drop=drop)
+    assert relerr(dx.cpu(), xr.grad + dres.double()) < 1e-5
+    assert relerr(drop.float().cpu(), xr.grad + dres.double()) < 1e-2
+    assert relerr(dgb[:d].cpu(), gr.grad) < 1e-5
+    assert relerr(dgb[d:].cpu(), br.grad) < 1e-5
+
+
+def test_colsum():
+    x = torch.randn(10000, 300)
+    out = torch.ones(300, device=dev)
+    K().colsum(x.to(dev), out)
+    assert relerr(out.cpu(), x.double().sum(0) + 1) < 1e-5
+
+
+# ------------------------------------------------------------------------------------------------ attention
+
+def ref_attention(q, k, v, scale, masked, p_keep=None):
+    """q (B,H,Lq,dh) etc. in fp64; masked bool (B,1|H,Lq,Lk); reference semantics layers.py:20-27."""
+    s = (q @ k.transpose(-1, -2)) * scale
+    s = s.masked_fill(masked, float("-inf"))
+    p = torch.nan_to_num(torch.softmax(s, -1))
+    pd = p if p_keep is None else p * p_keep
+    return pd @ v, p
+
+
+def _mk(B, H, Lq, Lk, dh, kind, g):
+    d = H * dh
+    q = torch.randn(B, Lq, d, generator=g)
+    kv = torch.randn(B, Lk, 2 * d, generator=g)
+    valid = torch.ones(B, max(Lq, Lk))
+    if kind == "decoder":
+        valid[0, Lq // 2:] = 0
+        valid[-1, 2:] = 0
+    return q, kv, valid
+
+
+def _masked(kind, B, Lq, Lk, valid):
+    if kind == "none":
+        return torch.zeros(B, 1, Lq, Lk, dtype=torch.bool)
+    pad = valid[:, :Lk].lt(1).unsqueeze(1).expand(-1, Lq, -1)
+    m = pad | pad.transpose(1, 2) | torch.triu(torch.ones(Lq, Lk, dtype=torch.bool), 1)
+    return m.unsqueeze(1)
+
+
+@pytest.mark.parametrize("dh", [32, 64])
+@pytest.mark.parametrize("B,H,Lq,Lk,kind", [(2, 4, 70, 70, "decoder"), (3, 2, 64, 249, "none"),
+                                           (2, 2, 249, 249, "none"), (1, 2, 100, 300, "none"),
+                                           (2, 3, 33, 33, "decoder")])
+def test_attention_fused(dh, B, H, Lq, Lk, kind):
+    from asrx.kernels import MaskSpec
+    g = torch.Generator().manual_seed(B * 100 + Lq + Lk + dh)
+    q, kv, valid = _mk(B, H, Lq, Lk, dh, kind, g)
+    d = H * dh
+    qb, kvb = bf(q), bf(kv)
+    qd, kvd = qb.to(dev), kvb.to(dev)
+    o = torch.empty(B * Lq, d, device=dev, dtype=torch.bfloat16)
+    if kind == "decoder":
+        vv = (valid[:, :Lq] >= 1).to(torch.uint8).to(dev)
+        spec = MaskSpec(1, True, vv, vv, vv.stride(0))
+    else:
+        spec = MaskSpec()
+    scale = (d) ** -0.5
+    st = ((d, Lq * d), (2 * d, Lk * 2 * d), (2 * d, Lk * 2 * d), (d, Lq * d))
+    lse = K().attention_fwd(qd, kvd, kvd[..., d:], o, B, H, Lq, Lk, dh, st, scale, spec)
+    qh = qb.double().view(B, Lq, H, dh).transpose(1, 2).requires_grad_(True)
+    kh = kvb[..., :d].double().reshape(B, Lk, H, dh).transpose(1, 2).contiguous().requires_grad_(True)
+    vh = kvb[..., d:].double().reshape(B, Lk, H, dh).transpose(1, 2).contiguous().requires_grad_(True)
+    masked = _masked(kind, B, Lq, Lk, valid)
+    ref, _ = ref_attention(qh, kh, vh, scale, masked)
+    out = o.float().cpu().view(B, Lq, H, dh).transpose(1, 2)
+    assert relerr(out, ref.detach()) < 1e-2
+    if kind == "decoder":
+        # fully-masked query rows (query padding) are exactly zero (nan_to_num, layers.py:25)
+        rows = (valid[:, :Lq] < 1)
+        assert torch.all(out.permute(0, 2, 1, 3)[rows] == 0)
+    # backward
+    dO = torch.randn(B, Lq, d, generator=g)
+    dOb = bf(dO)
+    ref.backward(dOb.double().view(B, Lq, H, dh).transpose(1, 2))
+    dq = torch.empty(B * Lq, d, device=dev, dtype=torch.bfloat16)
+    dkv = torch.empty(B * Lk, 2 * d, device=dev, dtype=torch.bfloat16)
+    gst = ((d, Lq * d), (d, Lq * d), (2 * d, Lk * 2 * d), (2 * d, Lk * 2 * d))
+    K().attention_bwd(qd, kvd, kvd[..., d:], o, lse, dOb.to(dev), dq, dkv, dkv[:, d:], B, H, Lq, Lk, dh, st, gst,
+                      scale, spec)
+    dq_ = dq.float().cpu().view(B, Lq, H, dh).transpose(1, 2)
+    dk_ = dkv[:, :d].float().cpu().view(B, Lk, H, dh).transpose(1, 2)
+    dv_ = dkv[:, d:].float().cpu().view(B, Lk, H, dh).transpose(1, 2)
+    assert relerr(dv_, vh.grad) < 2e-2
+    assert relerr(dk_, kh.grad) < 2e-2
+    assert relerr(dq_, qh.grad) < 2e-2
+
+
+def test_attention_dense_mask_and_dropout_consistency():
+    """Dense byte mask (mode 2) equals the structured decoder mask; dropout forward/backward are consistent
+    with an explicit mask regenerated from the same RNG stream."""
+    from asrx.kernels import MaskSpec
+    B, H, L, dh = 2, 2, 40, 64
+    d = H * dh
+    g = torch.Generator().manual_seed(9)
+    q, kv, valid = _mk(B, H, L, L, dh, "decoder", g)
+    qd, kvd = bf(q).to(dev), bf(kv).to(dev)
+    masked = _masked("decoder", B, L, L, valid)
+    vv = (valid[:, :L] >= 1).to(torch.uint8).to(dev)
+    s1 = MaskSpec(1, True, vv, vv, vv.stride(0))
+    s2 = MaskSpec.from_attention_mask(masked[:, 0].to(dev), B, L, L)
+    st = ((d, L * d), (2 * d, L * 2 * d), (2 * d, L * 2 * d), (d, L * d))
+    o1 = torch.empty(B * L, d, device=dev, dtype=torch.bfloat16)
+    o2 = torch.empty_like(o1)
+    K().attention_fwd(qd, kvd, kvd[..., d:], o1, B, H, L, L, dh, st, d ** -0.5, s1)
+    K().attention_fwd(qd, kvd, kvd[..., d:], o2, B, H, L, L, dh, st, d ** -0.5, s2)
+    assert torch.equal(o1, o2)
+    # dropout: fused kernel vs unfused (softmax kernel) path share the RNG index (bh*Lq + q)*Lk + key
+    p, seed = 0.3, 1234
+    o3 = torch.empty_like(o1)
+    K().attention_fwd(qd, kvd, kvd[..., d:], o3, B, H, L, L, dh, st, d ** -0.5, s1, p, seed)
+    keep = K().dropout_mask(B * H * L * L, p, seed, dev).view(B, H, L, L).cpu().double() / (1 - p)
+    qh = bf(q).double().view(B, L, H, dh).transpose(1, 2)
+    kh = bf(kv)[..., :d].double().reshape(B, L, H, dh).transpose(1, 2)
+    vh = bf(kv)[..., d:].double().reshape(B, L, H, dh).transpose(1, 2)
+    ref, _ = ref_attention(qh, kh, vh, d ** -0.5, masked, keep)
+    assert relerr(o3.float().cpu().view(B, L, H, dh).transpose(1, 2), ref) < 1e-2
+    frac = float((keep > 0).double().mean())
+    assert abs(frac - (1 - p)) < 0.01
+
+
+# ------------------------------------------------------------------------------------------------ softmax
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("Lk", [24, 64, 127, 249, 999])
+def test_softmax_masked(dtype, Lk):
+    from asrx.kernels import MaskSpec
+    B, H, Lq = 2, 3, min(Lk, 70)
+    g = torch.Generator().manual_seed(Lk)
+    ld = (Lk + 7) // 8 * 8
+    s = torch.randn(B * H, Lq, ld, generator=g) * 3
+    valid = torch.ones(B, Lk)
+    valid[1, Lk // 3:] = 0
+    vv = (valid >= 1).to(torch.uint8)
+    spec = MaskSpec(1, True, vv.to(dev), vv.to(dev), Lk) if Lq == Lk else MaskSpec(1, False, vv.to(dev), None, Lk)
+    sd = s.to(dev, dtype)
+    p = torch.empty_like(sd)
+    scale = 0.125
+    K().softmax_fwd(sd, p, None, B * H, H, Lq, Lk, ld, scale, spec)
+    x = sd[..., :Lk].double().cpu() * scale
+    pad = valid.lt(1)[:, None, None, :].expand(B, H, Lq, Lk)
+    m = pad.clone()
+    if Lq == Lk:
+        m = m | pad.transpose(-1, -2) | torch.triu(torch.ones(Lq, Lk, dtype=torch.bool), 1)
+    x = x.view(B, H, Lq, Lk).masked_fill(m, float("-inf"))
+    ref = torch.nan_to_num(torch.softmax(x, -1)).view(B * H, Lq, Lk)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert relerr(p[..., :Lk].float().cpu(), ref) < tol
+    dpd = torch.randn(B * H, Lq, ld, generator=g).to(dev, dtype)
+    ds = torch.empty_like(sd)
+    K().softmax_bwd(p, dpd, ds, B * H, Lq, Lk, ld, scale)
+    P = p[..., :Lk].double().cpu()
+    G = dpd[..., :Lk].double().cpu()
+    ref_ds = P * (G - (P * G).sum(-1, keepdim=True)) * scale
+    assert relerr(ds[..., :Lk].float().cpu(), ref_ds) < tol * 2
+
+
+# ------------------------------------------------------------------------------------------------ front-end
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_conv_frontend(dtype):
+    B, F, T = 2, 80, 61
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(B, 1, F, T, generator=g)
+    w1 = torch.randn(64, 1, 3, 3, generator=g) * 0.3
+    b1 = torch.randn(64, generator=g) * 0.1
+    w2 = torch.randn(64, 64, 3, 3, generator=g) * 0.05
+    F1, T1 = (F - 3) // 2 + 1, (T - 3) // 2 + 1
+    F2, T2 = (F1 - 3) // 2 + 1, (T1 - 3) // 2 + 1
+    y1 = torch.empty(B, F1, T1, 64, device=dev, dtype=dtype)
+    K().conv1_fwd(x.to(dev), w1.reshape(64, 9).to(dev), b1.to(dev), y1)
+    ref1 = torch.relu(torch.nn.functional.conv2d(x.double(), w1.double(), b1.double(), stride=2))
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert relerr(y1.float().cpu().permute(0, 3, 1, 2), ref1) < tol
+    cols = torch.empty(B * T2 * F2, 576, device=dev, dtype=dtype)
+    K().im2col_conv2(y1, cols)
+    w2p = w2.permute(0, 2, 3, 1).reshape(64, 576).to(dev, dtype)
+    y2 = torch.empty(B * T2 * F2, 64, device=dev, dtype=torch.float32)
+    K().gemm(cols, w2p, y2, B * T2 * F2, 64, 576, lda=576, ldb=576, ldc=64)
+    y1r = y1.float().cpu().permute(0, 3, 1, 2).double()
+    ref2 = torch.nn.functional.conv2d(y1r, w2.to(dtype).double(), stride=2)        # (B,64,F2,T2)
+    got = y2.cpu().view(B, T2, F2, 64).permute(0, 3, 2, 1)
+    assert relerr(got, ref2) < tol
+    # backward: dcols -> col2im (ReLU gate) and conv1 weight grads
+    y1g = y1r.clone().requires_grad_(True)
+    out2 = torch.nn.functional.conv2d(y1g, w2.to(dtype).double(), stride=2)
+    gy = torch.randn(out2.shape, generator=g).double()
+    out2.backward(gy)
+    dy2 = gy.permute(0, 3, 2, 1).reshape(B * T2 * F2, 64).to(dev, dtype)
+    dcols = torch.empty(B * T2 * F2, 576, device=dev, dtype=dtype)
+    K().gemm(dy2, w2p, dcols, B * T2 * F2, 576, 64, lda=64, ldb=576, ldc=576, b_trans=True)
+    dy1 = torch.empty(B, F1, T1, 64, device=dev)
+    K().col2im_conv2(dcols, y1, dy1)
+    ref_dy1 = (y1g.grad * (y1r > 0)).permute(0, 2, 3, 1)
+    assert relerr(dy1.cpu(), ref_dy1) < tol * 2
+    dw = torch.zeros(64, 9, device=dev)
+    db = torch.zeros(64, device=dev)
+    K().conv1_bwd_w(x.to(dev), dy1, dw, db)
+    xr = x.double()
+    w1r = w1.double().requires_grad_(True)
+    b1r = b1.double().requires_grad_(True)
+    pre = torch.nn.functional.conv2d(xr, w1r, b1r, stride=2)
+    pre.backward(dy1.cpu().double().permute(0, 3, 1, 2))
+    assert relerr(dw.cpu(), w1r.grad.reshape(64, 9)) < 1e-5
+    assert relerr(db.cpu(), b1r.grad) < 1e-5
+
+
+# ------------------------------------------------------------------------------------------------ misc
+
+def test_embedding_and_ce_and_adam():
+    V, d, B, L = 250, 128, 4, 16
+    g = torch.Generator().manual_seed(6)
+    E = torch.randn(V, d, generator=g)
+    pe = torch.randn(32, d, generator=g)
+    tok = torch.randint(0, V, (B, L), generator=g)
+    tok[0, -3:] = 4
+    out = torch.empty(B * L, d, device=dev)
+    K().embed_fwd(tok.to(dev), E.to(dev), pe.to(dev), out, L)
+    ref = E[tok.reshape(-1)] + pe[torch.arange(B * L) % L]
+    assert relerr(out.cpu(), ref) < 1e-6
+    dout = torch.randn(B * L, d, generator=g)
+    dE = torch.zeros(V, d, device=dev)
+    K().embed_bwd(tok.to(dev), dout.to(dev), dE, L, pad_id=4)
+    Er = E.clone().requires_grad_(True)
+    torch.nn.functional.embedding(tok.reshape(-1), Er, padding_idx=4).backward(dout)
+    assert relerr(dE.cpu(), Er.grad) < 1e-6
+    # cross entropy with padded logits
+    rows, Vp = 37, 256
+    logits = torch.randn(rows, Vp, generator=g) * 3
+    tgt = torch.randint(0, V, (rows,), generator=g)
+    tgt[5] = -100
+    loss, dl, am = K().cross_entropy(logits.to(dev), V, tgt.to(dev), want_argmax=True)
+    lr = logits[:, :V].double().requires_grad_(True)
+    lref = torch.nn.functional.cross_entropy(lr, tgt)
+    lref.backward()
+    assert abs(float(loss) - float(lref)) < 1e-5 * abs(float(lref))
+    assert relerr(dl[:, :V].float().cpu(), lr.grad) < 1e-2
+    assert torch.all(dl[:, V:] == 0)
+    assert torch.equal(am.cpu(), logits[:, :V].argmax(-1))
+    # adam vs torch.optim.Adam
+    n = 1003
+    p0 = torch.randn(n, generator=g)
+    gr = torch.randn(n, generator=g)
+    pt = p0.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([pt], lr=1e-3, betas=(0.9, 0.98), eps=1e-9, weight_decay=0.01)
+    pd, md, vd = p0.clone().to(dev), torch.zeros(n, device=dev), torch.zeros(n, device=dev)
+    pb = torch.empty(n, device=dev, dtype=torch.bfloat16)
+    for step in (1, 2, 3):
+        pt.grad = gr * step
+        opt.step()
+        K().adam(pd, (gr * step).to(dev), md, vd, pb, 1e-3, 0.9, 0.98, 1e-9, 0.01, step, decoupled=True)
+    assert relerr(pd.cpu(), pt.detach()) < 1e-6
+    assert relerr(pb.float().cpu(), pt.detach()) < 1e-2
