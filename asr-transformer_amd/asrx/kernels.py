@@ -45,6 +45,28 @@ def auto_splitk(m, n, k, batch=1, tile=64):
     return max(1, s)
 
 
+class KernelProbe:
+    """Brackets every launch of one GEMM kernel instantiation with HIP events on the launching stream, and
+    accumulates its algorithmic FLOPs (bench.py roofline; matches rocprofv3's per-kernel-name average)."""
+
+    def __init__(self, key):
+        self.key = key              # (in_dtype, a_trans, b_trans, tile, vec)
+        self.events = []
+        self.flops = 0
+        self.active = False
+
+    def durations_ms(self):
+        return [s.elapsed_time(e) for s, e in self.events]
+
+
+PROBE = None
+
+
+def choose_tile(m, n, batch, splitk):
+    t128 = math.ceil(m / 128) * math.ceil(n / 128) * batch * splitk
+    return 128 if t128 >= 400 else 64
+
+
 def gemm(a, b, c, m, n, k, *, lda, ldb, ldc, a_trans=False, b_trans=False, alpha=1.0, beta=0.0, bias=None,
          rowadd=None, rowadd_mod=1, ld_rowadd=0, relu=False, dropout_p=0.0, seed=0, gate=None, ld_gate=0,
          resid=None, ld_resid=0, batch=1, batch_inner=1, sa=(0, 0), sb=(0, 0), sc=(0, 0), splitk=1, tile=0):
@@ -54,6 +76,8 @@ def gemm(a, b, c, m, n, k, *, lda, ldb, ldc, a_trans=False, b_trans=False, alpha
         raise TypeError("asrx.gemm: A and B must share a dtype")
     if splitk == "auto":
         splitk = auto_splitk(m, n, k, batch)
+    if tile == 0 and a.dtype == torch.bfloat16:
+        tile = choose_tile(m, n, batch, splitk)
     d = GemmDesc()
     d.m, d.n, d.k = m, n, k
     d.in_dtype = code(a)
@@ -81,6 +105,19 @@ def gemm(a, b, c, m, n, k, *, lda, ldb, ldc, a_trans=False, b_trans=False, alpha
     else:
         d.splitk = 1
     d.tile = tile
+    probe = PROBE
+    if probe is not None and probe.active and a.dtype == torch.bfloat16:
+        vec = (lda % 8 == 0 and ldb % 8 == 0 and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0
+               and sa[0] % 8 == 0 and sa[1] % 8 == 0 and sb[0] % 8 == 0 and sb[1] % 8 == 0)
+        if (code(a), bool(a_trans), bool(b_trans), tile, vec) == probe.key and splitk == 1:
+            s0 = torch.cuda.Event(enable_timing=True)
+            s1 = torch.cuda.Event(enable_timing=True)
+            s0.record()
+            call("asrx_gemm", ctypes.byref(d), stream())
+            s1.record()
+            probe.events.append((s0, s1))
+            probe.flops += 2 * m * n * k * batch
+            return ws
     call("asrx_gemm", ctypes.byref(d), stream())
     return ws
 

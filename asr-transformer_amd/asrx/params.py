@@ -88,7 +88,7 @@ class FlatParams:
 
     def span(self, first, count_params, buf):
         """A contiguous view covering `count_params` consecutive parameters starting at `first`."""
-        idx = self.params.index(first)
+        idx = next(i for i, p in enumerate(self.params) if p is first)
         ps = self.params[idx:idx + count_params]
         o0 = self.offsets[id(ps[0])]
         o1 = self.offsets[id(ps[-1])] + ps[-1].numel()

@@ -1,0 +1,108 @@
+"""Training / evaluation loops.
+
+`train_epoch` / `eval_epoch` mirror modules/Transformer/train.py:6-108 (same arguments, same batch dict keys,
+same metrics dict) for drop-in use with any torch optimizer and loss.
+
+`Trainer` is the MI355X-native step: forward -> fused cross-entropy kernel -> explicit backward -> RCCL
+bucketed gradient all-reduce -> fused AdamW over the flat parameter buffer (which also refreshes the bf16
+operand copy).  No autograd graph, no per-parameter launches.
+"""
+import torch
+
+from . import kernels as K
+from .dist import GradAllReduce
+from .functions import get_store, make_ctx, model_backward, model_forward
+
+
+def train_epoch(model, data_loader, loss_function, optimizer, device):
+    """train.py:6-55 semantics, including the teacher-forcing shift of train.py:22-25 as written (a
+    batch-coupled index_put)."""
+    model.to(device)
+    model.train()
+    total = 0.0
+    preds, targets = [], []
+    for batch in data_loader:
+        spectrum = batch["spectrum"].to(device)
+        text = batch["text"].to(device)
+        mask = batch["mask"].to(device)
+        input_text = text.detach().clone()
+        input_text[:, mask.sum(dim=-1).long() - 1] = input_text[:, -1]
+        mask = mask.clone()
+        mask[:, mask.sum(dim=-1).long() - 1] = mask[:, -1]
+        input_text, mask = input_text[:, :-1], mask[:, :-1]
+        optimizer.zero_grad()
+        logits = model(spectrum, input_text, mask)
+        preds.append(logits.argmax(dim=-1).to("cpu"))
+        targets.append(text[:, :-1].to("cpu"))
+        loss = loss_function(logits.transpose(1, 2), text[:, 1:])
+        total += loss.item()
+        loss.backward()
+        optimizer.step()
+    return {"Train Loss": total / max(1, len(data_loader))}, preds, targets
+
+
+def eval_epoch(model, data_loader, eos_token_id, bos_token_id, loss_function, device):
+    """train.py:58-108: greedy decode per batch (Transformer.evaluate), logits padded/truncated to the
+    target length, CE loss averaged over batches."""
+    model.to(device)
+    model.eval()
+    total = 0.0
+    preds, targets = [], []
+    with torch.no_grad():
+        for batch in data_loader:
+            spectrum = batch["spectrum"].to(device)
+            text = batch["text"].to(device)
+            text_in = torch.full((text.shape[0], 1), bos_token_id, dtype=torch.int32).to(device)
+            pred, logits = model.evaluate(spectrum, text_in)
+            text = text[:, 1:]
+            for i in range(len(logits)):
+                if logits[i].shape[0] > text.shape[1]:
+                    logits[i] = logits[i][:text.shape[1]]
+                else:
+                    logits[i] = torch.cat((logits[i], torch.zeros((text.shape[1] - logits[i].shape[0],
+                                                                   logits[i].shape[1]), device=logits[i].device)),
+                                          dim=0)
+            logits = torch.stack(logits, dim=0)
+            preds.append(pred.to("cpu"))
+            targets.append(text.to("cpu"))
+            loss = loss_function(logits.transpose(1, 2), text)
+            total += loss.item()
+    return {"Val Loss": total / max(1, len(data_loader))}, preds[-1][-1]
+
+
+class Trainer:
+    """Native data-parallel training step for an asrx.Transformer."""
+
+    def __init__(self, model, lr=1e-4, betas=(0.9, 0.98), eps=1e-9, weight_decay=0.0, decoupled=True,
+                 ignore_index=-100, group=None, bucket_mb=64, allreduce_fn=None):
+        self.model = model
+        self.store = get_store(model)
+        self.m = torch.zeros_like(self.store.flat)
+        self.v = torch.zeros_like(self.store.flat)
+        self.lr, self.betas, self.eps, self.wd, self.decoupled = lr, betas, eps, weight_decay, decoupled
+        self.ignore_index = ignore_index
+        self.step_count = 0
+        self.reducer = GradAllReduce(self.store.grad, group=group, bucket_mb=bucket_mb, allreduce_fn=allreduce_fn)
+        self.store.refresh_shadow(force=True)
+
+    def forward_backward(self, spectrum, text, mask):
+        """text: (B, L+1) with BOS ... ; inputs text[:, :-1], targets text[:, 1:] (train.py:24,32)."""
+        model = self.model
+        C = make_ctx(model, model.decoder.p)
+        logits, S = model_forward(C, model, spectrum, text[:, :-1], mask[:, :-1])
+        V = model.decoder._classifier.V
+        tgt = text[:, 1:].reshape(-1).contiguous()
+        loss, dl, _ = K.cross_entropy(logits, V, tgt, ignore_index=self.ignore_index)
+        self.store.grad.zero_()
+        model_backward(C, model, S, dl.to(C.cd) if dl.dtype != C.cd else dl)
+        return loss
+
+    def step(self, spectrum, text, mask):
+        loss = self.forward_backward(spectrum, text, mask)
+        self.reducer()
+        self.step_count += 1
+        K.adam(self.store.flat, self.store.grad, self.m, self.v, self.store.shadow, self.lr, self.betas[0],
+               self.betas[1], self.eps, self.wd, self.step_count, grad_scale=1.0 / self.reducer.world,
+               decoupled=self.decoupled)
+        self.store.mark_shadow_fresh()
+        return loss

@@ -1,0 +1,149 @@
+"""Headline benchmark: encoder+decoder frames/s of the c3 training step (BASELINE.json configs[2]:
+12+12 layers, d_model 512, h 8, ff 2048, batch 64 per GPU, T=1000 frames of 80-bin log-mel, L=64 tokens,
+bf16, dropout 0.1, fused AdamW), data-parallel over N GPUs (weak scaling: 64 utterances per GPU).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
+        bench.py --gpus N --steps K --warmup W
+
+Prints ONE JSON line (rank 0). `value` = all ranks' frames / max-over-ranks wall time of the K timed steps.
+`roofline` = the dominant GEMM kernel instantiation (bf16 NT 128x128, every forward projection GEMM),
+timed live with HIP events on its launch stream; `cpu_baseline` = the oracle (fp32 eager PyTorch
+restatement of the reference) train step on the host cores, bounded sample, rank 0 at N=1 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "asr-transformer_amd"))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the config's)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-batch", type=int, default=4)
+    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--no-probe", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(cfg, frames, text_len, batch, steps):
+    """Oracle train step (fp32 eager CPU restatement of the reference, per-head loop) on the host cores."""
+    from oracle.ref_model import det_params, synthetic_batch, train_step_grads
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    torch.set_num_threads(threads)
+    P = {k: v.clone().requires_grad_(True) for k, v in det_params(cfg, 0).items()}
+    s, t, m = synthetic_batch(cfg, batch, frames, text_len + 1, seed=99)
+    train_step_grads(P, s, t, m, cfg, training=True)          # warmup
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        for v in P.values():
+            v.grad = None
+        train_step_grads(P, s, t, m, cfg, training=True)
+    dt = time.perf_counter() - t0
+    return {"value": round(batch * frames * steps / dt, 1), "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"oracle fp32 train step (fwd+CE+bwd, dropout {cfg.dropout}) {cfg.n_enc}+{cfg.n_dec} layers "
+                      f"d{cfg.d_model}, B={batch}, T={frames}, L={text_len}, {steps} steps after 1 warmup, "
+                      f"{dt:.1f}s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import asrx
+    from asrx import kernels as K
+    from asrx.train import Trainer
+    from oracle.ref_model import CONFIGS, synthetic_batch
+
+    spec = CONFIGS[args.config]
+    cfg = spec["cfg"]
+    B = args.batch or spec["batch"]
+    T, L = spec["frames"], spec["text_len"]
+    torch.manual_seed(0)
+    model = asrx.Transformer(cfg.vocab_size, cfg.input_dim, cfg.d_model, cfg.dec_len, cfg.enc_len, cfg.n_enc,
+                             cfg.n_dec, cfg.n_heads, cfg.ff_dim, dropout=cfg.dropout, precision="bf16").cuda().train()
+    if world > 1:   # identical initial weights on every rank
+        for p in model.parameters():
+            dist.broadcast(p.data, 0)
+    trainer = Trainer(model, lr=1e-4)
+    s, t, m = synthetic_batch(cfg, B, T, L + 1, seed=1234 + rank)
+    s, t, m = s.cuda(), t.cuda(), m.cuda()
+
+    for _ in range(args.warmup):
+        loss = trainer.step(s, t, m)
+    torch.cuda.synchronize()
+    probe = None
+    if not args.no_probe:
+        probe = K.KernelProbe((asrx._lib.BF16, False, False, 128, True))
+        probe.active = True
+        K.PROBE = probe
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = trainer.step(s, t, m)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    K.PROBE = None
+    if world > 1:
+        x = torch.tensor([dt], device="cuda", dtype=torch.float64)
+        dist.all_reduce(x, op=dist.ReduceOp.MAX)
+        dt = float(x)
+    frames = B * T * args.steps * world
+    value = frames / dt
+    roof = None
+    if probe is not None and probe.events:
+        durs = probe.durations_ms()
+        avg_ms = sum(durs) / len(durs)
+        achieved = probe.flops / (sum(durs) * 1e-3) / 1e12
+        roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                "kernel": "gemm_bf16_kernel<128,128,NT,vec> (all forward projection GEMMs)",
+                "launches_per_step": len(durs) // args.steps, "avg_launch_us": round(avg_ms * 1e3, 2),
+                "flop_per_launch_avg": probe.flops // len(durs)}
+    out = {"metric": "encoder+decoder frames/sec/GPU at d_model=512 T=1000; 1->8 GPU scaling",
+           "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random-init weights)",
+           "config": {"workload": f"{args.config}: {cfg.n_enc}+{cfg.n_dec} layers d_model={cfg.d_model} "
+                                  f"h={cfg.n_heads} ff={cfg.ff_dim}, B={B}/GPU, T={T} (T'={asrx.subsampled(T)}), "
+                                  f"L={L}, V={cfg.vocab_size}; bf16 train step fwd+CE+bwd+AdamW, dropout "
+                                  f"{cfg.dropout}",
+                      "model": "speech-transformer", "global_batch": B * world, "seq_len": T,
+                      "parallelism": f"dp{world}"},
+           "frames_per_sec_per_gpu": round(value / world, 1),
+           "loss": round(float(loss), 4),
+           "roofline": roof}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(cfg, T, L, args.cpu_batch, args.cpu_steps)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
