@@ -115,8 +115,14 @@ def test_train_grads_micro(golden_dir, precision, tol):
             assert n1 == n2
             p2.copy_(p1.grad.cpu() if p1.grad is not None else torch.zeros_like(p2))
     gsd = twin.state_dict()
+    gmax = max(float(np.abs(g["grad/" + k]).max()) for k in g["grad_names"])
     for key in g["grad_names"]:
         ref = g["grad/" + key]
+        if float(np.abs(ref).max()) < 1e-6 * gmax:
+            # mathematically zero gradient (e.g. the K bias: softmax is shift-invariant along keys) — the
+            # reference holds fp32 rounding noise there; require an absolute match at the global scale
+            assert float((gsd[key].double() - torch.from_numpy(ref).double()).abs().max()) < tol * 1e-2 * gmax, key
+            continue
         assert relerr(gsd[key], ref) < tol, key
 
 
