@@ -37,6 +37,7 @@ class GemmDesc(ctypes.Structure):
         ("resid", c_vp), ("ld_resid", c_i64), ("resid_dtype", c_i32),
         ("splitk", c_i32), ("workspace", c_vp), ("workspace_elems", c_i64),
         ("tile", c_i32),
+        ("rowsum_a", c_vp), ("rowsum_ws", c_vp),
     ]
 
 

@@ -162,15 +162,13 @@ def self_attn_bwd(C, S, dy, dy_c, dx_c_out=None, dx_c_p=0.0, dx_c_seed=0):
     W, G = C.W, C.G
     do = _empty((M, d), C.cd, x)
     K.linear_dgrad(dy_c, W(mha._out_linear.weight), do)
-    K.linear_wgrad(dy_c, o, G(mha._out_linear.weight))
-    K.colsum(dy_c, G(mha._out_linear.bias))
+    K.linear_wgrad(dy_c, o, G(mha._out_linear.weight), bias_grad=G(mha._out_linear.bias))
     dqkv = _empty((M, 3 * d), C.cd, x)
     gst = ((d, T * d),) + ((3 * d, T * 3 * d),) * 3
     attn_bwd(C, S["A"], qkv, qkv[:, d:], qkv[:, 2 * d:], o, do, dqkv, dqkv[:, d:], dqkv[:, 2 * d:], gst)
     dh = _empty((M, d), C.cd, x)
     K.linear_dgrad(dqkv, W(mha.wqkv), dh)
-    K.linear_wgrad(dqkv, h, G(mha.wqkv))
-    K.colsum(dqkv, G(mha.bqkv))
+    K.linear_wgrad(dqkv, h, G(mha.wqkv), bias_grad=G(mha.bqkv))
     return ln_bwd(C, x, dh, S["ln"], S["mean"], S["rstd"], dres=dy, drop_out=dx_c_out, drop_seed=dx_c_seed,
                   drop_p=dx_c_p)
 
@@ -200,15 +198,13 @@ def cross_attn_bwd(C, S, dy, dy_c, dkv, dx_c_out=None, dx_c_p=0.0, dx_c_seed=0):
     W, G = C.W, C.G
     do = _empty((M, d), C.cd, x)
     K.linear_dgrad(dy_c, W(mha._out_linear.weight), do)
-    K.linear_wgrad(dy_c, o, G(mha._out_linear.weight))
-    K.colsum(dy_c, G(mha._out_linear.bias))
+    K.linear_wgrad(dy_c, o, G(mha._out_linear.weight), bias_grad=G(mha._out_linear.bias))
     dq = _empty((M, d), C.cd, x)
     gst = ((d, L * d), (d, L * d), (kv_ld, Te * kv_ld), (kv_ld, Te * kv_ld))
     attn_bwd(C, S["A"], q, kv, kv[:, d:], o, do, dq, dkv, dkv[:, d:], gst)
     dh = _empty((M, d), C.cd, x)
     K.linear_dgrad(dq, W(mha.wq), dh)
-    K.linear_wgrad(dq, h, G(mha.wq))
-    K.colsum(dq, G(mha.bq))
+    K.linear_wgrad(dq, h, G(mha.wq), bias_grad=G(mha.bq))
     return ln_bwd(C, x, dh, S["ln"], S["mean"], S["rstd"], dres=dy, drop_out=dx_c_out, drop_seed=dx_c_seed,
                   drop_p=dx_c_p)
 
@@ -235,12 +231,10 @@ def ffn_bwd(C, S, dy, dy_c, dx_c_out=None, dx_c_p=0.0, dx_c_seed=0):
     keep_scale = 1.0 / (1.0 - C.p) if C.p > 0 else 1.0
     # f = Drop(ReLU(pre)) -> dpre = df * [f > 0] / (1-p)   (f > 0 <=> pre > 0 and kept)
     K.linear_dgrad(dy_c, W(ff.unsqueeze.weight), dpre, alpha=keep_scale, gate=f, ld_gate=nf)
-    K.linear_wgrad(dy_c, f, G(ff.unsqueeze.weight))
-    K.colsum(dy, G(ff.unsqueeze.bias))
+    K.linear_wgrad(dy_c, f, G(ff.unsqueeze.weight), bias_grad=G(ff.unsqueeze.bias))
     dh = _empty((M, d), C.cd, x)
     K.linear_dgrad(dpre, W(ff.squeeze.weight), dh)
-    K.linear_wgrad(dpre, h, G(ff.squeeze.weight))
-    K.colsum(dpre, G(ff.squeeze.bias))
+    K.linear_wgrad(dpre, h, G(ff.squeeze.weight), bias_grad=G(ff.squeeze.bias))
     return ln_bwd(C, x, dh, S["ln"], S["mean"], S["rstd"], dres=dy, drop_out=dx_c_out, drop_seed=dx_c_seed,
                   drop_p=dx_c_p)
 
@@ -305,10 +299,9 @@ def frontend_bwd(C, S, dfeats_c, conv1, conv2):
     dy2 = dfeats_c.view(M2, 64)
     cols = S["cols"]
     G = C.G
-    K.linear_wgrad(dy2, cols, G(conv2.weight))
+    K.linear_wgrad(dy2, cols, G(conv2.weight), bias_grad=G(conv2.bias))
     dcols = _empty((M2, 576), C.cd, dy2)
     K.linear_dgrad(dy2, C.W(conv2.weight), dcols)
-    K.colsum(dy2, G(conv2.bias))
     dy1 = _empty((B, F1, T1, 64), torch.float32, dy2)
     K.col2im_conv2(dcols, S["y1"], dy1)
     K.conv1_bwd_w(S["x"], dy1, G(conv1.weight).view(64, 9), G(conv1.bias))

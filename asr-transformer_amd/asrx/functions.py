@@ -135,8 +135,7 @@ def encoder_bwd(C, enc, S, dy, gate_feats):
         K.linear_dgrad(dx_c, C.W(w), dfeats, gate=feats, ld_gate=feats.shape[1])
     else:
         K.linear_dgrad(dx_c, C.W(w), dfeats)
-    K.linear_wgrad(dx_c, feats, C.G(w))
-    K.colsum(dx, C.G(enc._lin_in.bias))
+    K.linear_wgrad(dx_c, feats, C.G(w), bias_grad=C.G(enc._lin_in.bias))
     return dfeats
 
 
@@ -209,8 +208,7 @@ def decoder_bwd(C, dec, S, dlogits_c):
     Wkv, _, gW, gb = _kv_block(C, dec)
     denc = torch.empty(B * Te, d, dtype=torch.float32, device=dev)
     K.linear_dgrad(dkv, Wkv, denc)
-    K.linear_wgrad(dkv, S["enc"], gW)
-    K.colsum(dkv, gb)
+    K.linear_wgrad(dkv, S["enc"], gW, bias_grad=gb)
     return denc
 
 
@@ -455,8 +453,7 @@ class _MHAFn(torch.autograd.Function):
             dy_c.copy_(g2)
         do = torch.empty(B * Lq, d, dtype=C.cd, device=dev)
         K.linear_dgrad(dy_c, C.W(m._out_linear.weight), do)
-        K.linear_wgrad(dy_c, S["o"], C.G(m._out_linear.weight))
-        K.colsum(dy_c, C.G(m._out_linear.bias))
+        K.linear_wgrad(dy_c, S["o"], C.G(m._out_linear.weight), bias_grad=C.G(m._out_linear.bias))
         dq = torch.empty(B * Lq, d, dtype=C.cd, device=dev)
         dkv = torch.empty(B * Lk, 2 * d, dtype=C.cd, device=dev)
         q, kv = S["q"], S["kv"]
@@ -470,12 +467,10 @@ class _MHAFn(torch.autograd.Function):
             gWq, gbq, gWkv, gbkv = gw[:d], gb[:d], gw[d:], gb[d:]
         dx = torch.empty(B * Lq, d, dtype=torch.float32, device=dev)
         K.linear_dgrad(dq, Wq, dx)
-        K.linear_wgrad(dq, S["xc"], gWq)
-        K.colsum(dq, gbq)
+        K.linear_wgrad(dq, S["xc"], gWq, bias_grad=gbq)
         dk_in = torch.empty(B * Lk, d, dtype=torch.float32, device=dev)
         K.linear_dgrad(dkv, Wkv, dk_in)
-        K.linear_wgrad(dkv, S["kc"], gWkv)
-        K.colsum(dkv, gbkv)
+        K.linear_wgrad(dkv, S["kc"], gWkv, bias_grad=gbkv)
         if S["self_attn"]:
             dx.add_(dk_in)
             return (None, None, dx.view(B, Lq, d).to(S["xdtype"]), None, None) + (None,) * len(_params(m))
@@ -516,12 +511,10 @@ class _FFNFn(torch.autograd.Function):
         dpre = torch.empty(M, ff.ff_dim, dtype=C.cd, device=xc.device)
         K.linear_dgrad(g_c, C.W(ff.unsqueeze.weight), dpre, alpha=1.0 / (1.0 - C.p) if C.p > 0 else 1.0, gate=f,
                        ld_gate=ff.ff_dim)
-        K.linear_wgrad(g_c, f, C.G(ff.unsqueeze.weight))
-        K.colsum(g2, C.G(ff.unsqueeze.bias))
+        K.linear_wgrad(g_c, f, C.G(ff.unsqueeze.weight), bias_grad=C.G(ff.unsqueeze.bias))
         dx = torch.empty(M, ff.emb_dim, dtype=torch.float32, device=xc.device)
         K.linear_dgrad(dpre, C.W(ff.squeeze.weight), dx)
-        K.linear_wgrad(dpre, xc, C.G(ff.squeeze.weight))
-        K.colsum(dpre, C.G(ff.squeeze.bias))
+        K.linear_wgrad(dpre, xc, C.G(ff.squeeze.weight), bias_grad=C.G(ff.squeeze.bias))
         return (None, None, dx.view(shape).to(xdt)) + (None,) * len(_params(ff))
 
 
@@ -584,8 +577,7 @@ class _DecLayerFn(torch.autograd.Function):
         ca = layer._cross_attention
         denc = torch.empty(B * Te, d, dtype=torch.float32, device=g32.device)
         K.linear_dgrad(dkv, C.W(ca.wkv), denc)
-        K.linear_wgrad(dkv, enc_c, C.G(ca.wkv))
-        K.colsum(dkv, C.G(ca.bkv))
+        K.linear_wgrad(dkv, enc_c, C.G(ca.wkv), bias_grad=C.G(ca.bkv))
         return (None, None, dx.view(B, L, d).to(xdt), None, denc.view(B, Te, d).to(edt)) + \
             (None,) * len(_params(layer))
 

@@ -69,8 +69,10 @@ def choose_tile(m, n, batch, splitk):
 
 def gemm(a, b, c, m, n, k, *, lda, ldb, ldc, a_trans=False, b_trans=False, alpha=1.0, beta=0.0, bias=None,
          rowadd=None, rowadd_mod=1, ld_rowadd=0, relu=False, dropout_p=0.0, seed=0, gate=None, ld_gate=0,
-         resid=None, ld_resid=0, batch=1, batch_inner=1, sa=(0, 0), sb=(0, 0), sc=(0, 0), splitk=1, tile=0):
-    """C = epi(alpha * op(A) op(B)^T) — see asrx_gemm in include/asrx.h."""
+         resid=None, ld_resid=0, batch=1, batch_inner=1, sa=(0, 0), sb=(0, 0), sc=(0, 0), splitk=1, tile=0,
+         rowsum=None):
+    """C = epi(alpha * op(A) op(B)^T) — see asrx_gemm in include/asrx.h.  rowsum (fp32 [m], a_trans only):
+    += row sums of A (fused bias gradient)."""
     _cuda(a, b, c)
     if a.dtype != b.dtype:
         raise TypeError("asrx.gemm: A and B must share a dtype")
@@ -105,6 +107,12 @@ def gemm(a, b, c, m, n, k, *, lda, ldb, ldc, a_trans=False, b_trans=False, alpha
     else:
         d.splitk = 1
     d.tile = tile
+    if rowsum is not None:
+        _cuda(rowsum)
+        d.rowsum_a = rowsum.data_ptr()
+        if splitk > 1:
+            rws = torch.empty(splitk * m, device=c.device, dtype=torch.float32)
+            d.rowsum_ws = rws.data_ptr()
     probe = PROBE
     if probe is not None and probe.active and a.dtype == torch.bfloat16:
         vec = (lda % 8 == 0 and ldb % 8 == 0 and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0
@@ -136,12 +144,32 @@ def linear_dgrad(dy, w, out, **kw):
     return gemm(dy, w, out, m, k, n, lda=dy.stride(0), ldb=w.stride(0), ldc=out.stride(0), b_trans=True, **kw)
 
 
-def linear_wgrad(dy, x, wgrad, *, beta=1.0, **kw):
-    """wgrad[N,K] (+)= dy[M,N]^T . x[M,K]  (fp32 gradient buffer)."""
+def wgrad_plan(n_out, k_in, rows):
+    """Tile and split-K for dW = dY^T X (reduction over the B*T rows): 128x128 tiles, splits chosen so that
+    ~320 workgroups fill the 256 CUs while each split keeps >= 256 rows."""
+    tile = 128 if (n_out >= 128 and k_in >= 128) else 64
+    tiles = math.ceil(n_out / tile) * math.ceil(k_in / tile)
+    splitk = 1
+    if tiles < 256:
+        splitk = max(1, min(rows // 256, round(320 / tiles), 256))
+    return tile, splitk
+
+
+def linear_wgrad(dy, x, wgrad, *, beta=1.0, bias_grad=None, **kw):
+    """wgrad[N,K] (+)= dy[M,N]^T . x[M,K]  (fp32 gradient buffer); bias_grad[N] (+)= colsum(dy) fused into
+    the same GEMM (bf16 operands) or a separate native reduction (fp32 parity path)."""
     m, n = dy.shape
     k = x.shape[1]
-    return gemm(dy, x, wgrad, n, k, m, lda=dy.stride(0), ldb=x.stride(0), ldc=wgrad.stride(0), a_trans=True,
-                b_trans=True, beta=beta, splitk=kw.pop("splitk", "auto"), **kw)
+    tile, splitk = wgrad_plan(n, k, m)
+    if dy.dtype != torch.bfloat16:
+        tile = 0
+    fuse = bias_grad is not None and dy.dtype == torch.bfloat16
+    ws = gemm(dy, x, wgrad, n, k, m, lda=dy.stride(0), ldb=x.stride(0), ldc=wgrad.stride(0), a_trans=True,
+              b_trans=True, beta=beta, splitk=kw.pop("splitk", splitk), tile=kw.pop("tile", tile),
+              rowsum=bias_grad if fuse else None, **kw)
+    if bias_grad is not None and not fuse:
+        colsum(dy, bias_grad)
+    return ws
 
 
 def colsum(x, out, *, accumulate=True, rows=None, cols=None, ld=None):

@@ -153,13 +153,22 @@ __global__ __launch_bounds__(256) void conv1_bwd_w_kernel(const float* __restric
     part[(int64_t)blockIdx.x * 640 + i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
 }
 
+// one block per output (640 = 64 channels x (9 taps + bias)); partials summed by 256 threads + LDS tree
 __global__ __launch_bounds__(256) void conv1_bwd_finish(const float* part, int nblocks, float* dw, float* db) {
-  for (int i = threadIdx.x + blockIdx.x * 256; i < 640; i += gridDim.x * 256) {
-    float s = 0.f;
-    for (int p = 0; p < nblocks; ++p) s += part[(int64_t)p * 640 + i];
+  __shared__ float red[256];
+  const int i = blockIdx.x;
+  float s = 0.f;
+  for (int p = threadIdx.x; p < nblocks; p += 256) s += part[(int64_t)p * 640 + i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
     const int c = i / 10, k = i % 10;
-    if (k < 9) dw[c * 9 + k] += s;
-    else db[c] += s;
+    if (k < 9) dw[c * 9 + k] += red[0];
+    else db[c] += red[0];
   }
 }
 
@@ -185,20 +194,41 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
   }
 }
 
+// One block per vocabulary row.  Token ids are scanned 64 at a time; every wave ballots the same window and
+// all threads walk the set bits in token order, so each row sums its contributions in a fixed order:
+// deterministic, no atomics.  The padding row is skipped (nn.Embedding padding_idx, model.py:94).
 __global__ __launch_bounds__(256) void embed_bwd_kernel(const int64_t* __restrict__ tok, int64_t ntok, int d,
                                                         const float* __restrict__ dout, int pad_id, uint32_t thr,
                                                         float sc, uint64_t seed, float* __restrict__ dtable) {
   const int v = blockIdx.x;
   if (v == pad_id) return;
-  for (int c = threadIdx.x; c < d; c += 256) {
-    float s = 0.f;
-    for (int64_t r = 0; r < ntok; ++r) {
-      if (tok[r] != v) continue;
-      float g = dout[r * d + c];
-      if (thr) g = rng_keep(seed, (uint32_t)(r * d + c), thr) ? g * sc : 0.f;
-      s += g;
+  const int lane = threadIdx.x & 63;
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  for (int64_t base = 0; base < ntok; base += 64) {
+    const int64_t i = base + lane;
+    const bool hit = i < ntok && tok[i] == v;
+    unsigned long long mask = __ballot(hit);
+    while (mask) {
+      const int b = __ffsll(mask) - 1;
+      mask &= mask - 1;
+      const int64_t r = base + b;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = threadIdx.x + 256 * j;
+        if (c < d) {
+          float gv = dout[r * d + c];
+          if (thr) gv = rng_keep(seed, (uint32_t)(r * d + c), thr) ? gv * sc : 0.f;
+          acc[j] += gv;
+        }
+      }
     }
-    dtable[(int64_t)v * d + c] += s;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = threadIdx.x + 256 * j;
+    if (c < d) dtable[(int64_t)v * d + c] += acc[j];
   }
 }
 
@@ -394,7 +424,7 @@ extern "C" int asrx_conv1_bwd_w(const float* x, const float* dy1, int32_t B, int
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(conv1_bwd_w_kernel, dim3(nblocks), dim3(256), 0, st, x, dy1, B, F, T, F1, T1, part, per);
   ASRX_CHECK_LAUNCH();
-  hipLaunchKernelGGL(conv1_bwd_finish, dim3(3), dim3(256), 0, st, part, nblocks, dw, db);
+  hipLaunchKernelGGL(conv1_bwd_finish, dim3(640), dim3(256), 0, st, part, nblocks, dw, db);
   ASRX_CHECK_LAUNCH();
   return ASRX_OK;
 }
@@ -415,7 +445,7 @@ extern "C" int asrx_embed_bwd(const int64_t* tok, int64_t ntok, int32_t L, const
                               int32_t vocab, int32_t pad_id, float dropout_p, uint64_t seed, float* dtable,
                               void* stream) {
   (void)L;
-  if (!tok || !dout || !dtable || vocab <= 0) return ASRX_ERR_ARG;
+  if (!tok || !dout || !dtable || vocab <= 0 || d > 2048) return ASRX_ERR_ARG;
   const uint32_t thr = drop_threshold(dropout_p);
   const float sc = (dropout_p > 0.f && dropout_p < 1.f) ? 1.f / (1.f - dropout_p) : 1.f;
   hipLaunchKernelGGL(embed_bwd_kernel, dim3(vocab), dim3(256), 0, (hipStream_t)stream, tok, ntok, d, dout, pad_id, thr,

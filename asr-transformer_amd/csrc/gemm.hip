@@ -33,6 +33,8 @@ struct GemmArgs {
   int splitk; int k_per_split;    // k_per_split multiple of BK
   float* ws;                       // split-K partials [split][M][N]
   int cvec;                        // C row starts 4-element aligned
+  float* rowsum;                   // fused bias gradient: rowsum[m] += sum_k A(m,k)   (A k-strided only)
+  float* rowsum_ws;                // [splitk][M] partials when splitk > 1
 };
 
 ASRX_DEV float ld_any(const void* p, int dtype, int64_t i) {
@@ -237,8 +239,20 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs g) {
     for (int j = 0; j < TM; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
 
   s8_t ra[TA::PER_THREAD], rb[TB::PER_THREAD];
+  // fused bias gradient (row sums of a k-strided A): every staging thread always loads the same 8 rows
+  const bool do_rs = AT && g.rowsum != nullptr && (tile % ntn) == 0;
+  float rs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  auto acc_rs = [&]() {
+    if (do_rs) {
+#pragma unroll
+      for (int i = 0; i < TA::PER_THREAD; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) rs[j] += bf2f((bf16_t)ra[i][j]);
+    }
+  };
   if (nk > 0) {
     TA::template load<VEC>(ra, A, g.lda, m0, g.M, kbeg, kend);
+    acc_rs();
     TB::template load<VEC>(rb, B, g.ldb, n0, g.N, kbeg, kend);
     TA::store(lds, ra);
     TB::store(lds + TA::ELEMS, rb);
@@ -263,10 +277,30 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs g) {
         for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
     }
     if (kt + 1 < nk) {
+      acc_rs();
       TA::store(lds + (cur ^ 1) * STAGE, ra);
       TB::store(lds + (cur ^ 1) * STAGE + TA::ELEMS, rb);
     }
     __syncthreads();
+  }
+  if constexpr (AT) {
+    if (do_rs) {  // block-reduce the per-thread row sums through LDS (free after the main loop)
+      float* red = (float*)lds;
+      constexpr int CPRW = BM / 8;  // staging chunks per k-row of the [BK][BM] image
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[threadIdx.x * 8 + j] = rs[j];
+      __syncthreads();
+      if (threadIdx.x < BM) {
+        const int r = threadIdx.x, cc = r >> 3, j = r & 7;
+        float sum = 0.f;
+        for (int q = 0; q < 256 / CPRW; ++q) sum += red[(cc + CPRW * q) * 8 + j];
+        const int m = m0 + r;
+        if (m < g.M) {
+          if (g.splitk > 1) g.rowsum_ws[(int64_t)split * g.M + m] = sum;
+          else g.rowsum[m] += sum;
+        }
+      }
+    }
   }
 
   const int gq = l >> 4;
@@ -409,12 +443,27 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g) {
     const int m = (int)(t / nq), n0 = (int)(t % nq) * 4;
     float s[4] = {0.f, 0.f, 0.f, 0.f};
     const int nv = min(4, g.N - n0);
-    for (int sp = 0; sp < g.splitk; ++sp) {
-      const float* w = g.ws + ((int64_t)sp * g.M + m) * g.N + n0;
-      for (int i = 0; i < nv; ++i) s[i] += w[i];
+    if (nv == 4 && (g.N & 3) == 0) {
+      for (int sp = 0; sp < g.splitk; ++sp) {
+        const f4_t w = *(const f4_t*)(g.ws + ((int64_t)sp * g.M + m) * g.N + n0);
+        s[0] += w[0]; s[1] += w[1]; s[2] += w[2]; s[3] += w[3];
+      }
+    } else {
+      for (int sp = 0; sp < g.splitk; ++sp) {
+        const float* w = g.ws + ((int64_t)sp * g.M + m) * g.N + n0;
+        for (int i = 0; i < nv; ++i) s[i] += w[i];
+      }
     }
     epilogue4(g, 0, m, n0, s);
   }
+}
+
+__global__ __launch_bounds__(256) void rowsum_finish_kernel(const float* ws, int splitk, int M, float* out) {
+  const int m = blockIdx.x * 256 + threadIdx.x;
+  if (m >= M) return;
+  float s = 0.f;
+  for (int sp = 0; sp < splitk; ++sp) s += ws[(int64_t)sp * M + m];
+  out[m] += s;
 }
 
 template <int BM, int BN, bool AT, bool BT, bool VEC>
@@ -468,6 +517,10 @@ extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
   g.gate = d->gate; g.ld_gate = d->ld_gate; g.gate_dtype = d->gate_dtype;
   g.resid = d->resid; g.ld_resid = d->ld_resid; g.resid_dtype = d->resid_dtype;
   g.ws = d->workspace;
+  g.rowsum = d->rowsum_a;
+  g.rowsum_ws = d->rowsum_ws;
+  if (g.rowsum && (!d->a_trans || d->in_dtype != ASRX_BF16 || batch != 1)) return ASRX_ERR_UNSUPPORTED;
+  if (g.rowsum && splitk > 1 && !g.rowsum_ws) return ASRX_ERR_ARG;
   const int esz = d->c_dtype == ASRX_F32 ? 16 : 8;
   g.cvec = (d->ldc % 4 == 0) && ((uintptr_t)d->c % esz == 0) && (d->sc_outer % 4 == 0) && (d->sc_inner % 4 == 0);
 
@@ -505,6 +558,11 @@ extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
     const int blocks = (int)std::min<int64_t>((quads + 255) / 256, 4096);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, g);
     ASRX_CHECK_LAUNCH();
+    if (g.rowsum) {
+      hipLaunchKernelGGL(rowsum_finish_kernel, dim3((d->m + 255) / 256), dim3(256), 0, st, g.rowsum_ws, splitk,
+                         d->m, g.rowsum);
+      ASRX_CHECK_LAUNCH();
+    }
   }
   return ASRX_OK;
 }

@@ -162,12 +162,19 @@ __global__ __launch_bounds__(256) void colsum_stage1(int dtype, const void* in, 
     part[(int64_t)blockIdx.y * cols + c] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
 }
 
+// stage 2: one block per 64 columns; 4 row-groups of partials summed in fixed order, then combined in LDS.
 __global__ __launch_bounds__(256) void colsum_stage2(const float* part, int nparts, int cols, float* out, int acc) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= cols) return;
+  __shared__ float red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), sub = threadIdx.x >> 6;
   float s = 0.f;
-  for (int p = 0; p < nparts; ++p) s += part[(int64_t)p * cols + c];
-  out[c] = acc ? out[c] + s : s;
+  if (c < cols)
+    for (int p = sub; p < nparts; p += 4) s += part[(int64_t)p * cols + c];
+  red[sub][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (sub == 0 && c < cols) {
+    const float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    out[c] = acc ? out[c] + t : t;
+  }
 }
 
 template <int CH, int NJ>
@@ -239,7 +246,7 @@ extern "C" int asrx_reduce_rows(int32_t dtype, const void* in, int64_t rows, int
                        part, rpb);
     ASRX_CHECK_LAUNCH();
   }
-  hipLaunchKernelGGL(colsum_stage2, dim3((cols + 255) / 256), dim3(256), 0, st, part, nparts, cols, out, accumulate);
+  hipLaunchKernelGGL(colsum_stage2, dim3((cols + 63) / 64), dim3(256), 0, st, part, nparts, cols, out, accumulate);
   ASRX_CHECK_LAUNCH();
   return ASRX_OK;
 }

@@ -42,7 +42,7 @@ int asrx_version(void);
  *              (z*M + m)*N + n) -> *gate (keep where gate[m][n] > 0) -> +resid[m][n] -> +beta*C_old -> store
  * Replaces: nn.Linear (layers.py:10-12,36,48,51; model.py:32,102) = aten::addmm/linear, the per-head
  * q@k^T and attn@v aten::bmm (layers.py:20,27), and the conv2 implicit GEMM (model.py:168-171).
- * Split-K (splitk > 1, batch == 1) needs workspace of splitk*M*N floats.
+ * Split-K (splitk > 1, batch == 1) needs workspace of splitk*M*N floats (reduced in fixed split order).
  * ------------------------------------------------------------------------------------------------- */
 typedef struct asrx_gemm_desc {
   int32_t m, n, k;
@@ -61,6 +61,10 @@ typedef struct asrx_gemm_desc {
   const void* resid; int64_t ld_resid; int32_t resid_dtype;
   int32_t splitk; float* workspace; int64_t workspace_elems;
   int32_t tile;                 /* 0 = auto, 64 or 128 = forced square tile (bf16 path) */
+  /* rowsum_a[m] += sum_k A(m,k)  (a_trans = 1 only): the bias gradient of a weight-gradient GEMM
+   * dW = dY^T X is the row sum of its A operand dY^T — fused into the staging loads, no extra HBM pass.
+   * With splitk > 1 the per-split partials use rowsum_ws[splitk*M]. */
+  float* rowsum_a; float* rowsum_ws;
 } asrx_gemm_desc;
 
 int asrx_gemm(const asrx_gemm_desc* d, void* stream);
