@@ -122,8 +122,24 @@ def gen_model(name, train_grads_full):
     np.savez_compressed(os.path.join(OUT, f"model_{name}.npz"), **out)
 
 
+def gen_schema():
+    """Reference state_dict key order and shapes (drop-in schema check without the reference present)."""
+    import json
+    out = {}
+    for name in ("micro", "c1", "c3"):
+        cfg = CONFIGS[name]["cfg"]
+        m = build_ref(cfg) if name != "c3" else Transformer(cfg.vocab_size, cfg.input_dim, cfg.d_model, cfg.dec_len,
+                                                           cfg.enc_len, cfg.n_enc, cfg.n_dec, cfg.n_heads,
+                                                           cfg.ff_dim)
+        out[name] = [[k, list(v.shape)] for k, v in m.state_dict().items()]
+        out[name + "_nparams"] = sum(p.numel() for p in m.parameters())
+    with open(os.path.join(OUT, "ref_state_dict_schema.json"), "w") as f:
+        json.dump(out, f)
+
+
 if __name__ == "__main__":
     torch.manual_seed(0)
+    gen_schema()
     gen_pe()
     gen_ops()
     gen_model("micro", train_grads_full=True)

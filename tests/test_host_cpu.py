@@ -1,0 +1,123 @@
+"""Host-side checks that need no GPU: the C-ABI library loads and exports every declared symbol, the
+drop-in modules reproduce the reference state_dict schema exactly, and the storage re-layouts
+(fused per-head projections, permuted _lin_in columns, channels-last conv2, padded classifier, flat
+parameter store) are lossless."""
+import json
+import os
+import re
+
+import pytest
+import torch
+
+from oracle.ref_model import CONFIGS, det_params
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_symbols():
+    src = open(os.path.join(REPO, "include", "asrx.h")).read()
+    return sorted(set(re.findall(r"\bint\s+(asrx_\w+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    import asrx
+    from asrx._lib import SIGNATURES
+    lib = asrx.native()
+    syms = _declared_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(lib, s), s
+        assert s in SIGNATURES, s
+    assert set(SIGNATURES) == set(syms)
+    assert lib.asrx_version() >= 1
+
+
+def test_abi_rejects_bad_arguments_without_gpu():
+    """Argument validation happens before any launch: a NULL descriptor must return ASRX_ERR_ARG."""
+    import asrx
+    lib = asrx.native()
+    assert lib.asrx_gemm(None, None) == -1
+    assert lib.asrx_attention_fwd(None, None) == -1
+    assert lib.asrx_cast(0, None, 0, None, 10, None) == -1
+
+
+def _build(name, **kw):
+    import asrx
+    cfg = CONFIGS[name]["cfg"]
+    return asrx.Transformer(cfg.vocab_size, cfg.input_dim, cfg.d_model, cfg.dec_len, cfg.enc_len, cfg.n_enc,
+                            cfg.n_dec, cfg.n_heads, cfg.ff_dim, dropout=cfg.dropout, **kw), cfg
+
+
+@pytest.mark.parametrize("name", ["micro", "c1", "c3"])
+def test_state_dict_schema_matches_reference(golden_dir, name):
+    ref = json.load(open(os.path.join(golden_dir, "ref_state_dict_schema.json")))
+    m, cfg = _build(name)
+    sd = m.state_dict()
+    assert [[k, list(v.shape)] for k, v in sd.items()] == ref[name]
+    # parameter count: ours pads the classifier rows to a multiple of 64 and nothing else
+    pad = (m.decoder._classifier.Vp - cfg.vocab_size) * cfg.d_model
+    assert sum(p.numel() for p in m.parameters()) == ref[name + "_nparams"] + pad
+
+
+def test_reference_weights_round_trip_exactly():
+    m, cfg = _build("c1")
+    P = det_params(cfg, 3)
+    sd = m.state_dict()
+    sd.update(P)
+    m.load_state_dict(sd)
+    out = m.state_dict()
+    for k, v in P.items():
+        assert torch.equal(out[k], v), k
+    # internal layouts
+    d, H = cfg.d_model, cfg.n_heads
+    dh = d // H
+    mha = m.encoder._layers[1]._attention
+    for i in range(H):
+        assert torch.equal(mha.wqkv[i * dh:(i + 1) * dh], P[f"encoder._layers.1._attention._heads.{i}._q.weight"])
+        assert torch.equal(mha.wqkv[d + i * dh:d + (i + 1) * dh],
+                           P[f"encoder._layers.1._attention._heads.{i}._k.weight"])
+        assert torch.equal(mha.bqkv[2 * d + i * dh:2 * d + (i + 1) * dh],
+                           P[f"encoder._layers.1._attention._heads.{i}._v.bias"])
+    ca = m.decoder._layers[0]._cross_attention
+    assert torch.equal(ca.wkv[:d], torch.cat([P[f"decoder._layers.0._cross_attention._heads.{i}._k.weight"]
+                                              for i in range(H)]))
+    W = P["encoder._lin_in.weight"]              # (d, c*F2 + f)
+    F2 = W.shape[1] // 64
+    phys = m.encoder._lin_in.weight.detach()     # (d, f*64 + c)
+    assert torch.equal(phys.view(d, F2, 64)[:, 5, 7], W.view(d, 64, F2)[:, 7, 5])
+    w2 = m.input_layer[2].weight
+    assert w2.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(w2, P["input_layer.2.weight"])
+    assert torch.all(m.decoder._classifier.weight[cfg.vocab_size:] == 0)
+
+
+def test_flat_store_layout_on_cpu():
+    from asrx.functions import param_order
+    from asrx.params import ALIGN, FlatParams
+    m, cfg = _build("micro")
+    before = {k: v.clone() for k, v in m.state_dict().items()}
+    st = FlatParams(param_order(m), "cpu")
+    after = m.state_dict()
+    for k in before:
+        assert torch.equal(before[k], after[k]), k
+    for p in m.parameters():
+        assert p.data.data_ptr() == st.flat.data_ptr() + 4 * st.offset(p)
+        assert st.offset(p) % ALIGN == 0
+        assert p.grad is not None and p.grad.data_ptr() == st.grad.data_ptr() + 4 * st.offset(p)
+    # the decoder's cross-attention K/V projections form one contiguous [n_dec*2d, d] block
+    dec = m.decoder
+    n, d = len(dec._layers), cfg.d_model
+    span = st.span(dec._layers[0]._cross_attention.wkv, n, st.flat)
+    assert span is not None and span.numel() == n * 2 * d * d
+    # LayerNorm gamma/beta adjacent (one fused dgamma|dbeta reduction)
+    ln = m.encoder._layers[0]._norm1
+    assert st.offset(ln.bias) == st.offset(ln.weight) + d
+    # conv2 weight keeps its channels-last physical layout inside the store
+    assert m.input_layer[2].weight.is_contiguous(memory_format=torch.channels_last)
+
+
+def test_modules_refuse_cpu_execution():
+    """No CPU fallback: running the drop-in model without a GPU raises instead of silently computing."""
+    m, cfg = _build("micro")
+    with pytest.raises(RuntimeError):
+        m(torch.zeros(1, 1, 80, 60), torch.ones(1, 8, dtype=torch.long), torch.ones(1, 8))
