@@ -12,6 +12,8 @@
 //
 // Replaces the reference's nn.Linear / aten::addmm and aten::bmm calls (layers.py:10-12,16-18,20,27,36,48,51;
 // model.py:32,102) and, through im2col, the conv2 of the front-end (model.py:168-171).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -317,6 +319,159 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs g) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// bf16 kernel, direct-to-LDS staging (global_load_lds_dwordx4): 128x128x64 tiles, 4 waves (64x64 each),
+// two LDS buffers, one barrier per K-step.  Each wave-instruction writes 1 KiB of LDS lane-linearly, so the
+// bank-conflict swizzles live on the per-lane SOURCE addresses and are undone on the fragment reads:
+//   k-contiguous image [128 rows][64 k] (128-B rows): 16-B chunk c of row r stored at c ^ ((r >> 1) & 7)
+//     -> the ds_read_b128 fragment reads of a 16-lane group hit 16 distinct 16-B slots (conflict-free);
+//   k-strided image [64 k][128 cols] (256-B rows): 32-B chunk XOR ks_swz<128>(k) as in the register path.
+// Rows past M/N are clamped to the last valid row (their results are never stored); K must be a multiple
+// of 64 per split (host-checked).
+// ------------------------------------------------------------------------------------------------
+constexpr int GT = 128;                       // tile edge
+constexpr int GTILE_BYTES = GT * BK * 2;      // 16 KiB per operand per stage
+constexpr int G_INST = GTILE_BYTES / 4096;    // glds instructions per thread per operand per stage (4)
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef const __attribute__((address_space(1))) void gbl_void_t;
+
+template <bool KSTRIDED>
+ASRX_DEV void glds_stage(unsigned char* lds_tile, const bf16_t* base, int64_t ld, int r0, int rmax, int k0) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+#pragma unroll
+  for (int j = 0; j < G_INST; ++j) {
+    const int q = j * 4 + w;             // 1-KiB piece of the image written by this wave-instruction
+    const int o = q * 1024 + l * 16;     // image byte offset of this lane's 16 B
+    const bf16_t* src;
+    if constexpr (!KSTRIDED) {
+      const int r = o >> 7, cp = (o >> 4) & 7;
+      const int c = cp ^ ((r >> 1) & 7);
+      const int gr = min(r0 + r, rmax - 1);
+      src = base + (int64_t)gr * ld + k0 + c * 8;
+    } else {
+      const int kr = o >> 8, c16 = (o >> 4) & 15;
+      const int c32 = (c16 >> 1) ^ ks_swz<GT>(kr);
+      const int col = min(r0 + c32 * 16 + (c16 & 1) * 8, rmax - 8);
+      src = base + (int64_t)(k0 + kr) * ld + col;
+    }
+    __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(lds_tile + q * 1024), 16, 0, 0);
+  }
+}
+
+template <bool KSTRIDED>
+ASRX_DEV s8_t glds_frag(const unsigned char* lds_tile, int i0, int ks) {
+  const int l = threadIdx.x & 63, g = l >> 4;
+  if constexpr (!KSTRIDED) {
+    const int r = i0 + (l & 15);
+    const int c = (ks * 4 + g) ^ ((r >> 1) & 7);
+    return *(const s8_t*)(lds_tile + r * 128 + c * 16);
+  } else {
+    const bf16_t* t = (const bf16_t*)lds_tile;
+    const int i = l & 15, q = i >> 2, p = i & 3;
+    const int k1 = ks * 32 + 8 * g + q;
+    const int k2 = k1 + 4;
+    const bf16_t* a1 = t + k1 * GT + (((i0 >> 4) ^ ks_swz<GT>(k1)) << 4) + 4 * p;
+    const bf16_t* a2 = t + k2 * GT + (((i0 >> 4) ^ ks_swz<GT>(k2)) << 4) + 4 * p;
+    s4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4_t*)a1);
+    s4_t v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4_t*)a2);
+    return s8_t{v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
+  }
+}
+
+template <bool AT, bool BT>
+__global__ __launch_bounds__(256) void gemm_bf16_glds_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * 2 * GTILE_BYTES];
+  constexpr int TM = 4, TN = 4;
+  const int ntn = (g.N + GT - 1) / GT;
+  const int tile = blockIdx.x;
+  const int m0 = (tile / ntn) * GT, n0 = (tile % ntn) * GT;
+  const int split = blockIdx.y;
+  const int z = blockIdx.z;
+  const int zo = z / g.batch_inner, zi = z % g.batch_inner;
+  const bf16_t* A = (const bf16_t*)g.a + zo * g.sa_o + zi * g.sa_i;
+  const bf16_t* B = (const bf16_t*)g.b + zo * g.sb_o + zi * g.sb_i;
+  const int kbeg = split * g.k_per_split;
+  const int kend = min(g.K, kbeg + g.k_per_split);
+  const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
+  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const bool do_rs = AT && g.rowsum != nullptr && (tile % ntn) == 0 && wn == 0;
+  float rs[TM];
+#pragma unroll
+  for (int j = 0; j < TM; ++j) rs[j] = 0.f;
+
+  f4_t acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+    glds_stage<AT>(lds, A, g.lda, m0, g.M, kbeg);
+    glds_stage<BT>(lds + GTILE_BYTES, B, g.ldb, n0, g.N, kbeg);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    unsigned char* la = lds + cur * 2 * GTILE_BYTES;
+    unsigned char* lb = la + GTILE_BYTES;
+    if (kt + 1 < nk) {
+      unsigned char* na = lds + (cur ^ 1) * 2 * GTILE_BYTES;
+      glds_stage<AT>(na, A, g.lda, m0, g.M, kbeg + (kt + 1) * BK);
+      glds_stage<BT>(na + GTILE_BYTES, B, g.ldb, n0, g.N, kbeg + (kt + 1) * BK);
+    }
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      s8_t fa[TM], fb[TN];
+#pragma unroll
+      for (int j = 0; j < TM; ++j) fa[j] = glds_frag<AT>(la, wm + 16 * j, ks);
+#pragma unroll
+      for (int i = 0; i < TN; ++i) fb[i] = glds_frag<BT>(lb, wn + 16 * i, ks);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (do_rs) {
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) rs[j] += bf2f((bf16_t)fa[j][e]);
+      }
+    }
+    __syncthreads();
+  }
+
+  if constexpr (AT) {
+    if (do_rs) {
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        float v = rs[j];
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        const int m = m0 + wm + 16 * j + l;
+        if (l < 16 && m < g.M) {
+          if (g.splitk > 1) g.rowsum_ws[(int64_t)split * g.M + m] = v;
+          else g.rowsum[m] += v;
+        }
+      }
+    }
+  }
+  const int gq = l >> 4;
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int m = m0 + wm + 16 * j + (l & 15);
+      const int n = n0 + wn + 16 * i + 4 * gq;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (g.splitk > 1) store_partial4(g, split, m, n, v);
+      else epilogue4(g, z, m, n, v);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // fp32 kernel (exact fp32 MFMA; parity path)
 // ------------------------------------------------------------------------------------------------
 constexpr int FBM = 64, FBN = 64, FBK = 16, FSTRIDE = 64 + 16;
@@ -536,8 +691,22 @@ extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
     const int kb = (d->k + BK - 1) / BK;
     g.splitk = splitk;
     g.k_per_split = ((kb + splitk - 1) / splitk) * BK;
-    if (tile == 128) dispatch_bf16<128, 128>(g, d->a_trans, d->b_trans, vec, batch, st);
-    else dispatch_bf16<64, 64>(g, d->a_trans, d->b_trans, vec, batch, st);
+    const char* genv = getenv("ASRX_GEMM_GLDS");   // A/B switch for benchmarking (default on)
+    const int glds_on = genv ? atoi(genv) : 1;
+    const bool glds_ok = glds_on && tile == 128 && vec && d->k % BK == 0 && (!d->a_trans || d->m % 8 == 0) &&
+                         (!d->b_trans || d->n % 8 == 0) && d->m >= 8 && d->n >= 8;
+    if (glds_ok) {
+      const int ntiles = ((d->m + GT - 1) / GT) * ((d->n + GT - 1) / GT);
+      dim3 grid(ntiles, splitk, batch);
+      if (!d->a_trans && !d->b_trans) hipLaunchKernelGGL((gemm_bf16_glds_kernel<false, false>), grid, dim3(256), 0, st, g);
+      else if (!d->a_trans && d->b_trans) hipLaunchKernelGGL((gemm_bf16_glds_kernel<false, true>), grid, dim3(256), 0, st, g);
+      else if (d->a_trans && !d->b_trans) hipLaunchKernelGGL((gemm_bf16_glds_kernel<true, false>), grid, dim3(256), 0, st, g);
+      else hipLaunchKernelGGL((gemm_bf16_glds_kernel<true, true>), grid, dim3(256), 0, st, g);
+    } else if (tile == 128) {
+      dispatch_bf16<128, 128>(g, d->a_trans, d->b_trans, vec, batch, st);
+    } else {
+      dispatch_bf16<64, 64>(g, d->a_trans, d->b_trans, vec, batch, st);
+    }
   } else {
     const int vec = (d->lda % 4 == 0) && (d->ldb % 4 == 0) && ((uintptr_t)d->a % 16 == 0) &&
                     ((uintptr_t)d->b % 16 == 0) && (d->sa_outer % 4 == 0) && (d->sa_inner % 4 == 0) &&

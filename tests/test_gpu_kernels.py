@@ -33,17 +33,20 @@ def bf(x):
 
 # ------------------------------------------------------------------------------------------------ GEMM
 
+@pytest.mark.parametrize("tile", [0, 128])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("at,bt", [(False, False), (False, True), (True, False), (True, True)])
-@pytest.mark.parametrize("m,n,k", [(200, 136, 96), (1000, 250, 64), (129, 64, 576), (64, 1536, 512), (33, 17, 40)])
-def test_gemm_layouts(dtype, at, bt, m, n, k):
+@pytest.mark.parametrize("m,n,k", [(200, 136, 96), (1000, 250, 64), (129, 64, 576), (64, 1536, 512), (33, 17, 40),
+                                   (264, 392, 1216)])
+def test_gemm_layouts(dtype, at, bt, m, n, k, tile):
     g = torch.Generator(device="cpu").manual_seed(m * 7 + n * 3 + k)
     A = torch.randn(m, k, generator=g)
     B = torch.randn(n, k, generator=g)
     Ad = (A.t().contiguous() if at else A).to(dev, dtype)
     Bd = (B.t().contiguous() if bt else B).to(dev, dtype)
     C = torch.empty(m, n, device=dev, dtype=torch.float32)
-    K().gemm(Ad, Bd, C, m, n, k, lda=Ad.stride(0), ldb=Bd.stride(0), ldc=n, a_trans=at, b_trans=bt)
+    K().gemm(Ad, Bd, C, m, n, k, lda=Ad.stride(0), ldb=Bd.stride(0), ldc=n, a_trans=at, b_trans=bt,
+             tile=tile if dtype == torch.bfloat16 else 0)
     ref = A.to(dtype).double() @ B.to(dtype).double().t()
     tol = 1e-5 if dtype == torch.float32 else 2e-3
     assert relerr(C.cpu(), ref) < tol
@@ -82,6 +85,21 @@ def test_gemm_beta_splitk_and_bf16_out():
     Cb = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
     K().gemm(bf(A).to(dev), bf(B).to(dev), Cb, m, n, k, lda=m, ldb=n, ldc=n, a_trans=True, b_trans=True)
     assert relerr(Cb.float().cpu(), ref - C0.double()) < 1e-2
+
+
+@pytest.mark.parametrize("tile,splitk", [(64, 1), (128, 1), (64, 5), (128, 7)])
+def test_gemm_fused_rowsum(tile, splitk):
+    """wgrad GEMM dW = dY^T X with the bias gradient (row sums of dY^T) fused into the staging/fragments."""
+    rows, n_out, k_in = 2048, 384, 256
+    g = torch.Generator().manual_seed(tile + splitk)
+    dy = bf(torch.randn(rows, n_out, generator=g))
+    x = bf(torch.randn(rows, k_in, generator=g))
+    wg = torch.ones(n_out, k_in, device=dev)
+    bg = torch.full((n_out,), 2.0, device=dev)
+    K().gemm(dy.to(dev), x.to(dev), wg, n_out, k_in, rows, lda=n_out, ldb=k_in, ldc=k_in, a_trans=True,
+             b_trans=True, beta=1.0, tile=tile, splitk=splitk, rowsum=bg)
+    assert relerr(wg.cpu(), 1 + dy.double().t() @ x.double()) < 2e-3
+    assert relerr(bg.cpu(), 2 + dy.double().sum(0)) < 1e-5
 
 
 def test_gemm_batched_heads():
