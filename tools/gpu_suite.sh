@@ -16,6 +16,11 @@ run() {
   if [ "$rc" -ge 124 ]; then echo "FATAL: $name rc=$rc — stopping"; exit "$rc"; fi
   return 0
 }
+# refuse to run with a stale libasrx.so (sources newer than the library)
+LIB=asr-transformer_amd/asrx/lib/libasrx.so
+for src in asr-transformer_amd/csrc/* include/asrx.h; do
+  if [ "$src" -nt "$LIB" ]; then echo "STALE LIBRARY: $src is newer than $LIB"; exit 3; fi
+done
 for step in "$@"; do
   case "$step" in
     kernels) run kernels 900 python -m pytest tests/test_gpu_kernels.py -q -m gpu -rf --timeout=400 ;;
