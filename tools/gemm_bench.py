@@ -41,10 +41,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--variants", default="1,0")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--only", default="", help="comma-separated shape names")
     args = ap.parse_args()
     variants = args.variants.split(",")
     results = {}
     for name, M, N, Kd, kind in SHAPES:
+        if args.only and name not in args.only.split(","):
+            continue
         g = torch.Generator(device="cuda").manual_seed(0)
         if kind == "fwd":
             x = torch.randn(M, Kd, device="cuda", generator=g).bfloat16()
