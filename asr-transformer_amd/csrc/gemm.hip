@@ -12,6 +12,7 @@
 //
 // Replaces the reference's nn.Linear / aten::addmm and aten::bmm calls (layers.py:10-12,16-18,20,27,36,48,51;
 // model.py:32,102) and, through im2col, the conv2 of the front-end (model.py:168-171).
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.h"
@@ -378,13 +379,80 @@ ASRX_DEV s8_t glds_frag(const unsigned char* lds_tile, int i0, int ks) {
   }
 }
 
-template <bool AT, bool BT>
-__global__ __launch_bounds__(256) void gemm_bf16_glds_kernel(GemmArgs g) {
+// Compile-time epilogue flags: the projection GEMMs of the training step use a handful of fixed epilogues;
+// specialising them removes the per-element runtime branches of epilogue4 (the generic fallback).
+enum : int {
+  E_BIAS = 1, E_RELU = 2, E_DROP = 4, E_GATE = 8, E_RESID = 16, E_BETA = 32, E_F32 = 64, E_ALPHA = 128,
+  E_ROWADD = 256, E_GENERIC = 1 << 30
+};
+
+template <int EPI>
+ASRX_DEV void epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int wn, f4_t (&acc)[4][4]) {
+  const int l = threadIdx.x & 63, gq = l >> 4;
+  if constexpr (EPI == E_GENERIC) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        epilogue4(g, z, m0 + wm + 16 * j + (l & 15), n0 + wn + 16 * i + 4 * gq, v);
+      }
+  } else {
+    // fast path (host-checked): batch 1, N % 4 == 0, 16-B aligned rows; gate bf16, resid fp32
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = n0 + wn + 16 * i + 4 * gq;
+      if (n >= g.N) continue;
+      f4_t b4 = f4_t{0.f, 0.f, 0.f, 0.f};
+      if constexpr ((EPI & E_BIAS) != 0) b4 = *(const f4_t*)(g.bias + n);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = m0 + wm + 16 * j + (l & 15);
+        if (m >= g.M) continue;
+        f4_t v = acc[i][j];
+        if constexpr ((EPI & E_ALPHA) != 0) v *= g.alpha;
+        if constexpr ((EPI & E_BIAS) != 0) v += b4;
+        if constexpr ((EPI & E_ROWADD) != 0) v += *(const f4_t*)(g.rowadd + (int64_t)(m % g.rowadd_mod) * g.ld_rowadd + n);
+        if constexpr ((EPI & E_RELU) != 0) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
+        if constexpr ((EPI & E_DROP) != 0) {
+          const uint32_t base = (uint32_t)((int64_t)m * g.N + n);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = rng_keep(g.seed, base + e, g.drop_thr) ? v[e] * g.drop_scale : 0.f;
+        }
+        if constexpr ((EPI & E_GATE) != 0) {
+          const uint2 gt = *(const uint2*)((const bf16_t*)g.gate + (int64_t)m * g.ld_gate + n);
+          if (!(bf2f(gt.x & 0xffff) > 0.f)) v[0] = 0.f;
+          if (!(bf2f(gt.x >> 16) > 0.f)) v[1] = 0.f;
+          if (!(bf2f(gt.y & 0xffff) > 0.f)) v[2] = 0.f;
+          if (!(bf2f(gt.y >> 16) > 0.f)) v[3] = 0.f;
+        }
+        if constexpr ((EPI & E_RESID) != 0) v += *(const f4_t*)((const float*)g.resid + (int64_t)m * g.ld_resid + n);
+        if constexpr ((EPI & E_F32) != 0) {
+          f4_t* c = (f4_t*)((float*)g.c + (int64_t)m * g.ldc + n);
+          if constexpr ((EPI & E_BETA) != 0) v += *c;
+          *c = v;
+        } else {
+          uint2 u;
+          u.x = pack2bf(v[0], v[1]);
+          u.y = pack2bf(v[2], v[3]);
+          *(uint2*)((bf16_t*)g.c + (int64_t)m * g.ldc + n) = u;
+        }
+      }
+    }
+  }
+}
+
+// Persistent over output tiles: each workgroup walks tiles blockIdx.x, +gridDim.x, ... and issues the NEXT
+// (tile, k-step) stage — across tile boundaries too — before computing the current one, so the first stage
+// of a tile loads while the previous tile's epilogue runs.
+template <bool AT, bool BT, int EPI>
+__global__ __launch_bounds__(256) void gemm_bf16_glds_kernel(GemmArgs g, int ntiles) {
   __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * 2 * GTILE_BYTES];
   constexpr int TM = 4, TN = 4;
   const int ntn = (g.N + GT - 1) / GT;
-  const int tile = blockIdx.x;
-  const int m0 = (tile / ntn) * GT, n0 = (tile % ntn) * GT;
   const int split = blockIdx.y;
   const int z = blockIdx.z;
   const int zo = z / g.batch_inner, zi = z % g.batch_inner;
@@ -393,33 +461,37 @@ __global__ __launch_bounds__(256) void gemm_bf16_glds_kernel(GemmArgs g) {
   const int kbeg = split * g.k_per_split;
   const int kend = min(g.K, kbeg + g.k_per_split);
   const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
+  int t = blockIdx.x;
+  if (t >= ntiles || nk == 0) return;
   const int wave = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
-  const bool do_rs = AT && g.rowsum != nullptr && (tile % ntn) == 0 && wn == 0;
-  float rs[TM];
-#pragma unroll
-  for (int j = 0; j < TM; ++j) rs[j] = 0.f;
+
+  auto stage = [&](int buf, int tt, int kk) {
+    unsigned char* base = lds + buf * 2 * GTILE_BYTES;
+    glds_stage<AT>(base, A, g.lda, (tt / ntn) * GT, g.M, kbeg + kk * BK);
+    glds_stage<BT>(base + GTILE_BYTES, B, g.ldb, (tt % ntn) * GT, g.N, kbeg + kk * BK);
+  };
 
   f4_t acc[TN][TM];
 #pragma unroll
   for (int i = 0; i < TN; ++i)
 #pragma unroll
     for (int j = 0; j < TM; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+  float rs[TM];
+#pragma unroll
+  for (int j = 0; j < TM; ++j) rs[j] = 0.f;
 
-  if (nk > 0) {
-    glds_stage<AT>(lds, A, g.lda, m0, g.M, kbeg);
-    glds_stage<BT>(lds + GTILE_BYTES, B, g.ldb, n0, g.N, kbeg);
-  }
+  stage(0, t, 0);
   __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    unsigned char* la = lds + cur * 2 * GTILE_BYTES;
-    unsigned char* lb = la + GTILE_BYTES;
-    if (kt + 1 < nk) {
-      unsigned char* na = lds + (cur ^ 1) * 2 * GTILE_BYTES;
-      glds_stage<AT>(na, A, g.lda, m0, g.M, kbeg + (kt + 1) * BK);
-      glds_stage<BT>(na + GTILE_BYTES, B, g.ldb, n0, g.N, kbeg + (kt + 1) * BK);
-    }
+  int kt = 0, cur = 0;
+  while (true) {
+    int nt = t, nkt = kt + 1;
+    if (nkt == nk) { nt = t + gridDim.x; nkt = 0; }
+    const bool has_next = nt < ntiles;
+    if (has_next) stage(cur ^ 1, nt, nkt);
+    const unsigned char* la = lds + cur * 2 * GTILE_BYTES;
+    const unsigned char* lb = la + GTILE_BYTES;
+    const bool do_rs = AT && g.rowsum != nullptr && (t % ntn) == 0 && wn == 0;
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
       s8_t fa[TM], fb[TN];
@@ -433,42 +505,84 @@ __global__ __launch_bounds__(256) void gemm_bf16_glds_kernel(GemmArgs g) {
 #pragma unroll
         for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
-      if (do_rs) {
+      if constexpr (AT) {
+        if (do_rs) {
 #pragma unroll
-        for (int j = 0; j < TM; ++j)
+          for (int j = 0; j < TM; ++j)
 #pragma unroll
-          for (int e = 0; e < 8; ++e) rs[j] += bf2f((bf16_t)fa[j][e]);
-      }
-    }
-    __syncthreads();
-  }
-
-  if constexpr (AT) {
-    if (do_rs) {
-#pragma unroll
-      for (int j = 0; j < TM; ++j) {
-        float v = rs[j];
-        v += __shfl_xor(v, 16, 64);
-        v += __shfl_xor(v, 32, 64);
-        const int m = m0 + wm + 16 * j + l;
-        if (l < 16 && m < g.M) {
-          if (g.splitk > 1) g.rowsum_ws[(int64_t)split * g.M + m] = v;
-          else g.rowsum[m] += v;
+            for (int e = 0; e < 8; ++e) rs[j] += bf2f((bf16_t)fa[j][e]);
         }
       }
     }
-  }
-  const int gq = l >> 4;
+    if (kt == nk - 1) {
+      const int m0 = (t / ntn) * GT, n0 = (t % ntn) * GT;
+      if constexpr (AT) {
+        if (do_rs) {
 #pragma unroll
-  for (int i = 0; i < TN; ++i)
+          for (int j = 0; j < TM; ++j) {
+            float v = rs[j];
+            v += __shfl_xor(v, 16, 64);
+            v += __shfl_xor(v, 32, 64);
+            const int m = m0 + wm + 16 * j + l;
+            if (l < 16 && m < g.M) {
+              if (g.splitk > 1) g.rowsum_ws[(int64_t)split * g.M + m] = v;
+              else g.rowsum[m] += v;
+            }
+            rs[j] = 0.f;
+          }
+        }
+      }
+      if (g.splitk > 1) {
+        const int gq = l >> 4;
 #pragma unroll
-    for (int j = 0; j < TM; ++j) {
-      const int m = m0 + wm + 16 * j + (l & 15);
-      const int n = n0 + wn + 16 * i + 4 * gq;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (g.splitk > 1) store_partial4(g, split, m, n, v);
-      else epilogue4(g, z, m, n, v);
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int j = 0; j < TM; ++j) {
+            float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+            store_partial4(g, split, m0 + wm + 16 * j + (l & 15), n0 + wn + 16 * i + 4 * gq, v);
+          }
+      } else {
+        epilogue_tile<EPI>(g, z, m0, n0, wm, wn, acc);
+      }
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
     }
+    __syncthreads();
+    if (!has_next) break;
+    t = nt;
+    kt = nkt;
+    cur ^= 1;
+  }
+}
+
+template <bool AT, bool BT, int EPI>
+void launch_glds(const GemmArgs& g, int ntiles, int splitk, int batch, hipStream_t st) {
+  const int per = splitk * batch;
+  const int gx = std::max(1, std::min(ntiles, std::max(1, 512 / per)));
+  hipLaunchKernelGGL((gemm_bf16_glds_kernel<AT, BT, EPI>), dim3(gx, splitk, batch), dim3(256), 0, st, g, ntiles);
+}
+
+// Epilogue sets instantiated per layout; anything else runs the generic epilogue.
+#define ASRX_EPI_NT(X) X(E_BIAS) X(E_BIAS | E_RELU) X(E_BIAS | E_RELU | E_DROP) X(E_BIAS | E_RESID | E_F32) \
+  X(E_BIAS | E_DROP | E_RESID | E_F32) X(E_F32) X(E_BIAS | E_ROWADD | E_F32) X(0)
+#define ASRX_EPI_NN(X) X(0) X(E_GATE) X(E_GATE | E_ALPHA) X(E_F32)
+#define ASRX_EPI_TT(X) X(E_BETA | E_F32) X(E_F32)
+
+template <bool AT, bool BT>
+void dispatch_glds(const GemmArgs& g, int epi, int ntiles, int splitk, int batch, hipStream_t st) {
+#define ASRX_CASE(E) \
+  case (E): launch_glds<AT, BT, (E)>(g, ntiles, splitk, batch, st); return;
+  if constexpr (!AT && !BT) {
+    switch (epi) { ASRX_EPI_NT(ASRX_CASE) default: break; }
+  } else if constexpr (!AT && BT) {
+    switch (epi) { ASRX_EPI_NN(ASRX_CASE) default: break; }
+  } else if constexpr (AT && BT) {
+    switch (epi) { ASRX_EPI_TT(ASRX_CASE) default: break; }
+  }
+#undef ASRX_CASE
+  launch_glds<AT, BT, E_GENERIC>(g, ntiles, splitk, batch, st);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -697,11 +811,23 @@ extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
                          (!d->b_trans || d->n % 8 == 0) && d->m >= 8 && d->n >= 8;
     if (glds_ok) {
       const int ntiles = ((d->m + GT - 1) / GT) * ((d->n + GT - 1) / GT);
-      dim3 grid(ntiles, splitk, batch);
-      if (!d->a_trans && !d->b_trans) hipLaunchKernelGGL((gemm_bf16_glds_kernel<false, false>), grid, dim3(256), 0, st, g);
-      else if (!d->a_trans && d->b_trans) hipLaunchKernelGGL((gemm_bf16_glds_kernel<false, true>), grid, dim3(256), 0, st, g);
-      else if (d->a_trans && !d->b_trans) hipLaunchKernelGGL((gemm_bf16_glds_kernel<true, false>), grid, dim3(256), 0, st, g);
-      else hipLaunchKernelGGL((gemm_bf16_glds_kernel<true, true>), grid, dim3(256), 0, st, g);
+      // compile-time epilogue selection (fast path preconditions, else generic)
+      int epi = E_GENERIC;
+      const bool fast = batch == 1 && splitk == 1 && d->n % 4 == 0 && g.cvec && d->ldc % 4 == 0 &&
+                        (!d->bias || (uintptr_t)d->bias % 16 == 0) &&
+                        (!d->rowadd || (d->ld_rowadd % 4 == 0 && (uintptr_t)d->rowadd % 16 == 0)) &&
+                        (!d->gate || (d->gate_dtype == ASRX_BF16 && d->ld_gate % 4 == 0 && (uintptr_t)d->gate % 8 == 0)) &&
+                        (!d->resid || (d->resid_dtype == ASRX_F32 && d->ld_resid % 4 == 0 && (uintptr_t)d->resid % 16 == 0)) &&
+                        (d->beta == 0.f || (d->beta == 1.f && d->c_dtype == ASRX_F32));
+      if (fast) {
+        epi = (d->bias ? E_BIAS : 0) | (d->relu ? E_RELU : 0) | (g.drop_thr ? E_DROP : 0) | (d->gate ? E_GATE : 0) |
+              (d->resid ? E_RESID : 0) | (d->beta == 1.f ? E_BETA : 0) | (d->c_dtype == ASRX_F32 ? E_F32 : 0) |
+              (d->alpha != 1.f ? E_ALPHA : 0) | (d->rowadd ? E_ROWADD : 0);
+      }
+      if (!d->a_trans && !d->b_trans) dispatch_glds<false, false>(g, epi, ntiles, splitk, batch, st);
+      else if (!d->a_trans && d->b_trans) dispatch_glds<false, true>(g, epi, ntiles, splitk, batch, st);
+      else if (d->a_trans && !d->b_trans) dispatch_glds<true, false>(g, epi, ntiles, splitk, batch, st);
+      else dispatch_glds<true, true>(g, epi, ntiles, splitk, batch, st);
     } else if (tile == 128) {
       dispatch_bf16<128, 128>(g, d->a_trans, d->b_trans, vec, batch, st);
     } else {
