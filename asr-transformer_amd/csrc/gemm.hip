@@ -14,6 +14,7 @@
 // model.py:32,102) and, through im2col, the conv2 of the front-end (model.py:168-171).
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 
 #include "common.h"
 
@@ -586,6 +587,190 @@ void dispatch_glds(const GemmArgs& g, int epi, int ntiles, int splitk, int batch
 }
 
 // ------------------------------------------------------------------------------------------------
+// bf16 "p3" kernel: 256x128x64 tiles, 8 waves (4x2, 64x64 each), persistent, a 3-stage LDS-DMA ring
+// (3 x 48 KiB): stage s+2 is issued while stage s is computed, the wait before each K-step is a counted
+// `s_waitcnt vmcnt(P_INST)` (only the youngest stage left in flight) followed by a raw s_barrier — the
+// loads stay in flight across the barrier (a __syncthreads() would drain them).  One workgroup per CU.
+// ------------------------------------------------------------------------------------------------
+constexpr int P_BM = 256, P_BN = 128, P_THREADS = 512;
+constexpr int PA_BYTES = P_BM * BK * 2, PB_BYTES = P_BN * BK * 2, P_STAGE = PA_BYTES + PB_BYTES;
+constexpr int P_INST = (PA_BYTES + PB_BYTES) / (P_THREADS * 16);   // LDS-DMA instructions per thread per stage
+static_assert(P_INST == 6, "vmcnt literal below assumes 6 LDS-DMA instructions per stage");
+
+template <int R, bool KSTRIDED>
+ASRX_DEV void p_stage(unsigned char* img, const bf16_t* base, int64_t ld, int r0, int rmax, int k0) {
+  constexpr int NI = R * BK * 2 / (P_THREADS * 16);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int q = j * 8 + w;
+    const int o = q * 1024 + l * 16;
+    const bf16_t* src;
+    if constexpr (!KSTRIDED) {
+      const int r = o >> 7, cp = (o >> 4) & 7;
+      const int c = cp ^ ((r >> 1) & 7);
+      src = base + (int64_t)min(r0 + r, rmax - 1) * ld + k0 + c * 8;
+    } else {
+      constexpr int RB = R * 2;
+      const int kr = o / RB, c16 = (o % RB) >> 4;
+      const int c32 = (c16 >> 1) ^ ks_swz<128>(kr);
+      src = base + (int64_t)(k0 + kr) * ld + min(r0 + c32 * 16 + (c16 & 1) * 8, rmax - 8);
+    }
+    __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(img + q * 1024), 16, 0, 0);
+  }
+}
+
+template <int R, bool KSTRIDED>
+ASRX_DEV s8_t p_frag(const unsigned char* img, int i0, int ks) {
+  const int l = threadIdx.x & 63, g = l >> 4;
+  if constexpr (!KSTRIDED) {
+    const int r = i0 + (l & 15);
+    const int c = (ks * 4 + g) ^ ((r >> 1) & 7);
+    return *(const s8_t*)(img + r * 128 + c * 16);
+  } else {
+    const bf16_t* t = (const bf16_t*)img;
+    const int i = l & 15, q = i >> 2, p = i & 3;
+    const int k1 = ks * 32 + 8 * g + q;
+    const int k2 = k1 + 4;
+    const bf16_t* a1 = t + k1 * R + (((i0 >> 4) ^ ks_swz<128>(k1)) << 4) + 4 * p;
+    const bf16_t* a2 = t + k2 * R + (((i0 >> 4) ^ ks_swz<128>(k2)) << 4) + 4 * p;
+    s4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4_t*)a1);
+    s4_t v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4_t*)a2);
+    return s8_t{v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
+  }
+}
+
+template <bool AT, bool BT, int EPI>
+__global__ __launch_bounds__(512) void gemm_bf16_p3_kernel(GemmArgs g, int ntiles) {
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[3 * P_STAGE];
+  constexpr int TM = 4, TN = 4;
+  const int ntn = (g.N + P_BN - 1) / P_BN;
+  const int split = blockIdx.y;
+  const int z = blockIdx.z;
+  const int zo = z / g.batch_inner, zi = z % g.batch_inner;
+  const bf16_t* A = (const bf16_t*)g.a + zo * g.sa_o + zi * g.sa_i;
+  const bf16_t* B = (const bf16_t*)g.b + zo * g.sb_o + zi * g.sb_i;
+  const int kbeg = split * g.k_per_split;
+  const int kend = min(g.K, kbeg + g.k_per_split);
+  const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
+  const int G = gridDim.x;
+  if ((int)blockIdx.x >= ntiles || nk == 0) return;
+  const int my_tiles = (ntiles - (int)blockIdx.x + G - 1) / G;
+  const int total = my_tiles * nk;
+  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+
+  auto issue = [&](int s) {
+    const int tt = blockIdx.x + (s / nk) * G, kk = s % nk;
+    unsigned char* img = lds + (s % 3) * P_STAGE;
+    p_stage<P_BM, AT>(img, A, g.lda, (tt / ntn) * P_BM, g.M, kbeg + kk * BK);
+    p_stage<P_BN, BT>(img + PA_BYTES, B, g.ldb, (tt % ntn) * P_BN, g.N, kbeg + kk * BK);
+  };
+
+  f4_t acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+  float rs[TM];
+#pragma unroll
+  for (int j = 0; j < TM; ++j) rs[j] = 0.f;
+
+  issue(0);
+  if (total > 1) issue(1);
+  bool drain = false;
+  for (int s = 0; s < total; ++s) {
+    if (s + 1 < total && !drain) asm volatile("s_waitcnt vmcnt(6)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    drain = false;
+    if (s + 2 < total) issue(s + 2);
+    const unsigned char* la = lds + (s % 3) * P_STAGE;
+    const unsigned char* lb = la + PA_BYTES;
+    const int t = blockIdx.x + (s / nk) * G, kk = s % nk;
+    const bool do_rs = AT && g.rowsum != nullptr && (t % ntn) == 0 && wn == 0;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      s8_t fa[TM], fb[TN];
+#pragma unroll
+      for (int j = 0; j < TM; ++j) fa[j] = p_frag<P_BM, AT>(la, wm + 16 * j, ks);
+#pragma unroll
+      for (int i = 0; i < TN; ++i) fb[i] = p_frag<P_BN, BT>(lb, wn + 16 * i, ks);
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
+      if constexpr (AT) {
+        if (do_rs) {
+#pragma unroll
+          for (int j = 0; j < TM; ++j)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) rs[j] += bf2f((bf16_t)fa[j][e]);
+        }
+      }
+    }
+    if (kk == nk - 1) {
+      const int m0 = (t / ntn) * P_BM, n0 = (t % ntn) * P_BN;
+      if constexpr (AT) {
+        if (do_rs) {
+#pragma unroll
+          for (int j = 0; j < TM; ++j) {
+            float v = rs[j];
+            v += __shfl_xor(v, 16, 64);
+            v += __shfl_xor(v, 32, 64);
+            const int m = m0 + wm + 16 * j + l;
+            if (l < 16 && m < g.M) {
+              if (g.splitk > 1) g.rowsum_ws[(int64_t)split * g.M + m] = v;
+              else g.rowsum[m] += v;
+            }
+            rs[j] = 0.f;
+          }
+        }
+      }
+      if (g.splitk > 1) {
+        const int gq = l >> 4;
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int j = 0; j < TM; ++j) {
+            float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+            store_partial4(g, split, m0 + wm + 16 * j + (l & 15), n0 + wn + 16 * i + 4 * gq, v);
+          }
+      } else {
+        epilogue_tile<EPI>(g, z, m0, n0, wm, wn, acc);
+      }
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+      drain = true;
+    }
+  }
+}
+
+template <bool AT, bool BT, int EPI>
+void launch_p3(const GemmArgs& g, int ntiles, int splitk, int batch, hipStream_t st) {
+  const int per = splitk * batch;
+  const int gx = std::max(1, std::min(ntiles, std::max(1, 256 / per)));
+  hipLaunchKernelGGL((gemm_bf16_p3_kernel<AT, BT, EPI>), dim3(gx, splitk, batch), dim3(P_THREADS), 0, st, g, ntiles);
+}
+
+template <bool AT, bool BT>
+void dispatch_p3(const GemmArgs& g, int epi, int ntiles, int splitk, int batch, hipStream_t st) {
+#define ASRX_CASE(E) \
+  case (E): launch_p3<AT, BT, (E)>(g, ntiles, splitk, batch, st); return;
+  if constexpr (!AT && !BT) {
+    switch (epi) { ASRX_EPI_NT(ASRX_CASE) default: break; }
+  } else if constexpr (!AT && BT) {
+    switch (epi) { ASRX_EPI_NN(ASRX_CASE) default: break; }
+  } else if constexpr (AT && BT) {
+    switch (epi) { ASRX_EPI_TT(ASRX_CASE) default: break; }
+  }
+#undef ASRX_CASE
+  launch_p3<AT, BT, E_GENERIC>(g, ntiles, splitk, batch, st);
+}
+
+// ------------------------------------------------------------------------------------------------
 // fp32 kernel (exact fp32 MFMA; parity path)
 // ------------------------------------------------------------------------------------------------
 constexpr int FBM = 64, FBN = 64, FBK = 16, FSTRIDE = 64 + 16;
@@ -805,25 +990,38 @@ extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
     const int kb = (d->k + BK - 1) / BK;
     g.splitk = splitk;
     g.k_per_split = ((kb + splitk - 1) / splitk) * BK;
-    const char* genv = getenv("ASRX_GEMM_GLDS");   // A/B switch for benchmarking (default on)
-    const int glds_on = genv ? atoi(genv) : 1;
-    const bool glds_ok = glds_on && tile == 128 && vec && d->k % BK == 0 && (!d->a_trans || d->m % 8 == 0) &&
-                         (!d->b_trans || d->n % 8 == 0) && d->m >= 8 && d->n >= 8;
-    if (glds_ok) {
+    // kernel family: ASRX_GEMM_KERNEL = auto | p3 | glds | reg  (A/B switch for benchmarking)
+    const char* kenv = getenv("ASRX_GEMM_KERNEL");
+    const int kvar = !kenv ? 0 : (!strcmp(kenv, "p3") ? 1 : (!strcmp(kenv, "glds") ? 2 : (!strcmp(kenv, "reg") ? 3 : 0)));
+    const bool dma_ok = vec && d->k % BK == 0 && (!d->a_trans || d->m % 8 == 0) && (!d->b_trans || d->n % 8 == 0) &&
+                        d->m >= 8 && d->n >= 8;
+    const int nt_p3 = ((d->m + P_BM - 1) / P_BM) * ((d->n + P_BN - 1) / P_BN);
+    int use = 0;  // 1 = p3, 2 = glds, 0 = register path
+    if (dma_ok) {
+      if (kvar == 1) use = 1;
+      else if (kvar == 2) use = tile == 128 ? 2 : 0;
+      else if (kvar == 0) use = (nt_p3 * splitk * batch >= 192) ? 1 : (tile == 128 ? 2 : 0);
+    }
+    // compile-time epilogue selection (fast-path preconditions, else generic)
+    int epi = E_GENERIC;
+    const bool fast = batch == 1 && splitk == 1 && d->n % 4 == 0 && g.cvec && d->ldc % 4 == 0 &&
+                      (!d->bias || (uintptr_t)d->bias % 16 == 0) &&
+                      (!d->rowadd || (d->ld_rowadd % 4 == 0 && (uintptr_t)d->rowadd % 16 == 0)) &&
+                      (!d->gate || (d->gate_dtype == ASRX_BF16 && d->ld_gate % 4 == 0 && (uintptr_t)d->gate % 8 == 0)) &&
+                      (!d->resid || (d->resid_dtype == ASRX_F32 && d->ld_resid % 4 == 0 && (uintptr_t)d->resid % 16 == 0)) &&
+                      (d->beta == 0.f || (d->beta == 1.f && d->c_dtype == ASRX_F32));
+    if (fast) {
+      epi = (d->bias ? E_BIAS : 0) | (d->relu ? E_RELU : 0) | (g.drop_thr ? E_DROP : 0) | (d->gate ? E_GATE : 0) |
+            (d->resid ? E_RESID : 0) | (d->beta == 1.f ? E_BETA : 0) | (d->c_dtype == ASRX_F32 ? E_F32 : 0) |
+            (d->alpha != 1.f ? E_ALPHA : 0) | (d->rowadd ? E_ROWADD : 0);
+    }
+    if (use == 1) {
+      if (!d->a_trans && !d->b_trans) dispatch_p3<false, false>(g, epi, nt_p3, splitk, batch, st);
+      else if (!d->a_trans && d->b_trans) dispatch_p3<false, true>(g, epi, nt_p3, splitk, batch, st);
+      else if (d->a_trans && !d->b_trans) dispatch_p3<true, false>(g, epi, nt_p3, splitk, batch, st);
+      else dispatch_p3<true, true>(g, epi, nt_p3, splitk, batch, st);
+    } else if (use == 2) {
       const int ntiles = ((d->m + GT - 1) / GT) * ((d->n + GT - 1) / GT);
-      // compile-time epilogue selection (fast path preconditions, else generic)
-      int epi = E_GENERIC;
-      const bool fast = batch == 1 && splitk == 1 && d->n % 4 == 0 && g.cvec && d->ldc % 4 == 0 &&
-                        (!d->bias || (uintptr_t)d->bias % 16 == 0) &&
-                        (!d->rowadd || (d->ld_rowadd % 4 == 0 && (uintptr_t)d->rowadd % 16 == 0)) &&
-                        (!d->gate || (d->gate_dtype == ASRX_BF16 && d->ld_gate % 4 == 0 && (uintptr_t)d->gate % 8 == 0)) &&
-                        (!d->resid || (d->resid_dtype == ASRX_F32 && d->ld_resid % 4 == 0 && (uintptr_t)d->resid % 16 == 0)) &&
-                        (d->beta == 0.f || (d->beta == 1.f && d->c_dtype == ASRX_F32));
-      if (fast) {
-        epi = (d->bias ? E_BIAS : 0) | (d->relu ? E_RELU : 0) | (g.drop_thr ? E_DROP : 0) | (d->gate ? E_GATE : 0) |
-              (d->resid ? E_RESID : 0) | (d->beta == 1.f ? E_BETA : 0) | (d->c_dtype == ASRX_F32 ? E_F32 : 0) |
-              (d->alpha != 1.f ? E_ALPHA : 0) | (d->rowadd ? E_ROWADD : 0);
-      }
       if (!d->a_trans && !d->b_trans) dispatch_glds<false, false>(g, epi, ntiles, splitk, batch, st);
       else if (!d->a_trans && d->b_trans) dispatch_glds<false, true>(g, epi, ntiles, splitk, batch, st);
       else if (d->a_trans && !d->b_trans) dispatch_glds<true, false>(g, epi, ntiles, splitk, batch, st);

@@ -33,12 +33,25 @@ def bf(x):
 
 # ------------------------------------------------------------------------------------------------ GEMM
 
+@pytest.fixture
+def kernel_variant(request):
+    import os
+    old = os.environ.get("ASRX_GEMM_KERNEL")
+    os.environ["ASRX_GEMM_KERNEL"] = request.param
+    yield request.param
+    if old is None:
+        os.environ.pop("ASRX_GEMM_KERNEL", None)
+    else:
+        os.environ["ASRX_GEMM_KERNEL"] = old
+
+
+@pytest.mark.parametrize("kernel_variant", ["auto", "p3", "glds", "reg"], indirect=True)
 @pytest.mark.parametrize("tile", [0, 128])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("at,bt", [(False, False), (False, True), (True, False), (True, True)])
 @pytest.mark.parametrize("m,n,k", [(200, 136, 96), (1000, 250, 64), (129, 64, 576), (64, 1536, 512), (33, 17, 40),
                                    (264, 392, 1216)])
-def test_gemm_layouts(dtype, at, bt, m, n, k, tile):
+def test_gemm_layouts(dtype, at, bt, m, n, k, tile, kernel_variant):
     g = torch.Generator(device="cpu").manual_seed(m * 7 + n * 3 + k)
     A = torch.randn(m, k, generator=g)
     B = torch.randn(n, k, generator=g)
@@ -52,8 +65,9 @@ def test_gemm_layouts(dtype, at, bt, m, n, k, tile):
     assert relerr(C.cpu(), ref) < tol
 
 
+@pytest.mark.parametrize("kernel_variant", ["auto", "p3", "glds", "reg"], indirect=True)
 @pytest.mark.parametrize("tile", [64, 128])
-def test_gemm_epilogue(tile):
+def test_gemm_epilogue(tile, kernel_variant):
     m, n, k = 300, 192, 128
     g = torch.Generator().manual_seed(1)
     x = torch.randn(m, k, generator=g)
@@ -87,8 +101,9 @@ def test_gemm_beta_splitk_and_bf16_out():
     assert relerr(Cb.float().cpu(), ref - C0.double()) < 1e-2
 
 
+@pytest.mark.parametrize("kernel_variant", ["auto", "p3", "glds", "reg"], indirect=True)
 @pytest.mark.parametrize("tile,splitk", [(64, 1), (128, 1), (64, 5), (128, 7)])
-def test_gemm_fused_rowsum(tile, splitk):
+def test_gemm_fused_rowsum(tile, splitk, kernel_variant):
     """wgrad GEMM dW = dY^T X with the bias gradient (row sums of dY^T) fused into the staging/fragments."""
     rows, n_out, k_in = 2048, 384, 256
     g = torch.Generator().manual_seed(tile + splitk)

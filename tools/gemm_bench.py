@@ -39,7 +39,7 @@ def run_shape(M, N, Kd, kind, bufs):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="1,0")
+    ap.add_argument("--variants", default="auto,p3,glds,reg")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="", help="comma-separated shape names")
     args = ap.parse_args()
@@ -69,7 +69,7 @@ def main():
         times = {v: [] for v in variants}
         for r in range(args.reps + 2):
             for v in variants:
-                os.environ["ASRX_GEMM_GLDS"] = v
+                os.environ["ASRX_GEMM_KERNEL"] = v
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
                 run_shape(M, N, Kd, kind, bufs)
@@ -80,7 +80,7 @@ def main():
         line = f"{name:18s} M={M:6d} N={N:6d} K={Kd:6d}"
         for v in variants:
             t = sorted(times[v])[len(times[v]) // 2]
-            line += f" | v{v}: {t*1e3:8.1f}us {flops/t/1e9:7.1f}TF"
+            line += f" | {v}: {t*1e3:7.1f}us {flops/t/1e9:6.0f}TF"
             results.setdefault(v, 0.0)
             results[v] += t
         print(line, flush=True)
