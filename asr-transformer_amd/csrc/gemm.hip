@@ -640,6 +640,30 @@ ASRX_DEV s8_t p_frag(const unsigned char* img, int i0, int ks) {
   }
 }
 
+// XCD-aware persistent schedule (speed only, never correctness): workgroups b and b+8 share an XCD under
+// the observed round-robin placement, so row-block tm is owned by the workgroups with b % 8 == tm % 8 and
+// the ~ntn tiles that re-read its A rows hit that XCD's L2 instead of refetching from MALL/HBM per XCD.
+struct TileSched {
+  int x, r, gx, nrx, ntn, ntm, G, plain;
+  ASRX_DEV TileSched(int b, int G_, int ntm_, int ntn_) : G(G_), ntn(ntn_), ntm(ntm_) {
+    plain = ntm_ < 8 || G_ < 8;
+    x = b % 8;
+    r = b / 8;
+    gx = (G_ - x + 7) / 8;
+    nrx = x < ntm_ ? (ntm_ - x + 7) / 8 : 0;
+  }
+  ASRX_DEV int count(int b) const {
+    if (plain) { const int nt = ntm * ntn; return b < nt ? (nt - b + G - 1) / G : 0; }
+    const int L = nrx * ntn;
+    return r < L ? (L - r + gx - 1) / gx : 0;
+  }
+  ASRX_DEV int tile(int b, int i) const {   // i-th tile of workgroup b
+    if (plain) return b + i * G;
+    const int idx = r + i * gx;
+    return (x + 8 * (idx / ntn)) * ntn + idx % ntn;
+  }
+};
+
 template <bool AT, bool BT, int EPI>
 __global__ __launch_bounds__(512) void gemm_bf16_p3_kernel(GemmArgs g, int ntiles) {
   __shared__ __attribute__((aligned(1024))) unsigned char lds[3 * P_STAGE];
@@ -654,14 +678,15 @@ __global__ __launch_bounds__(512) void gemm_bf16_p3_kernel(GemmArgs g, int ntile
   const int kend = min(g.K, kbeg + g.k_per_split);
   const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
   const int G = gridDim.x;
-  if ((int)blockIdx.x >= ntiles || nk == 0) return;
-  const int my_tiles = (ntiles - (int)blockIdx.x + G - 1) / G;
+  const TileSched sched((int)blockIdx.x, G, (g.M + P_BM - 1) / P_BM, ntn);
+  const int my_tiles = sched.count((int)blockIdx.x);
+  if (my_tiles == 0 || nk == 0) return;
   const int total = my_tiles * nk;
   const int wave = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
 
   auto issue = [&](int s) {
-    const int tt = blockIdx.x + (s / nk) * G, kk = s % nk;
+    const int tt = sched.tile((int)blockIdx.x, s / nk), kk = s % nk;
     unsigned char* img = lds + (s % 3) * P_STAGE;
     p_stage<P_BM, AT>(img, A, g.lda, (tt / ntn) * P_BM, g.M, kbeg + kk * BK);
     p_stage<P_BN, BT>(img + PA_BYTES, B, g.ldb, (tt % ntn) * P_BN, g.N, kbeg + kk * BK);
@@ -687,7 +712,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_p3_kernel(GemmArgs g, int ntile
     if (s + 2 < total) issue(s + 2);
     const unsigned char* la = lds + (s % 3) * P_STAGE;
     const unsigned char* lb = la + PA_BYTES;
-    const int t = blockIdx.x + (s / nk) * G, kk = s % nk;
+    const int t = sched.tile((int)blockIdx.x, s / nk), kk = s % nk;
     const bool do_rs = AT && g.rowsum != nullptr && (t % ntn) == 0 && wn == 0;
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
