@@ -645,8 +645,11 @@ ASRX_DEV s8_t p_frag(const unsigned char* img, int i0, int ks) {
 // the ~ntn tiles that re-read its A rows hit that XCD's L2 instead of refetching from MALL/HBM per XCD.
 struct TileSched {
   int x, r, gx, nrx, ntn, ntm, G, plain;
-  ASRX_DEV TileSched(int b, int G_, int ntm_, int ntn_) : G(G_), ntn(ntn_), ntm(ntm_) {
-    plain = ntm_ < 8 || G_ < 8;
+  // Measured on MI355X: the XCD-owned order was 10-50% SLOWER than the plain order on every c3 shape
+  // (concurrent tiles hammer the same L2 lines; the plain order spreads the A row-blocks over MALL), so it
+  // is off by default (ASRX_XCD_SCHED=1 enables it for experiments).
+  ASRX_DEV TileSched(int b, int G_, int ntm_, int ntn_, int xcd_on = 0) : G(G_), ntn(ntn_), ntm(ntm_) {
+    plain = !xcd_on || ntm_ < 8 || G_ < 8;
     x = b % 8;
     r = b / 8;
     gx = (G_ - x + 7) / 8;
