@@ -597,28 +597,42 @@ constexpr int PA_BYTES = P_BM * BK * 2, PB_BYTES = P_BN * BK * 2, P_STAGE = PA_B
 constexpr int P_INST = (PA_BYTES + PB_BYTES) / (P_THREADS * 16);   // LDS-DMA instructions per thread per stage
 static_assert(P_INST == 6, "vmcnt literal below assumes 6 LDS-DMA instructions per stage");
 
+// Per-operand staging state for the p3 kernel: the per-lane byte offsets of its LDS-DMA pieces are computed
+// once per tile; each stage builds one wave-uniform buffer descriptor (SALU only) whose base is advanced to
+// the stage's k0 and whose record count ends at the operand's last valid byte, so rows/cols past M/N read
+// as 0 through the hardware range check (no clamps, no per-stage 64-bit VALU address math).
 template <int R, bool KSTRIDED>
-ASRX_DEV void p_stage(unsigned char* img, const bf16_t* base, int64_t ld, int r0, int rmax, int k0) {
-  constexpr int NI = R * BK * 2 / (P_THREADS * 16);
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+struct PStage {
+  static constexpr int NI = R * BK * 2 / (P_THREADS * 16);
+  uint32_t voff[NI];
+  ASRX_DEV void set_tile(int r0, int64_t ld) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
 #pragma unroll
-  for (int j = 0; j < NI; ++j) {
-    const int q = j * 8 + w;
-    const int o = q * 1024 + l * 16;
-    const bf16_t* src;
-    if constexpr (!KSTRIDED) {
-      const int r = o >> 7, cp = (o >> 4) & 7;
-      const int c = cp ^ ((r >> 1) & 7);
-      src = base + (int64_t)min(r0 + r, rmax - 1) * ld + k0 + c * 8;
-    } else {
-      constexpr int RB = R * 2;
-      const int kr = o / RB, c16 = (o % RB) >> 4;
-      const int c32 = (c16 >> 1) ^ ks_swz<128>(kr);
-      src = base + (int64_t)(k0 + kr) * ld + min(r0 + c32 * 16 + (c16 & 1) * 8, rmax - 8);
+    for (int j = 0; j < NI; ++j) {
+      const int o = (j * 8 + w) * 1024 + l * 16;
+      if constexpr (!KSTRIDED) {
+        const int r = o >> 7, c = ((o >> 4) & 7) ^ ((r >> 1) & 7);
+        voff[j] = (uint32_t)(((int64_t)(r0 + r) * ld + c * 8) * 2);
+      } else {
+        constexpr int RB = R * 2;
+        const int kr = o / RB, c16 = (o % RB) >> 4;
+        const int c32 = (c16 >> 1) ^ ks_swz<128>(kr);
+        voff[j] = (uint32_t)(((int64_t)kr * ld + r0 + c32 * 16 + (c16 & 1) * 8) * 2);
+      }
     }
-    __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(img + q * 1024), 16, 0, 0);
   }
-}
+  // base: operand start; total_bytes: one past its last valid byte; k0: first k of the stage
+  ASRX_DEV void issue(unsigned char* img, const bf16_t* base, int64_t ld, int64_t total_bytes, int k0) const {
+    const int64_t koff = KSTRIDED ? (int64_t)k0 * ld * 2 : (int64_t)k0 * 2;
+    const int64_t rem = total_bytes - koff;
+    __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const char*)base + koff), (short)0, (int)(rem > 0x7fffffff ? 0x7fffffff : rem), 0x00020000);
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_t*)(img + (j * 8 + w) * 1024), 16, voff[j], 0, 0, 0);
+  }
+};
 
 template <int R, bool KSTRIDED>
 ASRX_DEV s8_t p_frag(const unsigned char* img, int i0, int ks) {
@@ -640,32 +654,8 @@ ASRX_DEV s8_t p_frag(const unsigned char* img, int i0, int ks) {
   }
 }
 
-// XCD-aware persistent schedule (speed only, never correctness): workgroups b and b+8 share an XCD under
-// the observed round-robin placement, so row-block tm is owned by the workgroups with b % 8 == tm % 8 and
-// the ~ntn tiles that re-read its A rows hit that XCD's L2 instead of refetching from MALL/HBM per XCD.
-struct TileSched {
-  int x, r, gx, nrx, ntn, ntm, G, plain;
-  // Measured on MI355X: the XCD-owned order was 10-50% SLOWER than the plain order on every c3 shape
-  // (concurrent tiles hammer the same L2 lines; the plain order spreads the A row-blocks over MALL), so it
-  // is off by default (ASRX_XCD_SCHED=1 enables it for experiments).
-  ASRX_DEV TileSched(int b, int G_, int ntm_, int ntn_, int xcd_on = 0) : G(G_), ntn(ntn_), ntm(ntm_) {
-    plain = !xcd_on || ntm_ < 8 || G_ < 8;
-    x = b % 8;
-    r = b / 8;
-    gx = (G_ - x + 7) / 8;
-    nrx = x < ntm_ ? (ntm_ - x + 7) / 8 : 0;
-  }
-  ASRX_DEV int count(int b) const {
-    if (plain) { const int nt = ntm * ntn; return b < nt ? (nt - b + G - 1) / G : 0; }
-    const int L = nrx * ntn;
-    return r < L ? (L - r + gx - 1) / gx : 0;
-  }
-  ASRX_DEV int tile(int b, int i) const {   // i-th tile of workgroup b
-    if (plain) return b + i * G;
-    const int idx = r + i * gx;
-    return (x + 8 * (idx / ntn)) * ntn + idx % ntn;
-  }
-};
+// (An XCD-owned tile order — row-block tm served by the workgroups with b % 8 == tm % 8 — was measured
+// 10-50% SLOWER than this plain round-robin order on every c3 shape and was removed.)
 
 template <bool AT, bool BT, int EPI>
 __global__ __launch_bounds__(512) void gemm_bf16_p3_kernel(GemmArgs g, int ntiles) {
@@ -677,22 +667,33 @@ __global__ __launch_bounds__(512) void gemm_bf16_p3_kernel(GemmArgs g, int ntile
   const int zo = z / g.batch_inner, zi = z % g.batch_inner;
   const bf16_t* A = (const bf16_t*)g.a + zo * g.sa_o + zi * g.sa_i;
   const bf16_t* B = (const bf16_t*)g.b + zo * g.sb_o + zi * g.sb_i;
+  // one past the last valid byte of each operand (A: M rows x K, or K rows x M when k-strided)
+  const int64_t a_bytes = AT ? ((int64_t)(g.K - 1) * g.lda + g.M) * 2 : ((int64_t)(g.M - 1) * g.lda + g.K) * 2;
+  const int64_t b_bytes = BT ? ((int64_t)(g.K - 1) * g.ldb + g.N) * 2 : ((int64_t)(g.N - 1) * g.ldb + g.K) * 2;
   const int kbeg = split * g.k_per_split;
   const int kend = min(g.K, kbeg + g.k_per_split);
   const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
   const int G = gridDim.x;
-  const TileSched sched((int)blockIdx.x, G, (g.M + P_BM - 1) / P_BM, ntn);
-  const int my_tiles = sched.count((int)blockIdx.x);
-  if (my_tiles == 0 || nk == 0) return;
-  const int total = my_tiles * nk;
+  const int b0 = blockIdx.x;
+  if (b0 >= ntiles || nk == 0) return;
+  const int total = ((ntiles - b0 + G - 1) / G) * nk;
   const int wave = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
 
-  auto issue = [&](int s) {
-    const int tt = sched.tile((int)blockIdx.x, s / nk), kk = s % nk;
-    unsigned char* img = lds + (s % 3) * P_STAGE;
-    p_stage<P_BM, AT>(img, A, g.lda, (tt / ntn) * P_BM, g.M, kbeg + kk * BK);
-    p_stage<P_BN, BT>(img + PA_BYTES, B, g.ldb, (tt % ntn) * P_BN, g.N, kbeg + kk * BK);
+  PStage<P_BM, AT> sa;
+  PStage<P_BN, BT> sb;
+  // issue cursor (runs two steps ahead of the compute cursor)
+  int it = b0, ik = 0, ib = 0;
+  auto issue_next = [&]() {
+    if (ik == 0) {
+      sa.set_tile((it / ntn) * P_BM, g.lda);
+      sb.set_tile((it % ntn) * P_BN, g.ldb);
+    }
+    unsigned char* img = lds + ib * P_STAGE;
+    sa.issue(img, A, g.lda, a_bytes, kbeg + ik * BK);
+    sb.issue(img + PA_BYTES, B, g.ldb, b_bytes, kbeg + ik * BK);
+    if (++ik == nk) { ik = 0; it += G; }
+    ib = ib == 2 ? 0 : ib + 1;
   };
 
   f4_t acc[TN][TM];
@@ -704,18 +705,18 @@ __global__ __launch_bounds__(512) void gemm_bf16_p3_kernel(GemmArgs g, int ntile
 #pragma unroll
   for (int j = 0; j < TM; ++j) rs[j] = 0.f;
 
-  issue(0);
-  if (total > 1) issue(1);
+  issue_next();
+  if (total > 1) issue_next();
   bool drain = false;
+  int t = b0, kk = 0, cb = 0;   // compute cursor
   for (int s = 0; s < total; ++s) {
     if (s + 1 < total && !drain) asm volatile("s_waitcnt vmcnt(6)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     drain = false;
-    if (s + 2 < total) issue(s + 2);
-    const unsigned char* la = lds + (s % 3) * P_STAGE;
+    if (s + 2 < total) issue_next();
+    const unsigned char* la = lds + cb * P_STAGE;
     const unsigned char* lb = la + PA_BYTES;
-    const int t = sched.tile((int)blockIdx.x, s / nk), kk = s % nk;
     const bool do_rs = AT && g.rowsum != nullptr && (t % ntn) == 0 && wn == 0;
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
@@ -773,6 +774,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_p3_kernel(GemmArgs g, int ntile
         for (int j = 0; j < TM; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
       drain = true;
     }
+    if (++kk == nk) { kk = 0; t += G; }
+    cb = cb == 2 ? 0 : cb + 1;
   }
 }
 
