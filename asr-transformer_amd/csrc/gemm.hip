@@ -623,6 +623,8 @@ struct PStage {
   }
   // base: operand start; total_bytes: one past its last valid byte; k0: first k of the stage
   ASRX_DEV void issue(unsigned char* img, const bf16_t* base, int64_t ld, int64_t total_bytes, int k0) const {
+#if defined(__HIP_DEVICE_COMPILE__)  // the buffer-resource builtins do not exist in the host pass (which then
+                                     // silently dropped the kernel's host stubs)
     const int64_t koff = KSTRIDED ? (int64_t)k0 * ld * 2 : (int64_t)k0 * 2;
     const int64_t rem = total_bytes - koff;
     __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
@@ -631,6 +633,7 @@ struct PStage {
 #pragma unroll
     for (int j = 0; j < NI; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_t*)(img + (j * 8 + w) * 1024), 16, voff[j], 0, 0, 0);
+#endif
   }
 };
 
@@ -684,17 +687,20 @@ __global__ __launch_bounds__(512) void gemm_bf16_p3_kernel(GemmArgs g, int ntile
   PStage<P_BN, BT> sb;
   // issue cursor (runs two steps ahead of the compute cursor)
   int it = b0, ik = 0, ib = 0;
-  auto issue_next = [&]() {
-    if (ik == 0) {
-      sa.set_tile((it / ntn) * P_BM, g.lda);
-      sb.set_tile((it % ntn) * P_BN, g.ldb);
-    }
-    unsigned char* img = lds + ib * P_STAGE;
-    sa.issue(img, A, g.lda, a_bytes, kbeg + ik * BK);
-    sb.issue(img + PA_BYTES, B, g.ldb, b_bytes, kbeg + ik * BK);
-    if (++ik == nk) { ik = 0; it += G; }
-    ib = ib == 2 ? 0 : ib + 1;
-  };
+  // (a macro rather than a lambda: hipcc/ROCm 7.2 dropped the host device-stubs of most instantiations of this
+  //  kernel when the issue step was a capturing lambda)
+#define P3_ISSUE_NEXT()                                                      \
+  do {                                                                       \
+    if (ik == 0) {                                                           \
+      sa.set_tile((it / ntn) * P_BM, g.lda);                                 \
+      sb.set_tile((it % ntn) * P_BN, g.ldb);                                 \
+    }                                                                        \
+    unsigned char* img_ = lds + ib * P_STAGE;                                \
+    sa.issue(img_, A, g.lda, a_bytes, kbeg + ik * BK);                       \
+    sb.issue(img_ + PA_BYTES, B, g.ldb, b_bytes, kbeg + ik * BK);            \
+    if (++ik == nk) { ik = 0; it += G; }                                     \
+    ib = ib == 2 ? 0 : ib + 1;                                               \
+  } while (0)
 
   f4_t acc[TN][TM];
 #pragma unroll
@@ -705,8 +711,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_p3_kernel(GemmArgs g, int ntile
 #pragma unroll
   for (int j = 0; j < TM; ++j) rs[j] = 0.f;
 
-  issue_next();
-  if (total > 1) issue_next();
+  P3_ISSUE_NEXT();
+  if (total > 1) P3_ISSUE_NEXT();
   bool drain = false;
   int t = b0, kk = 0, cb = 0;   // compute cursor
   for (int s = 0; s < total; ++s) {
@@ -714,7 +720,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_p3_kernel(GemmArgs g, int ntile
     else asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     drain = false;
-    if (s + 2 < total) issue_next();
+    if (s + 2 < total) P3_ISSUE_NEXT();
     const unsigned char* la = lds + cb * P_STAGE;
     const unsigned char* lb = la + PA_BYTES;
     const bool do_rs = AT && g.rowsum != nullptr && (t % ntn) == 0 && wn == 0;
