@@ -66,6 +66,7 @@ class AttnDesc(ctypes.Structure):
 SIGNATURES = {
     "asrx_version": [],
     "asrx_gemm": [ctypes.POINTER(GemmDesc), c_vp],
+    "asrx_gemm_kernel_name": [ctypes.POINTER(GemmDesc), ctypes.c_char_p, c_i32],
     "asrx_attention_fwd": [ctypes.POINTER(AttnDesc), c_vp],
     "asrx_attention_bwd": [ctypes.POINTER(AttnDesc), c_vp],
     "asrx_attn_delta": [ctypes.POINTER(AttnDesc), c_vp],

@@ -46,17 +46,32 @@ def auto_splitk(m, n, k, batch=1, tile=64):
 
 
 class KernelProbe:
-    """Brackets every launch of one GEMM kernel instantiation with HIP events on the launching stream, and
-    accumulates its algorithmic FLOPs (bench.py roofline; matches rocprofv3's per-kernel-name average)."""
+    """Brackets GEMM launches with HIP events on the launching stream (bench.py roofline), keyed by the kernel
+    instantiation asrx_gemm_kernel_name reports — the same name rocprofv3 lists, so the live average agrees
+    with the profiler's.  target=None records every GEMM (to find the dominant one); otherwise only launches
+    of `target` are timed."""
 
-    def __init__(self, key):
-        self.key = key              # (in_dtype, a_trans, b_trans, tile, vec)
-        self.events = []
-        self.flops = 0
+    def __init__(self, target=None):
+        self.target = target
+        self.events = {}            # name -> [(start, end)]
+        self.flops = {}             # name -> algorithmic FLOPs
         self.active = False
 
-    def durations_ms(self):
-        return [s.elapsed_time(e) for s, e in self.events]
+    def record(self, name):
+        return self.active and (self.target is None or name == self.target)
+
+    def durations_ms(self, name):
+        return [s.elapsed_time(e) for s, e in self.events.get(name, [])]
+
+    def dominant(self):
+        tot = {n: sum(self.durations_ms(n)) for n in self.events}
+        return max(tot, key=tot.get) if tot else None
+
+
+def kernel_name(d):
+    buf = ctypes.create_string_buffer(128)
+    call("asrx_gemm_kernel_name", ctypes.byref(d), buf, 128)
+    return buf.value.decode()
 
 
 PROBE = None
@@ -114,17 +129,16 @@ def gemm(a, b, c, m, n, k, *, lda, ldb, ldc, a_trans=False, b_trans=False, alpha
             rws = torch.empty(splitk * m, device=c.device, dtype=torch.float32)
             d.rowsum_ws = rws.data_ptr()
     probe = PROBE
-    if probe is not None and probe.active and a.dtype == torch.bfloat16:
-        vec = (lda % 8 == 0 and ldb % 8 == 0 and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0
-               and sa[0] % 8 == 0 and sa[1] % 8 == 0 and sb[0] % 8 == 0 and sb[1] % 8 == 0)
-        if (code(a), bool(a_trans), bool(b_trans), tile, vec) == probe.key and splitk == 1:
+    if probe is not None and probe.active:
+        name = kernel_name(d)
+        if probe.record(name):
             s0 = torch.cuda.Event(enable_timing=True)
             s1 = torch.cuda.Event(enable_timing=True)
             s0.record()
             call("asrx_gemm", ctypes.byref(d), stream())
             s1.record()
-            probe.events.append((s0, s1))
-            probe.flops += 2 * m * n * k * batch
+            probe.events.setdefault(name, []).append((s0, s1))
+            probe.flops[name] = probe.flops.get(name, 0) + 2 * m * n * k * batch
             return ws
     call("asrx_gemm", ctypes.byref(d), stream())
     return ws

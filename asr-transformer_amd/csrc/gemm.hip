@@ -13,6 +13,7 @@
 // Replaces the reference's nn.Linear / aten::addmm and aten::bmm calls (layers.py:10-12,16-18,20,27,36,48,51;
 // model.py:32,102) and, through im2col, the conv2 of the front-end (model.py:168-171).
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -976,7 +977,89 @@ void dispatch_bf16(const GemmArgs& g, bool at, bool bt, bool vec, int batch, hip
 #undef ASRX_L
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// Kernel selection (shared by asrx_gemm and asrx_gemm_kernel_name so profiling can name the launch).
+struct GemmPlan {
+  int use;     // 1 = p3 (256x128 LDS-DMA ring), 2 = glds (128x128), 3 = register path 128, 4 = register path 64
+  bool vec;    // 16-byte aligned operands
+  int epi;     // instantiated epilogue flags (E_GENERIC when the fast-path set has no match)
+  int ntiles;  // output tiles of the chosen kernel
+};
+
+bool epi_instantiated(bool at, bool bt, int epi) {
+#define ASRX_HAS(E) if (epi == (E)) return true;
+  if (!at && !bt) { ASRX_EPI_NT(ASRX_HAS) }
+  else if (!at && bt) { ASRX_EPI_NN(ASRX_HAS) }
+  else if (at && bt) { ASRX_EPI_TT(ASRX_HAS) }
+#undef ASRX_HAS
+  return false;
+}
+
+GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
+  GemmPlan pl;
+  pl.vec = (d->lda % 8 == 0) && (d->ldb % 8 == 0) && ((uintptr_t)d->a % 16 == 0) && ((uintptr_t)d->b % 16 == 0) &&
+           (d->sa_outer % 8 == 0) && (d->sa_inner % 8 == 0) && (d->sb_outer % 8 == 0) && (d->sb_inner % 8 == 0);
+  int tile = d->tile;
+  if (tile != 64 && tile != 128) {
+    const long t128 = (long)((d->m + 127) / 128) * ((d->n + 127) / 128) * batch * splitk;
+    tile = t128 >= 400 ? 128 : 64;
+  }
+  // kernel family: ASRX_GEMM_KERNEL = auto | p3 | glds | reg  (A/B switch for benchmarking)
+  const char* kenv = getenv("ASRX_GEMM_KERNEL");
+  const int kvar = !kenv ? 0 : (!strcmp(kenv, "p3") ? 1 : (!strcmp(kenv, "glds") ? 2 : (!strcmp(kenv, "reg") ? 3 : 0)));
+  const bool dma_ok = pl.vec && d->k % BK == 0 && (!d->a_trans || d->m % 8 == 0) && (!d->b_trans || d->n % 8 == 0) &&
+                      d->m >= 8 && d->n >= 8;
+  const int nt_p3 = ((d->m + P_BM - 1) / P_BM) * ((d->n + P_BN - 1) / P_BN);
+  pl.use = tile == 128 ? 3 : 4;
+  if (dma_ok) {
+    if (kvar == 1) pl.use = 1;
+    else if (kvar == 2) pl.use = tile == 128 ? 2 : pl.use;
+    // auto (measured on the c3 shapes, tools/gemm_bench.py): the p3 ring wins every projection with K <= 4096;
+    // the register path wins the weight-gradient (A^T, reduction over B*T rows) and very long-K GEMMs.
+    else if (kvar == 0 && !d->a_trans && d->k <= 4096)
+      pl.use = (nt_p3 * splitk * batch >= 192) ? 1 : (tile == 128 ? 2 : pl.use);
+  }
+  pl.ntiles = pl.use == 1 ? nt_p3 : ((d->m + tile - 1) / tile) * ((d->n + tile - 1) / tile);
+  // compile-time epilogue selection (fast-path preconditions, else generic)
+  int epi = E_GENERIC;
+  const int esz = d->c_dtype == ASRX_F32 ? 16 : 8;
+  const bool cvec = (d->ldc % 4 == 0) && ((uintptr_t)d->c % esz == 0) && (d->sc_outer % 4 == 0) && (d->sc_inner % 4 == 0);
+  const bool fast = batch == 1 && splitk == 1 && d->n % 4 == 0 && cvec &&
+                    (!d->bias || (uintptr_t)d->bias % 16 == 0) &&
+                    (!d->rowadd || (d->ld_rowadd % 4 == 0 && (uintptr_t)d->rowadd % 16 == 0)) &&
+                    (!d->gate || (d->gate_dtype == ASRX_BF16 && d->ld_gate % 4 == 0 && (uintptr_t)d->gate % 8 == 0)) &&
+                    (!d->resid || (d->resid_dtype == ASRX_F32 && d->ld_resid % 4 == 0 && (uintptr_t)d->resid % 16 == 0)) &&
+                    (d->beta == 0.f || (d->beta == 1.f && d->c_dtype == ASRX_F32));
+  if (fast) {
+    epi = (d->bias ? E_BIAS : 0) | (d->relu ? E_RELU : 0) | (drop_threshold(d->dropout_p) ? E_DROP : 0) |
+          (d->gate ? E_GATE : 0) | (d->resid ? E_RESID : 0) | (d->beta == 1.f ? E_BETA : 0) |
+          (d->c_dtype == ASRX_F32 ? E_F32 : 0) | (d->alpha != 1.f ? E_ALPHA : 0) | (d->rowadd ? E_ROWADD : 0);
+  }
+  pl.epi = (pl.use <= 2 && epi_instantiated(d->a_trans, d->b_trans, epi)) ? epi : E_GENERIC;
+  return pl;
+}
+
 }  // namespace
+
+extern "C" int asrx_gemm_kernel_name(const asrx_gemm_desc* d, char* buf, int len) {
+  if (!d || !buf || len < 8) return ASRX_ERR_ARG;
+  const int batch = d->batch > 0 ? d->batch : 1;
+  const int splitk = d->splitk > 1 ? d->splitk : 1;
+  const char* tf[2] = {"false", "true"};
+  if (d->in_dtype == ASRX_F32) {
+    snprintf(buf, len, "gemm_f32_kernel<%s, %s>", tf[!!d->a_trans], tf[!!d->b_trans]);
+    return ASRX_OK;
+  }
+  const GemmPlan pl = plan_bf16(d, batch, splitk);
+  if (pl.use == 1 || pl.use == 2)
+    snprintf(buf, len, "gemm_bf16_%s_kernel<%s, %s, %d>", pl.use == 1 ? "p3" : "glds", tf[!!d->a_trans],
+             tf[!!d->b_trans], pl.epi);
+  else
+    snprintf(buf, len, "gemm_bf16_kernel<%d, %d, %s, %s, %s>", pl.use == 3 ? 128 : 64, pl.use == 3 ? 128 : 64,
+             tf[!!d->a_trans], tf[!!d->b_trans], tf[pl.vec]);
+  return ASRX_OK;
+}
 
 extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
   if (!d || d->m < 0 || d->n < 0 || d->k < 0 || !d->a || !d->b || !d->c) return ASRX_ERR_ARG;
@@ -1016,57 +1099,24 @@ extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
   g.cvec = (d->ldc % 4 == 0) && ((uintptr_t)d->c % esz == 0) && (d->sc_outer % 4 == 0) && (d->sc_inner % 4 == 0);
 
   if (d->in_dtype == ASRX_BF16) {
-    const bool vec = (d->lda % 8 == 0) && (d->ldb % 8 == 0) && ((uintptr_t)d->a % 16 == 0) &&
-                     ((uintptr_t)d->b % 16 == 0) && (d->sa_outer % 8 == 0) && (d->sa_inner % 8 == 0) &&
-                     (d->sb_outer % 8 == 0) && (d->sb_inner % 8 == 0);
-    int tile = d->tile;
-    if (tile != 64 && tile != 128) {
-      const long t128 = (long)((d->m + 127) / 128) * ((d->n + 127) / 128) * batch * splitk;
-      tile = t128 >= 400 ? 128 : 64;
-    }
-    const int kb = (d->k + BK - 1) / BK;
+    const GemmPlan pl = plan_bf16(d, batch, splitk);
     g.splitk = splitk;
-    g.k_per_split = ((kb + splitk - 1) / splitk) * BK;
-    // kernel family: ASRX_GEMM_KERNEL = auto | p3 | glds | reg  (A/B switch for benchmarking)
-    const char* kenv = getenv("ASRX_GEMM_KERNEL");
-    const int kvar = !kenv ? 0 : (!strcmp(kenv, "p3") ? 1 : (!strcmp(kenv, "glds") ? 2 : (!strcmp(kenv, "reg") ? 3 : 0)));
-    const bool dma_ok = vec && d->k % BK == 0 && (!d->a_trans || d->m % 8 == 0) && (!d->b_trans || d->n % 8 == 0) &&
-                        d->m >= 8 && d->n >= 8;
-    const int nt_p3 = ((d->m + P_BM - 1) / P_BM) * ((d->n + P_BN - 1) / P_BN);
-    int use = 0;  // 1 = p3, 2 = glds, 0 = register path
-    if (dma_ok) {
-      if (kvar == 1) use = 1;
-      else if (kvar == 2) use = tile == 128 ? 2 : 0;
-      else if (kvar == 0) use = (nt_p3 * splitk * batch >= 192) ? 1 : (tile == 128 ? 2 : 0);
-    }
-    // compile-time epilogue selection (fast-path preconditions, else generic)
-    int epi = E_GENERIC;
-    const bool fast = batch == 1 && splitk == 1 && d->n % 4 == 0 && g.cvec && d->ldc % 4 == 0 &&
-                      (!d->bias || (uintptr_t)d->bias % 16 == 0) &&
-                      (!d->rowadd || (d->ld_rowadd % 4 == 0 && (uintptr_t)d->rowadd % 16 == 0)) &&
-                      (!d->gate || (d->gate_dtype == ASRX_BF16 && d->ld_gate % 4 == 0 && (uintptr_t)d->gate % 8 == 0)) &&
-                      (!d->resid || (d->resid_dtype == ASRX_F32 && d->ld_resid % 4 == 0 && (uintptr_t)d->resid % 16 == 0)) &&
-                      (d->beta == 0.f || (d->beta == 1.f && d->c_dtype == ASRX_F32));
-    if (fast) {
-      epi = (d->bias ? E_BIAS : 0) | (d->relu ? E_RELU : 0) | (g.drop_thr ? E_DROP : 0) | (d->gate ? E_GATE : 0) |
-            (d->resid ? E_RESID : 0) | (d->beta == 1.f ? E_BETA : 0) | (d->c_dtype == ASRX_F32 ? E_F32 : 0) |
-            (d->alpha != 1.f ? E_ALPHA : 0) | (d->rowadd ? E_ROWADD : 0);
-    }
-    if (use == 1) {
-      if (!d->a_trans && !d->b_trans) dispatch_p3<false, false>(g, epi, nt_p3, splitk, batch, st);
-      else if (!d->a_trans && d->b_trans) dispatch_p3<false, true>(g, epi, nt_p3, splitk, batch, st);
-      else if (d->a_trans && !d->b_trans) dispatch_p3<true, false>(g, epi, nt_p3, splitk, batch, st);
-      else dispatch_p3<true, true>(g, epi, nt_p3, splitk, batch, st);
-    } else if (use == 2) {
-      const int ntiles = ((d->m + GT - 1) / GT) * ((d->n + GT - 1) / GT);
-      if (!d->a_trans && !d->b_trans) dispatch_glds<false, false>(g, epi, ntiles, splitk, batch, st);
-      else if (!d->a_trans && d->b_trans) dispatch_glds<false, true>(g, epi, ntiles, splitk, batch, st);
-      else if (d->a_trans && !d->b_trans) dispatch_glds<true, false>(g, epi, ntiles, splitk, batch, st);
-      else dispatch_glds<true, true>(g, epi, ntiles, splitk, batch, st);
-    } else if (tile == 128) {
-      dispatch_bf16<128, 128>(g, d->a_trans, d->b_trans, vec, batch, st);
+    g.k_per_split = ((((int)d->k + BK - 1) / BK + splitk - 1) / splitk) * BK;
+    const int epi = pl.epi;
+    if (pl.use == 1) {
+      if (!d->a_trans && !d->b_trans) dispatch_p3<false, false>(g, epi, pl.ntiles, splitk, batch, st);
+      else if (!d->a_trans && d->b_trans) dispatch_p3<false, true>(g, epi, pl.ntiles, splitk, batch, st);
+      else if (d->a_trans && !d->b_trans) dispatch_p3<true, false>(g, epi, pl.ntiles, splitk, batch, st);
+      else dispatch_p3<true, true>(g, epi, pl.ntiles, splitk, batch, st);
+    } else if (pl.use == 2) {
+      if (!d->a_trans && !d->b_trans) dispatch_glds<false, false>(g, epi, pl.ntiles, splitk, batch, st);
+      else if (!d->a_trans && d->b_trans) dispatch_glds<false, true>(g, epi, pl.ntiles, splitk, batch, st);
+      else if (d->a_trans && !d->b_trans) dispatch_glds<true, false>(g, epi, pl.ntiles, splitk, batch, st);
+      else dispatch_glds<true, true>(g, epi, pl.ntiles, splitk, batch, st);
+    } else if (pl.use == 3) {
+      dispatch_bf16<128, 128>(g, d->a_trans, d->b_trans, pl.vec, batch, st);
     } else {
-      dispatch_bf16<64, 64>(g, d->a_trans, d->b_trans, vec, batch, st);
+      dispatch_bf16<64, 64>(g, d->a_trans, d->b_trans, pl.vec, batch, st);
     }
   } else {
     const int vec = (d->lda % 4 == 0) && (d->ldb % 4 == 0) && ((uintptr_t)d->a % 16 == 0) &&

@@ -7,8 +7,8 @@ bf16, dropout 0.1, fused AdamW), data-parallel over N GPUs (weak scaling: 64 utt
         bench.py --gpus N --steps K --warmup W
 
 Prints ONE JSON line (rank 0). `value` = all ranks' frames / max-over-ranks wall time of the K timed steps.
-`roofline` = the dominant GEMM kernel instantiation (bf16 NT 128x128, every forward projection GEMM),
-timed live with HIP events on its launch stream; `cpu_baseline` = the oracle (fp32 eager PyTorch
+`roofline` = the dominant GEMM kernel instantiation (largest total time in the last warmup step, named as
+rocprofv3 names it), timed live with HIP events on its launch stream over the timed steps; `cpu_baseline` = the oracle (fp32 eager PyTorch
 restatement of the reference) train step on the host cores, bounded sample, rank 0 at N=1 only.
 """
 import argparse
@@ -37,7 +37,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=4)
-    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-steps", type=int, default=10)
     ap.add_argument("--no-probe", action="store_true")
     return ap.parse_args()
 
@@ -60,6 +60,18 @@ def cpu_baseline(cfg, frames, text_len, batch, steps):
             "sample": f"oracle fp32 train step (fwd+CE+bwd, dropout {cfg.dropout}) {cfg.n_enc}+{cfg.n_dec} layers "
                       f"d{cfg.d_model}, B={batch}, T={frames}, L={text_len}, {steps} steps after 1 warmup, "
                       f"{dt:.1f}s"}
+
+
+def pmc_traffic(kernel, config):
+    """HBM bytes per launch of `kernel` from the committed PMC summary (profiles/*pmc*.json, written by
+    tools/pmc_table.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes), or None."""
+    path = os.path.join(REPO, "profiles", f"{config}_pmc_traffic.json")
+    try:
+        with open(path) as f:
+            rec = json.load(f)["kernels"].get(kernel)
+    except (OSError, ValueError, KeyError):
+        return None
+    return None if rec is None else rec["hbm_bytes_per_launch"]
 
 
 def main():
@@ -89,12 +101,16 @@ def main():
     s, t, m = synthetic_batch(cfg, B, T, L + 1, seed=1234 + rank)
     s, t, m = s.cuda(), t.cuda(), m.cuda()
 
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
+        survey = not args.no_probe and i == args.warmup - 1
+        if survey:      # last warmup step: time every GEMM launch to find the dominant kernel instantiation
+            K.PROBE = K.KernelProbe()
+            K.PROBE.active = True
         loss = trainer.step(s, t, m)
     torch.cuda.synchronize()
     probe = None
-    if not args.no_probe:
-        probe = K.KernelProbe((asrx._lib.BF16, False, False, 128, True))
+    if K.PROBE is not None:
+        probe = K.KernelProbe(K.PROBE.dominant())
         probe.active = True
         K.PROBE = probe
     if world > 1:
@@ -115,15 +131,15 @@ def main():
     frames = B * T * args.steps * world
     value = frames / dt
     roof = None
-    if probe is not None and probe.events:
-        durs = probe.durations_ms()
+    if probe is not None and probe.events.get(probe.target):
+        durs = probe.durations_ms(probe.target)
         avg_ms = sum(durs) / len(durs)
-        achieved = probe.flops / (sum(durs) * 1e-3) / 1e12
+        achieved = probe.flops[probe.target] / (sum(durs) * 1e-3) / 1e12
         roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
-                "kernel": "gemm_bf16_kernel<128,128,NT,vec> (all forward projection GEMMs)",
-                "launches_per_step": len(durs) // args.steps, "avg_launch_us": round(avg_ms * 1e3, 2),
-                "flop_per_launch_avg": probe.flops // len(durs)}
+                "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": pmc_traffic(probe.target, args.config),
+                "kernel": probe.target, "launches_per_step": len(durs) // args.steps,
+                "avg_launch_us": round(avg_ms * 1e3, 2),
+                "flop_per_launch_avg": probe.flops[probe.target] // len(durs)}
     out = {"metric": "encoder+decoder frames/sec/GPU at d_model=512 T=1000; 1->8 GPU scaling",
            "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,

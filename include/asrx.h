@@ -69,6 +69,11 @@ typedef struct asrx_gemm_desc {
 
 int asrx_gemm(const asrx_gemm_desc* d, void* stream);
 
+/* Name of the kernel instantiation asrx_gemm would launch for d (as rocprofv3 lists it, without the
+ * namespace/argument list), e.g. "gemm_bf16_p3_kernel<false, false, 1>".  Host-only: no launch, no GPU
+ * needed.  Used by bench.py to time exactly the kernel the roofline names. */
+int asrx_gemm_kernel_name(const asrx_gemm_desc* d, char* buf, int32_t len);
+
 /* ---------------------------------------------------------------------------------------------------
  * Fused multi-head attention (bf16 in/out, fp32 softmax): per (batch b, head h)
  *   S = scale * Q K^T ; masked -> -inf ; P = nan_to_num(softmax(S)) ; O = dropout(P) V

@@ -121,3 +121,33 @@ def test_modules_refuse_cpu_execution():
     m, cfg = _build("micro")
     with pytest.raises(RuntimeError):
         m(torch.zeros(1, 1, 80, 60), torch.ones(1, 8, dtype=torch.long), torch.ones(1, 8))
+
+
+def test_gemm_kernel_plan_names_without_gpu():
+    """The kernel-selection policy is host logic: query it through the C-ABI with fake (aligned) pointers."""
+    from asrx._lib import BF16, F32, GemmDesc
+    from asrx.kernels import kernel_name
+
+    def desc(m, n, k, at=0, bt=0, bias=False, c_dtype=BF16, in_dtype=BF16):
+        d = GemmDesc()
+        d.m, d.n, d.k, d.in_dtype = m, n, k, in_dtype
+        d.a, d.lda, d.a_trans = 1 << 20, (m if at else k), at
+        d.b, d.ldb, d.b_trans = 2 << 20, (n if bt else k), bt
+        d.c, d.ldc, d.c_dtype = 3 << 20, n, c_dtype
+        d.alpha, d.batch, d.batch_inner, d.splitk = 1.0, 1, 1, 1
+        if bias:
+            d.bias = 4 << 20
+        return d
+
+    os.environ.pop("ASRX_GEMM_KERNEL", None)
+    assert kernel_name(desc(15936, 1536, 512, bias=True)) == "gemm_bf16_p3_kernel<false, false, 1>"
+    assert kernel_name(desc(15936, 512, 2048, bt=1)) == "gemm_bf16_p3_kernel<false, true, 0>"
+    wg = desc(2048, 512, 15936, at=1, bt=1, c_dtype=F32)
+    wg.tile = 128                     # as kernels.wgrad_plan sets it
+    assert kernel_name(wg) == "gemm_bf16_kernel<128, 128, true, true, true>"
+    assert kernel_name(desc(64, 64, 64, in_dtype=F32, c_dtype=F32)) == "gemm_f32_kernel<false, false>"
+    os.environ["ASRX_GEMM_KERNEL"] = "reg"
+    try:
+        assert kernel_name(desc(15936, 1536, 512)).startswith("gemm_bf16_kernel<128, 128, false, false, true>")
+    finally:
+        os.environ.pop("ASRX_GEMM_KERNEL")
