@@ -41,6 +41,19 @@ class GemmDesc(ctypes.Structure):
     ]
 
 
+class GemmGroup(ctypes.Structure):
+    _fields_ = [
+        ("m", c_i32), ("n", c_i32), ("k", c_i32),
+        ("a", c_vp), ("lda", c_i64),
+        ("b", c_vp), ("ldb", c_i64),
+        ("c", c_vp), ("ldc", c_i64),
+        ("rowsum_a", c_vp),
+    ]
+
+
+MAX_GROUPS = 48   # gemm.hip MAX_GROUPS (kernel-argument table)
+
+
 class AttnDesc(ctypes.Structure):
     _fields_ = [
         ("batch", c_i32), ("heads", c_i32), ("lq", c_i32), ("lk", c_i32), ("dh", c_i32),
@@ -67,6 +80,7 @@ SIGNATURES = {
     "asrx_version": [],
     "asrx_gemm": [ctypes.POINTER(GemmDesc), c_vp],
     "asrx_gemm_kernel_name": [ctypes.POINTER(GemmDesc), ctypes.c_char_p, c_i32],
+    "asrx_gemm_grouped": [ctypes.POINTER(GemmDesc), ctypes.POINTER(GemmGroup), c_i32, c_vp],
     "asrx_attention_fwd": [ctypes.POINTER(AttnDesc), c_vp],
     "asrx_attention_bwd": [ctypes.POINTER(AttnDesc), c_vp],
     "asrx_attn_delta": [ctypes.POINTER(AttnDesc), c_vp],

@@ -26,6 +26,7 @@ class Ctx:
         self.p = p_drop if train else 0.0
         self.seeds = seeds
         self.attn_impl = attn_impl
+        self.wq = None                  # list -> weight gradients are queued and issued grouped (flush_wgrad)
 
     def W(self, p):
         return self.store.w16(p) if self.cd == torch.bfloat16 else self.store.w32(p)
@@ -35,6 +36,24 @@ class Ctx:
 
     def seed(self):
         return self.seeds.next() if self.p > 0 else 0
+
+    def wgrad(self, dy, x, gw, gb=None):
+        """dW (+)= dy^T x, db (+)= colsum(dy).  Weight gradients feed nothing but the optimizer, so while a
+        queue is open they are deferred and later issued as grouped launches (no split-K)."""
+        if self.wq is not None and K.wgrad_groupable(dy, x, gw):
+            self.wq.append((dy, x, gw, gb))
+        else:
+            K.linear_wgrad(dy, x, gw, bias_grad=gb)
+
+    def defer_wgrad(self):
+        if self.cd == torch.bfloat16 and self.wq is None:
+            self.wq = []
+            return True
+        return False
+
+    def flush_wgrad(self):
+        q, self.wq = self.wq, None
+        K.linear_wgrad_grouped(q or [])
 
 
 class Seeds:
@@ -162,13 +181,13 @@ def self_attn_bwd(C, S, dy, dy_c, dx_c_out=None, dx_c_p=0.0, dx_c_seed=0):
     W, G = C.W, C.G
     do = _empty((M, d), C.cd, x)
     K.linear_dgrad(dy_c, W(mha._out_linear.weight), do)
-    K.linear_wgrad(dy_c, o, G(mha._out_linear.weight), bias_grad=G(mha._out_linear.bias))
+    C.wgrad(dy_c, o, G(mha._out_linear.weight), G(mha._out_linear.bias))
     dqkv = _empty((M, 3 * d), C.cd, x)
     gst = ((d, T * d),) + ((3 * d, T * 3 * d),) * 3
     attn_bwd(C, S["A"], qkv, qkv[:, d:], qkv[:, 2 * d:], o, do, dqkv, dqkv[:, d:], dqkv[:, 2 * d:], gst)
     dh = _empty((M, d), C.cd, x)
     K.linear_dgrad(dqkv, W(mha.wqkv), dh)
-    K.linear_wgrad(dqkv, h, G(mha.wqkv), bias_grad=G(mha.bqkv))
+    C.wgrad(dqkv, h, G(mha.wqkv), G(mha.bqkv))
     return ln_bwd(C, x, dh, S["ln"], S["mean"], S["rstd"], dres=dy, drop_out=dx_c_out, drop_seed=dx_c_seed,
                   drop_p=dx_c_p)
 
@@ -198,13 +217,13 @@ def cross_attn_bwd(C, S, dy, dy_c, dkv, dx_c_out=None, dx_c_p=0.0, dx_c_seed=0):
     W, G = C.W, C.G
     do = _empty((M, d), C.cd, x)
     K.linear_dgrad(dy_c, W(mha._out_linear.weight), do)
-    K.linear_wgrad(dy_c, o, G(mha._out_linear.weight), bias_grad=G(mha._out_linear.bias))
+    C.wgrad(dy_c, o, G(mha._out_linear.weight), G(mha._out_linear.bias))
     dq = _empty((M, d), C.cd, x)
     gst = ((d, L * d), (d, L * d), (kv_ld, Te * kv_ld), (kv_ld, Te * kv_ld))
     attn_bwd(C, S["A"], q, kv, kv[:, d:], o, do, dq, dkv, dkv[:, d:], gst)
     dh = _empty((M, d), C.cd, x)
     K.linear_dgrad(dq, W(mha.wq), dh)
-    K.linear_wgrad(dq, h, G(mha.wq), bias_grad=G(mha.bq))
+    C.wgrad(dq, h, G(mha.wq), G(mha.bq))
     return ln_bwd(C, x, dh, S["ln"], S["mean"], S["rstd"], dres=dy, drop_out=dx_c_out, drop_seed=dx_c_seed,
                   drop_p=dx_c_p)
 
@@ -231,10 +250,10 @@ def ffn_bwd(C, S, dy, dy_c, dx_c_out=None, dx_c_p=0.0, dx_c_seed=0):
     keep_scale = 1.0 / (1.0 - C.p) if C.p > 0 else 1.0
     # f = Drop(ReLU(pre)) -> dpre = df * [f > 0] / (1-p)   (f > 0 <=> pre > 0 and kept)
     K.linear_dgrad(dy_c, W(ff.unsqueeze.weight), dpre, alpha=keep_scale, gate=f, ld_gate=nf)
-    K.linear_wgrad(dy_c, f, G(ff.unsqueeze.weight), bias_grad=G(ff.unsqueeze.bias))
+    C.wgrad(dy_c, f, G(ff.unsqueeze.weight), G(ff.unsqueeze.bias))
     dh = _empty((M, d), C.cd, x)
     K.linear_dgrad(dpre, W(ff.squeeze.weight), dh)
-    K.linear_wgrad(dpre, h, G(ff.squeeze.weight), bias_grad=G(ff.squeeze.bias))
+    C.wgrad(dpre, h, G(ff.squeeze.weight), G(ff.squeeze.bias))
     return ln_bwd(C, x, dh, S["ln"], S["mean"], S["rstd"], dres=dy, drop_out=dx_c_out, drop_seed=dx_c_seed,
                   drop_p=dx_c_p)
 
@@ -299,7 +318,7 @@ def frontend_bwd(C, S, dfeats_c, conv1, conv2):
     dy2 = dfeats_c.view(M2, 64)
     cols = S["cols"]
     G = C.G
-    K.linear_wgrad(dy2, cols, G(conv2.weight), bias_grad=G(conv2.bias))
+    C.wgrad(dy2, cols, G(conv2.weight), G(conv2.bias))
     dcols = _empty((M2, 576), C.cd, dy2)
     K.linear_dgrad(dy2, C.W(conv2.weight), dcols)
     dy1 = _empty((B, F1, T1, 64), torch.float32, dy2)

@@ -135,7 +135,7 @@ def encoder_bwd(C, enc, S, dy, gate_feats):
         K.linear_dgrad(dx_c, C.W(w), dfeats, gate=feats, ld_gate=feats.shape[1])
     else:
         K.linear_dgrad(dx_c, C.W(w), dfeats)
-    K.linear_wgrad(dx_c, feats, C.G(w), bias_grad=C.G(enc._lin_in.bias))
+    C.wgrad(dx_c, feats, C.G(w), C.G(enc._lin_in.bias))
     return dfeats
 
 
@@ -195,7 +195,7 @@ def decoder_bwd(C, dec, S, dlogits_c):
     cls = dec._classifier
     dh = torch.empty(B * L, d, dtype=C.cd, device=dev)
     K.linear_dgrad(dlogits_c, C.W(cls.weight), dh)
-    K.linear_wgrad(dlogits_c, h, C.G(cls.weight))
+    C.wgrad(dlogits_c, h, C.G(cls.weight))
     dx_c = torch.empty(B * L, d, dtype=C.cd, device=dev)
     dx = Bk.ln_bwd(C, x, dh, dec._norm_layer, S["mean"], S["rstd"], drop_out=dx_c)
     dkv = torch.empty(B * Te, n * 2 * d, dtype=C.cd, device=dev)
@@ -208,7 +208,7 @@ def decoder_bwd(C, dec, S, dlogits_c):
     Wkv, _, gW, gb = _kv_block(C, dec)
     denc = torch.empty(B * Te, d, dtype=torch.float32, device=dev)
     K.linear_dgrad(dkv, Wkv, denc)
-    K.linear_wgrad(dkv, S["enc"], gW, bias_grad=gb)
+    C.wgrad(dkv, S["enc"], gW, gb)
     return denc
 
 
@@ -227,9 +227,12 @@ def model_forward(C, model, spectrum, text, mask):
 
 def model_backward(C, model, S, dlogits_c):
     _prepare_grads(C)
+    own = C.defer_wgrad()
     denc = decoder_bwd(C, model.decoder, S["d"], dlogits_c)
     dfeats = encoder_bwd(C, model.encoder, S["e"], denc, gate_feats=True)
     Bk.frontend_bwd(C, S["f"], dfeats, model.input_layer[0], model.input_layer[2])
+    if own:
+        C.flush_wgrad()
 
 
 def _dlogits_padded(C, dlogits, rows, V, Vp):
@@ -303,7 +306,10 @@ class _EncoderFn(torch.autograd.Function):
         C, S = ctx.C, ctx.S
         _prepare_grads(C)
         B, T, Cc, F2 = ctx.xshape
+        own = C.defer_wgrad()
         dfeats = encoder_bwd(C, ctx.enc, S, g.reshape(B * T, -1).contiguous(), gate_feats=False)
+        if own:
+            C.flush_wgrad()
         dx = dfeats.view(B, T, F2, Cc).permute(0, 3, 2, 1)
         return (None, None, dx) + (None,) * len(_params(ctx.enc))
 
@@ -331,7 +337,10 @@ class _DecoderFn(torch.autograd.Function):
         B, L, V, Vp, Te, d = ctx.shape
         C = ctx.C
         _prepare_grads(C)
+        own = C.defer_wgrad()
         denc = decoder_bwd(C, ctx.dec, ctx.S, _dlogits_padded(C, dlogits, B * L, V, Vp))
+        if own:
+            C.flush_wgrad()
         return (None, None, None, None, denc.view(B, Te, d)) + (None,) * len(_params(ctx.dec))
 
 

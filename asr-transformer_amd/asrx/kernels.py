@@ -5,7 +5,7 @@ import math
 
 import torch
 
-from ._lib import AttnDesc, BF16, F32, GemmDesc, call
+from ._lib import MAX_GROUPS, AttnDesc, BF16, F32, GemmDesc, GemmGroup, call
 
 _U64 = (1 << 64) - 1
 
@@ -184,6 +184,52 @@ def linear_wgrad(dy, x, wgrad, *, beta=1.0, bias_grad=None, **kw):
     if bias_grad is not None and not fuse:
         colsum(dy, bias_grad)
     return ws
+
+
+GROUPED_KERNEL = "gemm_bf16_grouped_kernel<true, true>"
+
+
+def wgrad_groupable(dy, x, wgrad):
+    """Can dW (+)= dy^T x join a grouped launch (bf16, 16-byte aligned rows, fp32 grads, moderate K)?"""
+    return (dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and wgrad.dtype == torch.float32
+            and dy.stride(1) == 1 and x.stride(1) == 1 and wgrad.stride(1) == 1
+            and dy.stride(0) % 8 == 0 and x.stride(0) % 8 == 0 and dy.data_ptr() % 16 == 0
+            and x.data_ptr() % 16 == 0 and dy.shape[0] <= 65536)
+
+
+def linear_wgrad_grouped(items, *, beta=1.0):
+    """Issue many independent weight gradients wgrad[N,K] (+)= dy[M,N]^T x[M,K] (+ bias_grad[N] += colsum dy)
+    as grouped launches (asrx_gemm_grouped): longest reductions first, MAX_GROUPS problems per launch."""
+    if not items:
+        return
+    items = sorted(items, key=lambda it: -it[0].shape[0])
+    common = GemmDesc()
+    common.in_dtype, common.a_trans, common.b_trans, common.c_dtype = BF16, 1, 1, F32
+    common.alpha, common.beta = 1.0, beta
+    for c0 in range(0, len(items), MAX_GROUPS):
+        chunk = items[c0:c0 + MAX_GROUPS]
+        arr = (GemmGroup * len(chunk))()
+        flops = 0
+        for g, (dy, x, wgrad, bias_grad) in zip(arr, chunk):
+            _cuda(dy, x, wgrad, bias_grad)
+            m, n = dy.shape
+            k = x.shape[1]
+            g.m, g.n, g.k = n, k, m
+            g.a, g.lda = dy.data_ptr(), dy.stride(0)
+            g.b, g.ldb = x.data_ptr(), x.stride(0)
+            g.c, g.ldc = wgrad.data_ptr(), wgrad.stride(0)
+            g.rowsum_a = _p(bias_grad)
+            flops += 2 * m * n * k
+        probe = PROBE
+        timed = probe is not None and probe.record(GROUPED_KERNEL)
+        if timed:
+            s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s0.record()
+        call("asrx_gemm_grouped", ctypes.byref(common), arr, len(chunk), stream())
+        if timed:
+            s1.record()
+            probe.events.setdefault(GROUPED_KERNEL, []).append((s0, s1))
+            probe.flops[GROUPED_KERNEL] = probe.flops.get(GROUPED_KERNEL, 0) + flops
 
 
 def colsum(x, out, *, accumulate=True, rows=None, cols=None, ld=None):

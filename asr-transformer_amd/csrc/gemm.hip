@@ -214,19 +214,19 @@ struct TileBF16 {
   }
 };
 
+template <int BM, int BN, bool AT, bool BT>
+constexpr int reg_lds_elems() { return 2 * (TileBF16<BM, AT>::ELEMS + TileBF16<BN, BT>::ELEMS); }
+
+// One output tile (tile index `tile` of the row-major tile grid, K split `split`, batch `z`).
 template <int BM, int BN, bool AT, bool BT, bool VEC>
-__global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs g) {
+ASRX_DEV void gemm_bf16_tile(const GemmArgs& g, int tile, int split, int z, bf16_t* lds) {
   using TA = TileBF16<BM, AT>;
   using TB = TileBF16<BN, BT>;
   constexpr int TM = BM / 32, TN = BN / 32;  // 16x16 subtiles per wave (2x2 waves)
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * (TA::ELEMS + TB::ELEMS)];
   constexpr int STAGE = TA::ELEMS + TB::ELEMS;
 
   const int ntn = (g.N + BN - 1) / BN;
-  const int tile = blockIdx.x;
   const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
-  const int split = blockIdx.y;
-  const int z = blockIdx.z;
   const int zo = z / g.batch_inner, zi = z % g.batch_inner;
   const bf16_t* A = (const bf16_t*)g.a + zo * g.sa_o + zi * g.sa_i;
   const bf16_t* B = (const bf16_t*)g.b + zo * g.sb_o + zi * g.sb_i;
@@ -319,6 +319,49 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs g) {
       if (g.splitk > 1) store_partial4(g, split, m, n, v);
       else epilogue4(g, z, m, n, v);
     }
+}
+
+template <int BM, int BN, bool AT, bool BT, bool VEC>
+__global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) bf16_t lds[reg_lds_elems<BM, BN, AT, BT>()];
+  gemm_bf16_tile<BM, BN, AT, BT, VEC>(g, blockIdx.x, blockIdx.y, blockIdx.z, lds);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Grouped GEMM: many independent problems (same layouts/epilogue, own shapes and pointers) in ONE launch.
+// The weight gradients of every layer (dW = dY^T X, reduction over the B*T rows) are independent of each
+// other, so the backward queues them and issues them together: enough 128x128 tiles to fill 256 CUs
+// several times over with no split-K (no fp32 partials, no reduce pass), long-K groups first.
+// The table travels in the kernel arguments (MAX_GROUPS entries, < 4 KiB).
+// ------------------------------------------------------------------------------------------------
+constexpr int MAX_GROUPS = 48;
+struct GroupEnt {
+  const void* a; const void* b; void* c; float* rowsum;
+  int lda, ldb, ldc;
+  int m, n, k;
+  int tile_start;   // first global tile index of this group
+  int pad;
+};
+struct GroupTable {
+  float alpha, beta;
+  int c_dtype, count, cvec;
+  GroupEnt e[MAX_GROUPS];
+};
+
+template <bool AT, bool BT>
+__global__ __launch_bounds__(256) void gemm_bf16_grouped_kernel(GroupTable t) {
+  __shared__ __attribute__((aligned(16))) bf16_t lds[reg_lds_elems<128, 128, AT, BT>()];
+  const int tid = blockIdx.x;
+  int gi = 0;
+  while (gi + 1 < t.count && t.e[gi + 1].tile_start <= tid) ++gi;   // wave-uniform scan of the kernarg table
+  const GroupEnt& e = t.e[gi];
+  GemmArgs g = {};
+  g.M = e.m; g.N = e.n; g.K = e.k;
+  g.a = e.a; g.lda = e.lda; g.b = e.b; g.ldb = e.ldb; g.c = e.c; g.ldc = e.ldc; g.c_dtype = t.c_dtype;
+  g.batch_inner = 1; g.alpha = t.alpha; g.beta = t.beta; g.rowadd_mod = 1;
+  g.splitk = 1; g.k_per_split = ((e.k + BK - 1) / BK) * BK; g.cvec = t.cvec;
+  g.rowsum = e.rowsum;
+  gemm_bf16_tile<128, 128, AT, BT, true>(g, tid - e.tile_start, 0, 0, lds);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1058,6 +1101,40 @@ extern "C" int asrx_gemm_kernel_name(const asrx_gemm_desc* d, char* buf, int len
   else
     snprintf(buf, len, "gemm_bf16_kernel<%d, %d, %s, %s, %s>", pl.use == 3 ? 128 : 64, pl.use == 3 ? 128 : 64,
              tf[!!d->a_trans], tf[!!d->b_trans], tf[pl.vec]);
+  return ASRX_OK;
+}
+
+extern "C" int asrx_gemm_grouped(const asrx_gemm_desc* common, const asrx_gemm_group* groups, int32_t count,
+                                 void* stream) {
+  if (!common || !groups || count < 0) return ASRX_ERR_ARG;
+  if (count == 0) return ASRX_OK;
+  if (count > MAX_GROUPS) return ASRX_ERR_ARG;
+  if (common->in_dtype != ASRX_BF16 || !common->a_trans || !common->b_trans) return ASRX_ERR_UNSUPPORTED;
+  if (common->c_dtype != ASRX_BF16 && common->c_dtype != ASRX_F32) return ASRX_ERR_ARG;
+  GroupTable t;
+  memset(&t, 0, sizeof(t));
+  t.alpha = common->alpha; t.beta = common->beta; t.c_dtype = common->c_dtype; t.count = count;
+  t.cvec = 1;
+  const int esz = common->c_dtype == ASRX_F32 ? 16 : 8;
+  int64_t tiles = 0;
+  for (int i = 0; i < count; ++i) {
+    const asrx_gemm_group& q = groups[i];
+    if (q.m <= 0 || q.n <= 0 || q.k < 0 || !q.a || !q.b || !q.c) return ASRX_ERR_ARG;
+    // 16-byte vector staging: k-strided operands need 8-element aligned rows/pointers
+    if (q.lda % 8 || q.ldb % 8 || (uintptr_t)q.a % 16 || (uintptr_t)q.b % 16) return ASRX_ERR_UNSUPPORTED;
+    if (q.lda > INT32_MAX || q.ldb > INT32_MAX || q.ldc > INT32_MAX) return ASRX_ERR_ARG;
+    if (q.ldc % 4 || (uintptr_t)q.c % esz) t.cvec = 0;
+    GroupEnt& e = t.e[i];
+    e.a = q.a; e.b = q.b; e.c = q.c; e.rowsum = q.rowsum_a;
+    e.lda = (int)q.lda; e.ldb = (int)q.ldb; e.ldc = (int)q.ldc;
+    e.m = q.m; e.n = q.n; e.k = q.k;
+    e.tile_start = (int)tiles;
+    tiles += (int64_t)((q.m + 127) / 128) * ((q.n + 127) / 128);
+  }
+  if (tiles > INT32_MAX) return ASRX_ERR_ARG;
+  hipLaunchKernelGGL((gemm_bf16_grouped_kernel<true, true>), dim3((unsigned)tiles), dim3(256), 0,
+                     (hipStream_t)stream, t);
+  ASRX_CHECK_LAUNCH();
   return ASRX_OK;
 }
 

@@ -69,6 +69,22 @@ typedef struct asrx_gemm_desc {
 
 int asrx_gemm(const asrx_gemm_desc* d, void* stream);
 
+/* Grouped GEMM: `count` independent problems C_i = epi(alpha * op(A_i) op(B_i)^T) in ONE launch (no split-K).
+ * Layout flags, dtypes, alpha/beta come from `common` (its pointers/shapes are ignored); each group has its own
+ * shape, operands, output and optional fused row-sum (bias gradient).  Supported: bf16 in, a_trans = b_trans
+ * = 1 (weight gradients dW = dY^T X), count <= 48, 16-byte aligned operand rows.
+ * Replaces: the per-layer weight-gradient aten::mm + bias-gradient sum of autograd's nn.Linear backward
+ * (layers.py:10-12,36,48,51; model.py:32) — issued together once the backward has produced every dY. */
+typedef struct asrx_gemm_group {
+  int32_t m, n, k;
+  const void* a; int64_t lda;
+  const void* b; int64_t ldb;
+  void* c; int64_t ldc;
+  float* rowsum_a;
+} asrx_gemm_group;
+
+int asrx_gemm_grouped(const asrx_gemm_desc* common, const asrx_gemm_group* groups, int32_t count, void* stream);
+
 /* Name of the kernel instantiation asrx_gemm would launch for d (as rocprofv3 lists it, without the
  * namespace/argument list), e.g. "gemm_bf16_p3_kernel<false, false, 1>".  Host-only: no launch, no GPU
  * needed.  Used by bench.py to time exactly the kernel the roofline names. */

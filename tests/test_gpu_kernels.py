@@ -117,6 +117,32 @@ def test_gemm_fused_rowsum(tile, splitk, kernel_variant):
     assert relerr(bg.cpu(), 2 + dy.double().sum(0)) < 1e-5
 
 
+@pytest.mark.parametrize("ngroups", [1, 7, 60])
+def test_gemm_grouped_wgrad(ngroups):
+    """Grouped weight gradients (asrx_gemm_grouped): ragged shapes, K not a multiple of 64, fused bias-grad row
+    sums, beta=1 accumulation into existing fp32 grads; > MAX_GROUPS problems split over several launches."""
+    g = torch.Generator(device=dev).manual_seed(ngroups)
+    shapes = [(1000, 136, 96), (4096, 512, 512), (333, 248, 64), (64, 8, 576), (2500, 1536, 512),
+              (77, 40, 1216), (249, 200, 24)]
+    items, refs = [], []
+    for i in range(ngroups):
+        M, N, Kd = shapes[i % len(shapes)]
+        dy = bf(torch.randn(M, N, device=dev, generator=g))
+        x = bf(torch.randn(M, Kd, device=dev, generator=g))
+        wg = torch.randn(N, Kd, device=dev, generator=g)
+        bg = torch.randn(N, device=dev, generator=g) if i % 2 == 0 else None
+        refs.append((wg + dy.float().t() @ x.float(), None if bg is None else bg + dy.float().sum(0)))
+        items.append((dy, x, wg, bg))
+    K().linear_wgrad_grouped(items)
+    torch.cuda.synchronize()
+    odd = bf(torch.randn(10, 250, device=dev))      # rows not 16-byte aligned: not groupable (C.wgrad runs it alone)
+    assert not K().wgrad_groupable(odd, bf(torch.randn(10, 64, device=dev)), torch.zeros(250, 64, device=dev))
+    for (dy, x, wg, bg), (rw, rb) in zip(items, refs):
+        assert relerr(wg, rw) < 1e-5, dy.shape
+        if bg is not None:
+            assert relerr(bg, rb) < 1e-5
+
+
 def test_gemm_batched_heads():
     """Two-level batch strides as used by the unfused attention: z = b*H + h."""
     Bn, H, L, dh = 3, 4, 37, 32

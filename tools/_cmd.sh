@@ -1,5 +1,7 @@
 set -e
-timeout -k 10 300 python tools/gemm_bench.py --variants auto,p3,reg > gpurun_out/gemm_ab.log 2>&1
-cat gpurun_out/gemm_ab.log
-rm -rf gpurun_out/prof gpurun_out/pmcf gpurun_out/pmcw
-bash tools/gpu_suite.sh prof pmcf pmcw bench
+timeout -k 10 300 python -m pytest tests/test_gpu_kernels.py -q -m gpu -x -k "grouped or fused_rowsum or layouts" > gpurun_out/k1.log 2>&1 || { tail -30 gpurun_out/k1.log; exit 1; }
+tail -2 gpurun_out/k1.log
+bash tools/gpu_suite.sh model benchq
+rm -rf gpurun_out/prof
+bash tools/gpu_suite.sh prof
+python tools/profsum.py gpurun_out/prof/run_kernel_stats.csv 7 25
