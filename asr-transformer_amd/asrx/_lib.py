@@ -72,6 +72,7 @@ class AttnDesc(ctypes.Structure):
         ("dk", c_vp), ("dk_rstride", c_i64), ("dk_bstride", c_i64),
         ("dv", c_vp), ("dv_rstride", c_i64), ("dv_bstride", c_i64),
         ("delta", c_vp), ("dq_acc", c_vp),
+        ("dropmask", c_vp),
     ]
 
 

@@ -106,7 +106,9 @@ def attn_fwd(C, q, k, v, o, B, H, Lq, Lk, dh, strides, scale, spec):
     seed = C.seed()
     S = {"seed": seed, "spec": spec, "dims": (B, H, Lq, Lk, dh), "strides": strides, "scale": scale}
     if C.cd == torch.bfloat16 and C.attn_impl == "fused" and dh in (32, 64):
-        S["lse"] = K.attention_fwd(q, k, v, o, B, H, Lq, Lk, dh, strides, scale, spec, C.p, seed)
+        S["dropmask"] = K.dropmask_buffer(B, H, Lq, Lk, dh, C.p, q.device)
+        S["lse"] = K.attention_fwd(q, k, v, o, B, H, Lq, Lk, dh, strides, scale, spec, C.p, seed,
+                                   dropmask=S["dropmask"])
         S["impl"] = "fused"
         return S
     S["impl"] = "unfused"
@@ -131,7 +133,7 @@ def attn_bwd(C, S, q, k, v, o, do, dq, dk, dv, gstrides):
     strides, scale, spec, seed = S["strides"], S["scale"], S["spec"], S["seed"]
     if S["impl"] == "fused":
         K.attention_bwd(q, k, v, o, S["lse"], do, dq, dk, dv, B, H, Lq, Lk, dh, strides, gstrides, scale, spec,
-                        C.p, seed)
+                        C.p, seed, dropmask=S["dropmask"])
         return
     (qr, qb), (kr, kb), (vr, vb), _ = strides
     (dor, dob), (dqr, dqb), (dkr, dkb), (dvr, dvb) = gstrides

@@ -321,21 +321,30 @@ def _attn_desc(q, k, v, o, B, H, Lq, Lk, dh, strides, scale, spec, dropout_p, se
     return d
 
 
-def attention_fwd(q, k, v, o, B, H, Lq, Lk, dh, strides, scale, spec, dropout_p=0.0, seed=0):
+def dropmask_buffer(B, H, Lq, Lk, dh, dropout_p, device):
+    """Keep-bit buffer the resident-K/V attention forward fills for its backward (None when unused)."""
+    if dropout_p <= 0.0 or dh != 64 or Lk > 256:
+        return None
+    return torch.empty(B * H * ((Lq + 31) // 32) * Lk, device=device, dtype=torch.int32)
+
+
+def attention_fwd(q, k, v, o, B, H, Lq, Lk, dh, strides, scale, spec, dropout_p=0.0, seed=0, dropmask=None):
     """Fused attention (bf16). Returns lse [B*H*Lq] (log2 domain)."""
-    _cuda(q, k, v, o)
+    _cuda(q, k, v, o, dropmask)
     lse = torch.empty(B * H * Lq, device=q.device, dtype=torch.float32)
     d = _attn_desc(q, k, v, o, B, H, Lq, Lk, dh, strides, scale, spec, dropout_p, seed)
     d.lse = lse.data_ptr()
+    d.dropmask = _p(dropmask)
     call("asrx_attention_fwd", ctypes.byref(d), stream())
     return lse
 
 
 def attention_bwd(q, k, v, o, lse, do, dq, dk, dv, B, H, Lq, Lk, dh, strides, gstrides, scale, spec,
-                  dropout_p=0.0, seed=0):
-    _cuda(q, k, v, o, lse, do, dq, dk, dv)
+                  dropout_p=0.0, seed=0, dropmask=None):
+    _cuda(q, k, v, o, lse, do, dq, dk, dv, dropmask)
     d = _attn_desc(q, k, v, o, B, H, Lq, Lk, dh, strides, scale, spec, dropout_p, seed)
     d.lse = lse.data_ptr()
+    d.dropmask = _p(dropmask)
     (dor, dob), (dqr, dqb), (dkr, dkb), (dvr, dvb) = gstrides
     d.dout, d.do_rstride, d.do_bstride = do.data_ptr(), dor, dob
     d.dq, d.dq_rstride, d.dq_bstride = dq.data_ptr(), dqr, dqb

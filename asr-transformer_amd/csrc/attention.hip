@@ -14,6 +14,10 @@
 // S and dP are recomputed with the query on the accumulator row, so P and dS feed dV^T and dK^T as B operands
 // directly; dS crosses LDS once (bf16) for dQ^T = K^T dS^T, reduced over the waves in LDS and stored (or
 // accumulated with fp32 atomics when several workgroups share a (b, h)).
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
 #include "common.h"
 
 namespace {
@@ -24,11 +28,8 @@ ASRX_DEV s4_t lds_tr(const bf16_t* p) { return __builtin_amdgcn_ds_read_tr16_b64
 ASRX_DEV s4_t lds_b64(const bf16_t* p) { return *(const s4_t*)p; }
 ASRX_DEV f4_t mfma16(s4_t a, s4_t b, f4_t c) { return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0); }
 
-ASRX_DEV s4_t to_bf4(f4_t v) {
-  s4_t r;
-  r[0] = (short)f2bf(v[0]); r[1] = (short)f2bf(v[1]); r[2] = (short)f2bf(v[2]); r[3] = (short)f2bf(v[3]);
-  return r;
-}
+typedef uint32_t u2_t __attribute__((ext_vector_type(2)));
+ASRX_DEV s4_t to_bf4(f4_t v) { return __builtin_bit_cast(s4_t, (u2_t){pack2bf(v[0], v[1]), pack2bf(v[2], v[3])}); }
 
 struct AttnArgs {
   int B, H, Lq, Lk;
@@ -47,6 +48,7 @@ struct AttnArgs {
   bf16_t* dk; int64_t dkr, dkb;
   bf16_t* dv; int64_t dvr, dvb;
   float* delta; float* dq_acc;
+  uint32_t* dropmask;
 };
 
 ASRX_DEV bool masked(const AttnArgs& a, int b, int q, int key) {
@@ -124,7 +126,6 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
   for (int u = 0; u < NU; ++u) oacc[u] = f4_t{0.f, 0.f, 0.f, 0.f};
   float m_run = -INFINITY, l_run = 0.f;
-  const uint32_t drow = (uint32_t)(((int64_t)bh * a.Lq + q) * a.Lk);
 
   if (ntiles > 0) gload(0);
   for (int kt = 0; kt < ntiles; ++kt) {
@@ -164,7 +165,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
         const float p = exp2f(s[t][r] - m_use);
         rs += p;
         float pd = p;
-        if (a.thr) pd = rng_keep(a.seed, drow + (uint32_t)(kt * 64 + 16 * t + 4 * g + r), a.thr) ? p * a.dscale : 0.f;
+        if (a.thr) pd = attn_keep(a.seed, bh, a.Lq, a.Lk, q, kt * 64 + 16 * t + 4 * g + r, a.thr) ? p * a.dscale : 0.f;
         s[t][r] = pd;
       }
       pf[t] = to_bf4(s[t]);
@@ -330,7 +331,7 @@ __global__ __launch_bounds__(512) void attn_bwd_kernel(AttnArgs a, int nw, int s
         float dpe = dp[t][r];
         float pdv = p;
         if (a.thr) {
-          const bool keep = rng_keep(a.seed, (uint32_t)(((int64_t)bh * a.Lq + qq) * a.Lk + key), a.thr);
+          const bool keep = attn_keep(a.seed, bh, a.Lq, a.Lk, qq, key, a.thr);
           dpe = keep ? dpe * a.dscale : 0.f;
           pdv = keep ? p * a.dscale : 0.f;
         }
@@ -403,6 +404,469 @@ __global__ __launch_bounds__(512) void attn_bwd_kernel(AttnArgs a, int nw, int s
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Resident-K/V kernels (dh = 64, Lk <= 256: every key of a head fits in LDS).  One workgroup owns whole heads'
+// key ranges, so no key tile is loaded twice and the backward needs neither atomics nor a dQ reduction.
+// v_mfma_f32_16x16x32_bf16 throughout.  Its k-slots may be assigned to keys/queries in any order as long as
+// A and B agree: slot 8g+j of lane group g is mapped to row 16*(j>>2) + 4g + (j&3) of a 32-row block, which is
+// exactly the rows a 16x16 accumulator tile pair holds in that lane, so exponentiated scores / dS feed the next
+// MFMA straight from registers, and the matching operand comes from two ds_read_b64_tr_b16 reads.
+// ---------------------------------------------------------------------------------------------------------
+constexpr int R_MAXK = 256;
+constexpr int R_KS = 64 + 8;    // K image (forward): 144-B rows, 16-B fragment reads
+constexpr int R_VS = 64 + 16;   // V image (forward) / K image (backward): 160-B rows for the transposed reads
+constexpr int R_CS = 64 + 16;   // Q / dO chunk images (backward): row and transposed reads
+
+ASRX_DEV f4_t mfma32(s8_t a, s8_t b, f4_t c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
+ASRX_DEV s8_t cat8(s4_t x, s4_t y) { return s8_t{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]}; }
+ASRX_DEV s8_t lds_b128(const bf16_t* p) { return *(const s8_t*)p; }
+// value held by lane l ^ 1 (DPP quad_perm [1,0,3,2])
+ASRX_DEV uint32_t xchg1(uint32_t v) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true); }
+
+// max / sum over the four lanes {l, l^16, l^32, l^48} (one query's 16-lane groups): VALU permlane swaps
+ASRX_DEV float xmax4(float v) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+ASRX_DEV float xsum4(float v) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// MODE: 0 = no mask, 1 = causal / key-valid / query-valid vectors (folded into per-key biases and lse),
+// 2 = dense byte mask (generic per-element test).
+// Forward grid (ceil(Lq/256), B*H), 8 waves x 32 queries (two 16-query sub-tiles per wave).
+template <int MODE>
+__global__ __launch_bounds__(512) void attn_fwd_res_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16_t sk[R_MAXK * R_KS];
+  __shared__ __attribute__((aligned(16))) bf16_t sv[R_MAXK * R_VS];
+  __shared__ __attribute__((aligned(16))) float skb[R_MAXK];   // per-key score bias: 0 or -inf
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, li = l & 15;
+  const int nkt = (a.Lk + 31) >> 5;
+  const int nk = nkt * 32;
+  const bf16_t* Kb = a.k + b * a.kb + h * 64;
+  const bf16_t* Vb = a.v + b * a.vb + h * 64;
+  // K/V staging: every load of a batch is issued before the first LDS write (one memory latency per batch)
+  for (int c0 = threadIdx.x; c0 < nk * 8; c0 += 512 * 4) {
+    uint4 kv[4], vv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = c0 + i * 512, row = c >> 3, dc = (c & 7) * 8;
+      kv[i] = vv[i] = make_uint4(0, 0, 0, 0);
+      if (c < nk * 8 && row < a.Lk) {
+        kv[i] = *(const uint4*)(Kb + (int64_t)row * a.kr + dc);
+        vv[i] = *(const uint4*)(Vb + (int64_t)row * a.vr + dc);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = c0 + i * 512, row = c >> 3, dc = (c & 7) * 8;
+      if (c < nk * 8) {
+        *(uint4*)(sk + row * R_KS + dc) = kv[i];
+        *(uint4*)(sv + row * R_VS + dc) = vv[i];
+      }
+    }
+  }
+  if (threadIdx.x < nk) {
+    const int key = threadIdx.x;
+    bool ok = key < a.Lk;
+    if (MODE == 1 && ok && a.kvalid) ok = a.kvalid[b * a.validb + key] != 0;
+    skb[key] = ok ? 0.f : -INFINITY;
+  }
+  const int qw0 = (blockIdx.x * 8 + w) * 32;
+  s8_t qf[2][2];
+  bool qdead[2];
+#pragma unroll
+  for (int qs = 0; qs < 2; ++qs) {
+    const int q = qw0 + 16 * qs + li;
+    const bf16_t* qp = a.q + b * a.qb + (int64_t)(q < a.Lq ? q : 0) * a.qr + h * 64 + 8 * g;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) qf[qs][c] = q < a.Lq ? *(const s8_t*)(qp + 32 * c) : s8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    qdead[qs] = MODE == 1 && q < a.Lq && a.qvalid && !a.qvalid[b * a.validb + q];
+  }
+  __syncthreads();
+  if (qw0 >= a.Lq) return;   // no barrier below
+
+  f4_t o[4][2];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) o[u][0] = o[u][1] = f4_t{0.f, 0.f, 0.f, 0.f};
+  float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
+  int ktn = nkt;
+  if (MODE == 1 && a.causal) ktn = min(nkt, (min(a.Lq, qw0 + 32) - 1) / 32 + 1);
+  const int odd = li & 1;
+  const uint32_t lqh = (uint32_t)((a.Lq + 1) >> 1);
+  uint32_t prow[2];   // attention RNG pair-row bases (common.h attn_pair), 32-bit wrap as on the host side
+#pragma unroll
+  for (int qs = 0; qs < 2; ++qs) prow[qs] = ((uint32_t)bh * lqh + (uint32_t)((qw0 + 16 * qs + li) >> 1)) * (uint32_t)a.Lk;
+  uint32_t* dmw = (a.thr && a.dropmask) ? a.dropmask + ((int64_t)bh * ((a.Lq + 31) >> 5) + (qw0 >> 5)) * a.Lk : nullptr;
+
+  for (int kt = 0; kt < ktn; ++kt) {
+    f4_t s[2][2];
+    f4_t kb[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const bf16_t* kr = sk + (kt * 32 + 16 * t + li) * R_KS + 8 * g;
+      const s8_t k0 = lds_b128(kr), k1 = lds_b128(kr + 32);
+      kb[t] = *(const f4_t*)(skb + kt * 32 + 16 * t + 4 * g);
+#pragma unroll
+      for (int qs = 0; qs < 2; ++qs) s[t][qs] = mfma32(k1, qf[qs][1], mfma32(k0, qf[qs][0], f4_t{0.f, 0.f, 0.f, 0.f}));
+    }
+    const bool diag = MODE == 1 && a.causal && kt * 32 + 31 > qw0;   // tile reaches above some query
+    s4_t pf[2][2];
+    bool kp[2][2][4];
+#pragma unroll
+    for (int qs = 0; qs < 2; ++qs) {
+      const int q = qw0 + 16 * qs + li;
+      float mt = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kt * 32 + 16 * t + 4 * g + r;
+          float x;
+          if (MODE == 2) x = masked(a, b, q, key) ? -INFINITY : s[t][qs][r] * a.scale2;
+          else {
+            x = fmaf(s[t][qs][r], a.scale2, kb[t][r]);
+            if (diag && key > q) x = -INFINITY;
+          }
+          s[t][qs][r] = x;
+          mt = fmaxf(mt, x);
+        }
+      mt = xmax4(mt);
+      const float m_new = fmaxf(m_run[qs], mt);
+      const float m_use = m_new == -INFINITY ? 0.f : m_new;
+      if (__ballot(m_new != m_run[qs])) {   // rescale only when some row's max grew (exact, wave-uniform)
+        const float alpha = exp2_raw(m_run[qs] - m_use);
+        l_run[qs] *= alpha;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) o[u][qs] *= alpha;
+        m_run[qs] = m_new;
+      }
+      float rs = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        f4_t pv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pv[r] = exp2_raw(s[t][qs][r] - m_use);
+          rs += pv[r];
+        }
+        if (a.thr) {   // lanes l, l^1 hold queries 2j, 2j+1: each hashes two of the four keys, then they swap
+          const uint32_t kbse = prow[qs] + (uint32_t)(kt * 32 + 16 * t + 4 * g + 2 * odd);
+          const uint32_t hA = rng_hash(a.seed, kbse), hB = rng_hash(a.seed, kbse + 1);
+          const uint32_t oA = xchg1(hA), oB = xchg1(hB);
+          const uint32_t hh[4] = {odd ? oA : hA, odd ? oB : hB, odd ? hA : oA, odd ? hB : oB};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            kp[qs][t][r] = rng_half(hh[r], odd) >= a.thr;
+            pv[r] = kp[qs][t][r] ? pv[r] * a.dscale : 0.f;
+          }
+        }
+        pf[t][qs] = to_bf4(pv);
+      }
+      l_run[qs] += xsum4(rs);
+    }
+    if (dmw) {   // publish the keep bits: word for key kt*32 + l (l < 32) = 32 queries of this wave
+      uint32_t word = 0;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint64_t b0 = __ballot(kp[0][t][r]), b1 = __ballot(kp[1][t][r]);
+          if ((l >> 4) == t && (l & 3) == r) {
+            const int gs = 16 * ((l >> 2) & 3);
+            word = (uint32_t)((b0 >> gs) & 0xffffu) | ((uint32_t)((b1 >> gs) & 0xffffu) << 16);
+          }
+        }
+      const int key = kt * 32 + l;
+      if (l < 32 && key < a.Lk) dmw[key] = word;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bf16_t* vp = sv + (kt * 32 + 4 * g + (li >> 2)) * R_VS + 16 * u + 4 * (li & 3);
+      const s8_t vt = cat8(lds_tr(vp), lds_tr(vp + 16 * R_VS));
+#pragma unroll
+      for (int qs = 0; qs < 2; ++qs) o[u][qs] = mfma32(vt, cat8(pf[0][qs], pf[1][qs]), o[u][qs]);
+    }
+  }
+
+#pragma unroll
+  for (int qs = 0; qs < 2; ++qs) {
+    const int q = qw0 + 16 * qs + li;
+    if (q >= a.Lq) continue;
+    const bool live = !qdead[qs] && l_run[qs] > 0.f;
+    const float inv = live ? 1.f / l_run[qs] : 0.f;
+    bf16_t* op = a.o + b * a.ob + (int64_t)q * a.orr + h * 64 + 4 * g;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      uint2 st;
+      st.x = pack2bf(o[u][qs][0] * inv, o[u][qs][1] * inv);
+      st.y = pack2bf(o[u][qs][2] * inv, o[u][qs][3] * inv);
+      *(uint2*)(op + 16 * u) = st;
+    }
+    if (g == 0 && a.lse) {
+      const float mu = m_run[qs] == -INFINITY ? 0.f : m_run[qs];
+      a.lse[(int64_t)bh * a.Lq + q] = live ? mu + log2f(l_run[qs]) : INFINITY;
+    }
+  }
+}
+
+// Backward: grid (B*H), nw = max(2, ceil(Lk/32)) waves; wave w owns keys [32w, 32w+32) (dK, dV in registers)
+// and the workgroup sweeps the queries in chunks of 32: S and dP are recomputed with the query on the accumulator
+// row; Pd / dS feed dV^T / dK^T as B operands directly; dS (bf16) is published in LDS and, after the chunk's only
+// barrier, the waves split the chunk's dQ = dS K tiles (full key range -> final values, no atomics).  Q / dO of
+// the next chunk are prefetched into registers during the current one (double-buffered LDS images).  Masks:
+// key validity / padding is a per-lane score bias, query validity is folded into lse (+inf), causality is a
+// compare only in blocks that reach above the diagonal.
+template <int MODE>
+__global__ __launch_bounds__(512) void attn_bwd_res_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int nkt = (a.Lk + 31) >> 5, nk = nkt * 32;
+  const int rds = nk + 8;                                   // dS image row stride (elements)
+  bf16_t* sk = (bf16_t*)smem;                                // [nk][R_VS]
+  bf16_t* sq = sk + nk * R_VS;                               // [2][32][R_CS]
+  bf16_t* sdo = sq + 2 * 32 * R_CS;                          // [2][32][R_CS]
+  bf16_t* sds = sdo + 2 * 32 * R_CS;                         // [2][32][rds]
+  float* slse = (float*)(sds + 2 * 32 * rds);                // [2][32]  (-lse, -inf for dead queries)
+  float* sdel = slse + 64;                                   // [2][32]
+
+  const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
+  const int nthr = blockDim.x, nw = nthr >> 6;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, g = l >> 4, li = l & 15;
+  const int kw0 = 32 * w;
+  const bool kown = kw0 < nk;
+
+  const bf16_t* Kb = a.k + b * a.kb + h * 64;
+  const bf16_t* Vb = a.v + b * a.vb + h * 64;
+  for (int c0 = tid; c0 < nk * 8; c0 += nthr * 4) {
+    uint4 kv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = c0 + i * nthr, row = c >> 3, dc = (c & 7) * 8;
+      kv[i] = make_uint4(0, 0, 0, 0);
+      if (c < nk * 8 && row < a.Lk) kv[i] = *(const uint4*)(Kb + (int64_t)row * a.kr + dc);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = c0 + i * nthr, row = c >> 3, dc = (c & 7) * 8;
+      if (c < nk * 8) *(uint4*)(sk + row * R_VS + dc) = kv[i];
+    }
+  }
+  s8_t kf[2][2], vf[2][2];
+  float kbias[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int key = kw0 + 16 * t + li;
+    bool ok = key < a.Lk;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      kf[t][c] = ok ? *(const s8_t*)(Kb + (int64_t)key * a.kr + 32 * c + 8 * g) : s8_t{0, 0, 0, 0, 0, 0, 0, 0};
+      vf[t][c] = ok ? *(const s8_t*)(Vb + (int64_t)key * a.vr + 32 * c + 8 * g) : s8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+    if (MODE == 1 && ok && a.kvalid) ok = a.kvalid[b * a.validb + key] != 0;
+    kbias[t] = ok ? 0.f : -INFINITY;
+  }
+  f4_t dva[4][2], dka[4][2];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) { dva[u][t] = f4_t{0.f, 0.f, 0.f, 0.f}; dka[u][t] = f4_t{0.f, 0.f, 0.f, 0.f}; }
+
+  const bf16_t* Qb = a.q + b * a.qb + h * 64;
+  const bf16_t* Db = a.dout + b * a.dob + h * 64;
+  const float* lseb = a.lse + (int64_t)bh * a.Lq;
+  const float* delb = a.delta + (int64_t)bh * a.Lq;
+  const bool causal = MODE == 1 && a.causal;
+  const int nch = (a.Lq + 31) >> 5;
+
+  // chunk prefetch: 512 16-B pieces (Q rows then dO rows) + 32 lse + 32 delta (+ this lane's dropout words)
+  uint4 pre[4];
+  float pls = 0.f;
+  const bool usebits = a.thr && a.dropmask;
+  const uint32_t* dmb = usebits ? a.dropmask + (int64_t)bh * nch * a.Lk : nullptr;
+  uint32_t dwn[2] = {0u, 0u}, dwc[2] = {0u, 0u};
+  auto fetch = [&](int ch) {
+    const int q0 = ch * 32;
+    if (usebits) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int key = kw0 + 16 * t + li;
+        dwn[t] = key < a.Lk ? dmb[(int64_t)ch * a.Lk + key] : 0u;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + nthr * i;
+      pre[i] = make_uint4(0, 0, 0, 0);
+      if (c < 512) {
+        const int which = c >> 8, row = (c >> 3) & 31, dc = (c & 7) * 8;
+        const int q = q0 + row;
+        if (q < a.Lq) pre[i] = *(const uint4*)((which ? Db + (int64_t)q * a.dor : Qb + (int64_t)q * a.qr) + dc);
+      }
+    }
+    if (tid < 64) {
+      const int q = q0 + (tid & 31);
+      if (tid < 32) {
+        bool live = q < a.Lq;
+        if (MODE == 1 && live && a.qvalid) live = a.qvalid[b * a.validb + q] != 0;
+        pls = live ? -lseb[q] : -INFINITY;
+      } else {
+        pls = q < a.Lq ? delb[q] : 0.f;
+      }
+    }
+  };
+  auto publish = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + nthr * i;
+      if (c < 512) {
+        const int which = c >> 8, row = (c >> 3) & 31, dc = (c & 7) * 8;
+        *(uint4*)((which ? sdo : sq) + (buf * 32 + row) * R_CS + dc) = pre[i];
+      }
+    }
+    if (tid < 64) (tid < 32 ? slse : sdel)[buf * 32 + (tid & 31)] = pls;
+  };
+
+  fetch(0);
+  publish(0);
+  __syncthreads();
+
+  for (int ch = 0; ch < nch; ++ch) {
+    const int buf = ch & 1, q0 = ch * 32;
+    dwc[0] = dwn[0]; dwc[1] = dwn[1];
+    if (ch + 1 < nch) fetch(ch + 1);
+    const bool active = kown && !(causal && kw0 > q0 + 31);   // causal: keys above every query of the chunk
+    if (active) {
+      const bf16_t* cq = sq + buf * 32 * R_CS;
+      const bf16_t* cdo = sdo + buf * 32 * R_CS;
+      f4_t s[2][2], dp[2][2];   // [qs][t]
+#pragma unroll
+      for (int qs = 0; qs < 2; ++qs) {
+        const bf16_t* qr = cq + (16 * qs + li) * R_CS + 8 * g;
+        const bf16_t* dr = cdo + (16 * qs + li) * R_CS + 8 * g;
+        const s8_t q0f = lds_b128(qr), q1f = lds_b128(qr + 32);
+        const s8_t d0f = lds_b128(dr), d1f = lds_b128(dr + 32);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          s[qs][t] = mfma32(q1f, kf[t][1], mfma32(q0f, kf[t][0], f4_t{0.f, 0.f, 0.f, 0.f}));
+          dp[qs][t] = mfma32(d1f, vf[t][1], mfma32(d0f, vf[t][0], f4_t{0.f, 0.f, 0.f, 0.f}));
+        }
+      }
+      const bool diag = causal && kw0 + 31 > q0;
+      s4_t pdb[2][2], dsb[2][2];
+#pragma unroll
+      for (int qs = 0; qs < 2; ++qs) {
+        const f4_t nlse4 = *(const f4_t*)(slse + buf * 32 + 16 * qs + 4 * g);
+        const f4_t del4 = *(const f4_t*)(sdel + buf * 32 + 16 * qs + 4 * g);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int key = kw0 + 16 * t + li;
+          const int qb = q0 + 16 * qs + 4 * g;
+          uint32_t h01 = 0, h23 = 0;
+          if (a.thr && !usebits) {
+            h01 = rng_hash(a.seed, attn_pair(bh, a.Lq, a.Lk, qb, key));
+            h23 = rng_hash(a.seed, attn_pair(bh, a.Lq, a.Lk, qb + 2, key));
+          }
+          f4_t pd, dsv;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float x;
+            if (MODE == 2) x = masked(a, b, qb + r, key) ? -INFINITY : fmaf(s[qs][t][r], a.scale2, nlse4[r]);
+            else {
+              x = fmaf(s[qs][t][r], a.scale2, nlse4[r]) + kbias[t];
+              if (diag && key > qb + r) x = -INFINITY;
+            }
+            const float p = exp2_raw(x);
+            float dpe = dp[qs][t][r], pdv = p;
+            if (a.thr) {
+              const bool keep = usebits ? ((dwc[t] >> (16 * qs + 4 * g + r)) & 1u)
+                                        : (rng_half(r < 2 ? h01 : h23, r & 1) >= a.thr);
+              dpe = keep ? dpe * a.dscale : 0.f;
+              pdv = keep ? p * a.dscale : 0.f;
+            }
+            pd[r] = pdv;
+            dsv[r] = p * (dpe - del4[r]);
+          }
+          pdb[qs][t] = to_bf4(pd);
+          dsb[qs][t] = to_bf4(dsv);
+          bf16_t* dsp = sds + (buf * 32 + 16 * qs + 4 * g) * rds + key;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dsp[r * rds] = (bf16_t)dsb[qs][t][r];
+        }
+      }
+      // dV^T += dO^T Pd ; dK^T += Q^T dS   (k-slots: queries 4g+j of sub-tile 0, then of sub-tile 1)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int off = (4 * g + (li >> 2)) * R_CS + 16 * u + 4 * (li & 3);
+        const s8_t doT = cat8(lds_tr(cdo + off), lds_tr(cdo + off + 16 * R_CS));
+        const s8_t qT = cat8(lds_tr(cq + off), lds_tr(cq + off + 16 * R_CS));
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          dva[u][t] = mfma32(doT, cat8(pdb[0][t], pdb[1][t]), dva[u][t]);
+          dka[u][t] = mfma32(qT, cat8(dsb[0][t], dsb[1][t]), dka[u][t]);
+        }
+      }
+    }
+    if (ch + 1 < nch) publish(buf ^ 1);
+    __syncthreads();
+    // dQ^T[d][q] = sum_key K^T[d][key] dS^T[key][q] over the chunk's 8 (sub-tile, 16-column) tiles; every
+    // operand of a tile is read before its MFMA chain starts
+    int kcn = nkt;
+    if (causal) kcn = min(nkt, (q0 + 31) / 32 + 1);
+    for (int tl = w; tl < 8; tl += nw) {
+      const int qs = tl >> 2, u = tl & 3;
+      const bf16_t* dsr = sds + (buf * 32 + 16 * qs + li) * rds + 8 * g;
+      const bf16_t* kp = sk + (8 * g + (li >> 2)) * R_VS + 16 * u + 4 * (li & 3);
+      s8_t ka[8], da[8];
+#pragma unroll
+      for (int kc = 0; kc < 8; ++kc)
+        if (kc < kcn) {
+          ka[kc] = cat8(lds_tr(kp + 32 * kc * R_VS), lds_tr(kp + (32 * kc + 4) * R_VS));
+          da[kc] = lds_b128(dsr + 32 * kc);
+        }
+      f4_t acc = f4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kc = 0; kc < 8; ++kc)
+        if (kc < kcn) acc = mfma32(ka[kc], da[kc], acc);
+      const int q = q0 + 16 * qs + li;
+      if (q < a.Lq) {
+        uint2 x;
+        x.x = pack2bf(acc[0] * a.scale, acc[1] * a.scale);
+        x.y = pack2bf(acc[2] * a.scale, acc[3] * a.scale);
+        *(uint2*)(a.dq + b * a.dqb + (int64_t)q * a.dqr + h * 64 + 16 * u + 4 * g) = x;
+      }
+    }
+  }
+
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int key = kw0 + 16 * t + li;
+    if (!kown || key >= a.Lk) continue;
+    bf16_t* dkp = a.dk + b * a.dkb + (int64_t)key * a.dkr + h * 64 + 4 * g;
+    bf16_t* dvp = a.dv + b * a.dvb + (int64_t)key * a.dvr + h * 64 + 4 * g;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      uint2 x;
+      x.x = pack2bf(dka[u][t][0] * a.scale, dka[u][t][1] * a.scale);
+      x.y = pack2bf(dka[u][t][2] * a.scale, dka[u][t][3] * a.scale);
+      *(uint2*)(dkp + 16 * u) = x;
+      x.x = pack2bf(dva[u][t][0], dva[u][t][1]);
+      x.y = pack2bf(dva[u][t][2], dva[u][t][3]);
+      *(uint2*)(dvp + 16 * u) = x;
+    }
+  }
+}
+
+size_t bwd_res_smem(int lk) {
+  const int nk = (lk + 31) / 32 * 32;
+  return (size_t)(nk * R_VS + 4 * 32 * R_CS + 2 * 32 * (nk + 8)) * 2 + 128 * 4;
+}
+
 // dq (bf16, strided) = scale * dq_acc (fp32 [B][Lq][H][DH])
 __global__ __launch_bounds__(256) void dq_finish_kernel(AttnArgs a, int dh) {
   const int64_t total = (int64_t)a.B * a.Lq * a.H * dh;
@@ -444,7 +908,15 @@ int fill_args(const asrx_attn_desc* d, AttnArgs& a) {
   a.dk = (bf16_t*)d->dk; a.dkr = d->dk_rstride; a.dkb = d->dk_bstride;
   a.dv = (bf16_t*)d->dv; a.dvr = d->dv_rstride; a.dvb = d->dv_bstride;
   a.delta = d->delta; a.dq_acc = d->dq_acc;
+  a.dropmask = d->dropmask;
   return ASRX_OK;
+}
+
+// Lk <= 256 and dh = 64 -> resident-K/V kernels (ASRX_ATTN_KERNEL=tiled forces the general tiled kernels)
+bool resident_ok(const asrx_attn_desc* d, const AttnArgs& a) {
+  const char* e = getenv("ASRX_ATTN_KERNEL");
+  if (e && !strcmp(e, "tiled")) return false;
+  return d->dh == 64 && a.Lk <= R_MAXK && (a.orr % 4) == 0 && (a.ob % 4) == 0;
 }
 
 size_t bwd_smem(int nw, int dh) {
@@ -459,9 +931,18 @@ extern "C" int asrx_attention_fwd(const asrx_attn_desc* d, void* stream) {
   int rc = fill_args(d, a);
   if (rc) return rc;
   if (!a.o || (a.orr % 4) || (a.ob % 4) || ((uintptr_t)a.o % 8)) return ASRX_ERR_UNSUPPORTED;
+  hipStream_t st = (hipStream_t)stream;
+  if (resident_ok(d, a)) {
+    // 8 waves always: idle query waves still help stage K/V, then leave
+    dim3 grid((a.Lq + 255) / 256, a.B * a.H);
+    if (a.mode == 0) hipLaunchKernelGGL(attn_fwd_res_kernel<0>, grid, dim3(512), 0, st, a);
+    else if (a.mode == 1) hipLaunchKernelGGL(attn_fwd_res_kernel<1>, grid, dim3(512), 0, st, a);
+    else hipLaunchKernelGGL(attn_fwd_res_kernel<2>, grid, dim3(512), 0, st, a);
+    ASRX_CHECK_LAUNCH();
+    return ASRX_OK;
+  }
   dim3 grid((a.Lq + 63) / 64, a.B * a.H);
   if (grid.y > 65535u * 1024u) return ASRX_ERR_ARG;
-  hipStream_t st = (hipStream_t)stream;
   if (d->dh == 64) hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL(attn_fwd_kernel<32>, grid, dim3(256), 0, st, a);
   ASRX_CHECK_LAUNCH();
@@ -492,6 +973,15 @@ extern "C" int asrx_attention_bwd(const asrx_attn_desc* d, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   rc = asrx_attn_delta(d, stream);
   if (rc) return rc;
+  if (resident_ok(d, a) && a.dqr % 4 == 0 && a.dqb % 4 == 0 && (uintptr_t)a.dq % 8 == 0) {
+    const int nw = std::max(2, (a.Lk + 31) / 32);
+    const size_t sm = bwd_res_smem(a.Lk);
+    if (a.mode == 0) hipLaunchKernelGGL(attn_bwd_res_kernel<0>, dim3(a.B * a.H), dim3(64 * nw), sm, st, a);
+    else if (a.mode == 1) hipLaunchKernelGGL(attn_bwd_res_kernel<1>, dim3(a.B * a.H), dim3(64 * nw), sm, st, a);
+    else hipLaunchKernelGGL(attn_bwd_res_kernel<2>, dim3(a.B * a.H), dim3(64 * nw), sm, st, a);
+    ASRX_CHECK_LAUNCH();
+    return ASRX_OK;
+  }
   int nw = (a.Lk + 31) / 32;
   if (nw > 8) nw = 8;
   const int nblk = (a.Lk + 32 * nw - 1) / (32 * nw);

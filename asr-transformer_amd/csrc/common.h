@@ -14,39 +14,54 @@ typedef float f4_t __attribute__((ext_vector_type(4)));
 
 ASRX_DEV float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 
-// round-to-nearest-even; NaN stays NaN
-ASRX_DEV bf16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (bf16_t)(u >> 16);
+// f32 -> bf16, round-to-nearest-even, NaN stays NaN: a plain conversion, which hipcc lowers to gfx950's
+// v_cvt_pk_bf16_f32 (one instruction per PAIR in pack2bf)
+typedef float f2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
+ASRX_DEV bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+ASRX_DEV uint32_t pack2bf(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f2_t){a, b}, bf2_t));
 }
 
-ASRX_DEV uint32_t pack2bf(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+// raw v_exp_f32 (2^x; -inf -> 0): the softmax arguments are <= 0, so no range reduction is needed
+ASRX_DEV float exp2_raw(float x) { return __builtin_amdgcn_exp2f(x); }
 
-// Counter-based dropout RNG: a keyed 32-bit mixer of (seed, element index). Not bitwise torch-compatible
-// (documented in DESIGN.md); forward and backward regenerate the same mask from (seed, index).
-ASRX_DEV uint32_t rng_hash(uint64_t seed, uint32_t idx) {
-  uint32_t x = idx ^ (uint32_t)seed;
-  x *= 0x9E3779B1u;
+// Counter-based dropout RNG (not bitwise torch-compatible; documented in DESIGN.md).  One 32-bit keyed mix
+// (lowbias32-style: 2 multiplies, 3 xor-shifts, seed folded in at both ends) per PAIR of elements: the low
+// 16 bits decide the first element, the high 16 bits the second, against a 16-bit threshold p * 65536.
+// Forward and backward regenerate the same decisions from (seed, index).
+//   element streams (GEMM epilogue, LayerNorm backward, embedding): element idx -> pair idx >> 1, half idx & 1
+//   attention probabilities [bh][q][key]: pair = (bh * ceil(Lq/2) + q/2) * Lk + key, half = q & 1 (pairs run
+//   along queries, so a lane holding 4 consecutive queries of one key needs 2 hashes)
+ASRX_DEV uint32_t rng_hash(uint64_t seed, uint32_t pidx) {
+  uint32_t x = pidx ^ (uint32_t)seed;
   x ^= x >> 16;
-  x = x * 0x85EBCA6Bu + (uint32_t)(seed >> 32);
-  x ^= x >> 13;
-  x *= 0xC2B2AE35u;
-  x ^= x >> 16;
-  x = x * 0x27D4EB2Fu + 0x165667B1u;
+  x *= 0x7feb352dU;
   x ^= x >> 15;
+  x = x * 0x846ca68bU + (uint32_t)(seed >> 32);
+  x ^= x >> 16;
   return x;
 }
 
-// keep with probability 1-p: threshold = p * 2^32
-ASRX_DEV bool rng_keep(uint64_t seed, uint32_t idx, uint32_t threshold) { return rng_hash(seed, idx) >= threshold; }
+ASRX_DEV uint32_t rng_half(uint32_t h, uint32_t which) { return which ? (h >> 16) : (h & 0xffffu); }
+
+// keep with probability 1 - p: threshold = p * 65536 (0 = no dropout)
+ASRX_DEV bool rng_keep(uint64_t seed, uint32_t idx, uint32_t threshold) {
+  return rng_half(rng_hash(seed, idx >> 1), idx & 1u) >= threshold;
+}
+
+ASRX_DEV uint32_t attn_pair(int64_t bh, int lq, int lk, int q, int key) {
+  return (uint32_t)((bh * ((lq + 1) >> 1) + (q >> 1)) * (int64_t)lk + key);
+}
+
+ASRX_DEV bool attn_keep(uint64_t seed, int64_t bh, int lq, int lk, int q, int key, uint32_t threshold) {
+  return rng_half(rng_hash(seed, attn_pair(bh, lq, lk, q, key)), q & 1) >= threshold;
+}
 
 static inline uint32_t drop_threshold(float p) {
   if (p <= 0.f) return 0u;
-  double t = (double)p * 4294967296.0;
-  if (t >= 4294967295.0) return 0xffffffffu;
-  return (uint32_t)t;
+  if (p >= 1.f) return 65536u;
+  return (uint32_t)((double)p * 65536.0 + 0.5);
 }
 
 ASRX_DEV float wave_sum(float v) {

@@ -118,9 +118,9 @@ __global__ __launch_bounds__(256) void softmax_fwd_kernel(SmArgs a) {
     for (int i = 0; i < V; ++i) o[i] = v[j][i] * inv;
     st_vec<V>(a.p, a.dtype, rr * a.ld + k0, o, nv);
     if (a.pd) {
-      const uint32_t base = (uint32_t)(rr * a.lk + k0);
 #pragma unroll
-      for (int i = 0; i < V; ++i) o[i] = (a.thr == 0u || rng_keep(a.seed, base + i, a.thr)) ? o[i] * a.dscale : 0.f;
+      for (int i = 0; i < V; ++i)
+        o[i] = (a.thr == 0u || attn_keep(a.seed, bh, a.lq, a.lk, q, k0 + i, a.thr)) ? o[i] * a.dscale : 0.f;
       st_vec<V>(a.pd, a.dtype, rr * a.ld + k0, o, nv);
     }
   }
@@ -142,10 +142,9 @@ __global__ __launch_bounds__(256) void softmax_bwd_kernel(SmArgs a, void* ds) {
     const int nv = max(0, min(V, a.lk - k0));
     ld_vec<V>(a.p, a.dtype, rr * a.ld + k0, pv[j], nv);
     ld_vec<V>(a.pd, a.dtype, rr * a.ld + k0, gv[j], nv);
-    const uint32_t base = (uint32_t)(rr * a.lk + k0);
 #pragma unroll
     for (int i = 0; i < V; ++i) {
-      if (a.thr) gv[j][i] = rng_keep(a.seed, base + i, a.thr) ? gv[j][i] * a.dscale : 0.f;
+      if (a.thr) gv[j][i] = attn_keep(a.seed, rr / a.lq, a.lq, a.lk, (int)(rr % a.lq), k0 + i, a.thr) ? gv[j][i] * a.dscale : 0.f;
       dot += pv[j][i] * gv[j][i];
     }
   }

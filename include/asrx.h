@@ -122,6 +122,10 @@ typedef struct asrx_attn_desc {
   void* dv; int64_t dv_rstride, dv_bstride;
   float* delta;                 /* [batch*heads*lq] workspace */
   float* dq_acc;                /* [batch*lq*heads*dh] fp32 workspace, used when lk > 256 */
+  /* optional dropout keep bits [batch*heads][ceil(lq/32)][lk] (bit i of a word = query 32*c + i): written by the
+   * forward when dh = 64, lk <= 256 and dropout_p > 0, read by the backward instead of re-hashing.  The bits
+   * equal the counter-based RNG's decisions, so passing NULL to either side gives identical results. */
+  uint32_t* dropmask;
 } asrx_attn_desc;
 
 int asrx_attention_fwd(const asrx_attn_desc* d, void* stream);

@@ -1,6 +1,8 @@
 """Per-kernel numerics of libasrx.so on the GPU vs plain PyTorch fp32/fp64 references."""
 import math
 
+import numpy as np
+
 import pytest
 import torch
 
@@ -226,11 +228,25 @@ def _masked(kind, B, Lq, Lk, valid):
     return m.unsqueeze(1)
 
 
+@pytest.fixture
+def attn_variant(request):
+    import os
+    old = os.environ.get("ASRX_ATTN_KERNEL")
+    os.environ["ASRX_ATTN_KERNEL"] = request.param
+    yield request.param
+    if old is None:
+        os.environ.pop("ASRX_ATTN_KERNEL", None)
+    else:
+        os.environ["ASRX_ATTN_KERNEL"] = old
+
+
+@pytest.mark.parametrize("attn_variant", ["auto", "tiled"], indirect=True)
 @pytest.mark.parametrize("dh", [32, 64])
 @pytest.mark.parametrize("B,H,Lq,Lk,kind", [(2, 4, 70, 70, "decoder"), (3, 2, 64, 249, "none"),
                                            (2, 2, 249, 249, "none"), (1, 2, 100, 300, "none"),
-                                           (2, 3, 33, 33, "decoder")])
-def test_attention_fused(dh, B, H, Lq, Lk, kind):
+                                           (2, 3, 33, 33, "decoder"), (1, 2, 300, 64, "none"),
+                                           (2, 2, 256, 256, "decoder"), (1, 1, 5, 17, "none")])
+def test_attention_fused(dh, B, H, Lq, Lk, kind, attn_variant):
     from asrx.kernels import MaskSpec
     g = torch.Generator().manual_seed(B * 100 + Lq + Lk + dh)
     q, kv, valid = _mk(B, H, Lq, Lk, dh, kind, g)
@@ -274,11 +290,15 @@ def test_attention_fused(dh, B, H, Lq, Lk, kind):
     assert relerr(dq_, qh.grad) < 2e-2
 
 
-def test_attention_dense_mask_and_dropout_consistency():
-    """Dense byte mask (mode 2) equals the structured decoder mask; dropout forward/backward are consistent
-    with an explicit mask regenerated from the same RNG stream."""
+@pytest.mark.parametrize("attn_variant", ["auto", "tiled"], indirect=True)
+@pytest.mark.parametrize("L", [40, 249])
+@pytest.mark.parametrize("bits", [False, True])
+def test_attention_dense_mask_and_dropout_consistency(L, attn_variant, bits):
+    """Dense byte mask (mode 2) equals the structured decoder mask; the dropout the kernels apply in forward AND
+    backward is exactly the keep mask of the numpy RNG restatement (tests/rng_ref.py)."""
     from asrx.kernels import MaskSpec
-    B, H, L, dh = 2, 2, 40, 64
+    from rng_ref import attn_keep, elem_keep
+    B, H, dh = 2, 2, 64
     d = H * dh
     g = torch.Generator().manual_seed(9)
     q, kv, valid = _mk(B, H, L, L, dh, "decoder", g)
@@ -293,18 +313,38 @@ def test_attention_dense_mask_and_dropout_consistency():
     K().attention_fwd(qd, kvd, kvd[..., d:], o1, B, H, L, L, dh, st, d ** -0.5, s1)
     K().attention_fwd(qd, kvd, kvd[..., d:], o2, B, H, L, L, dh, st, d ** -0.5, s2)
     assert torch.equal(o1, o2)
-    # dropout: fused kernel vs unfused (softmax kernel) path share the RNG index (bh*Lq + q)*Lk + key
     p, seed = 0.3, 1234
     o3 = torch.empty_like(o1)
-    K().attention_fwd(qd, kvd, kvd[..., d:], o3, B, H, L, L, dh, st, d ** -0.5, s1, p, seed)
-    keep = K().dropout_mask(B * H * L * L, p, seed, dev).view(B, H, L, L).cpu().double() / (1 - p)
-    qh = bf(q).double().view(B, L, H, dh).transpose(1, 2)
-    kh = bf(kv)[..., :d].double().reshape(B, L, H, dh).transpose(1, 2)
-    vh = bf(kv)[..., d:].double().reshape(B, L, H, dh).transpose(1, 2)
+    dm = K().dropmask_buffer(B, H, L, L, dh, p, dev) if bits else None
+    lse = K().attention_fwd(qd, kvd, kvd[..., d:], o3, B, H, L, L, dh, st, d ** -0.5, s1, p, seed, dropmask=dm)
+    if dm is not None and attn_variant == "auto":   # the forward's published keep bits == the RNG's decisions
+        ka = attn_keep(seed, B * H, L, L, p)
+        nq = (L + 31) // 32
+        words = dm.cpu().numpy().view(np.uint32).reshape(B * H, nq, L)
+        bits_np = (words[:, :, None, :] >> np.arange(32, dtype=np.uint32)[None, None, :, None]) & 1
+        got = bits_np.reshape(B * H, nq * 32, L)[:, :L, :].astype(bool)
+        live = ~masked.expand(B, H, L, L).reshape(B * H, L, L).numpy()   # words of masked-out tiles are never read
+        assert (got == ka)[live].all()
+    keep = torch.from_numpy(attn_keep(seed, B * H, L, L, p)).view(B, H, L, L).double() / (1 - p)
+    em = K().dropout_mask(B * H * L * L, p, seed, dev).cpu().numpy().astype(bool)
+    assert (em == elem_keep(seed, B * H * L * L, p)).all()   # element stream bit-exact vs the numpy restatement
+    qh = bf(q).double().view(B, L, H, dh).transpose(1, 2).requires_grad_(True)
+    kh = bf(kv)[..., :d].double().reshape(B, L, H, dh).transpose(1, 2).contiguous().requires_grad_(True)
+    vh = bf(kv)[..., d:].double().reshape(B, L, H, dh).transpose(1, 2).contiguous().requires_grad_(True)
     ref, _ = ref_attention(qh, kh, vh, d ** -0.5, masked, keep)
-    assert relerr(o3.float().cpu().view(B, L, H, dh).transpose(1, 2), ref) < 1e-2
+    assert relerr(o3.float().cpu().view(B, L, H, dh).transpose(1, 2), ref.detach()) < 1e-2
     frac = float((keep > 0).double().mean())
-    assert abs(frac - (1 - p)) < 0.01
+    assert abs(frac - (1 - p)) < 0.02
+    dO = bf(torch.randn(B, L, d, generator=g))
+    ref.backward(dO.double().view(B, L, H, dh).transpose(1, 2))
+    dq = torch.empty(B * L, d, device=dev, dtype=torch.bfloat16)
+    dkv = torch.empty(B * L, 2 * d, device=dev, dtype=torch.bfloat16)
+    gst = ((d, L * d), (d, L * d), (2 * d, L * 2 * d), (2 * d, L * 2 * d))
+    K().attention_bwd(qd, kvd, kvd[..., d:], o3, lse, dO.to(dev), dq, dkv, dkv[:, d:], B, H, L, L, dh, st, gst,
+                      d ** -0.5, s1, p, seed, dropmask=dm if (dm is not None and attn_variant == "auto") else None)
+    assert relerr(dkv[:, d:].float().cpu().view(B, L, H, dh).transpose(1, 2), vh.grad) < 2e-2
+    assert relerr(dkv[:, :d].float().cpu().view(B, L, H, dh).transpose(1, 2), kh.grad) < 2e-2
+    assert relerr(dq.float().cpu().view(B, L, H, dh).transpose(1, 2), qh.grad) < 2e-2
 
 
 # ------------------------------------------------------------------------------------------------ softmax

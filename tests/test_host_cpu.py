@@ -151,3 +151,18 @@ def test_gemm_kernel_plan_names_without_gpu():
         assert kernel_name(desc(15936, 1536, 512)).startswith("gemm_bf16_kernel<128, 128, false, false, true>")
     finally:
         os.environ.pop("ASRX_GEMM_KERNEL")
+
+
+def test_rng_restatement_statistics():
+    """The numpy RNG restatement (test oracle of the dropout masks) keeps 1-p of the elements, pairs halves of
+    one hash, and attention pairs run along queries."""
+    import numpy as np
+    from rng_ref import attn_keep, elem_keep, rng_hash, threshold
+    assert threshold(0.1) == 6554 and threshold(0) == 0 and threshold(1.0) == 65536
+    k = elem_keep(7, 1 << 20, 0.1)
+    assert abs(k.mean() - 0.9) < 0.002
+    h = rng_hash(7, np.arange(4, dtype=np.uint64))
+    assert len(set(h.tolist())) == 4
+    a = attn_keep(7, 3, 9, 13, 0.25)
+    assert a.shape == (3, 9, 13) and abs(a.mean() - 0.75) < 0.1
+    assert not elem_keep(7, 1000, 1.0).any() and elem_keep(7, 1000, 0.0).all()

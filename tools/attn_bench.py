@@ -1,0 +1,86 @@
+"""Attention micro-benchmark on the c3 shapes (B=64, h=8, dh=64): encoder self (249x249), cross (64x249),
+decoder self (64x64, causal + padding), forward and backward, dropout 0.1.
+
+    python tools/attn_bench.py [--reps 20] [--only enc,cross,dec] [--variant auto|tiled]
+"""
+import argparse
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "asr-transformer_amd"))
+
+import torch  # noqa: E402
+
+from asrx import kernels as K  # noqa: E402
+from asrx.kernels import MaskSpec  # noqa: E402
+
+B, H, DH = 64, 8, 64
+D = H * DH
+
+
+def case(name, Lq, Lk, causal):
+    g = torch.Generator(device="cuda").manual_seed(0)
+    q = torch.randn(B * Lq, D, device="cuda", generator=g).bfloat16()
+    kv = torch.randn(B * Lk, 2 * D, device="cuda", generator=g).bfloat16()
+    o = torch.empty(B * Lq, D, device="cuda", dtype=torch.bfloat16)
+    do = torch.randn(B * Lq, D, device="cuda", generator=g).bfloat16()
+    dq = torch.empty_like(q)
+    dkv = torch.empty_like(kv)
+    if causal:
+        valid = torch.ones(B, Lq, device="cuda", dtype=torch.uint8)
+        valid[:, Lq - 8:] = 0
+        spec = MaskSpec(1, True, valid, valid, valid.stride(0))
+    else:
+        spec = MaskSpec()
+    st = ((D, Lq * D), (2 * D, Lk * 2 * D), (2 * D, Lk * 2 * D), (D, Lq * D))
+    gst = ((D, Lq * D), (D, Lq * D), (2 * D, Lk * 2 * D), (2 * D, Lk * 2 * D))
+    p, seed = 0.1, 77
+    dm = K.dropmask_buffer(B, H, Lq, Lk, DH, p, "cuda")
+    state = {}
+
+    def fwd():
+        state["lse"] = K.attention_fwd(q, kv, kv[:, D:], o, B, H, Lq, Lk, DH, st, D ** -0.5, spec, p, seed,
+                                       dropmask=dm)
+
+    def bwd():
+        K.attention_bwd(q, kv, kv[:, D:], o, state["lse"], do, dq, dkv, dkv[:, D:], B, H, Lq, Lk, DH, st, gst,
+                        D ** -0.5, spec, p, seed, dropmask=dm)
+
+    flops_f = 4.0 * B * H * Lq * Lk * DH
+    return name, fwd, bwd, flops_f, 2.5 * flops_f
+
+
+def timeit(fn, reps):
+    ts = []
+    for _ in range(reps + 3):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        e.synchronize()
+        ts.append(s.elapsed_time(e))
+    ts = sorted(ts[3:])
+    return ts[len(ts) // 2]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--only", default="enc,cross,dec")
+    ap.add_argument("--variant", default="auto")
+    args = ap.parse_args()
+    os.environ["ASRX_ATTN_KERNEL"] = args.variant
+    cases = {"enc": ("enc_self", 249, 249, False), "cross": ("cross", 64, 249, False),
+             "dec": ("dec_self", 64, 64, True)}
+    for key in args.only.split(","):
+        name, fwd, bwd, ff, fb = case(*cases[key])
+        fwd()
+        tf = timeit(fwd, args.reps)
+        tb = timeit(bwd, args.reps)   # includes the delta prologue kernel
+        print(f"{name:9s} fwd {tf*1e3:7.1f}us {ff/tf/1e9:6.0f}TF | bwd {tb*1e3:7.1f}us {fb/tb/1e9:6.0f}TF "
+              f"(bwd counted as 2.5x fwd FLOPs)", flush=True)
+
+
+if __name__ == "__main__":
+    main()
