@@ -431,27 +431,27 @@ enum : int {
   E_ROWADD = 256, E_GENERIC = 1 << 30
 };
 
-template <int EPI>
-ASRX_DEV void epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int wn, f4_t (&acc)[4][4]) {
+template <int EPI, int TN, int TM>
+ASRX_DEV void epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int wn, f4_t (&acc)[TN][TM]) {
   const int l = threadIdx.x & 63, gq = l >> 4;
   if constexpr (EPI == E_GENERIC) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < TN; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < TM; ++j) {
         float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
         epilogue4(g, z, m0 + wm + 16 * j + (l & 15), n0 + wn + 16 * i + 4 * gq, v);
       }
   } else {
     // fast path (host-checked): batch 1, N % 4 == 0, 16-B aligned rows; gate bf16, resid fp32
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < TN; ++i) {
       const int n = n0 + wn + 16 * i + 4 * gq;
       if (n >= g.N) continue;
       f4_t b4 = f4_t{0.f, 0.f, 0.f, 0.f};
       if constexpr ((EPI & E_BIAS) != 0) b4 = *(const f4_t*)(g.bias + n);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < TM; ++j) {
         const int m = m0 + wm + 16 * j + (l & 15);
         if (m >= g.M) continue;
         f4_t v = acc[i][j];
@@ -462,10 +462,13 @@ ASRX_DEV void epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, in
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
         }
-        if constexpr ((EPI & E_DROP) != 0) {
-          const uint32_t base = (uint32_t)((int64_t)m * g.N + n);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = rng_keep(g.seed, base + e, g.drop_thr) ? v[e] * g.drop_scale : 0.f;
+        if constexpr ((EPI & E_DROP) != 0) {   // n % 4 == 0 and N even: two pair hashes cover the 4 elements
+          const uint32_t pb = (uint32_t)((int64_t)m * g.N + n) >> 1;
+          const uint32_t h0 = rng_hash(g.seed, pb), h1 = rng_hash(g.seed, pb + 1);
+          v[0] = rng_half(h0, 0) >= g.drop_thr ? v[0] * g.drop_scale : 0.f;
+          v[1] = rng_half(h0, 1) >= g.drop_thr ? v[1] * g.drop_scale : 0.f;
+          v[2] = rng_half(h1, 0) >= g.drop_thr ? v[2] * g.drop_scale : 0.f;
+          v[3] = rng_half(h1, 1) >= g.drop_thr ? v[3] * g.drop_scale : 0.f;
         }
         if constexpr ((EPI & E_GATE) != 0) {
           const uint2 gt = *(const uint2*)((const bf16_t*)g.gate + (int64_t)m * g.ld_gate + n);
@@ -854,6 +857,192 @@ void dispatch_p3(const GemmArgs& g, int epi, int ntiles, int splitk, int batch, 
 // ------------------------------------------------------------------------------------------------
 // fp32 kernel (exact fp32 MFMA; parity path)
 // ------------------------------------------------------------------------------------------------
+// ------------------------------------------------------------------------------------------------
+// bf16 "ring" kernel for small output grids (e.g. the decoder's M = B*L = 4096 projections): BMxBN tiles
+// (64x64 or 128x64), 4 waves (2x2), one tile per workgroup, a 4-stage LDS-DMA ring so three K-steps are in
+// flight while one is computed: a small tile is bound by bytes in flight per CU (latency x ingest rate), not
+// by its MFMAs.  Tiles are handed out XCD-contiguously (row panels share an L2).  Same images/swizzles/
+// descriptors as p3.
+// ------------------------------------------------------------------------------------------------
+constexpr int R_THREADS = 256;
+
+template <int R, bool KSTRIDED>
+struct RStage {
+  static constexpr int NI = R * BK * 2 / (R_THREADS * 16);
+  static_assert(NI >= 1, "tile too small for one LDS-DMA piece per thread");
+  uint32_t voff[NI];
+  ASRX_DEV void set_tile(int r0, int64_t ld) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int o = (j * 4 + w) * 1024 + l * 16;
+      if constexpr (!KSTRIDED) {
+        const int r = o >> 7, c = ((o >> 4) & 7) ^ ((r >> 1) & 7);
+        voff[j] = (uint32_t)(((int64_t)(r0 + r) * ld + c * 8) * 2);
+      } else {
+        constexpr int RB = R * 2;
+        const int kr = o / RB, c16 = (o % RB) >> 4;
+        const int c32 = (c16 >> 1) ^ ks_swz<(R >= 128 ? 128 : 64)>(kr);
+        voff[j] = (uint32_t)(((int64_t)kr * ld + r0 + c32 * 16 + (c16 & 1) * 8) * 2);
+      }
+    }
+  }
+  ASRX_DEV void issue(unsigned char* img, const bf16_t* base, int64_t ld, int64_t total_bytes, int k0) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const int64_t koff = KSTRIDED ? (int64_t)k0 * ld * 2 : (int64_t)k0 * 2;
+    const int64_t rem = total_bytes - koff;
+    __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const char*)base + koff), (short)0, (int)(rem > 0x7fffffff ? 0x7fffffff : rem), 0x00020000);
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_t*)(img + (j * 4 + w) * 1024), 16, voff[j], 0, 0, 0);
+#endif
+  }
+};
+
+template <int R, bool KSTRIDED>
+ASRX_DEV s8_t r_frag(const unsigned char* img, int i0, int ks) {
+  const int l = threadIdx.x & 63, g = l >> 4;
+  if constexpr (!KSTRIDED) {
+    const int r = i0 + (l & 15);
+    const int c = (ks * 4 + g) ^ ((r >> 1) & 7);
+    return *(const s8_t*)(img + r * 128 + c * 16);
+  } else {
+    constexpr int SW = R >= 128 ? 128 : 64;
+    const bf16_t* t = (const bf16_t*)img;
+    const int i = l & 15, q = i >> 2, p = i & 3;
+    const int k1 = ks * 32 + 8 * g + q;
+    const int k2 = k1 + 4;
+    const bf16_t* a1 = t + k1 * R + (((i0 >> 4) ^ ks_swz<SW>(k1)) << 4) + 4 * p;
+    const bf16_t* a2 = t + k2 * R + (((i0 >> 4) ^ ks_swz<SW>(k2)) << 4) + 4 * p;
+    s4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4_t*)a1);
+    s4_t v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4_t*)a2);
+    return s8_t{v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
+  }
+}
+
+// s_waitcnt with only the vector-memory counter constrained (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14,
+// expcnt and lgkmcnt at their no-wait maxima)
+template <int N>
+ASRX_DEV void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+// wait until at most `ahead` stages of P instructions each are still in flight (ahead is a runtime value)
+template <int P, int MAXA>
+ASRX_DEV void wait_stages(int ahead) {
+  if constexpr (MAXA > 0) {
+    if (ahead >= MAXA) { wait_vmcnt<MAXA * P>(); return; }
+    wait_stages<P, MAXA - 1>(ahead);
+  } else {
+    wait_vmcnt<0>();
+  }
+}
+
+// 4 stages (64 KiB for 64x64 -> two workgroups per CU; 96 KiB for 128x64): measured faster than 6 stages on
+// the decoder shapes (6 stages cost the second workgroup per CU / gained nothing at 128x64)
+template <int BM, int BN> constexpr int ring_stages() { return 4; }
+
+template <int BM, int BN, bool AT, bool BT, int EPI>
+__global__ __launch_bounds__(256) void gemm_bf16_ring_kernel(GemmArgs g, int ntiles, int xcd) {
+  constexpr int R_STAGES = ring_stages<BM, BN>();
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int P = RStage<BM, AT>::NI + RStage<BN, BT>::NI;   // LDS-DMA instructions per thread per stage
+  constexpr int TM = BM / 32, TN = BN / 32;                     // 16x16 fragments per wave (2x2 waves)
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[R_STAGES * STAGE];
+  const int ntn = (g.N + BN - 1) / BN;
+  // xcd: workgroup b runs on XCD b % 8; give each XCD a contiguous range of tiles, so the column tiles of
+  // a row panel share that XCD's L2 (grid.x = 8 * ceil(ntiles / 8), surplus workgroups leave)
+  const int tile = xcd ? (int)(blockIdx.x % 8) * (int)(gridDim.x / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+  if (tile >= ntiles) return;
+  const int split = blockIdx.y, z = blockIdx.z;
+  const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
+  const int zo = z / g.batch_inner, zi = z % g.batch_inner;
+  const bf16_t* A = (const bf16_t*)g.a + zo * g.sa_o + zi * g.sa_i;
+  const bf16_t* B = (const bf16_t*)g.b + zo * g.sb_o + zi * g.sb_i;
+  const int64_t a_bytes = AT ? ((int64_t)(g.K - 1) * g.lda + g.M) * 2 : ((int64_t)(g.M - 1) * g.lda + g.K) * 2;
+  const int64_t b_bytes = BT ? ((int64_t)(g.K - 1) * g.ldb + g.N) * 2 : ((int64_t)(g.N - 1) * g.ldb + g.K) * 2;
+  const int kbeg = split * g.k_per_split;
+  const int kend = min(g.K, kbeg + g.k_per_split);
+  const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
+  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int wm = (wave >> 1) * (BM / 2), wn = (wave & 1) * (BN / 2);
+
+  RStage<BM, AT> sa;
+  RStage<BN, BT> sb;
+  sa.set_tile(m0, g.lda);
+  sb.set_tile(n0, g.ldb);
+  f4_t acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < R_STAGES - 1; ++s)
+    if (s < nk) {
+      sa.issue(lds + s * STAGE, A, g.lda, a_bytes, kbeg + s * BK);
+      sb.issue(lds + s * STAGE + A_BYTES, B, g.ldb, b_bytes, kbeg + s * BK);
+    }
+  for (int kt = 0; kt < nk; ++kt) {
+    // stages issued so far: min(nk, kt + 3); keep the younger ones in flight, stage kt must have landed
+    const int ahead = min(nk, kt + R_STAGES - 1) - kt - 1;
+    wait_stages<P, R_STAGES - 2>(ahead);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + R_STAGES - 1 < nk) {
+      unsigned char* img = lds + ((kt + R_STAGES - 1) % R_STAGES) * STAGE;
+      sa.issue(img, A, g.lda, a_bytes, kbeg + (kt + R_STAGES - 1) * BK);
+      sb.issue(img + A_BYTES, B, g.ldb, b_bytes, kbeg + (kt + R_STAGES - 1) * BK);
+    }
+    const unsigned char* la = lds + (kt % R_STAGES) * STAGE;
+    const unsigned char* lb = la + A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      s8_t fa[TM], fb[TN];
+#pragma unroll
+      for (int j = 0; j < TM; ++j) fa[j] = r_frag<BM, AT>(la, wm + 16 * j, ks);
+#pragma unroll
+      for (int i = 0; i < TN; ++i) fb[i] = r_frag<BN, BT>(lb, wn + 16 * i, ks);
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  if (g.splitk > 1) {
+    const int gq = l >> 4;
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        store_partial4(g, split, m0 + wm + 16 * j + (l & 15), n0 + wn + 16 * i + 4 * gq, v);
+      }
+  } else {
+    epilogue_tile<EPI>(g, z, m0, n0, wm, wn, acc);
+  }
+}
+
+template <int BM, int BN, bool AT, bool BT>
+void dispatch_ring(const GemmArgs& g, int epi, int splitk, int batch, hipStream_t st) {
+  const int ntiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
+  const char* e = getenv("ASRX_RING_XCD");
+  const int xcd = e ? atoi(e) : 1;
+  dim3 grid(xcd ? 8 * ((ntiles + 7) / 8) : ntiles, splitk, batch);
+#define ASRX_CASE(E) \
+  case (E): hipLaunchKernelGGL((gemm_bf16_ring_kernel<BM, BN, AT, BT, (E)>), grid, dim3(R_THREADS), 0, st, g, ntiles, xcd); return;
+  if constexpr (!AT && !BT) {
+    switch (epi) { ASRX_EPI_NT(ASRX_CASE) default: break; }
+  } else if constexpr (!AT && BT) {
+    switch (epi) { ASRX_EPI_NN(ASRX_CASE) default: break; }
+  }
+#undef ASRX_CASE
+  hipLaunchKernelGGL((gemm_bf16_ring_kernel<BM, BN, AT, BT, E_GENERIC>), grid, dim3(R_THREADS), 0, st, g, ntiles, xcd);
+}
+
 constexpr int FBM = 64, FBN = 64, FBK = 16, FSTRIDE = 64 + 16;
 
 template <bool KSTRIDED>
@@ -1024,7 +1213,8 @@ void dispatch_bf16(const GemmArgs& g, bool at, bool bt, bool vec, int batch, hip
 // ------------------------------------------------------------------------------------------------
 // Kernel selection (shared by asrx_gemm and asrx_gemm_kernel_name so profiling can name the launch).
 struct GemmPlan {
-  int use;     // 1 = p3 (256x128 LDS-DMA ring), 2 = glds (128x128), 3 = register path 128, 4 = register path 64
+  int use;     // 1 = p3 (256x128 LDS-DMA ring), 2 = glds (128x128), 3 = register path 128, 4 = register path 64,
+               // 5 = ring 64x64, 6 = ring 128x64 (4-stage LDS-DMA, small grids)
   bool vec;    // 16-byte aligned operands
   int epi;     // instantiated epilogue flags (E_GENERIC when the fast-path set has no match)
   int ntiles;  // output tiles of the chosen kernel
@@ -1050,20 +1240,30 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
   }
   // kernel family: ASRX_GEMM_KERNEL = auto | p3 | glds | reg  (A/B switch for benchmarking)
   const char* kenv = getenv("ASRX_GEMM_KERNEL");
-  const int kvar = !kenv ? 0 : (!strcmp(kenv, "p3") ? 1 : (!strcmp(kenv, "glds") ? 2 : (!strcmp(kenv, "reg") ? 3 : 0)));
+  const int kvar = !kenv ? 0 : (!strcmp(kenv, "p3") ? 1 : (!strcmp(kenv, "glds") ? 2 : (!strcmp(kenv, "reg") ? 3 :
+                   (!strcmp(kenv, "ring") ? 4 : (!strcmp(kenv, "ring128") ? 5 : 0)))));
   const bool dma_ok = pl.vec && d->k % BK == 0 && (!d->a_trans || d->m % 8 == 0) && (!d->b_trans || d->n % 8 == 0) &&
                       d->m >= 8 && d->n >= 8;
   const int nt_p3 = ((d->m + P_BM - 1) / P_BM) * ((d->n + P_BN - 1) / P_BN);
   pl.use = tile == 128 ? 3 : 4;
+  const int nt_r128 = ((d->m + 127) / 128) * ((d->n + 63) / 64);
   if (dma_ok) {
     if (kvar == 1) pl.use = 1;
     else if (kvar == 2) pl.use = tile == 128 ? 2 : pl.use;
-    // auto (measured on the c3 shapes, tools/gemm_bench.py): the p3 ring wins every projection with K <= 4096;
-    // the register path wins the weight-gradient (A^T, reduction over B*T rows) and very long-K GEMMs.
-    else if (kvar == 0 && !d->a_trans && d->k <= 4096)
-      pl.use = (nt_p3 * splitk * batch >= 192) ? 1 : (tile == 128 ? 2 : pl.use);
+    else if (kvar == 4 && !d->a_trans) pl.use = 5;
+    else if (kvar == 5 && !d->a_trans) pl.use = 6;
+    // auto (measured on the c3 shapes, tools/gemm_bench.py): the p3 ring wins every projection with K <= 4096
+    // whose grid fills the chip; smaller grids (the decoder's 4096-row GEMMs) take the 4-stage ring kernel; the
+    // register path wins the weight-gradient (A^T, reduction over B*T rows) and very long-K GEMMs.
+    else if (kvar == 0 && !d->a_trans && d->k <= 4096) {
+      if (nt_p3 * splitk * batch >= 192) pl.use = 1;
+      else pl.use = nt_r128 * splitk * batch >= 192 ? 6 : 5;
+    }
   }
-  pl.ntiles = pl.use == 1 ? nt_p3 : ((d->m + tile - 1) / tile) * ((d->n + tile - 1) / tile);
+  if (pl.use == 1) pl.ntiles = nt_p3;
+  else if (pl.use == 5) pl.ntiles = ((d->m + 63) / 64) * ((d->n + 63) / 64);
+  else if (pl.use == 6) pl.ntiles = nt_r128;
+  else pl.ntiles = ((d->m + tile - 1) / tile) * ((d->n + tile - 1) / tile);
   // compile-time epilogue selection (fast-path preconditions, else generic)
   int epi = E_GENERIC;
   const int esz = d->c_dtype == ASRX_F32 ? 16 : 8;
@@ -1079,7 +1279,7 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
           (d->gate ? E_GATE : 0) | (d->resid ? E_RESID : 0) | (d->beta == 1.f ? E_BETA : 0) |
           (d->c_dtype == ASRX_F32 ? E_F32 : 0) | (d->alpha != 1.f ? E_ALPHA : 0) | (d->rowadd ? E_ROWADD : 0);
   }
-  pl.epi = (pl.use <= 2 && epi_instantiated(d->a_trans, d->b_trans, epi)) ? epi : E_GENERIC;
+  pl.epi = ((pl.use <= 2 || pl.use >= 5) && epi_instantiated(d->a_trans, d->b_trans, epi)) ? epi : E_GENERIC;
   return pl;
 }
 
@@ -1097,6 +1297,9 @@ extern "C" int asrx_gemm_kernel_name(const asrx_gemm_desc* d, char* buf, int len
   const GemmPlan pl = plan_bf16(d, batch, splitk);
   if (pl.use == 1 || pl.use == 2)
     snprintf(buf, len, "gemm_bf16_%s_kernel<%s, %s, %d>", pl.use == 1 ? "p3" : "glds", tf[!!d->a_trans],
+             tf[!!d->b_trans], pl.epi);
+  else if (pl.use >= 5)
+    snprintf(buf, len, "gemm_bf16_ring_kernel<%d, 64, %s, %s, %d>", pl.use == 6 ? 128 : 64, tf[!!d->a_trans],
              tf[!!d->b_trans], pl.epi);
   else
     snprintf(buf, len, "gemm_bf16_kernel<%d, %d, %s, %s, %s>", pl.use == 3 ? 128 : 64, pl.use == 3 ? 128 : 64,
@@ -1190,6 +1393,14 @@ extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
       else if (!d->a_trans && d->b_trans) dispatch_glds<false, true>(g, epi, pl.ntiles, splitk, batch, st);
       else if (d->a_trans && !d->b_trans) dispatch_glds<true, false>(g, epi, pl.ntiles, splitk, batch, st);
       else dispatch_glds<true, true>(g, epi, pl.ntiles, splitk, batch, st);
+    } else if (pl.use >= 5) {
+      if (!d->b_trans) {
+        if (pl.use == 6) dispatch_ring<128, 64, false, false>(g, epi, splitk, batch, st);
+        else dispatch_ring<64, 64, false, false>(g, epi, splitk, batch, st);
+      } else {
+        if (pl.use == 6) dispatch_ring<128, 64, false, true>(g, epi, splitk, batch, st);
+        else dispatch_ring<64, 64, false, true>(g, epi, splitk, batch, st);
+      }
     } else if (pl.use == 3) {
       dispatch_bf16<128, 128>(g, d->a_trans, d->b_trans, pl.vec, batch, st);
     } else {

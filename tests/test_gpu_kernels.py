@@ -47,7 +47,7 @@ def kernel_variant(request):
         os.environ["ASRX_GEMM_KERNEL"] = old
 
 
-@pytest.mark.parametrize("kernel_variant", ["auto", "p3", "glds", "reg"], indirect=True)
+@pytest.mark.parametrize("kernel_variant", ["auto", "p3", "glds", "reg", "ring", "ring128"], indirect=True)
 @pytest.mark.parametrize("tile", [0, 128])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("at,bt", [(False, False), (False, True), (True, False), (True, True)])
@@ -67,7 +67,7 @@ def test_gemm_layouts(dtype, at, bt, m, n, k, tile, kernel_variant):
     assert relerr(C.cpu(), ref) < tol
 
 
-@pytest.mark.parametrize("kernel_variant", ["auto", "p3", "glds", "reg"], indirect=True)
+@pytest.mark.parametrize("kernel_variant", ["auto", "p3", "glds", "reg", "ring", "ring128"], indirect=True)
 @pytest.mark.parametrize("tile", [64, 128])
 def test_gemm_epilogue(tile, kernel_variant):
     m, n, k = 300, 192, 128
@@ -103,7 +103,7 @@ def test_gemm_beta_splitk_and_bf16_out():
     assert relerr(Cb.float().cpu(), ref - C0.double()) < 1e-2
 
 
-@pytest.mark.parametrize("kernel_variant", ["auto", "p3", "glds", "reg"], indirect=True)
+@pytest.mark.parametrize("kernel_variant", ["auto", "p3", "glds", "reg", "ring", "ring128"], indirect=True)
 @pytest.mark.parametrize("tile,splitk", [(64, 1), (128, 1), (64, 5), (128, 7)])
 def test_gemm_fused_rowsum(tile, splitk, kernel_variant):
     """wgrad GEMM dW = dY^T X with the bias gradient (row sums of dY^T) fused into the staging/fragments."""

@@ -69,10 +69,15 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="enc,cross,dec")
     ap.add_argument("--variant", default="auto")
+    ap.add_argument("--sweep", action="store_true", help="Lq sweep at Lk=249 (per-chunk vs fixed cost)")
     args = ap.parse_args()
     os.environ["ASRX_ATTN_KERNEL"] = args.variant
     cases = {"enc": ("enc_self", 249, 249, False), "cross": ("cross", 64, 249, False),
              "dec": ("dec_self", 64, 64, True)}
+    if args.sweep:
+        for lq in (32, 64, 128, 192, 249):
+            cases[f"s{lq}"] = (f"lq{lq}", lq, 249, False)
+        args.only = ",".join(k for k in cases if k.startswith("s"))
     for key in args.only.split(","):
         name, fwd, bwd, ff, fb = case(*cases[key])
         fwd()

@@ -24,11 +24,22 @@ SHAPES = [
     ("enc_ffn1_wgrad", M_ENC, 2048, 512, "wgrad"), ("enc_qkv_wgrad", M_ENC, 1536, 512, "wgrad"),
     ("enc_out_wgrad", M_ENC, 512, 512, "wgrad"), ("cross_kv_wgrad", M_ENC, 12288, 512, "wgrad"),
     ("dec_ffn1_wgrad", M_DEC, 2048, 512, "wgrad"),
+    ("dec_out_fwd", M_DEC, 512, 512, "fwd"), ("dec_qkv_fwd", M_DEC, 1536, 512, "fwd"),
+    ("dec_out_dgrad", M_DEC, 512, 512, "dgrad"), ("dec_ffn1_dgrad", M_DEC, 512, 2048, "dgrad"),
+    ("dec_qkv_dgrad", M_DEC, 512, 1536, "dgrad"),
 ]
 
 
-def run_shape(M, N, Kd, kind, bufs):
+def run_shape(M, N, Kd, kind, bufs, variant="auto"):
     x, w, y, dy, wg, bg = bufs
+    if variant == "torch":   # hipBLASLt / rocBLAS through torch (reference point only, not used by asrx)
+        if kind == "fwd":
+            torch.matmul(x, w.t(), out=y)
+        elif kind == "dgrad":
+            torch.matmul(dy, w, out=y)
+        else:
+            wg.add_(torch.matmul(dy.t(), x).float())
+        return
     if kind == "fwd":
         K.linear(x, w, y)
     elif kind == "dgrad":
@@ -69,10 +80,16 @@ def main():
         times = {v: [] for v in variants}
         for r in range(args.reps + 2):
             for v in variants:
-                os.environ["ASRX_GEMM_KERNEL"] = v
+                kv = v.split("+")          # "ring+ASRX_RING_XCD=0": kernel family plus extra env settings
+                os.environ["ASRX_GEMM_KERNEL"] = kv[0]
+                for ev in kv[1:]:
+                    key, val = ev.split("=")
+                    os.environ[key] = val
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
-                run_shape(M, N, Kd, kind, bufs)
+                run_shape(M, N, Kd, kind, bufs, kv[0])
+                for ev in kv[1:]:
+                    os.environ.pop(ev.split("=")[0], None)
                 e.record()
                 e.synchronize()
                 if r >= 2:
