@@ -54,6 +54,13 @@ class GemmGroup(ctypes.Structure):
 MAX_GROUPS = 48   # gemm.hip MAX_GROUPS (kernel-argument table)
 
 
+class RowsumGroup(ctypes.Structure):
+    _fields_ = [("in_", c_vp), ("rows", c_i64), ("cols", c_i32), ("out", c_vp), ("accumulate", c_i32)]
+
+
+MAX_ROWSUM_GROUPS = 64   # norm.hip RG_MAX
+
+
 class AttnDesc(ctypes.Structure):
     _fields_ = [
         ("batch", c_i32), ("heads", c_i32), ("lq", c_i32), ("lk", c_i32), ("dh", c_i32),
@@ -82,6 +89,7 @@ SIGNATURES = {
     "asrx_gemm": [ctypes.POINTER(GemmDesc), c_vp],
     "asrx_gemm_kernel_name": [ctypes.POINTER(GemmDesc), ctypes.c_char_p, c_i32],
     "asrx_gemm_grouped": [ctypes.POINTER(GemmDesc), ctypes.POINTER(GemmGroup), c_i32, c_vp],
+    "asrx_reduce_rows_grouped": [ctypes.POINTER(RowsumGroup), c_i32, c_vp],
     "asrx_attention_fwd": [ctypes.POINTER(AttnDesc), c_vp],
     "asrx_attention_bwd": [ctypes.POINTER(AttnDesc), c_vp],
     "asrx_attn_delta": [ctypes.POINTER(AttnDesc), c_vp],

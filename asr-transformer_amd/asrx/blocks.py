@@ -27,6 +27,7 @@ class Ctx:
         self.seeds = seeds
         self.attn_impl = attn_impl
         self.wq = None                  # list -> weight gradients are queued and issued grouped (flush_wgrad)
+        self.lnq = None                 # list -> LayerNorm dgamma|dbeta partials queued for one grouped reduce
 
     def W(self, p):
         return self.store.w16(p) if self.cd == torch.bfloat16 else self.store.w32(p)
@@ -47,13 +48,15 @@ class Ctx:
 
     def defer_wgrad(self):
         if self.cd == torch.bfloat16 and self.wq is None:
-            self.wq = []
+            self.wq, self.lnq = [], []
             return True
         return False
 
     def flush_wgrad(self):
         q, self.wq = self.wq, None
+        lq, self.lnq = self.lnq, None
         K.linear_wgrad_grouped(q or [])
+        K.reduce_rows_grouped(lq or [])
 
 
 class Seeds:
@@ -91,7 +94,7 @@ def ln_bwd(C, x, dy, ln, mean, rstd, dres=None, drop_out=None, drop_seed=0, drop
     """dx (fp32) = LN^T dy + dres; optional drop_out (compute dtype) = dropout_bwd(dx)."""
     buf, split = ln_grad_buf(C, ln)
     dx = K.layernorm_bwd(x, dy, ln.weight.data, mean, rstd, buf, dres=dres, dx_drop=drop_out, dropout_p=drop_p,
-                         seed=drop_seed)
+                         seed=drop_seed, defer=C.lnq if split is None else None)
     if split is not None:
         d = split[0].numel()
         split[0].add_(buf[:d].view_as(split[0]))

@@ -5,7 +5,7 @@ import math
 
 import torch
 
-from ._lib import MAX_GROUPS, AttnDesc, BF16, F32, GemmDesc, GemmGroup, call
+from ._lib import MAX_GROUPS, MAX_ROWSUM_GROUPS, AttnDesc, BF16, F32, GemmDesc, GemmGroup, RowsumGroup, call
 
 _U64 = (1 << 64) - 1
 
@@ -256,9 +256,22 @@ def layernorm_fwd(x, gamma, beta, y, eps=1e-5):
     return mean, rstd
 
 
-def layernorm_bwd(x, dy, gamma, mean, rstd, dgb, *, dres=None, dx_drop=None, dropout_p=0.0, seed=0):
+def reduce_rows_grouped(items):
+    """out (+)= column sums of fp32 [rows, cols] matrices, many per launch: items = [(in, out, accumulate)]."""
+    for c0 in range(0, len(items), MAX_ROWSUM_GROUPS):
+        chunk = items[c0:c0 + MAX_ROWSUM_GROUPS]
+        arr = (RowsumGroup * len(chunk))()
+        for gr, (src, out, acc) in zip(arr, chunk):
+            _cuda(src, out)
+            gr.in_, gr.rows, gr.cols = src.data_ptr(), src.shape[0], src.shape[1]
+            gr.out, gr.accumulate = out.data_ptr(), int(acc)
+        call("asrx_reduce_rows_grouped", arr, len(chunk), stream())
+
+
+def layernorm_bwd(x, dy, gamma, mean, rstd, dgb, *, dres=None, dx_drop=None, dropout_p=0.0, seed=0, defer=None):
     """Returns dx (fp32). dgb: fp32 [2*d] grad buffer (gamma grads then beta grads), accumulated.
-    If dx_drop (bf16 or fp32) is given it receives dropout_bwd(dx) for the upstream sublayer."""
+    If dx_drop (bf16 or fp32) is given it receives dropout_bwd(dx) for the upstream sublayer.  With a `defer`
+    list the per-block dgamma|dbeta partials are queued for reduce_rows_grouped instead of reduced here."""
     _cuda(x, dy, gamma, mean, rstd, dgb)
     rows, d = x.shape
     dx = torch.empty(rows, d, device=x.device, dtype=torch.float32)
@@ -267,6 +280,9 @@ def layernorm_bwd(x, dy, gamma, mean, rstd, dgb, *, dres=None, dx_drop=None, dro
     call("asrx_layernorm_bwd", code(x), x.data_ptr(), code(dy), dy.data_ptr(), gamma.data_ptr(), mean.data_ptr(),
          rstd.data_ptr(), _p(dres), dx.data_ptr(), _p(dx_drop), code(dx_drop) if dx_drop is not None else 0,
          dropout_p, seed & _U64, part.data_ptr(), nblocks, rows, d, stream())
+    if defer is not None:
+        defer.append((part.view(nblocks, 2 * d), dgb, True))
+        return dx
     part2 = torch.empty(max(1, (nblocks + 63) // 64) * 2 * d, device=x.device, dtype=torch.float32)
     call("asrx_reduce_rows", F32, part.data_ptr(), nblocks, 2 * d, 2 * d, dgb.data_ptr(), 1, part2.data_ptr(),
          max(1, (nblocks + 63) // 64), stream())

@@ -177,6 +177,40 @@ __global__ __launch_bounds__(256) void colsum_stage2(const float* part, int npar
   }
 }
 
+// Grouped column sums of fp32 matrices (the deferred LayerNorm dgamma|dbeta partials of a whole backward pass):
+// one launch; block = (group, 64-column chunk), 4 row slices per block combined in LDS in fixed order.
+constexpr int RG_MAX = 64;
+struct RowsumGroup { const float* in; float* out; int rows, cols, chunk0, acc; };
+struct RowsumTable { int count; RowsumGroup gr[RG_MAX]; };
+
+__global__ __launch_bounds__(256) void reduce_rows_grouped_kernel(RowsumTable t) {
+  __shared__ float red[4][64];
+  const int bid = blockIdx.x;
+  int gi = 0;
+  while (gi + 1 < t.count && t.gr[gi + 1].chunk0 <= bid) ++gi;
+  const RowsumGroup& G = t.gr[gi];
+  const int c = (bid - G.chunk0) * 64 + (threadIdx.x & 63), sub = threadIdx.x >> 6;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (c < G.cols) {
+    const float* p = G.in + c;
+    const int64_t ld = G.cols;
+    int r = sub;
+    for (; r + 12 < G.rows; r += 16) {
+      s0 += p[(int64_t)r * ld];
+      s1 += p[(int64_t)(r + 4) * ld];
+      s2 += p[(int64_t)(r + 8) * ld];
+      s3 += p[(int64_t)(r + 12) * ld];
+    }
+    for (; r < G.rows; r += 4) s0 += p[(int64_t)r * ld];
+  }
+  red[sub][threadIdx.x & 63] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (sub == 0 && c < G.cols) {
+    const float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    G.out[c] = G.acc ? G.out[c] + v : v;
+  }
+}
+
 template <int CH, int NJ>
 bool ln_fwd_launch(int x_dtype, const void* x, int y_dtype, void* y, const float* gamma, const float* beta,
                    float* mean, float* rstd, int64_t rows, int d, float eps, hipStream_t st) {
@@ -247,6 +281,24 @@ extern "C" int asrx_reduce_rows(int32_t dtype, const void* in, int64_t rows, int
     ASRX_CHECK_LAUNCH();
   }
   hipLaunchKernelGGL(colsum_stage2, dim3((cols + 63) / 64), dim3(256), 0, st, part, nparts, cols, out, accumulate);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
+extern "C" int asrx_reduce_rows_grouped(const asrx_rowsum_group* groups, int32_t count, void* stream) {
+  if (!groups || count < 0 || count > RG_MAX) return ASRX_ERR_ARG;
+  if (count == 0) return ASRX_OK;
+  RowsumTable t;
+  t.count = count;
+  int chunks = 0;
+  for (int i = 0; i < count; ++i) {
+    const asrx_rowsum_group& q = groups[i];
+    if (!q.in || !q.out || q.rows < 0 || q.cols <= 0 || q.rows > INT32_MAX) return ASRX_ERR_ARG;
+    t.gr[i].in = q.in; t.gr[i].out = q.out; t.gr[i].rows = (int)q.rows; t.gr[i].cols = q.cols;
+    t.gr[i].acc = q.accumulate; t.gr[i].chunk0 = chunks;
+    chunks += (q.cols + 63) / 64;
+  }
+  hipLaunchKernelGGL(reduce_rows_grouped_kernel, dim3(chunks), dim3(256), 0, (hipStream_t)stream, t);
   ASRX_CHECK_LAUNCH();
   return ASRX_OK;
 }

@@ -166,6 +166,15 @@ int asrx_layernorm_bwd(int32_t x_dtype, const void* x, int32_t dy_dtype, const v
 int asrx_reduce_rows(int32_t dtype, const void* in, int64_t rows, int32_t cols, int64_t ld, float* out,
                      int32_t accumulate, float* part, int32_t nblocks, void* stream);
 
+/* Grouped version for many fp32 [rows][cols] matrices in ONE launch (count <= 64): out_g[c] (+)= sum_r in_g[r][c],
+ * rows summed in a fixed order (deterministic).  Used for the LayerNorm dgamma|dbeta partials of a whole backward
+ * pass, deferred like the weight gradients. */
+typedef struct asrx_rowsum_group {
+  const float* in; int64_t rows; int32_t cols; float* out; int32_t accumulate;
+} asrx_rowsum_group;
+
+int asrx_reduce_rows_grouped(const asrx_rowsum_group* groups, int32_t count, void* stream);
+
 /* ---------------------------------------------------------------------------------------------------
  * Conv2d front-end (model.py:168-171): conv(1->64,3x3,s2)+ReLU -> conv(64->64,3x3,s2)+ReLU, no padding.
  * conv1_fwd: x (B,1,F,T) fp32 -> y1 channels-last (B,F1,T1,64) in y_dtype (bf16 or fp32)

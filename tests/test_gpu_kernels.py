@@ -191,6 +191,24 @@ def test_layernorm(d, ydt):
     assert relerr(dgb[d:].cpu(), br.grad) < 1e-5
 
 
+@pytest.mark.parametrize("ngroups", [1, 70])
+def test_reduce_rows_grouped(ngroups):
+    """Deferred LayerNorm partial reductions: many fp32 matrices' column sums in grouped launches."""
+    g = torch.Generator(device=dev).manual_seed(ngroups)
+    items, refs = [], []
+    for i in range(ngroups):
+        rows, cols = [(512, 1024), (3, 70), (1, 64), (129, 256)][i % 4]
+        x = torch.randn(rows, cols, device=dev, generator=g)
+        out = torch.randn(cols, device=dev, generator=g)
+        acc = i % 3 != 0
+        refs.append((out.double() if acc else 0) + x.double().sum(0))
+        items.append((x, out, acc))
+    K().reduce_rows_grouped(items)
+    torch.cuda.synchronize()
+    for (x, out, acc), r in zip(items, refs):
+        assert relerr(out, r) < 1e-5
+
+
 def test_colsum():
     x = torch.randn(10000, 300)
     out = torch.ones(300, device=dev)
