@@ -119,15 +119,47 @@ def encoder_fwd(C, enc, feats, B, T):
     return y, dict(feats=feats, x=x, mean=mean, rstd=rstd, layers=Ss)
 
 
-def encoder_bwd(C, enc, S, dy, gate_feats):
-    """dy: grad of the encoder output (fp32 or compute dtype). Returns dfeats (compute dtype)."""
+def _spans(C, params):
+    """Maximal [start, end) element ranges of the flat gradient buffer covered by `params` (a module's params
+    need not be adjacent: e.g. Encoder._norm_out is registered before the layers).  Two params merge only if
+    the second starts at the first aligned offset after the first, so no other parameter lies in between."""
+    from .params import ALIGN
+    st = C.store
+    iv = sorted((st.offset(p), st.offset(p) + p.numel()) for p in params)
+    out = []
+    for a, b in iv:
+        if out and a == -(-out[-1][1] // ALIGN) * ALIGN:
+            out[-1][1] = b
+        else:
+            out.append([a, b])
+    return [tuple(x) for x in out]
+
+
+def _release(C, ready, params):
+    """Flush the queued weight-gradient / LayerNorm reductions, hand the finished ranges to the all-reduce and
+    re-open the queues (multi-GPU backward only)."""
+    if ready is None or C.wq is None:
+        return
+    C.flush_wgrad()
+    for a, b in _spans(C, params):
+        ready(a, b)
+    C.defer_wgrad()
+
+
+def encoder_bwd(C, enc, S, dy, gate_feats, ready=None):
+    """dy: grad of the encoder output (fp32 or compute dtype). Returns dfeats (compute dtype).  With `ready`,
+    the upper half of the layers (and _norm_out) is released to the gradient all-reduce once done."""
     x = S["x"]
     dx_c = torch.empty(x.shape, dtype=C.cd, device=x.device)
     dx = Bk.ln_bwd(C, x, dy, enc._norm_out, S["mean"], S["rstd"], drop_out=dx_c)
-    for layer_S in reversed(S["layers"]):
+    n = len(S["layers"])
+    for i, layer_S in reversed(list(enumerate(S["layers"]))):
         nxt = torch.empty(x.shape, dtype=C.cd, device=x.device)
         dx = Bk.enc_layer_bwd(C, layer_S, dx, dx_c, nxt)
         dx_c = nxt
+        if i == n // 2 and n > 1:
+            _release(C, ready, [p for l in enc._layers[n // 2:] for p in l.parameters()] +
+                     list(enc._norm_out.parameters()))
     feats = S["feats"]
     dfeats = torch.empty(feats.shape, dtype=C.cd, device=x.device)
     w = enc._lin_in.weight
@@ -225,11 +257,16 @@ def model_forward(C, model, spectrum, text, mask):
     return logits, dict(f=Sf, e=Se, d=Sd)
 
 
-def model_backward(C, model, S, dlogits_c):
+def model_backward(C, model, S, dlogits_c, ready=None):
+    """Backward of model_forward.  ready(start, end): optional callback that receives flat-gradient ranges as
+    they become final (decoder, then upper encoder half) so their all-reduce overlaps the rest of the backward;
+    whatever is not released that way is final when this returns."""
     _prepare_grads(C)
     own = C.defer_wgrad()
     denc = decoder_bwd(C, model.decoder, S["d"], dlogits_c)
-    dfeats = encoder_bwd(C, model.encoder, S["e"], denc, gate_feats=True)
+    if own:
+        _release(C, ready, list(model.decoder.parameters()))
+    dfeats = encoder_bwd(C, model.encoder, S["e"], denc, gate_feats=True, ready=ready if own else None)
     Bk.frontend_bwd(C, S["f"], dfeats, model.input_layer[0], model.input_layer[2])
     if own:
         C.flush_wgrad()

@@ -94,12 +94,13 @@ class Trainer:
         tgt = text[:, 1:].reshape(-1).contiguous()
         loss, dl, _ = K.cross_entropy(logits, V, tgt, ignore_index=self.ignore_index)
         self.store.grad.zero_()
-        model_backward(C, model, S, dl.to(C.cd) if dl.dtype != C.cd else dl)
+        model_backward(C, model, S, dl.to(C.cd) if dl.dtype != C.cd else dl,
+                       ready=self.reducer.ready if self.reducer.active else None)
         return loss
 
     def step(self, spectrum, text, mask):
         loss = self.forward_backward(spectrum, text, mask)
-        self.reducer()
+        self.reducer.finish()
         self.step_count += 1
         K.adam(self.store.flat, self.store.grad, self.m, self.v, self.store.shadow, self.lr, self.betas[0],
                self.betas[1], self.eps, self.wd, self.step_count, grad_scale=1.0 / self.reducer.world,

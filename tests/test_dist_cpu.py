@@ -93,3 +93,56 @@ def test_bucketing_fake_backend_order_and_coverage():
     assert torch.equal(flat, torch.arange(1000, dtype=torch.float32) * 3)
     assert r.world == 3
     assert sum(v.numel() for v in bucket_views(torch.zeros(10), 3)) == 10
+
+
+def test_ready_ranges_overlap_then_finish_covers_complement():
+    """Ranges released during the backward are reduced once each; finish() reduces exactly the rest."""
+    from asrx.dist import GradAllReduce
+    flat = torch.ones(1000)
+    counts = torch.zeros(1000)
+    base = flat.data_ptr()
+
+    def fake(b):
+        o = (b.data_ptr() - base) // 4
+        counts[o:o + b.numel()] += 1
+        b.mul_(2.0)
+    fake.world = 2
+    r = GradAllReduce(flat, bucket_mb=100 * 4 / 2 ** 20, allreduce_fn=fake)
+    r.ready(700, 1000)          # decoder span
+    r.ready(400, 700)           # upper encoder half
+    assert counts[400:].eq(1).all() and counts[:400].eq(0).all()
+    r.finish()
+    assert counts.eq(1).all() and flat.eq(2.0).all()
+    r.ready(0, 10)              # the next step starts from a clean slate
+    r.finish()
+    assert counts.eq(2).all()
+
+
+def _ready_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from asrx.dist import GradAllReduce
+    flat = torch.arange(5000, dtype=torch.float32) * (rank + 1)
+    r = GradAllReduce(flat, bucket_mb=0.002)
+    r.ready(3000, 5000)
+    r.ready(1234, 3000)
+    r.finish()
+    q.put((rank, flat))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_ws2_ready_ranges():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_ready_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = torch.arange(5000, dtype=torch.float32) * 3
+    assert torch.equal(res[0], want) and torch.equal(res[1], want)

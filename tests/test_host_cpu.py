@@ -166,3 +166,25 @@ def test_rng_restatement_statistics():
     a = attn_keep(7, 3, 9, 13, 0.25)
     assert a.shape == (3, 9, 13) and abs(a.mean() - 0.75) < 0.1
     assert not elem_keep(7, 1000, 1.0).any() and elem_keep(7, 1000, 0.0).all()
+
+
+def test_release_spans_are_exact():
+    """The gradient ranges released to the all-reduce cover exactly the given params (no neighbours)."""
+    from asrx.functions import _spans, param_order
+    from asrx.params import FlatParams
+    m, cfg = _build("c1")
+    st = FlatParams(param_order(m), "cpu")
+
+    class C:
+        store = st
+    enc = m.encoder
+    params = [p for p in enc._layers[1].parameters()] + list(enc._norm_out.parameters())
+    spans = _spans(C, params)
+    covered = sum(b - a for a, b in spans)
+    mine = {id(p) for p in params}
+    for p in st.params:   # no other parameter overlaps a span
+        o = st.offset(p)
+        inside = any(a <= o < b for a, b in spans)
+        assert inside == (id(p) in mine), p.shape
+    assert covered >= sum(p.numel() for p in params)
+    assert len(_spans(C, list(m.decoder.parameters()))) == 1
