@@ -49,7 +49,12 @@ struct AttnArgs {
   bf16_t* dv; int64_t dvr, dvb;
   float* delta; float* dq_acc;
   uint32_t* dropmask;
+  int dbg;   // phase timestamps of block 0 / wave 0 into g_attn_dbg (tools only; ASRX_ATTN_DBG=1)
 };
+
+__device__ unsigned long long g_attn_dbg[64];
+#define ATTN_TS(i) do { if (a.dbg && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && (i) < 64) \
+                          g_attn_dbg[(i)] = __builtin_amdgcn_s_memtime(); } while (0)
 
 ASRX_DEV bool masked(const AttnArgs& a, int b, int q, int key) {
   if (key >= a.Lk) return true;
@@ -623,38 +628,39 @@ __global__ __launch_bounds__(512) void attn_fwd_res_kernel(AttnArgs a) {
 // the next chunk are prefetched into registers during the current one (double-buffered LDS images).  Masks:
 // key validity / padding is a per-lane score bias, query validity is folded into lse (+inf), causality is a
 // compare only in blocks that reach above the diagonal.
-template <int MODE>
-__global__ __launch_bounds__(512) void attn_bwd_res_kernel(AttnArgs a) {
+template <int MODE, int NKT>
+__global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
+  // NKT 32-key blocks (= waves); keys past Lk are zero rows with a -inf score bias
+  constexpr int NK = NKT * 32, NTHR = NKT * 64;
+  constexpr int RDT = 32 + 8;                                     // dS^T image [key][32 queries] row stride
+  constexpr int PRE = 512 / NTHR;                                 // 16-B prefetch pieces per thread
+  constexpr int TPW = 8 / NKT;                                    // dQ tiles per wave per chunk
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int nkt = (a.Lk + 31) >> 5, nk = nkt * 32;
-  const int rds = nk + 8;                                   // dS image row stride (elements)
-  bf16_t* sk = (bf16_t*)smem;                                // [nk][R_VS]
-  bf16_t* sq = sk + nk * R_VS;                               // [2][32][R_CS]
+  bf16_t* sk = (bf16_t*)smem;                                // [NK][R_VS]
+  bf16_t* sq = sk + NK * R_VS;                               // [2][32][R_CS]
   bf16_t* sdo = sq + 2 * 32 * R_CS;                          // [2][32][R_CS]
-  bf16_t* sds = sdo + 2 * 32 * R_CS;                         // [2][32][rds]
-  float* slse = (float*)(sds + 2 * 32 * rds);                // [2][32]  (-lse, -inf for dead queries)
+  bf16_t* sds = sdo + 2 * 32 * R_CS;                         // [2][NK][RDT]  dS^T (bf16)
+  float* slse = (float*)(sds + 2 * NK * RDT);                // [2][32]  (-lse, -inf for dead queries)
   float* sdel = slse + 64;                                   // [2][32]
+  f4_t* slut = (f4_t*)(sdel + 64);                           // [16] dropout factors of a 4-bit keep mask
 
   const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
-  const int nthr = blockDim.x, nw = nthr >> 6;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, g = l >> 4, li = l & 15;
   const int kw0 = 32 * w;
-  const bool kown = kw0 < nk;
 
   const bf16_t* Kb = a.k + b * a.kb + h * 64;
   const bf16_t* Vb = a.v + b * a.vb + h * 64;
-  for (int c0 = tid; c0 < nk * 8; c0 += nthr * 4) {
-    uint4 kv[4];
+  {
+    uint4 kv[NK * 8 / NTHR];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = c0 + i * nthr, row = c >> 3, dc = (c & 7) * 8;
-      kv[i] = make_uint4(0, 0, 0, 0);
-      if (c < nk * 8 && row < a.Lk) kv[i] = *(const uint4*)(Kb + (int64_t)row * a.kr + dc);
+    for (int i = 0; i < NK * 8 / NTHR; ++i) {
+      const int c = tid + i * NTHR, row = c >> 3, dc = (c & 7) * 8;
+      kv[i] = *(const uint4*)(Kb + (int64_t)min(row, a.Lk - 1) * a.kr + dc);
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = c0 + i * nthr, row = c >> 3, dc = (c & 7) * 8;
-      if (c < nk * 8) *(uint4*)(sk + row * R_VS + dc) = kv[i];
+    for (int i = 0; i < NK * 8 / NTHR; ++i) {
+      const int c = tid + i * NTHR, row = c >> 3, dc = (c & 7) * 8;
+      *(uint4*)(sk + row * R_VS + dc) = row < a.Lk ? kv[i] : make_uint4(0, 0, 0, 0);
     }
   }
   s8_t kf[2][2], vf[2][2];
@@ -662,14 +668,21 @@ __global__ __launch_bounds__(512) void attn_bwd_res_kernel(AttnArgs a) {
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const int key = kw0 + 16 * t + li;
-    bool ok = key < a.Lk;
+    const int kc = min(key, a.Lk - 1);
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      kf[t][c] = ok ? *(const s8_t*)(Kb + (int64_t)key * a.kr + 32 * c + 8 * g) : s8_t{0, 0, 0, 0, 0, 0, 0, 0};
-      vf[t][c] = ok ? *(const s8_t*)(Vb + (int64_t)key * a.vr + 32 * c + 8 * g) : s8_t{0, 0, 0, 0, 0, 0, 0, 0};
+      kf[t][c] = *(const s8_t*)(Kb + (int64_t)kc * a.kr + 32 * c + 8 * g);
+      vf[t][c] = *(const s8_t*)(Vb + (int64_t)kc * a.vr + 32 * c + 8 * g);
     }
+    bool ok = key < a.Lk;
     if (MODE == 1 && ok && a.kvalid) ok = a.kvalid[b * a.validb + key] != 0;
-    kbias[t] = ok ? 0.f : -INFINITY;
+    kbias[t] = ok ? 0.f : -INFINITY;   // rows past Lk hold a clamped copy of the last key: masked here
+  }
+  if (tid < 16) {   // slut[n][r] = keep bit r of n ? 1/(1-p) : 0 (visible after the first barrier)
+    f4_t f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) f[r] = ((tid >> r) & 1) ? a.dscale : 0.f;
+    slut[tid] = f;
   }
   f4_t dva[4][2], dka[4][2];
 #pragma unroll
@@ -684,66 +697,129 @@ __global__ __launch_bounds__(512) void attn_bwd_res_kernel(AttnArgs a) {
   const bool causal = MODE == 1 && a.causal;
   const int nch = (a.Lq + 31) >> 5;
 
-  // chunk prefetch: 512 16-B pieces (Q rows then dO rows) + 32 lse + 32 delta (+ this lane's dropout words)
-  uint4 pre[4];
-  float pls = 0.f;
+  // chunk prefetch: 512 16-B pieces (Q rows then dO rows) + 32 lse + 32 delta (+ this lane's dropout words).
+  // Loads go to raw registers from clamped (always valid) addresses; every test on them waits until the chunk
+  // is published or used, so issuing the prefetch never stalls on its own latency.
+  uint4 pre[PRE];
+  float praw = 0.f;
   const bool usebits = a.thr && a.dropmask;
   const uint32_t* dmb = usebits ? a.dropmask + (int64_t)bh * nch * a.Lk : nullptr;
-  uint32_t dwn[2] = {0u, 0u}, dwc[2] = {0u, 0u};
+  uint32_t dwn[2] = {0u, 0u};
+  const int keyc[2] = {min(kw0 + li, a.Lk - 1), min(kw0 + 16 + li, a.Lk - 1)};
   auto fetch = [&](int ch) {
     const int q0 = ch * 32;
     if (usebits) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int key = kw0 + 16 * t + li;
-        dwn[t] = key < a.Lk ? dmb[(int64_t)ch * a.Lk + key] : 0u;
-      }
+      for (int t = 0; t < 2; ++t) dwn[t] = dmb[(int64_t)ch * a.Lk + keyc[t]];
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + nthr * i;
-      pre[i] = make_uint4(0, 0, 0, 0);
-      if (c < 512) {
-        const int which = c >> 8, row = (c >> 3) & 31, dc = (c & 7) * 8;
-        const int q = q0 + row;
-        if (q < a.Lq) pre[i] = *(const uint4*)((which ? Db + (int64_t)q * a.dor : Qb + (int64_t)q * a.qr) + dc);
-      }
+    for (int i = 0; i < PRE; ++i) {
+      const int c = tid + NTHR * i;
+      const int which = c >> 8, row = (c >> 3) & 31, dc = (c & 7) * 8;
+      const int q = min(q0 + row, a.Lq - 1);
+      pre[i] = *(const uint4*)((which ? Db + (int64_t)q * a.dor : Qb + (int64_t)q * a.qr) + dc);
+    }
+    if (tid < 64) {
+      const int q = min(q0 + (tid & 31), a.Lq - 1);
+      praw = tid < 32 ? lseb[q] : delb[q];
+    }
+  };
+  auto publish = [&](int buf, int ch) {
+    const int q0 = ch * 32;
+#pragma unroll
+    for (int i = 0; i < PRE; ++i) {
+      const int c = tid + NTHR * i;
+      const int which = c >> 8, row = (c >> 3) & 31, dc = (c & 7) * 8;
+      *(uint4*)((which ? sdo : sq) + (buf * 32 + row) * R_CS + dc) = q0 + row < a.Lq ? pre[i] : make_uint4(0, 0, 0, 0);
     }
     if (tid < 64) {
       const int q = q0 + (tid & 31);
+      float v;
       if (tid < 32) {
         bool live = q < a.Lq;
         if (MODE == 1 && live && a.qvalid) live = a.qvalid[b * a.validb + q] != 0;
-        pls = live ? -lseb[q] : -INFINITY;
+        v = live ? -praw : -INFINITY;
       } else {
-        pls = q < a.Lq ? delb[q] : 0.f;
+        v = q < a.Lq ? praw : 0.f;
       }
+      (tid < 32 ? slse : sdel)[buf * 32 + (tid & 31)] = v;
     }
   };
-  auto publish = [&](int buf) {
+
+  // dQ^T[d][q] = sum_key K^T[d][key] dS^T[key][q] for chunk cc: its 8 (sub-tile, 16-column) tiles, TPW per wave,
+  // every operand read before the MFMA chain (compile-time trip counts, no branches)
+  auto dq_chunk = [&](int cc) {
+    const int bq = cc & 1, q0 = cc * 32;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + nthr * i;
-      if (c < 512) {
-        const int which = c >> 8, row = (c >> 3) & 31, dc = (c & 7) * 8;
-        *(uint4*)((which ? sdo : sq) + (buf * 32 + row) * R_CS + dc) = pre[i];
+    for (int j = 0; j < TPW; ++j) {
+      const int tl = w + NKT * j;
+      const int qs = tl >> 2, u = tl & 3;
+      const bf16_t* dsr = sds + (bq * NK + 8 * g + (li >> 2)) * RDT + 16 * qs + 4 * (li & 3);
+      const bf16_t* kp = sk + (8 * g + (li >> 2)) * R_VS + 16 * u + 4 * (li & 3);
+      s8_t ka[NKT], da[NKT];
+#pragma unroll
+      for (int kc = 0; kc < NKT; ++kc) {
+        ka[kc] = cat8(lds_tr(kp + 32 * kc * R_VS), lds_tr(kp + (32 * kc + 4) * R_VS));
+        da[kc] = cat8(lds_tr(dsr + 32 * kc * RDT), lds_tr(dsr + (32 * kc + 4) * RDT));
       }
+      f4_t acc = f4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kc = 0; kc < NKT; ++kc) acc = mfma32(ka[kc], da[kc], acc);
+      const int q = min(q0 + 16 * qs + li, a.Lq - 1);   // rows past Lq: duplicate store of the last row's
+      uint2 x;                                           // (zero-dS) value would be wrong -> guarded below
+      x.x = pack2bf(acc[0] * a.scale, acc[1] * a.scale);
+      x.y = pack2bf(acc[2] * a.scale, acc[3] * a.scale);
+      if (q0 + 16 * qs + li < a.Lq) *(uint2*)(a.dq + b * a.dqb + (int64_t)q * a.dqr + h * 64 + 16 * u + 4 * g) = x;
     }
-    if (tid < 64) (tid < 32 ? slse : sdel)[buf * 32 + (tid & 31)] = pls;
   };
 
+  ATTN_TS(0);
   fetch(0);
-  publish(0);
+  publish(0, 0);
   __syncthreads();
+  ATTN_TS(1);
 
+  // software pipeline: iteration ch computes S/dP/dS/dV/dK of chunk ch AND dQ of chunk ch-1 in one
+  // straight-line block (the dQ MFMAs and LDS reads fill the gaps of the softmax-gradient VALU work); one
+  // barrier per chunk publishes dS(ch) and the next chunk's Q/dO.
   for (int ch = 0; ch < nch; ++ch) {
     const int buf = ch & 1, q0 = ch * 32;
-    dwc[0] = dwn[0]; dwc[1] = dwn[1];
+    // 4-bit keep masks of this lane's queries (16qs + 4g + r) for its two keys
+    uint32_t nib[2][2];
+    if (!a.thr) {
+      nib[0][0] = nib[0][1] = nib[1][0] = nib[1][1] = 15u;
+    } else if (usebits) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const uint32_t wv = kw0 + 16 * t + li < a.Lk ? dwn[t] : 0u;
+        nib[0][t] = (wv >> (4 * g)) & 15u;
+        nib[1][t] = (wv >> (16 + 4 * g)) & 15u;
+      }
+    } else {
+#pragma unroll
+      for (int qs = 0; qs < 2; ++qs)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int key = kw0 + 16 * t + li, qb = q0 + 16 * qs + 4 * g;
+          const uint32_t h01 = rng_hash(a.seed, attn_pair(bh, a.Lq, a.Lk, qb, key));
+          const uint32_t h23 = rng_hash(a.seed, attn_pair(bh, a.Lq, a.Lk, qb + 2, key));
+          nib[qs][t] = (uint32_t)(rng_half(h01, 0) >= a.thr) | ((uint32_t)(rng_half(h01, 1) >= a.thr) << 1) |
+                       ((uint32_t)(rng_half(h23, 0) >= a.thr) << 2) | ((uint32_t)(rng_half(h23, 1) >= a.thr) << 3);
+        }
+    }
     if (ch + 1 < nch) fetch(ch + 1);
-    const bool active = kown && !(causal && kw0 > q0 + 31);   // causal: keys above every query of the chunk
-    if (active) {
-      const bf16_t* cq = sq + buf * 32 * R_CS;
-      const bf16_t* cdo = sdo + buf * 32 * R_CS;
+    ATTN_TS(2 + 4 * ch);
+    const bf16_t* cq = sq + buf * 32 * R_CS;
+    const bf16_t* cdo = sdo + buf * 32 * R_CS;
+    if (causal && kw0 > q0 + 31) {
+      // every key of this wave lies above every query of the chunk: dS = 0 (keeps the dQ sweep branch-free)
+#pragma unroll
+      for (int qs = 0; qs < 2; ++qs)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          *(uint2*)(sds + (buf * NK + kw0 + 16 * t + li) * RDT + 16 * qs + 4 * g) = make_uint2(0, 0);
+      if (ch > 0) dq_chunk(ch - 1);
+    } else {
       f4_t s[2][2], dp[2][2];   // [qs][t]
 #pragma unroll
       for (int qs = 0; qs < 2; ++qs) {
@@ -757,6 +833,7 @@ __global__ __launch_bounds__(512) void attn_bwd_res_kernel(AttnArgs a) {
           dp[qs][t] = mfma32(d1f, vf[t][1], mfma32(d0f, vf[t][0], f4_t{0.f, 0.f, 0.f, 0.f}));
         }
       }
+      if (ch > 0) dq_chunk(ch - 1);
       const bool diag = causal && kw0 + 31 > q0;
       s4_t pdb[2][2], dsb[2][2];
 #pragma unroll
@@ -767,11 +844,7 @@ __global__ __launch_bounds__(512) void attn_bwd_res_kernel(AttnArgs a) {
         for (int t = 0; t < 2; ++t) {
           const int key = kw0 + 16 * t + li;
           const int qb = q0 + 16 * qs + 4 * g;
-          uint32_t h01 = 0, h23 = 0;
-          if (a.thr && !usebits) {
-            h01 = rng_hash(a.seed, attn_pair(bh, a.Lq, a.Lk, qb, key));
-            h23 = rng_hash(a.seed, attn_pair(bh, a.Lq, a.Lk, qb + 2, key));
-          }
+          const f4_t fk = slut[nib[qs][t]];   // dropout factor per element (keep ? 1/(1-p) : 0; 1 without dropout)
           f4_t pd, dsv;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -782,21 +855,14 @@ __global__ __launch_bounds__(512) void attn_bwd_res_kernel(AttnArgs a) {
               if (diag && key > qb + r) x = -INFINITY;
             }
             const float p = exp2_raw(x);
-            float dpe = dp[qs][t][r], pdv = p;
-            if (a.thr) {
-              const bool keep = usebits ? ((dwc[t] >> (16 * qs + 4 * g + r)) & 1u)
-                                        : (rng_half(r < 2 ? h01 : h23, r & 1) >= a.thr);
-              dpe = keep ? dpe * a.dscale : 0.f;
-              pdv = keep ? p * a.dscale : 0.f;
-            }
-            pd[r] = pdv;
-            dsv[r] = p * (dpe - del4[r]);
+            const float pk = p * fk[r];                       // dropped-out probability (feeds dV)
+            pd[r] = pk;
+            dsv[r] = fmaf(pk, dp[qs][t][r], -p * del4[r]);    // P * (dP_kept - delta)
           }
           pdb[qs][t] = to_bf4(pd);
           dsb[qs][t] = to_bf4(dsv);
-          bf16_t* dsp = sds + (buf * 32 + 16 * qs + 4 * g) * rds + key;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) dsp[r * rds] = (bf16_t)dsb[qs][t][r];
+          // dS^T image: this lane's 4 consecutive queries of one key -> one 8-byte write
+          *(s4_t*)(sds + (buf * NK + key) * RDT + 16 * qs + 4 * g) = dsb[qs][t];
         }
       }
       // dV^T += dO^T Pd ; dK^T += Q^T dS   (k-slots: queries 4g+j of sub-tile 0, then of sub-tile 1)
@@ -812,41 +878,17 @@ __global__ __launch_bounds__(512) void attn_bwd_res_kernel(AttnArgs a) {
         }
       }
     }
-    if (ch + 1 < nch) publish(buf ^ 1);
+    ATTN_TS(3 + 4 * ch);
+    if (ch + 1 < nch) publish(buf ^ 1, ch + 1);
     __syncthreads();
-    // dQ^T[d][q] = sum_key K^T[d][key] dS^T[key][q] over the chunk's 8 (sub-tile, 16-column) tiles; every
-    // operand of a tile is read before its MFMA chain starts
-    int kcn = nkt;
-    if (causal) kcn = min(nkt, (q0 + 31) / 32 + 1);
-    for (int tl = w; tl < 8; tl += nw) {
-      const int qs = tl >> 2, u = tl & 3;
-      const bf16_t* dsr = sds + (buf * 32 + 16 * qs + li) * rds + 8 * g;
-      const bf16_t* kp = sk + (8 * g + (li >> 2)) * R_VS + 16 * u + 4 * (li & 3);
-      s8_t ka[8], da[8];
-#pragma unroll
-      for (int kc = 0; kc < 8; ++kc)
-        if (kc < kcn) {
-          ka[kc] = cat8(lds_tr(kp + 32 * kc * R_VS), lds_tr(kp + (32 * kc + 4) * R_VS));
-          da[kc] = lds_b128(dsr + 32 * kc);
-        }
-      f4_t acc = f4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kc = 0; kc < 8; ++kc)
-        if (kc < kcn) acc = mfma32(ka[kc], da[kc], acc);
-      const int q = q0 + 16 * qs + li;
-      if (q < a.Lq) {
-        uint2 x;
-        x.x = pack2bf(acc[0] * a.scale, acc[1] * a.scale);
-        x.y = pack2bf(acc[2] * a.scale, acc[3] * a.scale);
-        *(uint2*)(a.dq + b * a.dqb + (int64_t)q * a.dqr + h * 64 + 16 * u + 4 * g) = x;
-      }
-    }
+    ATTN_TS(4 + 4 * ch);
   }
+  dq_chunk(nch - 1);
 
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const int key = kw0 + 16 * t + li;
-    if (!kown || key >= a.Lk) continue;
+    if (key >= a.Lk) continue;
     bf16_t* dkp = a.dk + b * a.dkb + (int64_t)key * a.dkr + h * 64 + 4 * g;
     bf16_t* dvp = a.dv + b * a.dvb + (int64_t)key * a.dvr + h * 64 + 4 * g;
 #pragma unroll
@@ -862,9 +904,11 @@ __global__ __launch_bounds__(512) void attn_bwd_res_kernel(AttnArgs a) {
   }
 }
 
+int bwd_res_nkt(int lk) { return lk <= 64 ? 2 : (lk <= 128 ? 4 : 8); }
+
 size_t bwd_res_smem(int lk) {
-  const int nk = (lk + 31) / 32 * 32;
-  return (size_t)(nk * R_VS + 4 * 32 * R_CS + 2 * 32 * (nk + 8)) * 2 + 128 * 4;
+  const int nk = bwd_res_nkt(lk) * 32;
+  return (size_t)(nk * R_VS + 4 * 32 * R_CS + 2 * nk * (32 + 8)) * 2 + 128 * 4 + 16 * 16;
 }
 
 // dq (bf16, strided) = scale * dq_acc (fp32 [B][Lq][H][DH])
@@ -909,6 +953,8 @@ int fill_args(const asrx_attn_desc* d, AttnArgs& a) {
   a.dv = (bf16_t*)d->dv; a.dvr = d->dv_rstride; a.dvb = d->dv_bstride;
   a.delta = d->delta; a.dq_acc = d->dq_acc;
   a.dropmask = d->dropmask;
+  const char* dbg = getenv("ASRX_ATTN_DBG");
+  a.dbg = dbg && dbg[0] == '1';
   return ASRX_OK;
 }
 
@@ -974,11 +1020,14 @@ extern "C" int asrx_attention_bwd(const asrx_attn_desc* d, void* stream) {
   rc = asrx_attn_delta(d, stream);
   if (rc) return rc;
   if (resident_ok(d, a) && a.dqr % 4 == 0 && a.dqb % 4 == 0 && (uintptr_t)a.dq % 8 == 0) {
-    const int nw = std::max(2, (a.Lk + 31) / 32);
+    const int nkt = bwd_res_nkt(a.Lk);
     const size_t sm = bwd_res_smem(a.Lk);
-    if (a.mode == 0) hipLaunchKernelGGL(attn_bwd_res_kernel<0>, dim3(a.B * a.H), dim3(64 * nw), sm, st, a);
-    else if (a.mode == 1) hipLaunchKernelGGL(attn_bwd_res_kernel<1>, dim3(a.B * a.H), dim3(64 * nw), sm, st, a);
-    else hipLaunchKernelGGL(attn_bwd_res_kernel<2>, dim3(a.B * a.H), dim3(64 * nw), sm, st, a);
+    const dim3 grid(a.B * a.H), blk(64 * nkt);
+#define ASRX_BWD_RES(M, N) hipLaunchKernelGGL((attn_bwd_res_kernel<M, N>), grid, blk, sm, st, a)
+    if (a.mode == 0) { if (nkt == 2) ASRX_BWD_RES(0, 2); else if (nkt == 4) ASRX_BWD_RES(0, 4); else ASRX_BWD_RES(0, 8); }
+    else if (a.mode == 1) { if (nkt == 2) ASRX_BWD_RES(1, 2); else if (nkt == 4) ASRX_BWD_RES(1, 4); else ASRX_BWD_RES(1, 8); }
+    else { if (nkt == 2) ASRX_BWD_RES(2, 2); else if (nkt == 4) ASRX_BWD_RES(2, 4); else ASRX_BWD_RES(2, 8); }
+#undef ASRX_BWD_RES
     ASRX_CHECK_LAUNCH();
     return ASRX_OK;
   }
@@ -1002,4 +1051,11 @@ extern "C" int asrx_attention_bwd(const asrx_attn_desc* d, void* stream) {
     ASRX_CHECK_LAUNCH();
   }
   return ASRX_OK;
+}
+
+// tools only (not part of include/asrx.h): copy the phase timestamps of the last debug launch
+extern "C" int asrx_attn_debug_read(unsigned long long* host, int n) {
+  if (!host || n < 0 || n > 64) return ASRX_ERR_ARG;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_attn_dbg), sizeof(unsigned long long) * n) == hipSuccess ? ASRX_OK
+                                                                                                       : ASRX_ERR_LAUNCH;
 }

@@ -70,6 +70,7 @@ def main():
     ap.add_argument("--only", default="enc,cross,dec")
     ap.add_argument("--variant", default="auto")
     ap.add_argument("--sweep", action="store_true", help="Lq sweep at Lk=249 (per-chunk vs fixed cost)")
+    ap.add_argument("--dbg", action="store_true", help="phase timestamps of block 0 / wave 0 of the backward")
     args = ap.parse_args()
     os.environ["ASRX_ATTN_KERNEL"] = args.variant
     cases = {"enc": ("enc_self", 249, 249, False), "cross": ("cross", 64, 249, False),
@@ -78,6 +79,29 @@ def main():
         for lq in (32, 64, 128, 192, 249):
             cases[f"s{lq}"] = (f"lq{lq}", lq, 249, False)
         args.only = ",".join(k for k in cases if k.startswith("s"))
+    if args.dbg:
+        import ctypes
+        from asrx._lib import lib
+        for key in args.only.split(","):
+            name, fwd, bwd, ff, fb = case(*cases[key])
+            fwd()
+            bwd()
+            torch.cuda.synchronize()
+            os.environ["ASRX_ATTN_DBG"] = "1"
+            bwd()
+            torch.cuda.synchronize()
+            os.environ.pop("ASRX_ATTN_DBG")
+            buf = (ctypes.c_ulonglong * 64)()
+            lib().asrx_attn_debug_read(buf, 64)
+            ts = list(buf)
+            t0 = ts[0]
+            print(name, "prologue", ts[1] - t0, "cycles")
+            for ch in range(8):
+                a, b, c, d = ts[2 + 4 * ch:6 + 4 * ch]
+                if a == 0 or a < t0:
+                    break
+                print(f"  chunk {ch}: fetch-issued {a - t0:7d}  compute {b - a:6d}  publish+barrier {c - b:6d}  dQ {d - c:6d}")
+        return
     for key in args.only.split(","):
         name, fwd, bwd, ff, fb = case(*cases[key])
         fwd()
