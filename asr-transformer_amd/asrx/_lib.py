@@ -79,7 +79,7 @@ class AttnDesc(ctypes.Structure):
         ("dk", c_vp), ("dk_rstride", c_i64), ("dk_bstride", c_i64),
         ("dv", c_vp), ("dv_rstride", c_i64), ("dv_bstride", c_i64),
         ("delta", c_vp), ("dq_acc", c_vp),
-        ("dropmask", c_vp),
+        ("dropmask", c_vp), ("dropmask_ready", c_i32),
     ]
 
 
@@ -91,6 +91,7 @@ SIGNATURES = {
     "asrx_gemm_grouped": [ctypes.POINTER(GemmDesc), ctypes.POINTER(GemmGroup), c_i32, c_vp],
     "asrx_reduce_rows_grouped": [ctypes.POINTER(RowsumGroup), c_i32, c_vp],
     "asrx_attention_fwd": [ctypes.POINTER(AttnDesc), c_vp],
+    "asrx_attn_dropgen": [ctypes.POINTER(AttnDesc), c_vp],
     "asrx_attention_bwd": [ctypes.POINTER(AttnDesc), c_vp],
     "asrx_attn_delta": [ctypes.POINTER(AttnDesc), c_vp],
     "asrx_softmax_fwd": [c_i32, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i64, c_f32, c_i32, c_i32, c_vp, c_vp,

@@ -38,6 +38,12 @@ class Ctx:
     def seed(self):
         return self.seeds.next() if self.p > 0 else 0
 
+    def side_stream(self, device):
+        st = getattr(self, "_side", None)
+        if st is None:
+            st = self._side = _side_stream(device)
+        return st
+
     def wgrad(self, dy, x, gw, gb=None):
         """dW (+)= dy^T x, db (+)= colsum(dy).  Weight gradients feed nothing but the optimizer, so while a
         queue is open they are deferred and later issued as grouped launches (no split-K)."""
@@ -68,6 +74,17 @@ class Seeds:
         self.i += 1
         x = (self.base * 0x9E3779B97F4A7C15 + self.i * 0xBF58476D1CE4E5B9) & ((1 << 64) - 1)
         return x ^ (x >> 31)
+
+
+_SIDE = {}
+
+
+def _side_stream(device):
+    """One auxiliary HIP stream per device for work that only depends on RNG seeds (dropout keep bits)."""
+    key = torch.device(device).index or 0
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device=device)
+    return _SIDE[key]
 
 
 def _empty(shape, dtype, like):
@@ -104,14 +121,41 @@ def ln_bwd(C, x, dy, ln, mean, rstd, dres=None, drop_out=None, drop_seed=0, drop
 
 # ------------------------------------------------------------------------------------------------ attention
 
-def attn_fwd(C, q, k, v, o, B, H, Lq, Lk, dh, strides, scale, spec):
+def attn_prepare(C, B, H, Lq, Lk, dh, device):
+    """Draw the attention-dropout seed and, where the resident kernels will consume them, start generating the
+    keep bits on the side stream now — they depend only on (seed, shapes), so they overlap the LayerNorm and
+    Q/K/V projection that precede the attention on the main stream."""
+    prep = {"seed": C.seed(), "dropmask": None, "event": None}
+    if C.cd == torch.bfloat16 and C.attn_impl == "fused" and C.p > 0:
+        dm = K.dropmask_buffer(B, H, Lq, Lk, dh, C.p, device)
+        if dm is not None:
+            main = torch.cuda.current_stream(device)
+            side = C.side_stream(device)
+            side.wait_stream(main)             # the buffer's allocation is ordered on the main stream
+            with torch.cuda.stream(side):
+                K.attention_dropgen(B, H, Lq, Lk, dh, C.p, prep["seed"], dm)
+                ev = torch.cuda.Event()
+                ev.record(side)
+            dm.record_stream(side)
+            prep["dropmask"], prep["event"] = dm, ev
+    return prep
+
+
+def attn_fwd(C, q, k, v, o, B, H, Lq, Lk, dh, strides, scale, spec, prep=None):
     """Fused LDS-tiled kernel on the bf16 path; materialised scores + row softmax otherwise."""
-    seed = C.seed()
+    if prep is None:
+        prep = {"seed": C.seed(), "dropmask": None, "event": None}
+    seed = prep["seed"]
     S = {"seed": seed, "spec": spec, "dims": (B, H, Lq, Lk, dh), "strides": strides, "scale": scale}
     if C.cd == torch.bfloat16 and C.attn_impl == "fused" and dh in (32, 64):
-        S["dropmask"] = K.dropmask_buffer(B, H, Lq, Lk, dh, C.p, q.device)
+        dm, ready = prep["dropmask"], prep["event"] is not None
+        if ready:
+            torch.cuda.current_stream(q.device).wait_event(prep["event"])
+        else:
+            dm = K.dropmask_buffer(B, H, Lq, Lk, dh, C.p, q.device)
+        S["dropmask"] = dm
         S["lse"] = K.attention_fwd(q, k, v, o, B, H, Lq, Lk, dh, strides, scale, spec, C.p, seed,
-                                   dropmask=S["dropmask"])
+                                   dropmask=dm, dropmask_ready=ready)
         S["impl"] = "fused"
         return S
     S["impl"] = "unfused"
@@ -164,12 +208,13 @@ def self_attn_fwd(C, x, ln, mha, B, T, H, spec):
     """x + Drop(MHA(LN(x))) with fused per-head projections (layers.py:10-12 -> one N=3d GEMM)."""
     M, d = x.shape
     dh = d // H
+    prep = attn_prepare(C, B, H, T, T, dh, x.device)
     h, mean, rstd = ln_fwd(C, x, ln)
     qkv = _empty((M, 3 * d), C.cd, x)
     K.linear(h, C.W(mha.wqkv), qkv, bias=mha.bqkv.data)
     o = _empty((M, d), C.cd, x)
     st = ((3 * d, T * 3 * d),) * 3 + ((d, T * d),)
-    A = attn_fwd(C, qkv, qkv[:, d:], qkv[:, 2 * d:], o, B, H, T, T, dh, st, d ** -0.5, spec)
+    A = attn_fwd(C, qkv, qkv[:, d:], qkv[:, 2 * d:], o, B, H, T, T, dh, st, d ** -0.5, spec, prep)
     y = _empty((M, d), torch.float32, x)
     sd = C.seed()
     K.linear(o, C.W(mha._out_linear.weight), y, bias=mha._out_linear.bias.data, dropout_p=C.p, seed=sd, resid=x,
@@ -201,12 +246,13 @@ def cross_attn_fwd(C, x, ln, mha, kv, kv_ld, B, L, Te, H):
     """x + Drop(MHA(LN(x), enc)) — no mask (model.py:71); K/V come from the precomputed all-layer projection."""
     M, d = x.shape
     dh = d // H
+    prep = attn_prepare(C, B, H, L, Te, dh, x.device)
     h, mean, rstd = ln_fwd(C, x, ln)
     q = _empty((M, d), C.cd, x)
     K.linear(h, C.W(mha.wq), q, bias=mha.bq.data)
     o = _empty((M, d), C.cd, x)
     st = ((d, L * d), (kv_ld, Te * kv_ld), (kv_ld, Te * kv_ld), (d, L * d))
-    A = attn_fwd(C, q, kv, kv[:, d:], o, B, H, L, Te, dh, st, d ** -0.5, MaskSpec())
+    A = attn_fwd(C, q, kv, kv[:, d:], o, B, H, L, Te, dh, st, d ** -0.5, MaskSpec(), prep)
     y = _empty((M, d), torch.float32, x)
     sd = C.seed()
     K.linear(o, C.W(mha._out_linear.weight), y, bias=mha._out_linear.bias.data, dropout_p=C.p, seed=sd, resid=x,

@@ -341,16 +341,29 @@ def dropmask_buffer(B, H, Lq, Lk, dh, dropout_p, device):
     """Keep-bit buffer the resident-K/V attention forward fills for its backward (None when unused)."""
     if dropout_p <= 0.0 or dh != 64 or Lk > 256:
         return None
-    return torch.empty(B * H * ((Lq + 31) // 32) * Lk, device=device, dtype=torch.int32)
+    return torch.empty(B * H * (((Lq + 31) // 32) * Lk + Lq * ((Lk + 31) // 32)), device=device, dtype=torch.int32)
 
 
-def attention_fwd(q, k, v, o, B, H, Lq, Lk, dh, strides, scale, spec, dropout_p=0.0, seed=0, dropmask=None):
+def attention_dropgen(B, H, Lq, Lk, dh, dropout_p, seed, dropmask):
+    """Generate the attention dropout keep bits into `dropmask` (see dropmask_buffer) on the current stream."""
+    _cuda(dropmask)
+    d = AttnDesc()
+    d.batch, d.heads, d.lq, d.lk, d.dh = B, H, Lq, Lk, dh
+    d.q = d.k = d.v = dropmask.data_ptr()      # not read; fill_args only checks them
+    d.dropout_p, d.seed = dropout_p, seed & _U64
+    d.dropmask = dropmask.data_ptr()
+    call("asrx_attn_dropgen", ctypes.byref(d), stream())
+
+
+def attention_fwd(q, k, v, o, B, H, Lq, Lk, dh, strides, scale, spec, dropout_p=0.0, seed=0, dropmask=None,
+                  dropmask_ready=False):
     """Fused attention (bf16). Returns lse [B*H*Lq] (log2 domain)."""
     _cuda(q, k, v, o, dropmask)
     lse = torch.empty(B * H * Lq, device=q.device, dtype=torch.float32)
     d = _attn_desc(q, k, v, o, B, H, Lq, Lk, dh, strides, scale, spec, dropout_p, seed)
     d.lse = lse.data_ptr()
     d.dropmask = _p(dropmask)
+    d.dropmask_ready = int(bool(dropmask_ready))
     call("asrx_attention_fwd", ctypes.byref(d), stream())
     return lse
 

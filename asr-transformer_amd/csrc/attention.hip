@@ -445,11 +445,48 @@ ASRX_DEV float xsum4(float v) {
 // MODE: 0 = no mask, 1 = causal / key-valid / query-valid vectors (folded into per-key biases and lse),
 // 2 = dense byte mask (generic per-element test).
 // Forward grid (ceil(Lq/256), B*H), 8 waves x 32 queries (two 16-query sub-tiles per wave).
+// Dropout keep bits for the resident kernels, generated once per attention call (the counter-based RNG of
+// common.h, pairs along queries), in two layouts so that each kernel reads whole words in its own lane order:
+//   key-major   kmaj[(bh * nqc + qc) * Lk + key], bit i = keep(query 32 qc + i, key)      (backward)
+//   query-major qmaj[(bh * Lq + q) * nkw + kw],   bit j = keep(q, key 32 kw + j)            (forward)
+// grid (nqc, B*H), 256 threads: thread = key (32 queries -> 16 pair hashes), LDS transpose for qmaj.
+__global__ __launch_bounds__(256) void attn_dropgen_kernel(AttnArgs a, uint32_t* kmaj, uint32_t* qmaj) {
+  __shared__ uint32_t sw[R_MAXK];
+  const int qc = blockIdx.x, bh = blockIdx.y, tid = threadIdx.x;
+  const int nqc = gridDim.x, nkw = (a.Lk + 31) >> 5, q0 = qc * 32;
+  const int key = tid;
+  uint32_t word = 0;
+  if (key < a.Lk) {
+    const uint32_t lqh = (uint32_t)((a.Lq + 1) >> 1);
+#pragma unroll 4
+    for (int i = 0; i < 16; ++i) {   // query pair (q0/2 + i): low half -> query q0 + 2i, high -> q0 + 2i + 1
+      const uint32_t h = rng_hash(a.seed, ((uint32_t)bh * lqh + (uint32_t)(q0 / 2 + i)) * (uint32_t)a.Lk + (uint32_t)key);
+      word |= (uint32_t)(rng_half(h, 0) >= a.thr) << (2 * i);
+      word |= (uint32_t)(rng_half(h, 1) >= a.thr) << (2 * i + 1);
+    }
+    kmaj[((int64_t)bh * nqc + qc) * a.Lk + key] = word;
+  }
+  if (key < R_MAXK) sw[key] = key < a.Lk ? word : 0u;
+  __syncthreads();
+  const int ql = tid & 31, kw = tid >> 5;
+  if (kw < nkw && q0 + ql < a.Lq) {
+    uint32_t qw = 0;
+#pragma unroll 8
+    for (int j = 0; j < 32; ++j) qw |= ((sw[32 * kw + j] >> ql) & 1u) << j;
+    qmaj[((int64_t)bh * a.Lq + q0 + ql) * nkw + kw] = qw;
+  }
+}
+
+// MODE: 0 = no mask, 1 = causal / key-valid / query-valid vectors (folded into per-key biases and lse),
+// 2 = dense byte mask (generic per-element test).
+// Forward grid (ceil(Lq/256), B*H), 8 waves x 32 queries (two 16-query sub-tiles per wave).  Dropout factors
+// come from the query-major keep bits (a 4-bit nibble per (sub-tile, 16-key half) -> one LDS table read).
 template <int MODE>
-__global__ __launch_bounds__(512) void attn_fwd_res_kernel(AttnArgs a) {
+__global__ __launch_bounds__(512) void attn_fwd_res_kernel(AttnArgs a, const uint32_t* qmaj) {
   __shared__ __attribute__((aligned(16))) bf16_t sk[R_MAXK * R_KS];
   __shared__ __attribute__((aligned(16))) bf16_t sv[R_MAXK * R_VS];
   __shared__ __attribute__((aligned(16))) float skb[R_MAXK];   // per-key score bias: 0 or -inf
+  __shared__ __attribute__((aligned(16))) f4_t slut[16];       // dropout factors of a 4-bit keep mask
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, li = l & 15;
   const int nkt = (a.Lk + 31) >> 5;
@@ -461,19 +498,16 @@ __global__ __launch_bounds__(512) void attn_fwd_res_kernel(AttnArgs a) {
     uint4 kv[4], vv[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int c = c0 + i * 512, row = c >> 3, dc = (c & 7) * 8;
-      kv[i] = vv[i] = make_uint4(0, 0, 0, 0);
-      if (c < nk * 8 && row < a.Lk) {
-        kv[i] = *(const uint4*)(Kb + (int64_t)row * a.kr + dc);
-        vv[i] = *(const uint4*)(Vb + (int64_t)row * a.vr + dc);
-      }
+      const int c = c0 + i * 512, row = min(c >> 3, a.Lk - 1), dc = (c & 7) * 8;
+      kv[i] = *(const uint4*)(Kb + (int64_t)row * a.kr + dc);
+      vv[i] = *(const uint4*)(Vb + (int64_t)row * a.vr + dc);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int c = c0 + i * 512, row = c >> 3, dc = (c & 7) * 8;
       if (c < nk * 8) {
-        *(uint4*)(sk + row * R_KS + dc) = kv[i];
-        *(uint4*)(sv + row * R_VS + dc) = vv[i];
+        *(uint4*)(sk + row * R_KS + dc) = row < a.Lk ? kv[i] : make_uint4(0, 0, 0, 0);
+        *(uint4*)(sv + row * R_VS + dc) = row < a.Lk ? vv[i] : make_uint4(0, 0, 0, 0);
       }
     }
   }
@@ -483,16 +517,28 @@ __global__ __launch_bounds__(512) void attn_fwd_res_kernel(AttnArgs a) {
     if (MODE == 1 && ok && a.kvalid) ok = a.kvalid[b * a.validb + key] != 0;
     skb[key] = ok ? 0.f : -INFINITY;
   }
+  if (threadIdx.x < 16) {
+    f4_t f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) f[r] = ((threadIdx.x >> r) & 1) ? a.dscale : 0.f;
+    slut[threadIdx.x] = f;
+  }
   const int qw0 = (blockIdx.x * 8 + w) * 32;
   s8_t qf[2][2];
   bool qdead[2];
+  uint32_t dw[2][8];   // query-major keep words of this lane's two queries (one per 32-key tile)
+  const int nkw = nkt;
 #pragma unroll
   for (int qs = 0; qs < 2; ++qs) {
     const int q = qw0 + 16 * qs + li;
-    const bf16_t* qp = a.q + b * a.qb + (int64_t)(q < a.Lq ? q : 0) * a.qr + h * 64 + 8 * g;
+    const int qc = min(q, a.Lq - 1);
+    const bf16_t* qp = a.q + b * a.qb + (int64_t)qc * a.qr + h * 64 + 8 * g;
 #pragma unroll
-    for (int c = 0; c < 2; ++c) qf[qs][c] = q < a.Lq ? *(const s8_t*)(qp + 32 * c) : s8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    for (int c = 0; c < 2; ++c) qf[qs][c] = *(const s8_t*)(qp + 32 * c);
     qdead[qs] = MODE == 1 && q < a.Lq && a.qvalid && !a.qvalid[b * a.validb + q];
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt)
+      dw[qs][kt] = (qmaj && kt < nkw) ? qmaj[((int64_t)bh * a.Lq + qc) * nkw + kt] : 0xffffffffu;
   }
   __syncthreads();
   if (qw0 >= a.Lq) return;   // no barrier below
@@ -503,14 +549,10 @@ __global__ __launch_bounds__(512) void attn_fwd_res_kernel(AttnArgs a) {
   float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
   int ktn = nkt;
   if (MODE == 1 && a.causal) ktn = min(nkt, (min(a.Lq, qw0 + 32) - 1) / 32 + 1);
-  const int odd = li & 1;
-  const uint32_t lqh = (uint32_t)((a.Lq + 1) >> 1);
-  uint32_t prow[2];   // attention RNG pair-row bases (common.h attn_pair), 32-bit wrap as on the host side
-#pragma unroll
-  for (int qs = 0; qs < 2; ++qs) prow[qs] = ((uint32_t)bh * lqh + (uint32_t)((qw0 + 16 * qs + li) >> 1)) * (uint32_t)a.Lk;
-  uint32_t* dmw = (a.thr && a.dropmask) ? a.dropmask + ((int64_t)bh * ((a.Lq + 31) >> 5) + (qw0 >> 5)) * a.Lk : nullptr;
 
-  for (int kt = 0; kt < ktn; ++kt) {
+#pragma unroll
+  for (int kt = 0; kt < 8; ++kt) {
+    if (kt >= ktn) break;
     f4_t s[2][2];
     f4_t kb[2];
 #pragma unroll
@@ -523,7 +565,6 @@ __global__ __launch_bounds__(512) void attn_fwd_res_kernel(AttnArgs a) {
     }
     const bool diag = MODE == 1 && a.causal && kt * 32 + 31 > qw0;   // tile reaches above some query
     s4_t pf[2][2];
-    bool kp[2][2][4];
 #pragma unroll
     for (int qs = 0; qs < 2; ++qs) {
       const int q = qw0 + 16 * qs + li;
@@ -555,41 +596,17 @@ __global__ __launch_bounds__(512) void attn_fwd_res_kernel(AttnArgs a) {
       float rs = 0.f;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
+        const f4_t fk = slut[(dw[qs][kt] >> (16 * t + 4 * g)) & 15u];
         f4_t pv;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          pv[r] = exp2_raw(s[t][qs][r] - m_use);
-          rs += pv[r];
-        }
-        if (a.thr) {   // lanes l, l^1 hold queries 2j, 2j+1: each hashes two of the four keys, then they swap
-          const uint32_t kbse = prow[qs] + (uint32_t)(kt * 32 + 16 * t + 4 * g + 2 * odd);
-          const uint32_t hA = rng_hash(a.seed, kbse), hB = rng_hash(a.seed, kbse + 1);
-          const uint32_t oA = xchg1(hA), oB = xchg1(hB);
-          const uint32_t hh[4] = {odd ? oA : hA, odd ? oB : hB, odd ? hA : oA, odd ? hB : oB};
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            kp[qs][t][r] = rng_half(hh[r], odd) >= a.thr;
-            pv[r] = kp[qs][t][r] ? pv[r] * a.dscale : 0.f;
-          }
+          const float e = exp2_raw(s[t][qs][r] - m_use);
+          rs += e;
+          pv[r] = e * fk[r];
         }
         pf[t][qs] = to_bf4(pv);
       }
       l_run[qs] += xsum4(rs);
-    }
-    if (dmw) {   // publish the keep bits: word for key kt*32 + l (l < 32) = 32 queries of this wave
-      uint32_t word = 0;
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const uint64_t b0 = __ballot(kp[0][t][r]), b1 = __ballot(kp[1][t][r]);
-          if ((l >> 4) == t && (l & 3) == r) {
-            const int gs = 16 * ((l >> 2) & 3);
-            word = (uint32_t)((b0 >> gs) & 0xffffu) | ((uint32_t)((b1 >> gs) & 0xffffu) << 16);
-          }
-        }
-      const int key = kt * 32 + l;
-      if (l < 32 && key < a.Lk) dmw[key] = word;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -972,18 +989,42 @@ size_t bwd_smem(int nw, int dh) {
 
 }  // namespace
 
+extern "C" int asrx_attn_dropgen(const asrx_attn_desc* d, void* stream) {
+  AttnArgs a;
+  int rc = fill_args(d, a);
+  if (rc) return rc;
+  if (!a.dropmask || a.Lk > R_MAXK) return ASRX_ERR_ARG;
+  if (!a.thr) return ASRX_OK;
+  const int nqc = (a.Lq + 31) / 32;
+  uint32_t* kmaj = a.dropmask;
+  uint32_t* qmaj = a.dropmask + (int64_t)a.B * a.H * nqc * a.Lk;
+  hipLaunchKernelGGL(attn_dropgen_kernel, dim3(nqc, a.B * a.H), dim3(256), 0, (hipStream_t)stream, a, kmaj, qmaj);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
 extern "C" int asrx_attention_fwd(const asrx_attn_desc* d, void* stream) {
   AttnArgs a;
   int rc = fill_args(d, a);
   if (rc) return rc;
   if (!a.o || (a.orr % 4) || (a.ob % 4) || ((uintptr_t)a.o % 8)) return ASRX_ERR_UNSUPPORTED;
   hipStream_t st = (hipStream_t)stream;
-  if (resident_ok(d, a)) {
+  if (resident_ok(d, a) && (!a.thr || a.dropmask)) {
+    // dropout: keep bits (key-major for the backward, query-major for this kernel), generated here unless the
+    // caller already did (asrx_attn_dropgen, e.g. on a side stream while the Q/K/V projection runs)
+    const uint32_t* qmaj = nullptr;
+    if (a.thr) {
+      if (!d->dropmask_ready) {
+        const int rc2 = asrx_attn_dropgen(d, stream);
+        if (rc2) return rc2;
+      }
+      qmaj = a.dropmask + (int64_t)a.B * a.H * ((a.Lq + 31) / 32) * a.Lk;
+    }
     // 8 waves always: idle query waves still help stage K/V, then leave
     dim3 grid((a.Lq + 255) / 256, a.B * a.H);
-    if (a.mode == 0) hipLaunchKernelGGL(attn_fwd_res_kernel<0>, grid, dim3(512), 0, st, a);
-    else if (a.mode == 1) hipLaunchKernelGGL(attn_fwd_res_kernel<1>, grid, dim3(512), 0, st, a);
-    else hipLaunchKernelGGL(attn_fwd_res_kernel<2>, grid, dim3(512), 0, st, a);
+    if (a.mode == 0) hipLaunchKernelGGL(attn_fwd_res_kernel<0>, grid, dim3(512), 0, st, a, qmaj);
+    else if (a.mode == 1) hipLaunchKernelGGL(attn_fwd_res_kernel<1>, grid, dim3(512), 0, st, a, qmaj);
+    else hipLaunchKernelGGL(attn_fwd_res_kernel<2>, grid, dim3(512), 0, st, a, qmaj);
     ASRX_CHECK_LAUNCH();
     return ASRX_OK;
   }

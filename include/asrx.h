@@ -122,13 +122,19 @@ typedef struct asrx_attn_desc {
   void* dv; int64_t dv_rstride, dv_bstride;
   float* delta;                 /* [batch*heads*lq] workspace */
   float* dq_acc;                /* [batch*lq*heads*dh] fp32 workspace, used when lk > 256 */
-  /* optional dropout keep bits [batch*heads][ceil(lq/32)][lk] (bit i of a word = query 32*c + i): written by the
-   * forward when dh = 64, lk <= 256 and dropout_p > 0, read by the backward instead of re-hashing.  The bits
-   * equal the counter-based RNG's decisions, so passing NULL to either side gives identical results. */
+  /* optional dropout keep-bit workspace (dh = 64, lk <= 256, dropout_p > 0): key-major words
+   * [batch*heads][ceil(lq/32)][lk] (bit i = query 32c+i) followed by query-major words
+   * [batch*heads][lq][ceil(lk/32)] (bit j = key 32c+j), generated by the forward and read by the backward
+   * instead of re-hashing.  The bits equal the counter-based RNG's decisions, so results do not depend on it;
+   * without it the forward uses the tiled kernel. */
   uint32_t* dropmask;
+  int32_t dropmask_ready;       /* nonzero: the forward finds the bits already generated (asrx_attn_dropgen) */
 } asrx_attn_desc;
 
 int asrx_attention_fwd(const asrx_attn_desc* d, void* stream);
+/* Fill d->dropmask with the dropout keep bits of (seed, dropout_p, shapes) — both layouts (see dropmask).  Only
+ * the shape/dropout fields of d are read; independent of the Q/K/V data, so it can run ahead on another stream. */
+int asrx_attn_dropgen(const asrx_attn_desc* d, void* stream);
 int asrx_attention_bwd(const asrx_attn_desc* d, void* stream);
 
 /* ---------------------------------------------------------------------------------------------------

@@ -338,7 +338,10 @@ def test_attention_dense_mask_and_dropout_consistency(L, attn_variant, bits):
     if dm is not None and attn_variant == "auto":   # the forward's published keep bits == the RNG's decisions
         ka = attn_keep(seed, B * H, L, L, p)
         nq = (L + 31) // 32
-        words = dm.cpu().numpy().view(np.uint32).reshape(B * H, nq, L)
+        words = dm.cpu().numpy().view(np.uint32)[:B * H * nq * L].reshape(B * H, nq, L)
+        qwords = dm.cpu().numpy().view(np.uint32)[B * H * nq * L:].reshape(B * H, L, nq)
+        qbits = (qwords[:, :, :, None] >> np.arange(32, dtype=np.uint32)[None, None, None, :]) & 1
+        assert (qbits.reshape(B * H, L, nq * 32)[:, :, :L].astype(bool) == ka).all()   # query-major copy
         bits_np = (words[:, :, None, :] >> np.arange(32, dtype=np.uint32)[None, None, :, None]) & 1
         got = bits_np.reshape(B * H, nq * 32, L)[:, :L, :].astype(bool)
         live = ~masked.expand(B, H, L, L).reshape(B * H, L, L).numpy()   # words of masked-out tiles are never read
