@@ -105,6 +105,7 @@ SIGNATURES = {
     "asrx_im2col_conv2": [c_i32, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp],
     "asrx_col2im_conv2": [c_i32, c_vp, c_i32, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp],
     "asrx_conv1_bwd_w": [c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp],
+    "asrx_conv1_bwd_fused": [c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp],
     "asrx_embed_fwd": [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp, c_f32, c_u64, c_vp, c_vp],
     "asrx_embed_bwd": [c_vp, c_i64, c_i32, c_vp, c_i32, c_i32, c_i32, c_f32, c_u64, c_vp, c_vp],
     "asrx_cross_entropy": [c_vp, c_i64, c_i32, c_i64, c_vp, c_i64, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp],

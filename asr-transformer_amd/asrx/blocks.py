@@ -372,6 +372,4 @@ def frontend_bwd(C, S, dfeats_c, conv1, conv2):
     C.wgrad(dy2, cols, G(conv2.weight), G(conv2.bias))
     dcols = _empty((M2, 576), C.cd, dy2)
     K.linear_dgrad(dy2, C.W(conv2.weight), dcols)
-    dy1 = _empty((B, F1, T1, 64), torch.float32, dy2)
-    K.col2im_conv2(dcols, S["y1"], dy1)
-    K.conv1_bwd_w(S["x"], dy1, G(conv1.weight).view(64, 9), G(conv1.bias))
+    K.conv1_bwd_fused(dcols, S["y1"], S["x"], G(conv1.weight).view(64, 9), G(conv1.bias))

@@ -445,6 +445,16 @@ def conv1_bwd_w(x, dy1, dw, db):
          db.data_ptr(), stream())
 
 
+def conv1_bwd_fused(dcols, y1, x, dw, db):
+    """conv1 weight/bias gradients directly from the conv2 column gradient (no dy1 tensor)."""
+    _cuda(dcols, y1, x, dw, db)
+    B, _, F, T = x.shape
+    nblocks = (B * y1.shape[1] * 8 + 3) // 4  # 8 waves per conv1 output row (b, f1): frontend.hip CB_SEG
+    part = torch.empty(nblocks * 640, device=x.device, dtype=torch.float32)
+    call("asrx_conv1_bwd_fused", code(dcols), dcols.data_ptr(), code(y1), y1.data_ptr(), x.data_ptr(), B, F, T,
+         part.data_ptr(), nblocks, dw.data_ptr(), db.data_ptr(), stream())
+
+
 def embed_fwd(tok, table, pe, out, L, dropout_p=0.0, seed=0):
     _cuda(tok, table, pe, out)
     call("asrx_embed_fwd", tok.data_ptr(), tok.numel(), L, table.data_ptr(), table.shape[1], pe.data_ptr(),

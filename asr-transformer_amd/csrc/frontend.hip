@@ -153,6 +153,92 @@ __global__ __launch_bounds__(256) void conv1_bwd_w_kernel(const float* __restric
     part[(int64_t)blockIdx.x * 640 + i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
 }
 
+// Fused conv1 weight/bias gradient: dy1 (the conv1 output gradient) is never materialised.  Lane = output
+// channel c; one wave per conv1 output row (b, f1).  With stride 2 and a 3-tap kernel, the conv2 taps that read
+// position (f1, t1) depend only on the parities of f1 and t1, so the wave sweeps the even and then the odd t1
+// of its row with a fixed tap set: straight-line, wave-uniform addressing, four positions per step so their
+// loads are in flight together.  dy1[pos][c] = relu'(y1) * (sum of those taps of dcols); acc += dy1 * x-taps.
+// Per-block partials [640] finish in conv1_bwd_finish.
+constexpr int CB_SEG = 8;   // waves per conv1 output row (t1 segments)
+
+template <typename DT, typename YT>
+ASRX_DEV float ldf(const DT* p) {
+  if constexpr (sizeof(DT) == 2) return bf2f((bf16_t)*p);
+  else return (float)*p;
+}
+
+template <typename DT, typename YT>
+__global__ __launch_bounds__(256) void conv1_bwd_fused_kernel(const DT* __restrict__ dcols, const YT* __restrict__ y1,
+                                                              const float* __restrict__ x, int B, int F, int T, int F1,
+                                                              int T1, int F2, int T2, float* __restrict__ part) {
+  const int c = threadIdx.x & 63;
+  const int sub = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: all addressing is scalar
+  const int wid = blockIdx.x * 4 + sub;                              // (row, segment of the row's t1 range)
+  const int row = wid / CB_SEG, seg = wid % CB_SEG;
+  const int tlen = ((T1 + CB_SEG - 1) / CB_SEG + 1) & ~1;            // even segment length: parities align
+  const int tlo = seg * tlen, thi = min(T1, tlo + tlen);
+  float acc[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) acc[k] = 0.f;
+  if (row < B * F1) {
+    const int b = row / F1, f1 = row % F1;
+    // conv2 rows (kh, f2) reading this f1: f1 even -> kh 0 (f2 = f1/2) and kh 2 (f2 = f1/2 - 1); odd -> kh 1
+    const bool fe = !(f1 & 1);
+    const int khs[2] = {fe ? 0 : 1, 2};
+    const int f2s[2] = {fe ? f1 / 2 : (f1 - 1) / 2, fe ? f1 / 2 - 1 : 0};
+    const bool hvs[2] = {f2s[0] < F2, fe && f1 >= 2 && f2s[1] < F2};
+    const float* xr = x + ((int64_t)b * F + 2 * f1) * T;
+    const YT* yr = y1 + (int64_t)row * T1 * C1 + c;
+    for (int pt = 0; pt < 2; ++pt) {
+      // taps along t for this parity: even t1 -> kw 0 (t2 = t1/2) and kw 2 (t2 = t1/2 - 1); odd -> kw 1
+      for (int t0 = tlo + pt; t0 < thi; t0 += 8) {
+        float g[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int t1 = t0 + 2 * j;
+          const bool tv = t1 < thi;
+          const int t1c = tv ? t1 : pt;
+          float sum = 0.f;
+#pragma unroll
+          for (int ih = 0; ih < 2; ++ih) {
+            const bool hv = hvs[ih];
+            const int kh = khs[ih], f2 = hv ? f2s[ih] : 0;
+#pragma unroll
+            for (int iw = 0; iw < 2; ++iw) {
+              const int kw = pt ? 1 : 2 * iw;
+              const int td = t1c - kw;
+              const bool wv = (pt == 0 || iw == 0) && td >= 0 && (td >> 1) < T2;
+              const int t2 = wv ? (td >> 1) : 0;
+              const float v = ldf<DT, YT>(dcols + (((int64_t)b * T2 + t2) * F2 + f2) * 576 + (kh * 3 + kw) * C1 + c);
+              sum += (hv && wv && tv) ? v : 0.f;
+            }
+          }
+          float gy;
+          if constexpr (sizeof(YT) == 2) gy = bf2f((bf16_t)yr[(int64_t)t1c * C1]);
+          else gy = (float)yr[(int64_t)t1c * C1];
+          g[j] = (tv && gy > 0.f) ? sum : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int t1c = min(t0 + 2 * j, T1 - 1);
+          const float* xp = xr + 2 * t1c;
+#pragma unroll
+          for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) acc[kh * 3 + kw] += g[j] * xp[(int64_t)kh * T + kw];
+          acc[9] += g[j];
+        }
+      }
+    }
+  }
+  __shared__ float red[4][640];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) red[sub][c * 10 + k] = acc[k];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 640; i += 256)
+    part[(int64_t)blockIdx.x * 640 + i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+}
+
 // one block per output (640 = 64 channels x (9 taps + bias)); partials summed by 256 threads + LDS tree
 __global__ __launch_bounds__(256) void conv1_bwd_finish(const float* part, int nblocks, float* dw, float* db) {
   __shared__ float red[256];
@@ -503,6 +589,29 @@ extern "C" int asrx_dropout_mask(uint8_t* keep, int64_t n, float p, uint64_t see
   if (n == 0) return ASRX_OK;
   hipLaunchKernelGGL(dropout_mask_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, keep, n,
                      drop_threshold(p), seed);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
+extern "C" int asrx_conv1_bwd_fused(int32_t dcols_dtype, const void* dcols, int32_t y1_dtype, const void* y1,
+                                    const float* x, int32_t B, int32_t F, int32_t T, float* part, int32_t nblocks,
+                                    float* dw, float* db, void* stream) {
+  // nblocks must be ceil(B * F1 / 4) (one wave per conv1 output row); part holds nblocks x 640 floats
+  if (!dcols || !y1 || !x || !part || !dw || !db || B <= 0) return ASRX_ERR_ARG;
+  const int F1 = (F - 3) / 2 + 1, T1 = (T - 3) / 2 + 1;
+  const int F2 = (F1 - 3) / 2 + 1, T2 = (T1 - 3) / 2 + 1;
+  if (F1 <= 0 || T1 <= 0 || F2 <= 0 || T2 <= 0) return ASRX_ERR_ARG;
+  if (nblocks != (B * F1 * CB_SEG + 3) / 4) return ASRX_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+#define ASRX_FUSED(DT, YT) hipLaunchKernelGGL((conv1_bwd_fused_kernel<DT, YT>), dim3(nblocks), dim3(256), 0, st, \
+      (const DT*)dcols, (const YT*)y1, x, B, F, T, F1, T1, F2, T2, part)
+  if (dcols_dtype == ASRX_BF16 && y1_dtype == ASRX_BF16) ASRX_FUSED(bf16_t, bf16_t);
+  else if (dcols_dtype == ASRX_F32 && y1_dtype == ASRX_F32) ASRX_FUSED(float, float);
+  else if (dcols_dtype == ASRX_BF16 && y1_dtype == ASRX_F32) ASRX_FUSED(bf16_t, float);
+  else ASRX_FUSED(float, bf16_t);
+#undef ASRX_FUSED
+  ASRX_CHECK_LAUNCH();
+  hipLaunchKernelGGL(conv1_bwd_finish, dim3(640), dim3(256), 0, st, part, nblocks, dw, db);
   ASRX_CHECK_LAUNCH();
   return ASRX_OK;
 }

@@ -452,6 +452,12 @@ def test_conv_frontend(dtype):
     pre.backward(dy1.cpu().double().permute(0, 3, 1, 2))
     assert relerr(dw.cpu(), w1r.grad.reshape(64, 9)) < 1e-5
     assert relerr(db.cpu(), b1r.grad) < 1e-5
+    # fused path (training): the same gradients straight from dcols, dy1 never materialised
+    dw2 = torch.zeros(64, 9, device=dev)
+    db2 = torch.zeros(64, device=dev)
+    K().conv1_bwd_fused(dcols, y1, x.to(dev), dw2, db2)
+    assert relerr(dw2.cpu(), w1r.grad.reshape(64, 9)) < 1e-4
+    assert relerr(db2.cpu(), b1r.grad) < 1e-4
 
 
 # ------------------------------------------------------------------------------------------------ misc
