@@ -710,7 +710,6 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
   const bf16_t* Qb = a.q + b * a.qb + h * 64;
   const bf16_t* Db = a.dout + b * a.dob + h * 64;
   const float* lseb = a.lse + (int64_t)bh * a.Lq;
-  const float* delb = a.delta + (int64_t)bh * a.Lq;
   const bool causal = MODE == 1 && a.causal;
   const int nch = (a.Lq + 31) >> 5;
 
@@ -723,6 +722,10 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
   const uint32_t* dmb = usebits ? a.dropmask + (int64_t)bh * nch * a.Lk : nullptr;
   uint32_t dwn[2] = {0u, 0u};
   const int keyc[2] = {min(kw0 + li, a.Lk - 1), min(kw0 + 16 + li, a.Lk - 1)};
+  // delta = rowsum(dO * O) is formed here too: the threads that stage a dO piece also load the matching O
+  // piece, dot the 8 elements and reduce over the row's 8 pieces (adjacent lanes) — no separate delta pass.
+  const bf16_t* Ob = a.o + b * a.ob + h * 64;
+  uint4 preo[PRE];
   auto fetch = [&](int ch) {
     const int q0 = ch * 32;
     if (usebits) {
@@ -735,11 +738,9 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
       const int which = c >> 8, row = (c >> 3) & 31, dc = (c & 7) * 8;
       const int q = min(q0 + row, a.Lq - 1);
       pre[i] = *(const uint4*)((which ? Db + (int64_t)q * a.dor : Qb + (int64_t)q * a.qr) + dc);
+      if (which) preo[i] = *(const uint4*)(Ob + (int64_t)q * a.orr + dc);
     }
-    if (tid < 64) {
-      const int q = min(q0 + (tid & 31), a.Lq - 1);
-      praw = tid < 32 ? lseb[q] : delb[q];
-    }
+    if (tid < 32) praw = lseb[min(q0 + tid, a.Lq - 1)];
   };
   auto publish = [&](int buf, int ch) {
     const int q0 = ch * 32;
@@ -747,19 +748,26 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
     for (int i = 0; i < PRE; ++i) {
       const int c = tid + NTHR * i;
       const int which = c >> 8, row = (c >> 3) & 31, dc = (c & 7) * 8;
-      *(uint4*)((which ? sdo : sq) + (buf * 32 + row) * R_CS + dc) = q0 + row < a.Lq ? pre[i] : make_uint4(0, 0, 0, 0);
-    }
-    if (tid < 64) {
-      const int q = q0 + (tid & 31);
-      float v;
-      if (tid < 32) {
-        bool live = q < a.Lq;
-        if (MODE == 1 && live && a.qvalid) live = a.qvalid[b * a.validb + q] != 0;
-        v = live ? -praw : -INFINITY;
-      } else {
-        v = q < a.Lq ? praw : 0.f;
+      const bool qv = q0 + row < a.Lq;
+      *(uint4*)((which ? sdo : sq) + (buf * 32 + row) * R_CS + dc) = qv ? pre[i] : make_uint4(0, 0, 0, 0);
+      if (which) {   // wave-uniform: a wave's 64 pieces are all Q or all dO
+        const uint32_t* dd = (const uint32_t*)&pre[i];
+        const uint32_t* oo = (const uint32_t*)&preo[i];
+        float dot = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          dot += bf2f(dd[e] & 0xffff) * bf2f(oo[e] & 0xffff) + bf2f(dd[e] >> 16) * bf2f(oo[e] >> 16);
+        dot += __shfl_xor(dot, 1, 64);
+        dot += __shfl_xor(dot, 2, 64);
+        dot += __shfl_xor(dot, 4, 64);
+        if ((c & 7) == 0) sdel[buf * 32 + row] = qv ? dot : 0.f;
       }
-      (tid < 32 ? slse : sdel)[buf * 32 + (tid & 31)] = v;
+    }
+    if (tid < 32) {
+      const int q = q0 + tid;
+      bool live = q < a.Lq;
+      if (MODE == 1 && live && a.qvalid) live = a.qvalid[b * a.validb + q] != 0;
+      slse[buf * 32 + tid] = live ? -praw : -INFINITY;
     }
   };
 
@@ -1058,9 +1066,7 @@ extern "C" int asrx_attention_bwd(const asrx_attn_desc* d, void* stream) {
   const int64_t ostr[] = {a.orr, a.ob, a.dor, a.dob, a.dkr, a.dkb, a.dvr, a.dvb};
   for (int64_t s : ostr) if (s % 8) return ASRX_ERR_UNSUPPORTED;
   hipStream_t st = (hipStream_t)stream;
-  rc = asrx_attn_delta(d, stream);
-  if (rc) return rc;
-  if (resident_ok(d, a) && a.dqr % 4 == 0 && a.dqb % 4 == 0 && (uintptr_t)a.dq % 8 == 0) {
+  if (resident_ok(d, a) && a.dqr % 4 == 0 && a.dqb % 4 == 0 && (uintptr_t)a.dq % 8 == 0) {   // forms delta itself
     const int nkt = bwd_res_nkt(a.Lk);
     const size_t sm = bwd_res_smem(a.Lk);
     const dim3 grid(a.B * a.H), blk(64 * nkt);
@@ -1072,6 +1078,8 @@ extern "C" int asrx_attention_bwd(const asrx_attn_desc* d, void* stream) {
     ASRX_CHECK_LAUNCH();
     return ASRX_OK;
   }
+  rc = asrx_attn_delta(d, stream);
+  if (rc) return rc;
   int nw = (a.Lk + 31) / 32;
   if (nw > 8) nw = 8;
   const int nblk = (a.Lk + 32 * nw - 1) / (32 * nw);
