@@ -51,11 +51,12 @@ class KernelProbe:
     with the profiler's.  target=None records every GEMM (to find the dominant one); otherwise only launches
     of `target` are timed."""
 
-    def __init__(self, target=None):
+    def __init__(self, target=None, log=None):
         self.target = target
         self.events = {}            # name -> [(start, end)]
         self.flops = {}             # name -> algorithmic FLOPs
         self.active = False
+        self.log = log              # optional list: (kernel name, m, n, k, batch, splitk) of every GEMM launch
 
     def record(self, name):
         return self.active and (self.target is None or name == self.target)
@@ -131,6 +132,8 @@ def gemm(a, b, c, m, n, k, *, lda, ldb, ldc, a_trans=False, b_trans=False, alpha
     probe = PROBE
     if probe is not None and probe.active:
         name = kernel_name(d)
+        if probe.log is not None:
+            probe.log.append((name, m, n, k, batch, splitk))
         if probe.record(name):
             s0 = torch.cuda.Event(enable_timing=True)
             s1 = torch.cuda.Event(enable_timing=True)
@@ -187,6 +190,7 @@ def linear_wgrad(dy, x, wgrad, *, beta=1.0, bias_grad=None, **kw):
 
 
 GROUPED_KERNEL = "gemm_bf16_grouped_kernel<true, true>"
+GROUPED_TABLE_KERNEL = "gemm_bf16_grouped_dev_kernel<true, true>"
 
 
 def wgrad_groupable(dy, x, wgrad):
@@ -197,15 +201,63 @@ def wgrad_groupable(dy, x, wgrad):
             and x.data_ptr() % 16 == 0 and dy.shape[0] <= 65536)
 
 
+def _grouped_table(items, common):
+    """One launch for any number of problems: the 64-B group entries and the tile -> group map are packed into
+    one pinned host buffer and copied to the device on the stream (asrx_gemm_grouped_table)."""
+    import numpy as np
+    ents = np.zeros((len(items), 8), dtype=np.int64)
+    ints = ents.view(np.int32)
+    maps, start, flops, cvec = [], 0, 0, 1
+    for i, (dy, x, wgrad, bias_grad) in enumerate(items):
+        _cuda(dy, x, wgrad, bias_grad)
+        m, n = dy.shape
+        k = x.shape[1]
+        ents[i, 0], ents[i, 1], ents[i, 2] = dy.data_ptr(), x.data_ptr(), wgrad.data_ptr()
+        ents[i, 3] = bias_grad.data_ptr() if bias_grad is not None else 0
+        ints[i, 8:16] = [dy.stride(0), x.stride(0), wgrad.stride(0), n, k, m, start, 0]
+        nt = ((n + 127) // 128) * ((k + 127) // 128)
+        maps.append(np.full(nt, i, dtype=np.uint16))
+        start += nt
+        flops += 2 * m * n * k
+        if wgrad.stride(0) % 4 or wgrad.data_ptr() % 16:
+            cvec = 0
+    tmap = np.concatenate(maps)
+    nbytes = ents.nbytes + (tmap.nbytes + 63) // 64 * 64
+    host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    hv = host.numpy()
+    hv[:ents.nbytes] = ents.view(np.uint8).reshape(-1)
+    hv[ents.nbytes:ents.nbytes + tmap.nbytes] = tmap.view(np.uint8)
+    dev = host.to(items[0][0].device, non_blocking=True)
+    call("asrx_gemm_grouped_table", ctypes.byref(common), dev.data_ptr(), dev.data_ptr() + ents.nbytes, len(items),
+         start, cvec, stream())
+    return flops, dev
+
+
 def linear_wgrad_grouped(items, *, beta=1.0):
-    """Issue many independent weight gradients wgrad[N,K] (+)= dy[M,N]^T x[M,K] (+ bias_grad[N] += colsum dy)
-    as grouped launches (asrx_gemm_grouped): longest reductions first, MAX_GROUPS problems per launch."""
+    """Issue many independent weight gradients wgrad[N,K] (+)= dy[M,N]^T . x[M,K] (+ bias_grad[N] += colsum dy)
+    as ONE grouped launch (longest reductions first): a kernel-argument table for <= MAX_GROUPS problems, a
+    device table beyond."""
     if not items:
         return
     items = sorted(items, key=lambda it: -it[0].shape[0])
     common = GemmDesc()
     common.in_dtype, common.a_trans, common.b_trans, common.c_dtype = BF16, 1, 1, F32
     common.alpha, common.beta = 1.0, beta
+    if len(items) > MAX_GROUPS:
+        probe = PROBE
+        timed = probe is not None and probe.record(GROUPED_TABLE_KERNEL)
+        if probe is not None and probe.active and probe.log is not None:
+            probe.log.append((GROUPED_TABLE_KERNEL, len(items), 0,
+                              sum(it[0].shape[0] * it[0].shape[1] * it[1].shape[1] for it in items), 1, 1))
+        if timed:
+            s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s0.record()
+        flops, _ = _grouped_table(items, common)
+        if timed:
+            s1.record()
+            probe.events.setdefault(GROUPED_TABLE_KERNEL, []).append((s0, s1))
+            probe.flops[GROUPED_TABLE_KERNEL] = probe.flops.get(GROUPED_TABLE_KERNEL, 0) + flops
+        return
     for c0 in range(0, len(items), MAX_GROUPS):
         chunk = items[c0:c0 + MAX_GROUPS]
         arr = (GemmGroup * len(chunk))()
@@ -221,6 +273,8 @@ def linear_wgrad_grouped(items, *, beta=1.0):
             g.rowsum_a = _p(bias_grad)
             flops += 2 * m * n * k
         probe = PROBE
+        if probe is not None and probe.active and probe.log is not None:
+            probe.log.append((GROUPED_KERNEL, len(chunk), 0, flops // 2, 1, 1))
         timed = probe is not None and probe.record(GROUPED_KERNEL)
         if timed:
             s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

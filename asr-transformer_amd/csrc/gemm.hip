@@ -364,6 +364,25 @@ __global__ __launch_bounds__(256) void gemm_bf16_grouped_kernel(GroupTable t) {
   gemm_bf16_tile<128, 128, AT, BT, true>(g, tid - e.tile_start, 0, 0, lds);
 }
 
+// Same, table in device memory (any number of groups, one launch): entry i = asrx_gemm_group_dev of the
+// C-ABI (64 B, layout-identical to GroupEnt), tile_group[tile] = its group.
+template <bool AT, bool BT>
+__global__ __launch_bounds__(256) void gemm_bf16_grouped_dev_kernel(float alpha, float beta, int c_dtype, int cvec,
+                                                                    const GroupEnt* __restrict__ ents,
+                                                                    const uint16_t* __restrict__ tile_group) {
+  __shared__ __attribute__((aligned(16))) bf16_t lds[reg_lds_elems<128, 128, AT, BT>()];
+  const int tid = blockIdx.x;
+  const int gi = __builtin_amdgcn_readfirstlane((int)tile_group[tid]);
+  const GroupEnt e = ents[gi];
+  GemmArgs g = {};
+  g.M = e.m; g.N = e.n; g.K = e.k;
+  g.a = e.a; g.lda = e.lda; g.b = e.b; g.ldb = e.ldb; g.c = e.c; g.ldc = e.ldc; g.c_dtype = c_dtype;
+  g.batch_inner = 1; g.alpha = alpha; g.beta = beta; g.rowadd_mod = 1;
+  g.splitk = 1; g.k_per_split = ((e.k + BK - 1) / BK) * BK; g.cvec = cvec;
+  g.rowsum = e.rowsum;
+  gemm_bf16_tile<128, 128, AT, BT, true>(g, tid - e.tile_start, 0, 0, lds);
+}
+
 // ------------------------------------------------------------------------------------------------
 // bf16 kernel, direct-to-LDS staging (global_load_lds_dwordx4): 128x128x64 tiles, 4 waves (64x64 each),
 // two LDS buffers, one barrier per K-step.  Each wave-instruction writes 1 KiB of LDS lane-linearly, so the
@@ -1337,6 +1356,22 @@ extern "C" int asrx_gemm_grouped(const asrx_gemm_desc* common, const asrx_gemm_g
   if (tiles > INT32_MAX) return ASRX_ERR_ARG;
   hipLaunchKernelGGL((gemm_bf16_grouped_kernel<true, true>), dim3((unsigned)tiles), dim3(256), 0,
                      (hipStream_t)stream, t);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
+static_assert(sizeof(GroupEnt) == sizeof(asrx_gemm_group_dev), "device group table layout");
+
+extern "C" int asrx_gemm_grouped_table(const asrx_gemm_desc* common, const asrx_gemm_group_dev* groups,
+                                       const uint16_t* tile_group, int32_t count, int32_t tiles, int32_t cvec,
+                                       void* stream) {
+  if (!common || !groups || !tile_group || count <= 0 || count > 65535 || tiles < 0) return ASRX_ERR_ARG;
+  if (tiles == 0) return ASRX_OK;
+  if (common->in_dtype != ASRX_BF16 || !common->a_trans || !common->b_trans) return ASRX_ERR_UNSUPPORTED;
+  if (common->c_dtype != ASRX_BF16 && common->c_dtype != ASRX_F32) return ASRX_ERR_ARG;
+  hipLaunchKernelGGL((gemm_bf16_grouped_dev_kernel<true, true>), dim3((unsigned)tiles), dim3(256), 0,
+                     (hipStream_t)stream, common->alpha, common->beta, common->c_dtype, cvec ? 1 : 0,
+                     (const GroupEnt*)groups, tile_group);
   ASRX_CHECK_LAUNCH();
   return ASRX_OK;
 }

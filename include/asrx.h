@@ -85,6 +85,18 @@ typedef struct asrx_gemm_group {
 
 int asrx_gemm_grouped(const asrx_gemm_desc* common, const asrx_gemm_group* groups, int32_t count, void* stream);
 
+/* Same with the group table in DEVICE memory (any count, one launch): entries of 64 B, 128x128 output tiles
+ * numbered consecutively per group from tile_start; tile_group[t] (device) = the group of tile t.  The caller
+ * guarantees the same alignment preconditions as asrx_gemm_grouped (the table is not inspected on the host);
+ * cvec: every C row start is 16-byte aligned. */
+typedef struct asrx_gemm_group_dev {
+  const void* a; const void* b; void* c; float* rowsum_a;
+  int32_t lda, ldb, ldc, m, n, k, tile_start, reserved;
+} asrx_gemm_group_dev;
+
+int asrx_gemm_grouped_table(const asrx_gemm_desc* common, const asrx_gemm_group_dev* groups,
+                            const uint16_t* tile_group, int32_t count, int32_t tiles, int32_t cvec, void* stream);
+
 /* Name of the kernel instantiation asrx_gemm would launch for d (as rocprofv3 lists it, without the
  * namespace/argument list), e.g. "gemm_bf16_p3_kernel<false, false, 1>".  Host-only: no launch, no GPU
  * needed.  Used by bench.py to time exactly the kernel the roofline names. */
