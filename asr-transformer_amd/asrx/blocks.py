@@ -9,6 +9,7 @@ Reference call sites (modules/Transformer): pre-LN sublayers model.py:18-25 / 65
 FeedForward layers.py:53-58; front-end model.py:168-171 + 41-47; decoder embedding model.py:117.
 """
 import math
+import os
 
 import torch
 
@@ -77,6 +78,9 @@ class Seeds:
 
 
 _SIDE = {}
+# generating the keep bits on a side stream (overlapping the LN + Q/K/V GEMM) measured SLOWER than generating
+# them in line (18.2 vs 17.75 ms/step: the VALU-heavy generator steals the GEMM's CUs): off by default
+_SIDE_DROPGEN = os.environ.get("ASRX_DROPGEN_SIDE", "0") == "1"
 
 
 def _side_stream(device):
@@ -126,7 +130,7 @@ def attn_prepare(C, B, H, Lq, Lk, dh, device):
     keep bits on the side stream now — they depend only on (seed, shapes), so they overlap the LayerNorm and
     Q/K/V projection that precede the attention on the main stream."""
     prep = {"seed": C.seed(), "dropmask": None, "event": None}
-    if C.cd == torch.bfloat16 and C.attn_impl == "fused" and C.p > 0:
+    if C.cd == torch.bfloat16 and C.attn_impl == "fused" and C.p > 0 and _SIDE_DROPGEN:
         dm = K.dropmask_buffer(B, H, Lq, Lk, dh, C.p, device)
         if dm is not None:
             main = torch.cuda.current_stream(device)

@@ -723,11 +723,11 @@ ASRX_DEV s8_t p_frag(const unsigned char* img, int i0, int ks) {
   }
 }
 
-// (An XCD-owned tile order — row-block tm served by the workgroups with b % 8 == tm % 8 — was measured
-// 10-50% SLOWER than this plain round-robin order on every c3 shape and was removed.)
+// (An XCD-owned ROW order — row-block tm served by the workgroups with b % 8 == tm % 8 — was measured 10-50%
+// slower on every c3 shape; the XCD-contiguous TILE ranges of gemm_bf16_p3_kernel's `xcd` mode are 1-7% faster.)
 
 template <bool AT, bool BT, int EPI>
-__global__ __launch_bounds__(512) void gemm_bf16_p3_kernel(GemmArgs g, int ntiles) {
+__global__ __launch_bounds__(512) void gemm_bf16_p3_kernel(GemmArgs g, int ntiles, int xcd) {
   __shared__ __attribute__((aligned(1024))) unsigned char lds[3 * P_STAGE];
   constexpr int TM = 4, TN = 4;
   const int ntn = (g.N + P_BN - 1) / P_BN;
@@ -745,26 +745,37 @@ __global__ __launch_bounds__(512) void gemm_bf16_p3_kernel(GemmArgs g, int ntile
   const int G = gridDim.x;
   const int b0 = blockIdx.x;
   if (b0 >= ntiles || nk == 0) return;
-  const int total = ((ntiles - b0 + G - 1) / G) * nk;
+  // tile order: round-robin (tile = b0 + v*G) or XCD-contiguous (workgroup b runs on XCD b % 8; XCD x owns the
+  // contiguous tile range [x*per, (x+1)*per) and its G/8 workgroups sweep it together, so the column tiles of a
+  // row panel are computed on one XCD at about the same time and share its L2)
+  const int xcdm = xcd && (G % 8) == 0;
+  const int G8 = G / 8, xg = b0 % 8, jg = b0 / 8;
+  const int per8 = (ntiles + 7) / 8;
+  const int lo8 = xg * per8, hi8 = min(ntiles, lo8 + per8);
+  const int ntl = xcdm ? (hi8 - lo8 > jg ? (hi8 - lo8 - jg + G8 - 1) / G8 : 0) : (ntiles - b0 + G - 1) / G;
+  if (ntl == 0) return;
+#define P3_TILE(v) (xcdm ? lo8 + jg + (v) * G8 : b0 + (v) * G)
+  const int total = ntl * nk;
   const int wave = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
 
   PStage<P_BM, AT> sa;
   PStage<P_BN, BT> sb;
   // issue cursor (runs two steps ahead of the compute cursor)
-  int it = b0, ik = 0, ib = 0;
+  int iv = 0, ik = 0, ib = 0;
   // (a macro rather than a lambda: hipcc/ROCm 7.2 dropped the host device-stubs of most instantiations of this
   //  kernel when the issue step was a capturing lambda)
 #define P3_ISSUE_NEXT()                                                      \
   do {                                                                       \
     if (ik == 0) {                                                           \
-      sa.set_tile((it / ntn) * P_BM, g.lda);                                 \
-      sb.set_tile((it % ntn) * P_BN, g.ldb);                                 \
+      const int pt_ = P3_TILE(iv);                                           \
+      sa.set_tile((pt_ / ntn) * P_BM, g.lda);                                \
+      sb.set_tile((pt_ % ntn) * P_BN, g.ldb);                                \
     }                                                                        \
     unsigned char* img_ = lds + ib * P_STAGE;                                \
     sa.issue(img_, A, g.lda, a_bytes, kbeg + ik * BK);                       \
     sb.issue(img_ + PA_BYTES, B, g.ldb, b_bytes, kbeg + ik * BK);            \
-    if (++ik == nk) { ik = 0; it += G; }                                     \
+    if (++ik == nk) { ik = 0; ++iv; }                                        \
     ib = ib == 2 ? 0 : ib + 1;                                               \
   } while (0)
 
@@ -780,7 +791,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_p3_kernel(GemmArgs g, int ntile
   P3_ISSUE_NEXT();
   if (total > 1) P3_ISSUE_NEXT();
   bool drain = false;
-  int t = b0, kk = 0, cb = 0;   // compute cursor
+  int vc = 0, kk = 0, cb = 0;   // compute cursor
   for (int s = 0; s < total; ++s) {
     if (s + 1 < total && !drain) asm volatile("s_waitcnt vmcnt(6)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
@@ -789,6 +800,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_p3_kernel(GemmArgs g, int ntile
     if (s + 2 < total) P3_ISSUE_NEXT();
     const unsigned char* la = lds + cb * P_STAGE;
     const unsigned char* lb = la + PA_BYTES;
+    const int t = P3_TILE(vc);
     const bool do_rs = AT && g.rowsum != nullptr && (t % ntn) == 0 && wn == 0;
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
@@ -846,16 +858,20 @@ __global__ __launch_bounds__(512) void gemm_bf16_p3_kernel(GemmArgs g, int ntile
         for (int j = 0; j < TM; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
       drain = true;
     }
-    if (++kk == nk) { kk = 0; t += G; }
+    if (++kk == nk) { kk = 0; ++vc; }
     cb = cb == 2 ? 0 : cb + 1;
   }
+#undef P3_TILE
 }
 
 template <bool AT, bool BT, int EPI>
 void launch_p3(const GemmArgs& g, int ntiles, int splitk, int batch, hipStream_t st) {
   const int per = splitk * batch;
   const int gx = std::max(1, std::min(ntiles, std::max(1, 256 / per)));
-  hipLaunchKernelGGL((gemm_bf16_p3_kernel<AT, BT, EPI>), dim3(gx, splitk, batch), dim3(P_THREADS), 0, st, g, ntiles);
+  const char* e = getenv("ASRX_P3_XCD");   // XCD-contiguous tile order: measured 1-7% faster on the c3 shapes
+  const int xcd = e ? atoi(e) : 1;
+  hipLaunchKernelGGL((gemm_bf16_p3_kernel<AT, BT, EPI>), dim3(gx, splitk, batch), dim3(P_THREADS), 0, st, g, ntiles,
+                     xcd);
 }
 
 template <bool AT, bool BT>
