@@ -1,6 +1,7 @@
 """Tensor-level wrappers around the C-ABI (include/asrx.h). All calls are asynchronous on torch's current
 HIP stream; every call goes to the native library (no CPU / PyTorch fallback)."""
 import ctypes
+import os
 import math
 
 import torch
@@ -191,6 +192,8 @@ def linear_wgrad(dy, x, wgrad, *, beta=1.0, bias_grad=None, **kw):
 
 GROUPED_KERNEL = "gemm_bf16_grouped_kernel<true, true>"
 GROUPED_TABLE_KERNEL = "gemm_bf16_grouped_dev_kernel<true, true>"
+GROUPED_P5_KERNEL = "gemm_bf16_p5g_kernel<true, true, 96>"    # beta = 1 (accumulate into the fp32 grads)
+GROUPED_P5_KERNEL0 = "gemm_bf16_p5g_kernel<true, true, 64>"   # beta = 0
 
 
 def wgrad_groupable(dy, x, wgrad):
@@ -201,7 +204,89 @@ def wgrad_groupable(dy, x, wgrad):
             and x.data_ptr() % 16 == 0 and dy.shape[0] <= 65536)
 
 
-def _grouped_table(items, common):
+# Weight-gradient tile: 256 = the p5 LDS-DMA ring kernel (256x256x32, gemm_p5.hip), 128 = register-staged
+# 128x128 tiles (gemm.hip).  ASRX_WGRAD_TILE overrides (A/B benchmarking).
+WGRAD_TILE = int(os.environ.get("ASRX_WGRAD_TILE", "128"))
+
+
+def _grouped_p5_ok(items, beta):
+    return WGRAD_TILE == 256 and beta in (0.0, 1.0) and all(
+        x.shape[1] % 4 == 0 and wgrad.stride(0) % 4 == 0 and wgrad.data_ptr() % 16 == 0
+        for (_, x, wgrad, _) in items)
+
+
+_XCD_PLANS = {}
+
+
+def xcd_plan(shapes, tile=256, nxcd=8):
+    """Lay grouped weight-gradient tiles out over the 8 XCDs (workgroup b runs on XCD b % 8): whole groups
+    (longest reductions, then largest groups first) go to the least-loaded XCD, so the tiles of a group run on
+    one XCD at the same time and share its L2, and every XCD gets about the same work.
+    shapes: (m, n, k) per group (C[m,n], reduction k).  Returns (group order, tiles per group, block -> tile map)."""
+    import numpy as np
+    key = (tuple(shapes), tile, nxcd)
+    if key in _XCD_PLANS:
+        return _XCD_PLANS[key]
+    nts = [((m + tile - 1) // tile) * ((n + tile - 1) // tile) for (m, n, k) in shapes]
+    order = sorted(range(len(shapes)), key=lambda i: (-shapes[i][2], -nts[i], i))
+    load = [0] * nxcd
+    per_xcd = [[] for _ in range(nxcd)]
+    for i in order:
+        x = min(range(nxcd), key=lambda j: (load[j], j))
+        per_xcd[x].append(i)
+        load[x] += nts[i] * shapes[i][2]
+    group_order = [i for x in range(nxcd) for i in per_xcd[x]]
+    first = {}
+    t = 0
+    for i in group_order:
+        first[i] = t
+        t += nts[i]
+    slots = [[first[i] + j for i in per_xcd[x] for j in range(nts[i])] for x in range(nxcd)]
+    depth = max(len(sl) for sl in slots)
+    block_tile = np.full(depth * nxcd, 0xFFFF, dtype=np.uint16)
+    for x in range(nxcd):
+        block_tile[x:x + nxcd * len(slots[x]):nxcd] = slots[x]
+    plan = (group_order, nts, block_tile)
+    _XCD_PLANS[key] = plan
+    return plan
+
+
+def _grouped_xcd(items, common):
+    """p5 grouped weight gradients (asrx_gemm_grouped_xcd): 64-B group entries, tile -> group map and the
+    XCD-aware block -> tile map in one pinned host buffer, copied to the device on the stream."""
+    import numpy as np
+    shapes = [(dy.shape[1], x.shape[1], dy.shape[0]) for (dy, x, _, _) in items]
+    group_order, nts, block_tile = xcd_plan(shapes, nxcd=8 if os.environ.get("ASRX_WGRAD_XCD", "1") != "0" else 1)
+    ents = np.zeros((len(items), 8), dtype=np.int64)
+    ints = ents.view(np.int32)
+    maps, start, flops = [], 0, 0
+    for slot, i in enumerate(group_order):
+        dy, x, wgrad, bias_grad = items[i]
+        _cuda(dy, x, wgrad, bias_grad)
+        m, n = dy.shape
+        k = x.shape[1]
+        ents[slot, 0], ents[slot, 1], ents[slot, 2] = dy.data_ptr(), x.data_ptr(), wgrad.data_ptr()
+        ents[slot, 3] = bias_grad.data_ptr() if bias_grad is not None else 0
+        ints[slot, 8:16] = [dy.stride(0), x.stride(0), wgrad.stride(0), n, k, m, start, 0]
+        maps.append(np.full(nts[i], slot, dtype=np.uint16))
+        start += nts[i]
+        flops += 2 * m * n * k
+    tmap = np.concatenate(maps)
+    o1 = ents.nbytes
+    o2 = o1 + (tmap.nbytes + 63) // 64 * 64
+    host = torch.empty(o2 + block_tile.nbytes, dtype=torch.uint8, pin_memory=True)
+    hv = host.numpy()
+    hv[:o1] = ents.view(np.uint8).reshape(-1)
+    hv[o1:o1 + tmap.nbytes] = tmap.view(np.uint8)
+    hv[o2:] = block_tile.view(np.uint8)
+    dev = host.to(items[0][0].device, non_blocking=True)
+    base = dev.data_ptr()
+    call("asrx_gemm_grouped_xcd", ctypes.byref(common), base, base + o1, base + o2, len(items), start,
+         len(block_tile), stream())
+    return flops, dev
+
+
+def _grouped_table(items, common, tile=128):
     """One launch for any number of problems: the 64-B group entries and the tile -> group map are packed into
     one pinned host buffer and copied to the device on the stream (asrx_gemm_grouped_table)."""
     import numpy as np
@@ -215,13 +300,14 @@ def _grouped_table(items, common):
         ents[i, 0], ents[i, 1], ents[i, 2] = dy.data_ptr(), x.data_ptr(), wgrad.data_ptr()
         ents[i, 3] = bias_grad.data_ptr() if bias_grad is not None else 0
         ints[i, 8:16] = [dy.stride(0), x.stride(0), wgrad.stride(0), n, k, m, start, 0]
-        nt = ((n + 127) // 128) * ((k + 127) // 128)
+        nt = ((n + tile - 1) // tile) * ((k + tile - 1) // tile)
         maps.append(np.full(nt, i, dtype=np.uint16))
         start += nt
         flops += 2 * m * n * k
         if wgrad.stride(0) % 4 or wgrad.data_ptr() % 16:
             cvec = 0
     tmap = np.concatenate(maps)
+    common.tile = tile
     nbytes = ents.nbytes + (tmap.nbytes + 63) // 64 * 64
     host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
     hv = host.numpy()
@@ -243,20 +329,22 @@ def linear_wgrad_grouped(items, *, beta=1.0):
     common = GemmDesc()
     common.in_dtype, common.a_trans, common.b_trans, common.c_dtype = BF16, 1, 1, F32
     common.alpha, common.beta = 1.0, beta
-    if len(items) > MAX_GROUPS:
+    p5 = _grouped_p5_ok(items, beta)
+    if p5 or len(items) > MAX_GROUPS:
+        kname = (GROUPED_P5_KERNEL if beta == 1.0 else GROUPED_P5_KERNEL0) if p5 else GROUPED_TABLE_KERNEL
         probe = PROBE
-        timed = probe is not None and probe.record(GROUPED_TABLE_KERNEL)
+        timed = probe is not None and probe.record(kname)
         if probe is not None and probe.active and probe.log is not None:
-            probe.log.append((GROUPED_TABLE_KERNEL, len(items), 0,
+            probe.log.append((kname, len(items), 0,
                               sum(it[0].shape[0] * it[0].shape[1] * it[1].shape[1] for it in items), 1, 1))
         if timed:
             s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s0.record()
-        flops, _ = _grouped_table(items, common)
+        flops, _ = _grouped_xcd(items, common) if p5 else _grouped_table(items, common)
         if timed:
             s1.record()
-            probe.events.setdefault(GROUPED_TABLE_KERNEL, []).append((s0, s1))
-            probe.flops[GROUPED_TABLE_KERNEL] = probe.flops.get(GROUPED_TABLE_KERNEL, 0) + flops
+            probe.events.setdefault(kname, []).append((s0, s1))
+            probe.flops[kname] = probe.flops.get(kname, 0) + flops
         return
     for c0 in range(0, len(items), MAX_GROUPS):
         chunk = items[c0:c0 + MAX_GROUPS]

@@ -9,6 +9,8 @@ typedef uint16_t bf16_t;
 typedef short s4_t __attribute__((ext_vector_type(4)));
 typedef short s8_t __attribute__((ext_vector_type(8)));
 typedef float f4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int v2u_t __attribute__((ext_vector_type(2)));
+typedef unsigned int v4u_t __attribute__((ext_vector_type(4)));
 
 #define ASRX_DEV __device__ __forceinline__
 

@@ -17,124 +17,15 @@
 #include <cstdlib>
 #include <cstring>
 
-#include "common.h"
+#include "gemm_common.h"
 
 namespace {
+using namespace asrxg;
 
-struct GemmArgs {
-  int M, N, K;
-  const void* a; int64_t lda;
-  const void* b; int64_t ldb;
-  void* c; int64_t ldc; int c_dtype;
-  int batch_inner;
-  int64_t sa_o, sa_i, sb_o, sb_i, sc_o, sc_i;
-  float alpha, beta;
-  const float* bias;
-  const float* rowadd; int64_t ld_rowadd; int rowadd_mod;
-  int relu;
-  uint32_t drop_thr; float drop_scale; uint64_t seed;
-  const void* gate; int64_t ld_gate; int gate_dtype;
-  const void* resid; int64_t ld_resid; int resid_dtype;
-  int splitk; int k_per_split;    // k_per_split multiple of BK
-  float* ws;                       // split-K partials [split][M][N]
-  int cvec;                        // C row starts 4-element aligned
-  float* rowsum;                   // fused bias gradient: rowsum[m] += sum_k A(m,k)   (A k-strided only)
-  float* rowsum_ws;                // [splitk][M] partials when splitk > 1
-};
-
-ASRX_DEV float ld_any(const void* p, int dtype, int64_t i) {
-  return dtype == ASRX_BF16 ? bf2f(((const bf16_t*)p)[i]) : ((const float*)p)[i];
-}
-
-// Full epilogue for 4 consecutive columns n0..n0+3 of row m (batch z).
-ASRX_DEV void epilogue4(const GemmArgs& g, int z, int m, int n0, const float* acc) {
-  if (m >= g.M || n0 >= g.N) return;
-  const int zo = z / g.batch_inner, zi = z % g.batch_inner;
-  const int64_t coff = zo * g.sc_o + zi * g.sc_i;
-  float r[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) r[i] = acc[i] * g.alpha;
-  const int nv = min(4, g.N - n0);
-  if (g.bias) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) if (i < nv) r[i] += g.bias[n0 + i];
-  }
-  if (g.rowadd) {
-    const float* ra = g.rowadd + (int64_t)(m % g.rowadd_mod) * g.ld_rowadd + n0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) if (i < nv) r[i] += ra[i];
-  }
-  if (g.relu) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) r[i] = fmaxf(r[i], 0.f);
-  }
-  if (g.drop_thr) {
-    const uint32_t base = (uint32_t)(((int64_t)z * g.M + m) * g.N + n0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) r[i] = rng_keep(g.seed, base + i, g.drop_thr) ? r[i] * g.drop_scale : 0.f;
-  }
-  if (g.gate) {
-    const int64_t o = (int64_t)m * g.ld_gate + n0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) if (i < nv && !(ld_any(g.gate, g.gate_dtype, o + i) > 0.f)) r[i] = 0.f;
-  }
-  if (g.resid) {
-    const int64_t o = (int64_t)m * g.ld_resid + n0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) if (i < nv) r[i] += ld_any(g.resid, g.resid_dtype, o + i);
-  }
-  const int64_t co = coff + (int64_t)m * g.ldc + n0;
-  if (g.c_dtype == ASRX_F32) {
-    float* c = (float*)g.c + co;
-    if (g.beta != 0.f) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) if (i < nv) r[i] += g.beta * c[i];
-    }
-    if (nv == 4 && g.cvec) {
-      *(f4_t*)c = f4_t{r[0], r[1], r[2], r[3]};
-    } else {
-      for (int i = 0; i < nv; ++i) c[i] = r[i];
-    }
-  } else {
-    bf16_t* c = (bf16_t*)g.c + co;
-    if (g.beta != 0.f) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) if (i < nv) r[i] += g.beta * bf2f(c[i]);
-    }
-    if (nv == 4 && g.cvec) {
-      uint2 u;
-      u.x = pack2bf(r[0], r[1]);
-      u.y = pack2bf(r[2], r[3]);
-      *(uint2*)c = u;
-    } else {
-      for (int i = 0; i < nv; ++i) c[i] = f2bf(r[i]);
-    }
-  }
-}
-
-// Raw split-K partial store (no epilogue).
-ASRX_DEV void store_partial4(const GemmArgs& g, int split, int m, int n0, const float* acc) {
-  if (m >= g.M || n0 >= g.N) return;
-  float* w = g.ws + ((int64_t)split * g.M + m) * g.N + n0;
-  const int nv = min(4, g.N - n0);
-  if (nv == 4 && (g.N & 3) == 0) {
-    *(f4_t*)w = f4_t{acc[0], acc[1], acc[2], acc[3]};
-  } else {
-    for (int i = 0; i < nv; ++i) w[i] = acc[i];
-  }
-}
 
 // ------------------------------------------------------------------------------------------------
 // bf16 kernel
 // ------------------------------------------------------------------------------------------------
-constexpr int BK = 64;
-constexpr int KC_STRIDE = BK + 8;  // elements; 144 B rows for k-contiguous images
-
-template <int R>
-ASRX_DEV int ks_swz(int krow) {  // 32-byte-chunk XOR for the [BK][R] k-strided image
-  if constexpr (R == 128) return (krow & 3) | (((krow >> 3) & 1) << 2);
-  else return ((krow >> 1) & 1) | (((krow >> 3) & 1) << 1);
-}
 
 template <int R, bool KSTRIDED>
 struct TileBF16 {
@@ -335,13 +226,6 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs g) {
 // The table travels in the kernel arguments (MAX_GROUPS entries, < 4 KiB).
 // ------------------------------------------------------------------------------------------------
 constexpr int MAX_GROUPS = 48;
-struct GroupEnt {
-  const void* a; const void* b; void* c; float* rowsum;
-  int lda, ldb, ldc;
-  int m, n, k;
-  int tile_start;   // first global tile index of this group
-  int pad;
-};
 struct GroupTable {
   float alpha, beta;
   int c_dtype, count, cvec;
@@ -401,8 +285,6 @@ constexpr int GT = 128;                       // tile edge
 constexpr int GTILE_BYTES = GT * BK * 2;      // 16 KiB per operand per stage
 constexpr int G_INST = GTILE_BYTES / 4096;    // glds instructions per thread per operand per stage (4)
 
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef const __attribute__((address_space(1))) void gbl_void_t;
 
 template <bool KSTRIDED>
 ASRX_DEV void glds_stage(unsigned char* lds_tile, const bf16_t* base, int64_t ld, int r0, int rmax, int k0) {
@@ -447,74 +329,6 @@ ASRX_DEV s8_t glds_frag(const unsigned char* lds_tile, int i0, int ks) {
   }
 }
 
-// Compile-time epilogue flags: the projection GEMMs of the training step use a handful of fixed epilogues;
-// specialising them removes the per-element runtime branches of epilogue4 (the generic fallback).
-enum : int {
-  E_BIAS = 1, E_RELU = 2, E_DROP = 4, E_GATE = 8, E_RESID = 16, E_BETA = 32, E_F32 = 64, E_ALPHA = 128,
-  E_ROWADD = 256, E_GENERIC = 1 << 30
-};
-
-template <int EPI, int TN, int TM>
-ASRX_DEV void epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int wn, f4_t (&acc)[TN][TM]) {
-  const int l = threadIdx.x & 63, gq = l >> 4;
-  if constexpr (EPI == E_GENERIC) {
-#pragma unroll
-    for (int i = 0; i < TN; ++i)
-#pragma unroll
-      for (int j = 0; j < TM; ++j) {
-        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-        epilogue4(g, z, m0 + wm + 16 * j + (l & 15), n0 + wn + 16 * i + 4 * gq, v);
-      }
-  } else {
-    // fast path (host-checked): batch 1, N % 4 == 0, 16-B aligned rows; gate bf16, resid fp32
-#pragma unroll
-    for (int i = 0; i < TN; ++i) {
-      const int n = n0 + wn + 16 * i + 4 * gq;
-      if (n >= g.N) continue;
-      f4_t b4 = f4_t{0.f, 0.f, 0.f, 0.f};
-      if constexpr ((EPI & E_BIAS) != 0) b4 = *(const f4_t*)(g.bias + n);
-#pragma unroll
-      for (int j = 0; j < TM; ++j) {
-        const int m = m0 + wm + 16 * j + (l & 15);
-        if (m >= g.M) continue;
-        f4_t v = acc[i][j];
-        if constexpr ((EPI & E_ALPHA) != 0) v *= g.alpha;
-        if constexpr ((EPI & E_BIAS) != 0) v += b4;
-        if constexpr ((EPI & E_ROWADD) != 0) v += *(const f4_t*)(g.rowadd + (int64_t)(m % g.rowadd_mod) * g.ld_rowadd + n);
-        if constexpr ((EPI & E_RELU) != 0) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-        }
-        if constexpr ((EPI & E_DROP) != 0) {   // n % 4 == 0 and N even: two pair hashes cover the 4 elements
-          const uint32_t pb = (uint32_t)((int64_t)m * g.N + n) >> 1;
-          const uint32_t h0 = rng_hash(g.seed, pb), h1 = rng_hash(g.seed, pb + 1);
-          v[0] = rng_half(h0, 0) >= g.drop_thr ? v[0] * g.drop_scale : 0.f;
-          v[1] = rng_half(h0, 1) >= g.drop_thr ? v[1] * g.drop_scale : 0.f;
-          v[2] = rng_half(h1, 0) >= g.drop_thr ? v[2] * g.drop_scale : 0.f;
-          v[3] = rng_half(h1, 1) >= g.drop_thr ? v[3] * g.drop_scale : 0.f;
-        }
-        if constexpr ((EPI & E_GATE) != 0) {
-          const uint2 gt = *(const uint2*)((const bf16_t*)g.gate + (int64_t)m * g.ld_gate + n);
-          if (!(bf2f(gt.x & 0xffff) > 0.f)) v[0] = 0.f;
-          if (!(bf2f(gt.x >> 16) > 0.f)) v[1] = 0.f;
-          if (!(bf2f(gt.y & 0xffff) > 0.f)) v[2] = 0.f;
-          if (!(bf2f(gt.y >> 16) > 0.f)) v[3] = 0.f;
-        }
-        if constexpr ((EPI & E_RESID) != 0) v += *(const f4_t*)((const float*)g.resid + (int64_t)m * g.ld_resid + n);
-        if constexpr ((EPI & E_F32) != 0) {
-          f4_t* c = (f4_t*)((float*)g.c + (int64_t)m * g.ldc + n);
-          if constexpr ((EPI & E_BETA) != 0) v += *c;
-          *c = v;
-        } else {
-          uint2 u;
-          u.x = pack2bf(v[0], v[1]);
-          u.y = pack2bf(v[2], v[3]);
-          *(uint2*)((bf16_t*)g.c + (int64_t)m * g.ldc + n) = u;
-        }
-      }
-    }
-  }
-}
 
 // Persistent over output tiles: each workgroup walks tiles blockIdx.x, +gridDim.x, ... and issues the NEXT
 // (tile, k-step) stage — across tile boundaries too — before computing the current one, so the first stage
@@ -635,11 +449,6 @@ void launch_glds(const GemmArgs& g, int ntiles, int splitk, int batch, hipStream
   hipLaunchKernelGGL((gemm_bf16_glds_kernel<AT, BT, EPI>), dim3(gx, splitk, batch), dim3(256), 0, st, g, ntiles);
 }
 
-// Epilogue sets instantiated per layout; anything else runs the generic epilogue.
-#define ASRX_EPI_NT(X) X(E_BIAS) X(E_BIAS | E_RELU) X(E_BIAS | E_RELU | E_DROP) X(E_BIAS | E_RESID | E_F32) \
-  X(E_BIAS | E_DROP | E_RESID | E_F32) X(E_F32) X(E_BIAS | E_ROWADD | E_F32) X(0)
-#define ASRX_EPI_NN(X) X(0) X(E_GATE) X(E_GATE | E_ALPHA) X(E_F32)
-#define ASRX_EPI_TT(X) X(E_BETA | E_F32) X(E_F32)
 
 template <bool AT, bool BT>
 void dispatch_glds(const GemmArgs& g, int epi, int ntiles, int splitk, int batch, hipStream_t st) {
@@ -854,7 +663,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_p3_kernel(GemmArgs g, int ntile
             store_partial4(g, split, m0 + wm + 16 * j + (l & 15), n0 + wn + 16 * i + 4 * gq, v);
           }
       } else {
-        epilogue_tile<EPI>(g, z, m0, n0, wm, wn, acc);
+        if (g.dbg == 1) keep_live(acc); else epilogue_tile<EPI>(g, z, m0, n0, wm, wn, acc);
       }
 #pragma unroll
       for (int i = 0; i < TN; ++i)
@@ -961,24 +770,6 @@ ASRX_DEV s8_t r_frag(const unsigned char* img, int i0, int ks) {
   }
 }
 
-// s_waitcnt with only the vector-memory counter constrained (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14,
-// expcnt and lgkmcnt at their no-wait maxima)
-template <int N>
-ASRX_DEV void wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
-}
-
-// wait until at most `ahead` stages of P instructions each are still in flight (ahead is a runtime value)
-template <int P, int MAXA>
-ASRX_DEV void wait_stages(int ahead) {
-  if constexpr (MAXA > 0) {
-    if (ahead >= MAXA) { wait_vmcnt<MAXA * P>(); return; }
-    wait_stages<P, MAXA - 1>(ahead);
-  } else {
-    wait_vmcnt<0>();
-  }
-}
 
 // 4 stages (64 KiB for 64x64 -> two workgroups per CU; 96 KiB for 128x64): measured faster than 6 stages on
 // the decoder shapes (6 stages cost the second workgroup per CU / gained nothing at 128x64)
@@ -1280,7 +1071,8 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
   // kernel family: ASRX_GEMM_KERNEL = auto | p3 | glds | reg  (A/B switch for benchmarking)
   const char* kenv = getenv("ASRX_GEMM_KERNEL");
   const int kvar = !kenv ? 0 : (!strcmp(kenv, "p3") ? 1 : (!strcmp(kenv, "glds") ? 2 : (!strcmp(kenv, "reg") ? 3 :
-                   (!strcmp(kenv, "ring") ? 4 : (!strcmp(kenv, "ring128") ? 5 : 0)))));
+                   (!strcmp(kenv, "ring") ? 4 : (!strcmp(kenv, "ring128") ? 5 : (!strcmp(kenv, "p5") ? 6 :
+                   (!strcmp(kenv, "p5m") ? 7 : 0)))))));
   const bool dma_ok = pl.vec && d->k % BK == 0 && (!d->a_trans || d->m % 8 == 0) && (!d->b_trans || d->n % 8 == 0) &&
                       d->m >= 8 && d->n >= 8;
   const int nt_p3 = ((d->m + P_BM - 1) / P_BM) * ((d->n + P_BN - 1) / P_BN);
@@ -1291,6 +1083,8 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
     else if (kvar == 2) pl.use = tile == 128 ? 2 : pl.use;
     else if (kvar == 4 && !d->a_trans) pl.use = 5;
     else if (kvar == 5 && !d->a_trans) pl.use = 6;
+    else if (kvar == 6) pl.use = 7;
+    else if (kvar == 7) pl.use = 8;
     // auto (measured on the c3 shapes, tools/gemm_bench.py): the p3 ring wins every projection with K <= 4096
     // whose grid fills the chip; smaller grids (the decoder's 4096-row GEMMs) take the 4-stage ring kernel; the
     // register path wins the weight-gradient (A^T, reduction over B*T rows) and very long-K GEMMs.
@@ -1300,6 +1094,8 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
     }
   }
   if (pl.use == 1) pl.ntiles = nt_p3;
+  else if (pl.use == 7) pl.ntiles = ((d->m + 255) / 256) * ((d->n + 255) / 256);
+  else if (pl.use == 8) pl.ntiles = ((d->m + 127) / 128) * ((d->n + 255) / 256);
   else if (pl.use == 5) pl.ntiles = ((d->m + 63) / 64) * ((d->n + 63) / 64);
   else if (pl.use == 6) pl.ntiles = nt_r128;
   else pl.ntiles = ((d->m + tile - 1) / tile) * ((d->n + tile - 1) / tile);
@@ -1336,6 +1132,9 @@ extern "C" int asrx_gemm_kernel_name(const asrx_gemm_desc* d, char* buf, int len
   const GemmPlan pl = plan_bf16(d, batch, splitk);
   if (pl.use == 1 || pl.use == 2)
     snprintf(buf, len, "gemm_bf16_%s_kernel<%s, %s, %d>", pl.use == 1 ? "p3" : "glds", tf[!!d->a_trans],
+             tf[!!d->b_trans], pl.epi);
+  else if (pl.use == 7 || pl.use == 8)
+    snprintf(buf, len, "gemm_bf16_p5_kernel<%d, %s, %s, %d>", pl.use == 7 ? 256 : 128, tf[!!d->a_trans],
              tf[!!d->b_trans], pl.epi);
   else if (pl.use >= 5)
     snprintf(buf, len, "gemm_bf16_ring_kernel<%d, 64, %s, %s, %d>", pl.use == 6 ? 128 : 64, tf[!!d->a_trans],
@@ -1389,6 +1188,15 @@ extern "C" int asrx_gemm_grouped_table(const asrx_gemm_desc* common, const asrx_
   if (tiles == 0) return ASRX_OK;
   if (common->in_dtype != ASRX_BF16 || !common->a_trans || !common->b_trans) return ASRX_ERR_UNSUPPORTED;
   if (common->c_dtype != ASRX_BF16 && common->c_dtype != ASRX_F32) return ASRX_ERR_ARG;
+  // 256x256 p5 tiles (host numbered the tiles for that size): every group's N % 4 == 0, 16-B aligned fp32 C rows
+  if (common->tile == 256) {
+    if (!cvec || common->c_dtype != ASRX_F32) return ASRX_ERR_ARG;
+    if (launch_p5_grouped(common->alpha, common->beta, common->c_dtype, (const GroupEnt*)groups, tile_group, nullptr,
+                          tiles, tiles, (hipStream_t)stream) != 0)
+      return ASRX_ERR_UNSUPPORTED;
+    ASRX_CHECK_LAUNCH();
+    return ASRX_OK;
+  }
   // XCD-contiguous tiles measured 1.5x SLOWER here (every workgroup of an XCD sweeping the same operand panel in
   // lockstep concentrates the L2 traffic); round-robin is the default
   const char* e = getenv("ASRX_GROUPED_XCD");
@@ -1433,6 +1241,9 @@ extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
   g.ws = d->workspace;
   g.rowsum = d->rowsum_a;
   g.rowsum_ws = d->rowsum_ws;
+  { const char* e = getenv("ASRX_GEMM_DBG"); g.dbg = e ? atoi(e) : 0; }
+  { const char* e = getenv("ASRX_P5_EXACT"); g.exact = (d->n % 256 == 0) && batch == 1 && (!e || atoi(e) != 0) &&
+                ((uintptr_t)d->c % 16 == 0) && (d->ldc % (d->c_dtype == ASRX_F32 ? 4 : 8) == 0); }
   if (g.rowsum && (!d->a_trans || d->in_dtype != ASRX_BF16 || batch != 1)) return ASRX_ERR_UNSUPPORTED;
   if (g.rowsum && splitk > 1 && !g.rowsum_ws) return ASRX_ERR_ARG;
   const int esz = d->c_dtype == ASRX_F32 ? 16 : 8;
@@ -1453,6 +1264,8 @@ extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
       else if (!d->a_trans && d->b_trans) dispatch_glds<false, true>(g, epi, pl.ntiles, splitk, batch, st);
       else if (d->a_trans && !d->b_trans) dispatch_glds<true, false>(g, epi, pl.ntiles, splitk, batch, st);
       else dispatch_glds<true, true>(g, epi, pl.ntiles, splitk, batch, st);
+    } else if (pl.use == 7 || pl.use == 8) {
+      dispatch_p5(g, pl.use == 7 ? 256 : 128, d->a_trans, d->b_trans, epi, pl.ntiles, splitk, batch, st);
     } else if (pl.use >= 5) {
       if (!d->b_trans) {
         if (pl.use == 6) dispatch_ring<128, 64, false, false>(g, epi, splitk, batch, st);
@@ -1492,5 +1305,20 @@ extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
       ASRX_CHECK_LAUNCH();
     }
   }
+  return ASRX_OK;
+}
+
+extern "C" int asrx_gemm_grouped_xcd(const asrx_gemm_desc* common, const asrx_gemm_group_dev* groups,
+                                     const uint16_t* tile_group, const uint16_t* block_tile, int32_t count,
+                                     int32_t tiles, int32_t blocks, void* stream) {
+  if (!common || !groups || !tile_group || !block_tile || count <= 0 || count > 65535 || tiles < 0 || blocks < 0 ||
+      tiles > 65535)
+    return ASRX_ERR_ARG;
+  if (tiles == 0 || blocks == 0) return ASRX_OK;
+  if (common->in_dtype != ASRX_BF16 || !common->a_trans || !common->b_trans) return ASRX_ERR_UNSUPPORTED;
+  if (launch_p5_grouped(common->alpha, common->beta, common->c_dtype, (const GroupEnt*)groups, tile_group, block_tile,
+                        tiles, blocks, (hipStream_t)stream) != 0)
+    return ASRX_ERR_UNSUPPORTED;
+  ASRX_CHECK_LAUNCH();
   return ASRX_OK;
 }

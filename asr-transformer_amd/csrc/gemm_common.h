@@ -1,0 +1,287 @@
+// Shared pieces of the bf16/f32 GEMM kernels (gemm.hip, gemm_p5.hip): kernel arguments, the fused
+// epilogues, LDS image helpers and counted-vmcnt waits.
+#pragma once
+#include "common.h"
+
+namespace asrxg {
+
+struct GemmArgs {
+  int M, N, K;
+  const void* a; int64_t lda;
+  const void* b; int64_t ldb;
+  void* c; int64_t ldc; int c_dtype;
+  int batch_inner;
+  int64_t sa_o, sa_i, sb_o, sb_i, sc_o, sc_i;
+  float alpha, beta;
+  const float* bias;
+  const float* rowadd; int64_t ld_rowadd; int rowadd_mod;
+  int relu;
+  uint32_t drop_thr; float drop_scale; uint64_t seed;
+  const void* gate; int64_t ld_gate; int gate_dtype;
+  const void* resid; int64_t ld_resid; int resid_dtype;
+  int splitk; int k_per_split;    // k_per_split multiple of BK
+  float* ws;                       // split-K partials [split][M][N]
+  int cvec;                        // C row starts 4-element aligned
+  float* rowsum;                   // fused bias gradient: rowsum[m] += sum_k A(m,k)   (A k-strided only)
+  float* rowsum_ws;                // [splitk][M] partials when splitk > 1
+  int dbg;                         // diagnostics only (ASRX_GEMM_DBG): 1 = skip the epilogue stores
+  int exact;                       // p5: N % 256 == 0 -> store-only epilogues use exact-count buffer stores
+};
+
+ASRX_DEV float ld_any(const void* p, int dtype, int64_t i) {
+  return dtype == ASRX_BF16 ? bf2f(((const bf16_t*)p)[i]) : ((const float*)p)[i];
+}
+
+// Full epilogue for 4 consecutive columns n0..n0+3 of row m (batch z).
+ASRX_DEV void epilogue4(const GemmArgs& g, int z, int m, int n0, const float* acc) {
+  if (m >= g.M || n0 >= g.N) return;
+  const int zo = z / g.batch_inner, zi = z % g.batch_inner;
+  const int64_t coff = zo * g.sc_o + zi * g.sc_i;
+  float r[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = acc[i] * g.alpha;
+  const int nv = min(4, g.N - n0);
+  if (g.bias) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) if (i < nv) r[i] += g.bias[n0 + i];
+  }
+  if (g.rowadd) {
+    const float* ra = g.rowadd + (int64_t)(m % g.rowadd_mod) * g.ld_rowadd + n0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) if (i < nv) r[i] += ra[i];
+  }
+  if (g.relu) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = fmaxf(r[i], 0.f);
+  }
+  if (g.drop_thr) {
+    const uint32_t base = (uint32_t)(((int64_t)z * g.M + m) * g.N + n0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = rng_keep(g.seed, base + i, g.drop_thr) ? r[i] * g.drop_scale : 0.f;
+  }
+  if (g.gate) {
+    const int64_t o = (int64_t)m * g.ld_gate + n0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) if (i < nv && !(ld_any(g.gate, g.gate_dtype, o + i) > 0.f)) r[i] = 0.f;
+  }
+  if (g.resid) {
+    const int64_t o = (int64_t)m * g.ld_resid + n0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) if (i < nv) r[i] += ld_any(g.resid, g.resid_dtype, o + i);
+  }
+  const int64_t co = coff + (int64_t)m * g.ldc + n0;
+  if (g.c_dtype == ASRX_F32) {
+    float* c = (float*)g.c + co;
+    if (g.beta != 0.f) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) if (i < nv) r[i] += g.beta * c[i];
+    }
+    if (nv == 4 && g.cvec) {
+      *(f4_t*)c = f4_t{r[0], r[1], r[2], r[3]};
+    } else {
+      for (int i = 0; i < nv; ++i) c[i] = r[i];
+    }
+  } else {
+    bf16_t* c = (bf16_t*)g.c + co;
+    if (g.beta != 0.f) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) if (i < nv) r[i] += g.beta * bf2f(c[i]);
+    }
+    if (nv == 4 && g.cvec) {
+      uint2 u;
+      u.x = pack2bf(r[0], r[1]);
+      u.y = pack2bf(r[2], r[3]);
+      *(uint2*)c = u;
+    } else {
+      for (int i = 0; i < nv; ++i) c[i] = f2bf(r[i]);
+    }
+  }
+}
+
+// Raw split-K partial store (no epilogue).
+ASRX_DEV void store_partial4(const GemmArgs& g, int split, int m, int n0, const float* acc) {
+  if (m >= g.M || n0 >= g.N) return;
+  float* w = g.ws + ((int64_t)split * g.M + m) * g.N + n0;
+  const int nv = min(4, g.N - n0);
+  if (nv == 4 && (g.N & 3) == 0) {
+    *(f4_t*)w = f4_t{acc[0], acc[1], acc[2], acc[3]};
+  } else {
+    for (int i = 0; i < nv; ++i) w[i] = acc[i];
+  }
+}
+
+constexpr int BK = 64;
+constexpr int KC_STRIDE = BK + 8;  // elements; 144 B rows for k-contiguous images
+
+template <int R>
+ASRX_DEV int ks_swz(int krow) {  // 32-byte-chunk XOR for the [BK][R] k-strided image
+  if constexpr (R == 128) return (krow & 3) | (((krow >> 3) & 1) << 2);
+  else return ((krow >> 1) & 1) | (((krow >> 3) & 1) << 1);
+}
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef const __attribute__((address_space(1))) void gbl_void_t;
+
+// Compile-time epilogue flags: the projection GEMMs of the training step use a handful of fixed epilogues;
+// specialising them removes the per-element runtime branches of epilogue4 (the generic fallback).
+enum : int {
+  E_BIAS = 1, E_RELU = 2, E_DROP = 4, E_GATE = 8, E_RESID = 16, E_BETA = 32, E_F32 = 64, E_ALPHA = 128,
+  E_ROWADD = 256, E_GENERIC = 1 << 30
+};
+
+// The fused element-wise epilogue of the fast path for the 4 consecutive columns n..n+3 of row m (valid
+// m < M, n < N); gate/resid/rowadd are read here, C is not.
+template <int EPI>
+ASRX_DEV f4_t epi_vals(const GemmArgs& g, int m, int n, f4_t v, f4_t b4) {
+  if constexpr ((EPI & E_ALPHA) != 0) v *= g.alpha;
+  if constexpr ((EPI & E_BIAS) != 0) v += b4;
+  if constexpr ((EPI & E_ROWADD) != 0) v += *(const f4_t*)(g.rowadd + (int64_t)(m % g.rowadd_mod) * g.ld_rowadd + n);
+  if constexpr ((EPI & E_RELU) != 0) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+  }
+  if constexpr ((EPI & E_DROP) != 0) {   // n % 4 == 0 and N even: two pair hashes cover the 4 elements
+    const uint32_t pb = (uint32_t)((int64_t)m * g.N + n) >> 1;
+    const uint32_t h0 = rng_hash(g.seed, pb), h1 = rng_hash(g.seed, pb + 1);
+    v[0] = rng_half(h0, 0) >= g.drop_thr ? v[0] * g.drop_scale : 0.f;
+    v[1] = rng_half(h0, 1) >= g.drop_thr ? v[1] * g.drop_scale : 0.f;
+    v[2] = rng_half(h1, 0) >= g.drop_thr ? v[2] * g.drop_scale : 0.f;
+    v[3] = rng_half(h1, 1) >= g.drop_thr ? v[3] * g.drop_scale : 0.f;
+  }
+  if constexpr ((EPI & E_GATE) != 0) {
+    const uint2 gt = *(const uint2*)((const bf16_t*)g.gate + (int64_t)m * g.ld_gate + n);
+    if (!(bf2f(gt.x & 0xffff) > 0.f)) v[0] = 0.f;
+    if (!(bf2f(gt.x >> 16) > 0.f)) v[1] = 0.f;
+    if (!(bf2f(gt.y & 0xffff) > 0.f)) v[2] = 0.f;
+    if (!(bf2f(gt.y >> 16) > 0.f)) v[3] = 0.f;
+  }
+  if constexpr ((EPI & E_RESID) != 0) v += *(const f4_t*)((const float*)g.resid + (int64_t)m * g.ld_resid + n);
+  return v;
+}
+
+template <int EPI, int TN, int TM>
+ASRX_DEV void epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int wn, f4_t (&acc)[TN][TM]) {
+  const int l = threadIdx.x & 63, gq = l >> 4;
+  if constexpr (EPI == E_GENERIC) {
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        epilogue4(g, z, m0 + wm + 16 * j + (l & 15), n0 + wn + 16 * i + 4 * gq, v);
+      }
+    return;
+  }
+  // fast path (host-checked): batch 1, N % 4 == 0, 16-B aligned rows; gate bf16, resid fp32
+  if constexpr ((EPI & E_F32) == 0 && TN % 2 == 0) {
+    if ((g.N & 7) == 0 && (g.ldc & 7) == 0 && ((uintptr_t)g.c & 15) == 0) {
+      // bf16 C, 16-byte stores: fragments i and i+1 of a row pair up across lanes l and l ^ 16
+      // (v_permlane16_swap), so lane group gq stores 8 consecutive columns of fragment i + (gq & 1) at column
+      // offset 8 (gq >> 1): one store instruction covers 16 rows x 64 contiguous bytes (T21).
+#pragma unroll
+      for (int i = 0; i < TN; i += 2) {
+        const int na = n0 + wn + 16 * i + 4 * gq, nb = na + 16;
+        f4_t ba = f4_t{0.f, 0.f, 0.f, 0.f}, bb = ba;
+        if constexpr ((EPI & E_BIAS) != 0) {
+          if (na < g.N) ba = *(const f4_t*)(g.bias + na);
+          if (nb < g.N) bb = *(const f4_t*)(g.bias + nb);
+        }
+        const int ncol = n0 + wn + 16 * (i + (gq & 1)) + 8 * (gq >> 1);
+#pragma unroll
+        for (int j = 0; j < TM; ++j) {
+          const int m = m0 + wm + 16 * j + (l & 15);
+          f4_t va = acc[i][j], vb = acc[i + 1][j];
+          if (m < g.M) {
+            if (na < g.N) va = epi_vals<EPI>(g, m, na, va, ba);
+            if (nb < g.N) vb = epi_vals<EPI>(g, m, nb, vb, bb);
+          }
+          const uint32_t ax = pack2bf(va[0], va[1]), ay = pack2bf(va[2], va[3]);
+          const uint32_t bx = pack2bf(vb[0], vb[1]), by = pack2bf(vb[2], vb[3]);
+          const auto sx = __builtin_amdgcn_permlane16_swap(ax, bx, false, false);
+          const auto sy = __builtin_amdgcn_permlane16_swap(ay, by, false, false);
+          if (m < g.M && ncol < g.N) {
+            v4u_t u = {sx[0], sy[0], sx[1], sy[1]};
+            *(v4u_t*)((bf16_t*)g.c + (int64_t)m * g.ldc + ncol) = u;
+          }
+        }
+      }
+      return;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < TN; ++i) {
+    const int n = n0 + wn + 16 * i + 4 * gq;
+    if (n >= g.N) continue;
+    f4_t b4 = f4_t{0.f, 0.f, 0.f, 0.f};
+    if constexpr ((EPI & E_BIAS) != 0) b4 = *(const f4_t*)(g.bias + n);
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int m = m0 + wm + 16 * j + (l & 15);
+      if (m >= g.M) continue;
+      f4_t v = epi_vals<EPI>(g, m, n, acc[i][j], b4);
+      if constexpr ((EPI & E_F32) != 0) {
+        f4_t* c = (f4_t*)((float*)g.c + (int64_t)m * g.ldc + n);
+        if constexpr ((EPI & E_BETA) != 0) v += *c;
+        *c = v;
+      } else {
+        uint2 u;
+        u.x = pack2bf(v[0], v[1]);
+        u.y = pack2bf(v[2], v[3]);
+        *(uint2*)((bf16_t*)g.c + (int64_t)m * g.ldc + n) = u;
+      }
+    }
+  }
+}
+
+// Epilogue sets instantiated per layout; anything else runs the generic epilogue.
+#define ASRX_EPI_NT(X) X(E_BIAS) X(E_BIAS | E_RELU) X(E_BIAS | E_RELU | E_DROP) X(E_BIAS | E_RESID | E_F32) \
+  X(E_BIAS | E_DROP | E_RESID | E_F32) X(E_F32) X(E_BIAS | E_ROWADD | E_F32) X(0)
+#define ASRX_EPI_NN(X) X(0) X(E_GATE) X(E_GATE | E_ALPHA) X(E_F32)
+#define ASRX_EPI_TT(X) X(E_BETA | E_F32) X(E_F32)
+
+// s_waitcnt with only the vector-memory counter constrained (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14,
+// expcnt and lgkmcnt at their no-wait maxima)
+template <int N>
+ASRX_DEV void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+// wait until at most `ahead` stages of P instructions each are still in flight (ahead is a runtime value)
+template <int P, int MAXA>
+ASRX_DEV void wait_stages(int ahead) {
+  if constexpr (MAXA > 0) {
+    if (ahead >= MAXA) { wait_vmcnt<MAXA * P>(); return; }
+    wait_stages<P, MAXA - 1>(ahead);
+  } else {
+    wait_vmcnt<0>();
+  }
+}
+
+// one problem of a grouped launch (layout-identical to asrx_gemm_group_dev of the C-ABI)
+struct GroupEnt {
+  const void* a; const void* b; void* c; float* rowsum;
+  int lda, ldb, ldc;
+  int m, n, k;
+  int tile_start;   // first global tile index of this group
+  int pad;
+};
+
+// p5 family (gemm_p5.hip): BM x 256 x 32 tiles, BM = 256 or 128
+void dispatch_p5(const GemmArgs& g, int bm, bool at, bool bt, int epi, int ntiles, int splitk, int batch,
+                 hipStream_t st);
+
+template <int TN, int TM>
+ASRX_DEV void keep_live(f4_t (&acc)[TN][TM]) {
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) asm volatile("" ::"v"(acc[i][j]));
+}
+
+// grouped weight gradients on 256x256 p5 tiles (A^T, B^T operands, fp32 C, alpha 1, beta 0 or 1); 0 = launched
+// block_tile: workgroup -> tile map (nullptr: identity, blocks == ntiles)
+int launch_p5_grouped(float alpha, float beta, int c_dtype, const GroupEnt* ents, const uint16_t* tile_group,
+                      const uint16_t* block_tile, int ntiles, int blocks, hipStream_t st);
+
+}  // namespace asrxg

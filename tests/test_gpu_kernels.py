@@ -47,12 +47,12 @@ def kernel_variant(request):
         os.environ["ASRX_GEMM_KERNEL"] = old
 
 
-@pytest.mark.parametrize("kernel_variant", ["auto", "p3", "glds", "reg", "ring", "ring128"], indirect=True)
+@pytest.mark.parametrize("kernel_variant", ["auto", "p3", "p5", "p5m", "glds", "reg", "ring", "ring128"], indirect=True)
 @pytest.mark.parametrize("tile", [0, 128])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("at,bt", [(False, False), (False, True), (True, False), (True, True)])
 @pytest.mark.parametrize("m,n,k", [(200, 136, 96), (1000, 250, 64), (129, 64, 576), (64, 1536, 512), (33, 17, 40),
-                                   (264, 392, 1216)])
+                                   (264, 392, 1216), (300, 512, 128)])
 def test_gemm_layouts(dtype, at, bt, m, n, k, tile, kernel_variant):
     g = torch.Generator(device="cpu").manual_seed(m * 7 + n * 3 + k)
     A = torch.randn(m, k, generator=g)
@@ -67,7 +67,7 @@ def test_gemm_layouts(dtype, at, bt, m, n, k, tile, kernel_variant):
     assert relerr(C.cpu(), ref) < tol
 
 
-@pytest.mark.parametrize("kernel_variant", ["auto", "p3", "glds", "reg", "ring", "ring128"], indirect=True)
+@pytest.mark.parametrize("kernel_variant", ["auto", "p3", "p5", "p5m", "glds", "reg", "ring", "ring128"], indirect=True)
 @pytest.mark.parametrize("tile", [64, 128])
 def test_gemm_epilogue(tile, kernel_variant):
     m, n, k = 300, 192, 128
@@ -87,6 +87,23 @@ def test_gemm_epilogue(tile, kernel_variant):
     assert relerr(out.cpu(), ref) < 2e-3
 
 
+@pytest.mark.parametrize("kernel_variant", ["p5", "p5m"], indirect=True)
+@pytest.mark.parametrize("m,n,k,bt", [(1000, 512, 256, False), (700, 768, 64, True), (1300, 256, 2048, False)])
+def test_gemm_exact_store_epilogue(m, n, k, bt, kernel_variant):
+    """p5 store-only epilogues with exact-count buffer stores (N % 256 == 0, ragged M): persistent tiles back to
+    back, bf16 and fp32 C, C rows padded (ldc > N) so a stray store would show."""
+    g = torch.Generator().manual_seed(m + n + k)
+    A = bf(torch.randn(m, k, generator=g))
+    B = bf(torch.randn(n, k, generator=g))
+    Bd = (B.t().contiguous() if bt else B).to(dev)
+    ref = A.double() @ B.double().t()
+    for cdt in (torch.bfloat16, torch.float32):
+        C = torch.full((m, n + 64), 7.0, device=dev, dtype=cdt)
+        K().gemm(A.to(dev), Bd, C, m, n, k, lda=k, ldb=Bd.stride(0), ldc=n + 64, b_trans=bt)
+        assert relerr(C[:, :n].float().cpu(), ref) < 1e-2
+        assert bool((C[:, n:] == 7.0).all())
+
+
 def test_gemm_beta_splitk_and_bf16_out():
     m, n, k = 64, 96, 5000
     g = torch.Generator().manual_seed(2)
@@ -103,7 +120,7 @@ def test_gemm_beta_splitk_and_bf16_out():
     assert relerr(Cb.float().cpu(), ref - C0.double()) < 1e-2
 
 
-@pytest.mark.parametrize("kernel_variant", ["auto", "p3", "glds", "reg", "ring", "ring128"], indirect=True)
+@pytest.mark.parametrize("kernel_variant", ["auto", "p3", "p5", "p5m", "glds", "reg", "ring", "ring128"], indirect=True)
 @pytest.mark.parametrize("tile,splitk", [(64, 1), (128, 1), (64, 5), (128, 7)])
 def test_gemm_fused_rowsum(tile, splitk, kernel_variant):
     """wgrad GEMM dW = dY^T X with the bias gradient (row sums of dY^T) fused into the staging/fragments."""
@@ -119,13 +136,15 @@ def test_gemm_fused_rowsum(tile, splitk, kernel_variant):
     assert relerr(bg.cpu(), 2 + dy.double().sum(0)) < 1e-5
 
 
+@pytest.mark.parametrize("wtile", [128, 256])
 @pytest.mark.parametrize("ngroups", [1, 7, 60])
-def test_gemm_grouped_wgrad(ngroups):
+def test_gemm_grouped_wgrad(ngroups, wtile, monkeypatch):
     """Grouped weight gradients (asrx_gemm_grouped): ragged shapes, K not a multiple of 64, fused bias-grad row
     sums, beta=1 accumulation into existing fp32 grads; > MAX_GROUPS problems split over several launches."""
     g = torch.Generator(device=dev).manual_seed(ngroups)
     shapes = [(1000, 136, 96), (4096, 512, 512), (333, 248, 64), (64, 8, 576), (2500, 1536, 512),
               (77, 40, 1216), (249, 200, 24)]
+    monkeypatch.setattr(K(), "WGRAD_TILE", wtile)
     items, refs = [], []
     for i in range(ngroups):
         M, N, Kd = shapes[i % len(shapes)]
