@@ -410,6 +410,9 @@ def reduce_rows_grouped(items):
         call("asrx_reduce_rows_grouped", arr, len(chunk), stream())
 
 
+LN_BWD_BLOCKS = int(os.environ.get("ASRX_LN_BWD_BLOCKS", "1024"))
+
+
 def layernorm_bwd(x, dy, gamma, mean, rstd, dgb, *, dres=None, dx_drop=None, dropout_p=0.0, seed=0, defer=None):
     """Returns dx (fp32). dgb: fp32 [2*d] grad buffer (gamma grads then beta grads), accumulated.
     If dx_drop (bf16 or fp32) is given it receives dropout_bwd(dx) for the upstream sublayer.  With a `defer`
@@ -417,7 +420,7 @@ def layernorm_bwd(x, dy, gamma, mean, rstd, dgb, *, dres=None, dx_drop=None, dro
     _cuda(x, dy, gamma, mean, rstd, dgb)
     rows, d = x.shape
     dx = torch.empty(rows, d, device=x.device, dtype=torch.float32)
-    nblocks = max(1, min(512, (rows + 15) // 16))
+    nblocks = max(1, min(LN_BWD_BLOCKS, (rows + 7) // 8))   # >= 2 rows per wave: the kernel prefetches the next
     part = torch.empty(nblocks * 2 * d, device=x.device, dtype=torch.float32)
     call("asrx_layernorm_bwd", code(x), x.data_ptr(), code(dy), dy.data_ptr(), gamma.data_ptr(), mean.data_ptr(),
          rstd.data_ptr(), _p(dres), dx.data_ptr(), _p(dx_drop), code(dx_drop) if dx_drop is not None else 0,

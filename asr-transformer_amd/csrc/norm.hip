@@ -69,8 +69,11 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int x_dtype, const void* x,
   if (l == 0) { mean[row] = mu; rstd[row] = rs; }
 }
 
-// Backward. Each block: 4 waves, grid-stride over rows; per-column dgamma/dbeta partials kept in registers
-// and reduced across the block's waves into part[block][2*D].
+// Backward. Each block: 4 waves, grid-stride over rows (one row per wave per iteration); the NEXT row's
+// x / dy / dres / mean / rstd are loaded before the current row is reduced and stored, so every wave keeps two
+// rows of loads in flight (the per-row chain load -> wave reductions -> store is latency-bound otherwise).
+// Per-column dgamma/dbeta partials stay in registers and are reduced across the block's waves into
+// part[block][2*D].
 template <int CH, int NJ>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(int x_dtype, const void* x, int dy_dtype, const void* dy,
                                                      const float* gamma, const float* mean, const float* rstd,
@@ -85,26 +88,38 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int x_dtype, const void* x,
   for (int j = 0; j < NJ; ++j)
 #pragma unroll
     for (int i = 0; i < CH; ++i) { pg[j][i] = 0.f; pb[j][i] = 0.f; ga[j][i] = gamma[(j * 64 + l) * CH + i]; }
-  for (int64_t row = (int64_t)blockIdx.x * 4 + w; row < rows; row += (int64_t)gridDim.x * 4) {
-    const float mu = mean[row], rs = rstd[row];
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  int64_t row = (int64_t)blockIdx.x * 4 + w;
+  float xv[NJ][CH], dv[NJ][CH], rv[NJ][CH], mu = 0.f, rs = 0.f;
+  auto load_row = [&](int64_t r, float (&X)[NJ][CH], float (&Dv)[NJ][CH], float (&R)[NJ][CH], float& M, float& S) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int64_t off = r * D + (j * 64 + l) * CH;
+      load_ch<CH>(x, x_dtype, off, X[j]);
+      load_ch<CH>(dy, dy_dtype, off, Dv[j]);
+      if (dres) load_ch<CH>(dres, ASRX_F32, off, R[j]);
+    }
+    M = mean[r];
+    S = rstd[r];
+  };
+  if (row < rows) load_row(row, xv, dv, rv, mu, rs);
+  while (row < rows) {
+    const int64_t nrow = row + stride;
+    float xn[NJ][CH], dn[NJ][CH], rn[NJ][CH], mun = 0.f, rsn = 0.f;
+    if (nrow < rows) load_row(nrow, xn, dn, rn, mun, rsn);
     float xh[NJ][CH], g[NJ][CH];
     float sg = 0.f, sgx = 0.f;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int64_t off = row * D + (j * 64 + l) * CH;
-      float xv[CH], dv[CH];
-      load_ch<CH>(x, x_dtype, off, xv);
-      load_ch<CH>(dy, dy_dtype, off, dv);
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int i = 0; i < CH; ++i) {
-        xh[j][i] = (xv[i] - mu) * rs;
-        g[j][i] = dv[i] * ga[j][i];
+        xh[j][i] = (xv[j][i] - mu) * rs;
+        g[j][i] = dv[j][i] * ga[j][i];
         sg += g[j][i];
         sgx += g[j][i] * xh[j][i];
-        pg[j][i] += dv[i] * xh[j][i];
-        pb[j][i] += dv[i];
+        pg[j][i] += dv[j][i] * xh[j][i];
+        pb[j][i] += dv[j][i];
       }
-    }
     sg = wave_sum(sg) * (1.f / D);
     sgx = wave_sum(sgx) * (1.f / D);
 #pragma unroll
@@ -112,13 +127,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int x_dtype, const void* x,
       const int64_t off = row * D + (j * 64 + l) * CH;
       float o[CH];
 #pragma unroll
-      for (int i = 0; i < CH; ++i) o[i] = rs * (g[j][i] - sg - xh[j][i] * sgx);
-      if (dres) {
-        float r[CH];
-        load_ch<CH>(dres, ASRX_F32, off, r);
-#pragma unroll
-        for (int i = 0; i < CH; ++i) o[i] += r[i];
-      }
+      for (int i = 0; i < CH; ++i) o[i] = rs * (g[j][i] - sg - xh[j][i] * sgx) + (dres ? rv[j][i] : 0.f);
       store_ch<CH>(dx_out, ASRX_F32, off, o);
       if (dx_drop) {
         float od[CH];
@@ -128,6 +137,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int x_dtype, const void* x,
         store_ch<CH>(dx_drop, drop_dtype, off, od);
       }
     }
+    row = nrow;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int i = 0; i < CH; ++i) { xv[j][i] = xn[j][i]; dv[j][i] = dn[j][i]; rv[j][i] = rn[j][i]; }
+    mu = mun;
+    rs = rsn;
   }
 #pragma unroll
   for (int j = 0; j < NJ; ++j)
