@@ -64,6 +64,27 @@ class Ctx:
         lq, self.lnq = self.lnq, None
         K.linear_wgrad_grouped(q or [])
         K.reduce_rows_grouped(lq or [])
+        side = getattr(self, "_wside", None)
+        if side is not None:          # weight gradients issued on the side stream are final only after it
+            torch.cuda.current_stream(side.device).wait_stream(side)
+            self._wside = None
+
+    def flush_wgrad_side(self):
+        """Issue the weight gradients queued so far on the side stream, so they overlap the rest of the backward
+        chain (they feed only the optimizer / all-reduce, which wait for them in flush_wgrad)."""
+        if not WGRAD_OVERLAP or not self.wq:
+            return
+        q, self.wq = self.wq, []
+        dev = q[0][0].device
+        main = torch.cuda.current_stream(dev)
+        side = self.side_stream(dev)
+        side.wait_stream(main)
+        for dy, x, _, _ in q:           # keep the operands' memory from being reused on the main stream
+            dy.record_stream(side)
+            x.record_stream(side)
+        with torch.cuda.stream(side):
+            K.linear_wgrad_grouped(q)
+        self._wside = side
 
 
 class Seeds:
@@ -78,6 +99,8 @@ class Seeds:
 
 
 _SIDE = {}
+# weight gradients of each finished layer issued on the side stream, overlapping the backward chain
+WGRAD_OVERLAP = os.environ.get("ASRX_WGRAD_OVERLAP", "0") == "1"
 # generating the keep bits on a side stream (overlapping the LN + Q/K/V GEMM) measured SLOWER than generating
 # them in line (18.2 vs 17.75 ms/step: the VALU-heavy generator steals the GEMM's CUs): off by default
 _SIDE_DROPGEN = os.environ.get("ASRX_DROPGEN_SIDE", "0") == "1"

@@ -157,6 +157,7 @@ def encoder_bwd(C, enc, S, dy, gate_feats, ready=None):
         nxt = torch.empty(x.shape, dtype=C.cd, device=x.device)
         dx = Bk.enc_layer_bwd(C, layer_S, dx, dx_c, nxt)
         dx_c = nxt
+        C.flush_wgrad_side()
         if i == n // 2 and n > 1:
             _release(C, ready, [p for l in enc._layers[n // 2:] for p in l.parameters()] +
                      list(enc._norm_out.parameters()))
@@ -265,6 +266,7 @@ def model_backward(C, model, S, dlogits_c, ready=None):
     own = C.defer_wgrad()
     denc = decoder_bwd(C, model.decoder, S["d"], dlogits_c)
     if own:
+        C.flush_wgrad_side()
         _release(C, ready, list(model.decoder.parameters()))
     dfeats = encoder_bwd(C, model.encoder, S["e"], denc, gate_feats=True, ready=ready if own else None)
     Bk.frontend_bwd(C, S["f"], dfeats, model.input_layer[0], model.input_layer[2])

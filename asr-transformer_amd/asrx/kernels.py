@@ -207,6 +207,8 @@ def wgrad_groupable(dy, x, wgrad):
 # Weight-gradient tile: 256 = the p5 LDS-DMA ring kernel (256x256x32, gemm_p5.hip), 128 = register-staged
 # 128x128 tiles (gemm.hip).  ASRX_WGRAD_TILE overrides (A/B benchmarking).
 WGRAD_TILE = int(os.environ.get("ASRX_WGRAD_TILE", "128"))
+# 128-tile grouped launch with the XCD-aware tile layout (xcd_plan) instead of the tile order of the table
+WGRAD_XCD = os.environ.get("ASRX_WGRAD_XCD128", "1") == "1"
 
 
 def _grouped_p5_ok(items, beta):
@@ -251,12 +253,16 @@ def xcd_plan(shapes, tile=256, nxcd=8):
     return plan
 
 
-def _grouped_xcd(items, common):
-    """p5 grouped weight gradients (asrx_gemm_grouped_xcd): 64-B group entries, tile -> group map and the
-    XCD-aware block -> tile map in one pinned host buffer, copied to the device on the stream."""
+def _grouped_xcd(items, common, tile=256):
+    """Grouped weight gradients with an XCD-aware workgroup -> tile map (asrx_gemm_grouped_xcd): 64-B group
+    entries, tile -> group map and block -> tile map in one pinned host buffer, copied to the device on the
+    stream."""
     import numpy as np
     shapes = [(dy.shape[1], x.shape[1], dy.shape[0]) for (dy, x, _, _) in items]
-    group_order, nts, block_tile = xcd_plan(shapes, nxcd=8 if os.environ.get("ASRX_WGRAD_XCD", "1") != "0" else 1)
+    group_order, nts, block_tile = xcd_plan(shapes, tile=tile,
+                                            nxcd=8 if os.environ.get("ASRX_WGRAD_XCD", "1") != "0" else 1)
+    common.tile = tile
+    cvec = 1
     ents = np.zeros((len(items), 8), dtype=np.int64)
     ints = ents.view(np.int32)
     maps, start, flops = [], 0, 0
@@ -271,6 +277,9 @@ def _grouped_xcd(items, common):
         maps.append(np.full(nts[i], slot, dtype=np.uint16))
         start += nts[i]
         flops += 2 * m * n * k
+        if wgrad.stride(0) % 4 or wgrad.data_ptr() % 16:
+            cvec = 0
+    common.relu = cvec
     tmap = np.concatenate(maps)
     o1 = ents.nbytes
     o2 = o1 + (tmap.nbytes + 63) // 64 * 64
@@ -330,7 +339,7 @@ def linear_wgrad_grouped(items, *, beta=1.0):
     common.in_dtype, common.a_trans, common.b_trans, common.c_dtype = BF16, 1, 1, F32
     common.alpha, common.beta = 1.0, beta
     p5 = _grouped_p5_ok(items, beta)
-    if p5 or len(items) > MAX_GROUPS:
+    if p5 or WGRAD_XCD or len(items) > MAX_GROUPS:
         kname = (GROUPED_P5_KERNEL if beta == 1.0 else GROUPED_P5_KERNEL0) if p5 else GROUPED_TABLE_KERNEL
         probe = PROBE
         timed = probe is not None and probe.record(kname)
@@ -340,7 +349,12 @@ def linear_wgrad_grouped(items, *, beta=1.0):
         if timed:
             s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s0.record()
-        flops, _ = _grouped_xcd(items, common) if p5 else _grouped_table(items, common)
+        if p5:
+            flops, _ = _grouped_xcd(items, common, 256)
+        elif WGRAD_XCD:
+            flops, _ = _grouped_xcd(items, common, 128)
+        else:
+            flops, _ = _grouped_table(items, common)
         if timed:
             s1.record()
             probe.events.setdefault(kname, []).append((s0, s1))

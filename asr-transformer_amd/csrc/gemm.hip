@@ -254,11 +254,15 @@ template <bool AT, bool BT>
 __global__ __launch_bounds__(256) void gemm_bf16_grouped_dev_kernel(float alpha, float beta, int c_dtype, int cvec,
                                                                     const GroupEnt* __restrict__ ents,
                                                                     const uint16_t* __restrict__ tile_group,
-                                                                    int ntiles, int xcd) {
+                                                                    int ntiles, int xcd,
+                                                                    const uint16_t* __restrict__ block_tile) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[reg_lds_elems<128, 128, AT, BT>()];
-  // xcd: workgroup b runs on XCD b % 8 -> give each XCD a contiguous tile range, so tiles sharing an operand
-  // panel (consecutive tiles of a group) run on one XCD together and share its L2 (grid = 8 * ceil(tiles / 8))
-  const int tid = xcd ? (int)(blockIdx.x % 8) * (int)(gridDim.x / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+  // block_tile: explicit workgroup -> tile map (asrx_gemm_grouped_xcd: the host lays each group's tiles on one
+  // XCD at the same time).  xcd: workgroup b runs on XCD b % 8 -> give each XCD a contiguous tile range
+  // (grid = 8 * ceil(tiles / 8)).
+  const int tid = block_tile ? (int)block_tile[blockIdx.x]
+                             : (xcd ? (int)(blockIdx.x % 8) * (int)(gridDim.x / 8) + (int)(blockIdx.x / 8)
+                                    : (int)blockIdx.x);
   if (tid >= ntiles) return;
   const int gi = __builtin_amdgcn_readfirstlane((int)tile_group[tid]);
   const GroupEnt e = ents[gi];
@@ -471,7 +475,7 @@ void dispatch_glds(const GemmArgs& g, int epi, int ntiles, int splitk, int batch
 // `s_waitcnt vmcnt(P_INST)` (only the youngest stage left in flight) followed by a raw s_barrier — the
 // loads stay in flight across the barrier (a __syncthreads() would drain them).  One workgroup per CU.
 // ------------------------------------------------------------------------------------------------
-constexpr int P_BM = 256, P_BN = 128, P_THREADS = 512;
+constexpr int P_BM = 256, P_BN = 128, P_THREADS = 512, P_BIAS_BYTES = 16384;
 constexpr int PA_BYTES = P_BM * BK * 2, PB_BYTES = P_BN * BK * 2, P_STAGE = PA_BYTES + PB_BYTES;
 constexpr int P_INST = (PA_BYTES + PB_BYTES) / (P_THREADS * 16);   // LDS-DMA instructions per thread per stage
 static_assert(P_INST == 6, "vmcnt literal below assumes 6 LDS-DMA instructions per stage");
@@ -505,13 +509,10 @@ struct PStage {
 #if defined(__HIP_DEVICE_COMPILE__)  // the buffer-resource builtins do not exist in the host pass (which then
                                      // silently dropped the kernel's host stubs)
     const int64_t koff = KSTRIDED ? (int64_t)k0 * ld * 2 : (int64_t)k0 * 2;
-    const int64_t rem = total_bytes - koff;
-    __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)((const char*)base + koff), (short)0, (int)(rem > 0x7fffffff ? 0x7fffffff : rem), 0x00020000);
+    const v4i_t srd = make_srd((const char*)base + koff, total_bytes - koff);
     const int w = threadIdx.x >> 6;
 #pragma unroll
-    for (int j = 0; j < NI; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_t*)(img + (j * 8 + w) * 1024), 16, voff[j], 0, 0, 0);
+    for (int j = 0; j < NI; ++j) dma16_asm(img + (j * 8 + w) * 1024, srd, voff[j]);
 #endif
   }
 };
@@ -541,7 +542,9 @@ ASRX_DEV s8_t p_frag(const unsigned char* img, int i0, int ks) {
 
 template <bool AT, bool BT, int EPI>
 __global__ __launch_bounds__(512) void gemm_bf16_p3_kernel(GemmArgs g, int ntiles, int xcd) {
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[3 * P_STAGE];
+  // 3 ring stages + 16 KiB holding the whole bias vector (N <= 4096, bias epilogues): it is loaded once before
+  // the ring starts, so the epilogues issue no global load (which would wait for every LDS-DMA stage in flight)
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[3 * P_STAGE + P_BIAS_BYTES];
   constexpr int TM = 4, TN = 4;
   const int ntn = (g.N + P_BN - 1) / P_BN;
   const int split = blockIdx.y;
@@ -601,15 +604,26 @@ __global__ __launch_bounds__(512) void gemm_bf16_p3_kernel(GemmArgs g, int ntile
 #pragma unroll
   for (int j = 0; j < TM; ++j) rs[j] = 0.f;
 
+  // bias epilogues: the host splits N > 4096 into column chunks, so the whole bias fits the LDS region
+  constexpr bool use_lb = (EPI & E_BIAS) != 0;
+  if constexpr (use_lb) {
+    float* lb = (float*)(lds + 3 * P_STAGE);
+    for (int c = threadIdx.x * 4; c < g.N; c += P_THREADS * 4) *(f4_t*)(lb + c) = *(const f4_t*)(g.bias + c);
+    __syncthreads();
+  }
   P3_ISSUE_NEXT();
   if (total > 1) P3_ISSUE_NEXT();
-  bool drain = false;
+  // younger-operation ledger: stage s was issued in step s - 2; younger than it are the epilogue stores of steps
+  // s - 2 and s - 1 (e2, e1: the exact store counts epilogue_tile reports, else 0) and stage s + 1 (6 pieces,
+  // 7 with a bias DMA: 6 is a lower bound).  A lower bound only over-waits.
+  int e1 = 0, e2 = 0;
   int vc = 0, kk = 0, cb = 0;   // compute cursor
   for (int s = 0; s < total; ++s) {
-    if (s + 1 < total && !drain) asm volatile("s_waitcnt vmcnt(6)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+    wait_vmcnt_rt(e2 + (s + 1 < total ? P_INST : 0) + e1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    drain = false;
+    e2 = e1;
+    e1 = 0;
     if (s + 2 < total) P3_ISSUE_NEXT();
     const unsigned char* la = lds + cb * P_STAGE;
     const unsigned char* lb = la + PA_BYTES;
@@ -663,13 +677,18 @@ __global__ __launch_bounds__(512) void gemm_bf16_p3_kernel(GemmArgs g, int ntile
             store_partial4(g, split, m0 + wm + 16 * j + (l & 15), n0 + wn + 16 * i + 4 * gq, v);
           }
       } else {
-        if (g.dbg == 1) keep_live(acc); else epilogue_tile<EPI>(g, z, m0, n0, wm, wn, acc);
+        if (g.dbg == 1) {
+          keep_live(acc);
+        } else {
+          const int full = m0 + P_BM <= g.M && n0 + P_BN <= g.N;
+          e1 = epilogue_tile<EPI, TN, TM, use_lb>(g, z, m0, n0, wm, wn, acc, (lds_cfloat_t*)(lds + 3 * P_STAGE) + n0,
+                                                  full);
+        }
       }
 #pragma unroll
       for (int i = 0; i < TN; ++i)
 #pragma unroll
         for (int j = 0; j < TM; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
-      drain = true;
     }
     if (++kk == nk) { kk = 0; ++vc; }
     cb = cb == 2 ? 0 : cb + 1;
@@ -1090,7 +1109,8 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
     // register path wins the weight-gradient (A^T, reduction over B*T rows) and very long-K GEMMs.
     else if (kvar == 0 && !d->a_trans && d->k <= 4096) {
       if (nt_p3 * splitk * batch >= 192) pl.use = 1;
-      else pl.use = nt_r128 * splitk * batch >= 192 ? 6 : 5;
+      // (64x64 tiles also win the long-K decoder GEMMs, K >= 1536: 4 x more workgroups to cover the latency)
+      else pl.use = (nt_r128 * splitk * batch >= 192 && d->k < 1536) ? 6 : 5;
     }
   }
   if (pl.use == 1) pl.ntiles = nt_p3;
@@ -1204,7 +1224,7 @@ extern "C" int asrx_gemm_grouped_table(const asrx_gemm_desc* common, const asrx_
   const unsigned grid = xcd ? 8u * (unsigned)((tiles + 7) / 8) : (unsigned)tiles;
   hipLaunchKernelGGL((gemm_bf16_grouped_dev_kernel<true, true>), dim3(grid), dim3(256), 0,
                      (hipStream_t)stream, common->alpha, common->beta, common->c_dtype, cvec ? 1 : 0,
-                     (const GroupEnt*)groups, tile_group, (int)tiles, xcd);
+                     (const GroupEnt*)groups, tile_group, (int)tiles, xcd, nullptr);
   ASRX_CHECK_LAUNCH();
   return ASRX_OK;
 }
@@ -1254,7 +1274,23 @@ extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
     g.splitk = splitk;
     g.k_per_split = ((((int)d->k + BK - 1) / BK + splitk - 1) / splitk) * BK;
     const int epi = pl.epi;
-    if (pl.use == 1) {
+    if (pl.use == 1 && (epi & E_BIAS) && epi != E_GENERIC && d->n > P_BIAS_BYTES / 4) {
+      // the p3 bias epilogue stages the whole bias vector in LDS (16 KiB): wider outputs run as column chunks
+      // (fast-path epilogues without dropout only: their element math does not depend on N)
+      if ((epi & E_DROP) || d->a_trans || d->b_trans || batch != 1 || splitk != 1) return ASRX_ERR_UNSUPPORTED;
+      for (int c0 = 0; c0 < d->n; c0 += P_BIAS_BYTES / 4) {
+        GemmArgs gc = g;
+        gc.N = std::min(P_BIAS_BYTES / 4, d->n - c0);
+        gc.b = (const bf16_t*)d->b + (int64_t)c0 * d->ldb;
+        gc.bias = d->bias + c0;
+        gc.c = (char*)d->c + (int64_t)c0 * (d->c_dtype == ASRX_F32 ? 4 : 2);
+        if (gc.rowadd) gc.rowadd = d->rowadd + c0;
+        if (gc.resid) gc.resid = (const float*)d->resid + c0;
+        if (gc.gate) gc.gate = (const bf16_t*)d->gate + c0;
+        const int nt = ((d->m + P_BM - 1) / P_BM) * ((gc.N + P_BN - 1) / P_BN);
+        dispatch_p3<false, false>(gc, epi, nt, 1, 1, st);
+      }
+    } else if (pl.use == 1) {
       if (!d->a_trans && !d->b_trans) dispatch_p3<false, false>(g, epi, pl.ntiles, splitk, batch, st);
       else if (!d->a_trans && d->b_trans) dispatch_p3<false, true>(g, epi, pl.ntiles, splitk, batch, st);
       else if (d->a_trans && !d->b_trans) dispatch_p3<true, false>(g, epi, pl.ntiles, splitk, batch, st);
@@ -1316,9 +1352,15 @@ extern "C" int asrx_gemm_grouped_xcd(const asrx_gemm_desc* common, const asrx_ge
     return ASRX_ERR_ARG;
   if (tiles == 0 || blocks == 0) return ASRX_OK;
   if (common->in_dtype != ASRX_BF16 || !common->a_trans || !common->b_trans) return ASRX_ERR_UNSUPPORTED;
-  if (launch_p5_grouped(common->alpha, common->beta, common->c_dtype, (const GroupEnt*)groups, tile_group, block_tile,
-                        tiles, blocks, (hipStream_t)stream) != 0)
+  if (common->c_dtype != ASRX_BF16 && common->c_dtype != ASRX_F32) return ASRX_ERR_ARG;
+  if (common->tile == 128) {   // register-staged 128x128 tiles (gemm_bf16_tile): any alignment-checked table
+    hipLaunchKernelGGL((gemm_bf16_grouped_dev_kernel<true, true>), dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                       common->alpha, common->beta, common->c_dtype, common->relu ? 1 : 0, (const GroupEnt*)groups,
+                       tile_group, (int)tiles, 0, block_tile);
+  } else if (launch_p5_grouped(common->alpha, common->beta, common->c_dtype, (const GroupEnt*)groups, tile_group,
+                               block_tile, tiles, blocks, (hipStream_t)stream) != 0) {
     return ASRX_ERR_UNSUPPORTED;
+  }
   ASRX_CHECK_LAUNCH();
   return ASRX_OK;
 }

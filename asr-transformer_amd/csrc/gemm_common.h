@@ -159,8 +159,15 @@ ASRX_DEV f4_t epi_vals(const GemmArgs& g, int m, int n, f4_t v, f4_t b4) {
   return v;
 }
 
-template <int EPI, int TN, int TM>
-ASRX_DEV void epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int wn, f4_t (&acc)[TN][TM]) {
+typedef __attribute__((address_space(3))) const float lds_cfloat_t;
+
+// Returns a lower bound on the vector-memory instructions it issued (the 16-byte stores of a full tile on the
+// paired path; 0 elsewhere): a persistent kernel adds it to the count of operations younger than its next
+// stage, so it does not wait for these stores.  lbias (optional): the tile's bias columns [n0, n0 + BN) staged
+// in LDS (no global load in the epilogue: such a load would wait for every older LDS-DMA stage in flight).
+template <int EPI, int TN, int TM, bool LB = false>
+ASRX_DEV int epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int wn, f4_t (&acc)[TN][TM],
+                           lds_cfloat_t* lbias = nullptr, int full = 0) {
   const int l = threadIdx.x & 63, gq = l >> 4;
   if constexpr (EPI == E_GENERIC) {
 #pragma unroll
@@ -170,7 +177,7 @@ ASRX_DEV void epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, in
         float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
         epilogue4(g, z, m0 + wm + 16 * j + (l & 15), n0 + wn + 16 * i + 4 * gq, v);
       }
-    return;
+    return 0;
   }
   // fast path (host-checked): batch 1, N % 4 == 0, 16-B aligned rows; gate bf16, resid fp32
   if constexpr ((EPI & E_F32) == 0 && TN % 2 == 0) {
@@ -183,8 +190,13 @@ ASRX_DEV void epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, in
         const int na = n0 + wn + 16 * i + 4 * gq, nb = na + 16;
         f4_t ba = f4_t{0.f, 0.f, 0.f, 0.f}, bb = ba;
         if constexpr ((EPI & E_BIAS) != 0) {
-          if (na < g.N) ba = *(const f4_t*)(g.bias + na);
-          if (nb < g.N) bb = *(const f4_t*)(g.bias + nb);
+          if constexpr (LB) {
+            ba = *(const __attribute__((address_space(3))) f4_t*)(lbias + (na - n0));
+            bb = *(const __attribute__((address_space(3))) f4_t*)(lbias + (nb - n0));
+          } else {
+            if (na < g.N) ba = *(const f4_t*)(g.bias + na);
+            if (nb < g.N) bb = *(const f4_t*)(g.bias + nb);
+          }
         }
         const int ncol = n0 + wn + 16 * (i + (gq & 1)) + 8 * (gq >> 1);
 #pragma unroll
@@ -205,7 +217,7 @@ ASRX_DEV void epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, in
           }
         }
       }
-      return;
+      return full ? TN * TM / 2 : 0;
     }
   }
 #pragma unroll
@@ -213,7 +225,10 @@ ASRX_DEV void epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, in
     const int n = n0 + wn + 16 * i + 4 * gq;
     if (n >= g.N) continue;
     f4_t b4 = f4_t{0.f, 0.f, 0.f, 0.f};
-    if constexpr ((EPI & E_BIAS) != 0) b4 = *(const f4_t*)(g.bias + n);
+    if constexpr ((EPI & E_BIAS) != 0) {
+      if constexpr (LB) b4 = *(const __attribute__((address_space(3))) f4_t*)(lbias + (n - n0));
+      else b4 = *(const f4_t*)(g.bias + n);
+    }
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
       const int m = m0 + wm + 16 * j + (l & 15);
@@ -231,6 +246,7 @@ ASRX_DEV void epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, in
       }
     }
   }
+  return 0;
 }
 
 // Epilogue sets instantiated per layout; anything else runs the generic epilogue.
@@ -256,6 +272,42 @@ ASRX_DEV void wait_stages(int ahead) {
   } else {
     wait_vmcnt<0>();
   }
+}
+
+// s_waitcnt vmcnt(n) for a runtime, wave-uniform n (binary search over the immediates; n > 63 waits for 63)
+template <int LO, int HI>
+ASRX_DEV void wait_vmcnt_bs(int n) {
+  if constexpr (LO == HI) {
+    wait_vmcnt<LO>();
+  } else {
+    constexpr int MID = (LO + HI) / 2;
+    if (n <= MID) wait_vmcnt_bs<LO, MID>(n);
+    else wait_vmcnt_bs<MID + 1, HI>(n);
+  }
+}
+ASRX_DEV void wait_vmcnt_rt(int n) { wait_vmcnt_bs<0, 63>(n < 63 ? n : 63); }
+
+// One 16-byte-per-lane LDS-DMA wave-instruction (buffer_load_dwordx4 ... lds) written as inline asm, so the
+// compiler does not see an LDS write in flight: it then inserts no conservative vmcnt(0) in front of the
+// kernel's LDS fragment reads (it did in some epilogue instantiations), and the kernel's own counted vmcnt
+// waits + barriers order the DMA against its readers.  dst: LDS byte address (wave-uniform, M0); the
+// descriptor words are wave-uniform (SGPRs); voff: per-lane byte offset.
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+ASRX_DEV v4i_t make_srd(const void* base, int64_t num_bytes) {
+  const uint64_t a = (uint64_t)base;
+  const int n = (int)(num_bytes > 0x7fffffff ? 0x7fffffff : (num_bytes < 0 ? 0 : num_bytes));
+  v4i_t r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  r[1] = __builtin_amdgcn_readfirstlane((int)((a >> 32) & 0xffff));
+  r[2] = __builtin_amdgcn_readfirstlane(n);
+  r[3] = 0x00020000;
+  return r;
+}
+ASRX_DEV void dma16_asm(const void* lds_dst, v4i_t srd, uint32_t voff) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)lds_dst);
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0), "v"(voff), "s"(srd)
+               : "memory", "m0");
 }
 
 // one problem of a grouped launch (layout-identical to asrx_gemm_group_dev of the C-ABI)

@@ -91,19 +91,6 @@ ASRX_DEV s8_t p5_frag(const unsigned char* img, int i0) {
   }
 }
 
-// s_waitcnt vmcnt(n) for a runtime, wave-uniform n (binary search over the immediates; n > 63 waits for 63)
-template <int LO, int HI>
-ASRX_DEV void wait_vmcnt_bs(int n) {
-  if constexpr (LO == HI) {
-    wait_vmcnt<LO>();
-  } else {
-    constexpr int MID = (LO + HI) / 2;
-    if (n <= MID) wait_vmcnt_bs<LO, MID>(n);
-    else wait_vmcnt_bs<MID + 1, HI>(n);
-  }
-}
-ASRX_DEV void wait_vmcnt_rt(int n) { wait_vmcnt_bs<0, 63>(n < 63 ? n : 63); }
-
 // Store-only epilogues whose VMEM instruction count is exact: every (i, j) fragment issues ONE buffer store
 // (rows past M fall outside the descriptor's record count and are dropped by the hardware; the host
 // guarantees N % 256 == 0, so no column overflows).  The ring's waits then count these stores exactly and do

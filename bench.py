@@ -8,8 +8,11 @@ bf16, dropout 0.1, fused AdamW), data-parallel over N GPUs (weak scaling: 64 utt
 
 Prints ONE JSON line (rank 0). `value` = all ranks' frames / max-over-ranks wall time of the K timed steps.
 `roofline` = the dominant GEMM kernel instantiation (largest total time in the last warmup step, named as
-rocprofv3 names it), timed live with HIP events on its launch stream over the timed steps; `cpu_baseline` = the oracle (fp32 eager PyTorch
-restatement of the reference) train step on the host cores, bounded sample, rank 0 at N=1 only.
+rocprofv3 names it), timed live with HIP events on its launch stream over the timed steps; `sub_rooflines` = the
+north_star's per-kernel figures (attention projection GEMM and fused attention: MFMA fraction; LayerNorm and the
+unfused softmax: HBM fraction) at the workload's encoder shapes, after the timed region; `cpu_baseline` = the
+oracle (fp32 eager PyTorch restatement of the reference) train step on the host cores, bounded sample, rank 0 at
+N=1 only.
 """
 import argparse
 import json
@@ -39,6 +42,7 @@ def parse():
     ap.add_argument("--cpu-batch", type=int, default=4)
     ap.add_argument("--cpu-steps", type=int, default=10)
     ap.add_argument("--no-probe", action="store_true")
+    ap.add_argument("--no-sub", action="store_true", help="skip the per-kernel sub-rooflines")
     return ap.parse_args()
 
 
@@ -72,6 +76,88 @@ def pmc_traffic(kernel, config):
     except (OSError, ValueError, KeyError):
         return None
     return None if rec is None else rec["hbm_bytes_per_launch"]
+
+
+def _graph_time_ms(fn, launches=20, rounds=5):
+    """GPU time of one fn() call: `launches` calls captured in a HIP graph, replayed between HIP events on the
+    capturing stream (no host launch gaps inside the timed region); median over rounds."""
+    fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(launches):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(rounds):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        g.replay()
+        e.record()
+        e.synchronize()
+        ts.append(s.elapsed_time(e) / launches)
+    return sorted(ts)[len(ts) // 2]
+
+
+def sub_rooflines(B, T2, d, H, ff, p_drop):
+    """The north_star's per-kernel sub-rooflines at the workload's encoder shapes (rows = B*T'): MFMA
+    utilisation of the attention projection GEMM and the fused attention forward, HBM fraction of LayerNorm
+    fwd/bwd and of the (unfused-path) masked softmax.  Algorithmic bytes: every operand read once, every
+    output written once."""
+    from asrx import kernels as K
+    from asrx.kernels import MaskSpec
+    rows, dh = B * T2, d // H
+    gen = torch.Generator(device="cuda").manual_seed(7)
+    out = {}
+
+    def mfma(name, flops, fn, note):
+        t = _graph_time_ms(fn)
+        tf = flops / (t * 1e-3) / 1e12
+        out[name] = {"bound": "mfma", "achieved": round(tf, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(tf / PEAK_BF16_TFLOPS, 4), "us": round(t * 1e3, 2), "shape": note}
+
+    def hbm(name, nbytes, fn, note):
+        t = _graph_time_ms(fn)
+        gbs = nbytes / (t * 1e-3) / 1e9
+        out[name] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": round(gbs / PEAK_HBM_GBS, 4), "us": round(t * 1e3, 2), "shape": note}
+
+    x = (torch.randn(rows, d, device="cuda", generator=gen) * 0.5).bfloat16()
+    wqkv = (torch.randn(3 * d, d, device="cuda", generator=gen) * 0.05).bfloat16()
+    bqkv = torch.randn(3 * d, device="cuda", generator=gen) * 0.1
+    qkv = torch.empty(rows, 3 * d, device="cuda", dtype=torch.bfloat16)
+    mfma("qkv_projection_gemm", 2.0 * rows * 3 * d * d, lambda: K.linear(x, wqkv, qkv, bias=bqkv),
+         f"[{rows}x{d}] x [{d}x{3 * d}] + bias, bf16 out")
+    o = torch.empty(rows, d, device="cuda", dtype=torch.bfloat16)
+    st = ((3 * d, T2 * 3 * d),) * 3 + ((d, T2 * d),)
+    dm = K.dropmask_buffer(B, H, T2, T2, dh, p_drop, x.device)
+    mfma("attention_fwd", 4.0 * B * H * T2 * T2 * dh,
+         lambda: K.attention_fwd(qkv, qkv[:, d:], qkv[:, 2 * d:], o, B, H, T2, T2, dh, st, d ** -0.5,
+                                 MaskSpec(), p_drop, 11, dropmask=dm),
+         f"B*H={B * H} Lq=Lk={T2} dh={dh}, dropout {p_drop} (incl. the keep-bit generation kernel)")
+    xr = torch.randn(rows, d, device="cuda", generator=gen)
+    gam = torch.rand(d, device="cuda", generator=gen) + 0.5
+    bet = torch.randn(d, device="cuda", generator=gen)
+    y = torch.empty(rows, d, device="cuda", dtype=torch.bfloat16)
+    mean, rstd = K.layernorm_fwd(xr, gam, bet, y)
+    hbm("layernorm_fwd", rows * d * (4 + 2) + rows * 8, lambda: K.layernorm_fwd(xr, gam, bet, y),
+        f"[{rows}x{d}] fp32 in, bf16 out, fp32 mean/rstd")
+    dy = torch.randn(rows, d, device="cuda", generator=gen).bfloat16()
+    dres = torch.randn(rows, d, device="cuda", generator=gen)
+    dxd = torch.empty(rows, d, device="cuda", dtype=torch.bfloat16)
+    dgb = torch.zeros(2 * d, device="cuda")
+    hbm("layernorm_bwd", rows * d * (4 + 2 + 4 + 4 + 2) + rows * 8,
+        lambda: K.layernorm_bwd(xr, dy, gam, mean, rstd, dgb, dres=dres, dx_drop=dxd, dropout_p=p_drop, seed=5,
+                                defer=[]),
+        f"[{rows}x{d}]: x fp32, dy bf16, dres fp32 in; dx fp32, dropout(dx) bf16 out")
+    nbh, ld = B * H, (T2 + 7) // 8 * 8
+    sc = torch.randn(nbh, T2, ld, device="cuda", generator=gen).bfloat16()
+    pr = torch.empty_like(sc)
+    hbm("softmax_fwd", 2 * nbh * T2 * T2 * 2, lambda: K.softmax_fwd(sc, pr, None, nbh, H, T2, T2, ld, d ** -0.5,
+                                                                    MaskSpec()),
+        f"unfused path (attention=\"unfused\"): {nbh}x{T2}x{T2} bf16 scores -> probabilities")
+    return out
 
 
 def main():
@@ -153,6 +239,9 @@ def main():
            "frames_per_sec_per_gpu": round(value / world, 1),
            "loss": round(float(loss), 4),
            "roofline": roof}
+    if rank == 0 and not args.no_sub:
+        out["sub_rooflines"] = sub_rooflines(B, asrx.subsampled(T), cfg.d_model, cfg.n_heads, cfg.ff_dim,
+                                             cfg.dropout)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, T, L, args.cpu_batch, args.cpu_steps)
     if rank == 0:

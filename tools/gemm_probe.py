@@ -50,15 +50,19 @@ def main():
             a = (torch.rand(M, Kd, device="cuda", generator=g) * 2 - 1).bfloat16()
         if kind == "wgrad":
             pass
-        elif kind == "fwd":
+        elif kind in ("fwd", "fwdb"):
             w = (torch.rand(N, Kd, device="cuda", generator=g) * 2 - 1).bfloat16()
         else:
             w = (torch.rand(Kd, N, device="cuda", generator=g) * 2 - 1).bfloat16()
         if kind != "wgrad":
             y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
 
+        bias = torch.randn(N, device="cuda", generator=g) if kind == "fwdb" else None
+
         def run():
-            if kind == "wgrad":
+            if kind == "fwdb":
+                K.linear(a, w, y, bias=bias)
+            elif kind == "wgrad":
                 K.gemm(a, w, y, M, N, Kd, lda=M, ldb=N, ldc=N, a_trans=True, b_trans=True, beta=1.0, splitk=1)
             elif kind == "fwd":
                 K.linear(a, w, y)
