@@ -192,8 +192,9 @@ def linear_wgrad(dy, x, wgrad, *, beta=1.0, bias_grad=None, **kw):
 
 GROUPED_KERNEL = "gemm_bf16_grouped_kernel<true, true>"
 GROUPED_TABLE_KERNEL = "gemm_bf16_grouped_dev_kernel<true, true>"
-GROUPED_P5_KERNEL = "gemm_bf16_p5g_kernel<true, true, 96>"    # beta = 1 (accumulate into the fp32 grads)
-GROUPED_P5_KERNEL0 = "gemm_bf16_p5g_kernel<true, true, 64>"   # beta = 0
+# (beta != 1, beta == 1) instantiations (96 = E_BETA | E_F32: accumulate into the fp32 grads)
+GROUPED_KERNELS = {"p3": ("gemm_bf16_p3g_kernel<64>", "gemm_bf16_p3g_kernel<96>"),
+                   "p5": ("gemm_bf16_p5g_kernel<true, true, 64>", "gemm_bf16_p5g_kernel<true, true, 96>")}
 
 
 def wgrad_groupable(dy, x, wgrad):
@@ -204,15 +205,16 @@ def wgrad_groupable(dy, x, wgrad):
             and x.data_ptr() % 16 == 0 and dy.shape[0] <= 65536)
 
 
-# Weight-gradient tile: 256 = the p5 LDS-DMA ring kernel (256x256x32, gemm_p5.hip), 128 = register-staged
-# 128x128 tiles (gemm.hip).  ASRX_WGRAD_TILE overrides (A/B benchmarking).
-WGRAD_TILE = int(os.environ.get("ASRX_WGRAD_TILE", "128"))
+# Weight-gradient kernel: "p3" = the 256x128 LDS-DMA ring (gemm.hip p3_body, measured fastest), "p5" = the
+# 256x256x32 ring (gemm_p5.hip), "reg" = register-staged 128x128 tiles.  ASRX_WGRAD_KIND overrides (A/B).
+WGRAD_KIND = os.environ.get("ASRX_WGRAD_KIND", "p3")
 # 128-tile grouped launch with the XCD-aware tile layout (xcd_plan) instead of the tile order of the table
 WGRAD_XCD = os.environ.get("ASRX_WGRAD_XCD128", "1") == "1"
 
 
 def _grouped_p5_ok(items, beta):
-    return WGRAD_TILE == 256 and beta in (0.0, 1.0) and all(
+    """Can the LDS-DMA ring kernels (WGRAD_KIND p3 | p5) take these weight gradients?"""
+    return WGRAD_KIND in ("p3", "p5") and beta in (0.0, 1.0) and all(
         x.shape[1] % 4 == 0 and wgrad.stride(0) % 4 == 0 and wgrad.data_ptr() % 16 == 0
         for (_, x, wgrad, _) in items)
 
@@ -229,7 +231,8 @@ def xcd_plan(shapes, tile=256, nxcd=8):
     key = (tuple(shapes), tile, nxcd)
     if key in _XCD_PLANS:
         return _XCD_PLANS[key]
-    nts = [((m + tile - 1) // tile) * ((n + tile - 1) // tile) for (m, n, k) in shapes]
+    tm, tn = tile if isinstance(tile, tuple) else (tile, tile)
+    nts = [((m + tm - 1) // tm) * ((n + tn - 1) // tn) for (m, n, k) in shapes]
     order = sorted(range(len(shapes)), key=lambda i: (-shapes[i][2], -nts[i], i))
     load = [0] * nxcd
     per_xcd = [[] for _ in range(nxcd)]
@@ -253,15 +256,19 @@ def xcd_plan(shapes, tile=256, nxcd=8):
     return plan
 
 
-def _grouped_xcd(items, common, tile=256):
+_TILE_CODE = {"p3": ((256, 128), 3), "p5": ((256, 256), 256), "reg": ((128, 128), 128)}
+
+
+def _grouped_xcd(items, common, kind="p3"):
     """Grouped weight gradients with an XCD-aware workgroup -> tile map (asrx_gemm_grouped_xcd): 64-B group
     entries, tile -> group map and block -> tile map in one pinned host buffer, copied to the device on the
     stream."""
     import numpy as np
     shapes = [(dy.shape[1], x.shape[1], dy.shape[0]) for (dy, x, _, _) in items]
+    tile, code = _TILE_CODE[kind]
     group_order, nts, block_tile = xcd_plan(shapes, tile=tile,
                                             nxcd=8 if os.environ.get("ASRX_WGRAD_XCD", "1") != "0" else 1)
-    common.tile = tile
+    common.tile = code
     cvec = 1
     ents = np.zeros((len(items), 8), dtype=np.int64)
     ints = ents.view(np.int32)
@@ -340,7 +347,7 @@ def linear_wgrad_grouped(items, *, beta=1.0):
     common.alpha, common.beta = 1.0, beta
     p5 = _grouped_p5_ok(items, beta)
     if p5 or WGRAD_XCD or len(items) > MAX_GROUPS:
-        kname = (GROUPED_P5_KERNEL if beta == 1.0 else GROUPED_P5_KERNEL0) if p5 else GROUPED_TABLE_KERNEL
+        kname = GROUPED_KERNELS[WGRAD_KIND][beta == 1.0] if p5 else GROUPED_TABLE_KERNEL
         probe = PROBE
         timed = probe is not None and probe.record(kname)
         if probe is not None and probe.active and probe.log is not None:
@@ -350,9 +357,9 @@ def linear_wgrad_grouped(items, *, beta=1.0):
             s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s0.record()
         if p5:
-            flops, _ = _grouped_xcd(items, common, 256)
+            flops, _ = _grouped_xcd(items, common, WGRAD_KIND)
         elif WGRAD_XCD:
-            flops, _ = _grouped_xcd(items, common, 128)
+            flops, _ = _grouped_xcd(items, common, "reg")
         else:
             flops, _ = _grouped_table(items, common)
         if timed:

@@ -540,15 +540,13 @@ ASRX_DEV s8_t p_frag(const unsigned char* img, int i0, int ks) {
 // (An XCD-owned ROW order — row-block tm served by the workgroups with b % 8 == tm % 8 — was measured 10-50%
 // slower on every c3 shape; the XCD-contiguous TILE ranges of gemm_bf16_p3_kernel's `xcd` mode are 1-7% faster.)
 
+// The p3 main loop over a workgroup's tile sequence tl (the ring runs across tile boundaries).
+// lds: 3 ring stages + P_BIAS_BYTES (the bias vector of bias epilogues, N <= 4096: it is loaded once before the
+// ring starts, so the epilogues issue no global load, which would wait for every LDS-DMA stage in flight).
 template <bool AT, bool BT, int EPI>
-__global__ __launch_bounds__(512) void gemm_bf16_p3_kernel(GemmArgs g, int ntiles, int xcd) {
-  // 3 ring stages + 16 KiB holding the whole bias vector (N <= 4096, bias epilogues): it is loaded once before
-  // the ring starts, so the epilogues issue no global load (which would wait for every LDS-DMA stage in flight)
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[3 * P_STAGE + P_BIAS_BYTES];
+ASRX_DEV void p3_body(const GemmArgs& g, const TileSeq tl, int split, int z, unsigned char* lds) {
   constexpr int TM = 4, TN = 4;
   const int ntn = (g.N + P_BN - 1) / P_BN;
-  const int split = blockIdx.y;
-  const int z = blockIdx.z;
   const int zo = z / g.batch_inner, zi = z % g.batch_inner;
   const bf16_t* A = (const bf16_t*)g.a + zo * g.sa_o + zi * g.sa_i;
   const bf16_t* B = (const bf16_t*)g.b + zo * g.sb_o + zi * g.sb_i;
@@ -557,20 +555,11 @@ __global__ __launch_bounds__(512) void gemm_bf16_p3_kernel(GemmArgs g, int ntile
   const int64_t b_bytes = BT ? ((int64_t)(g.K - 1) * g.ldb + g.N) * 2 : ((int64_t)(g.N - 1) * g.ldb + g.K) * 2;
   const int kbeg = split * g.k_per_split;
   const int kend = min(g.K, kbeg + g.k_per_split);
-  const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
-  const int G = gridDim.x;
-  const int b0 = blockIdx.x;
-  if (b0 >= ntiles || nk == 0) return;
-  // tile order: round-robin (tile = b0 + v*G) or XCD-contiguous (workgroup b runs on XCD b % 8; XCD x owns the
-  // contiguous tile range [x*per, (x+1)*per) and its G/8 workgroups sweep it together, so the column tiles of a
-  // row panel are computed on one XCD at about the same time and share its L2)
-  const int xcdm = xcd && (G % 8) == 0;
-  const int G8 = G / 8, xg = b0 % 8, jg = b0 / 8;
-  const int per8 = (ntiles + 7) / 8;
-  const int lo8 = xg * per8, hi8 = min(ntiles, lo8 + per8);
-  const int ntl = xcdm ? (hi8 - lo8 > jg ? (hi8 - lo8 - jg + G8 - 1) / G8 : 0) : (ntiles - b0 + G - 1) / G;
-  if (ntl == 0) return;
-#define P3_TILE(v) (xcdm ? lo8 + jg + (v) * G8 : b0 + (v) * G)
+  // ragged K (K % 64 != 0) only with k-strided operands (grouped weight gradients): rows past K read as zero
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  if (nk == 0 || tl.count == 0) return;
+#define P3_TILE(v) tl(v)
+  const int ntl = tl.count;
   const int total = ntl * nk;
   const int wave = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
@@ -697,6 +686,49 @@ __global__ __launch_bounds__(512) void gemm_bf16_p3_kernel(GemmArgs g, int ntile
 }
 
 template <bool AT, bool BT, int EPI>
+__global__ __launch_bounds__(512) void gemm_bf16_p3_kernel(GemmArgs g, int ntiles, int xcd) {
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[3 * P_STAGE + P_BIAS_BYTES];
+  const int G = gridDim.x, b0 = blockIdx.x;
+  if (b0 >= ntiles) return;
+  p3_body<AT, BT, EPI>(g, TileSeq::persistent(ntiles, xcd, b0, G), blockIdx.y, blockIdx.z, lds);
+}
+
+// Grouped weight gradients (dW (+)= dY^T X of every layer in one launch) on p3 tiles: one 256x128 tile per
+// workgroup, block -> tile through block_tile (XCD-aware host layout) and tile -> group through tile_group.
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_bf16_p3g_kernel(float alpha, float beta, int c_dtype,
+                                                            const GroupEnt* __restrict__ ents,
+                                                            const uint16_t* __restrict__ tile_group,
+                                                            const uint16_t* __restrict__ block_tile, int ntiles) {
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[3 * P_STAGE + P_BIAS_BYTES];
+  const int tid = block_tile ? (int)block_tile[blockIdx.x] : (int)blockIdx.x;
+  if (tid >= ntiles) return;
+  const int gi = __builtin_amdgcn_readfirstlane((int)tile_group[tid]);
+  const GroupEnt e = ents[gi];
+  GemmArgs g = {};
+  g.M = e.m; g.N = e.n; g.K = e.k;
+  g.a = e.a; g.lda = e.lda; g.b = e.b; g.ldb = e.ldb; g.c = e.c; g.ldc = e.ldc; g.c_dtype = c_dtype;
+  g.batch_inner = 1; g.alpha = alpha; g.beta = beta; g.rowadd_mod = 1;
+  g.splitk = 1; g.k_per_split = e.k; g.cvec = 1;
+  g.rowsum = e.rowsum;
+  p3_body<true, true, EPI>(g, TileSeq::single(tid - e.tile_start), 0, 0, lds);
+}
+
+int launch_p3_grouped(const asrx_gemm_desc* common, const GroupEnt* ents, const uint16_t* tile_group,
+                      const uint16_t* block_tile, int ntiles, int blocks, hipStream_t st) {
+  if (common->c_dtype != ASRX_F32 || common->alpha != 1.f) return -1;
+  if (common->beta == 1.f)
+    hipLaunchKernelGGL((gemm_bf16_p3g_kernel<E_BETA | E_F32>), dim3(blocks), dim3(P_THREADS), 0, st, common->alpha,
+                       common->beta, common->c_dtype, ents, tile_group, block_tile, ntiles);
+  else if (common->beta == 0.f)
+    hipLaunchKernelGGL((gemm_bf16_p3g_kernel<E_F32>), dim3(blocks), dim3(P_THREADS), 0, st, common->alpha,
+                       common->beta, common->c_dtype, ents, tile_group, block_tile, ntiles);
+  else
+    return -1;
+  return 0;
+}
+
+template <bool AT, bool BT, int EPI>
 void launch_p3(const GemmArgs& g, int ntiles, int splitk, int batch, hipStream_t st) {
   const int per = splitk * batch;
   const int gx = std::max(1, std::min(ntiles, std::max(1, 256 / per)));
@@ -757,13 +789,10 @@ struct RStage {
   ASRX_DEV void issue(unsigned char* img, const bf16_t* base, int64_t ld, int64_t total_bytes, int k0) const {
 #if defined(__HIP_DEVICE_COMPILE__)
     const int64_t koff = KSTRIDED ? (int64_t)k0 * ld * 2 : (int64_t)k0 * 2;
-    const int64_t rem = total_bytes - koff;
-    __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)((const char*)base + koff), (short)0, (int)(rem > 0x7fffffff ? 0x7fffffff : rem), 0x00020000);
+    const v4i_t srd = make_srd((const char*)base + koff, total_bytes - koff);   // inline-asm DMA: gemm_common.h
     const int w = threadIdx.x >> 6;
 #pragma unroll
-    for (int j = 0; j < NI; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_t*)(img + (j * 4 + w) * 1024), 16, voff[j], 0, 0, 0);
+    for (int j = 0; j < NI; ++j) dma16_asm(img + (j * 4 + w) * 1024, srd, voff[j]);
 #endif
   }
 };
@@ -1353,7 +1382,11 @@ extern "C" int asrx_gemm_grouped_xcd(const asrx_gemm_desc* common, const asrx_ge
   if (tiles == 0 || blocks == 0) return ASRX_OK;
   if (common->in_dtype != ASRX_BF16 || !common->a_trans || !common->b_trans) return ASRX_ERR_UNSUPPORTED;
   if (common->c_dtype != ASRX_BF16 && common->c_dtype != ASRX_F32) return ASRX_ERR_ARG;
-  if (common->tile == 128) {   // register-staged 128x128 tiles (gemm_bf16_tile): any alignment-checked table
+  if (common->tile == 3) {     // p3 LDS-DMA ring tiles, 256x128 (fp32 C, 16-B rows, n % 4 == 0, alpha 1, beta 0|1)
+    if (launch_p3_grouped(common, (const GroupEnt*)groups, tile_group, block_tile, tiles, blocks,
+                          (hipStream_t)stream) != 0)
+      return ASRX_ERR_UNSUPPORTED;
+  } else if (common->tile == 128) {   // register-staged 128x128 tiles (gemm_bf16_tile): any alignment-checked table
     hipLaunchKernelGGL((gemm_bf16_grouped_dev_kernel<true, true>), dim3(blocks), dim3(256), 0, (hipStream_t)stream,
                        common->alpha, common->beta, common->c_dtype, common->relu ? 1 : 0, (const GroupEnt*)groups,
                        tile_group, (int)tiles, 0, block_tile);

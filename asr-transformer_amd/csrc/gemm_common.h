@@ -310,6 +310,26 @@ ASRX_DEV void dma16_asm(const void* lds_dst, v4i_t srd, uint32_t voff) {
                : "memory", "m0");
 }
 
+// Tile sequence of one persistent workgroup: tile(v) for v < count.  XCD-contiguous (workgroup b runs on XCD
+// b % 8, which owns a contiguous tile range swept by its G/8 workgroups together, so the column tiles of a row
+// panel share one L2) or round-robin; single(t): a grouped launch's one tile per workgroup.
+struct TileSeq {
+  int xcdm, lo8, jg, G8, b0, G, count;
+  ASRX_DEV int operator()(int v) const { return xcdm ? lo8 + jg + v * G8 : b0 + v * G; }
+  ASRX_DEV static TileSeq single(int t) { return TileSeq{0, 0, 0, 0, t, 1, 1}; }
+  ASRX_DEV static TileSeq persistent(int ntiles, int xcd, int b0, int G) {
+    TileSeq tl;
+    tl.xcdm = xcd && (G % 8) == 0;
+    tl.G8 = G / 8; tl.jg = b0 / 8; tl.b0 = b0; tl.G = G;
+    const int per8 = (ntiles + 7) / 8;
+    tl.lo8 = (b0 % 8) * per8;
+    const int hi8 = min(ntiles, tl.lo8 + per8);
+    tl.count = tl.xcdm ? (hi8 - tl.lo8 > tl.jg ? (hi8 - tl.lo8 - tl.jg + tl.G8 - 1) / tl.G8 : 0)
+                       : (ntiles - b0 + G - 1) / G;
+    return tl;
+  }
+};
+
 // one problem of a grouped launch (layout-identical to asrx_gemm_group_dev of the C-ABI)
 struct GroupEnt {
   const void* a; const void* b; void* c; float* rowsum;

@@ -62,13 +62,10 @@ struct P5Stage {
   ASRX_DEV void issue(unsigned char* img, const bf16_t* base, int64_t ld, int64_t total_bytes, int k0) const {
 #if defined(__HIP_DEVICE_COMPILE__)
     const int64_t koff = KSTRIDED ? (int64_t)k0 * ld * 2 : (int64_t)k0 * 2;
-    const int64_t rem = total_bytes - koff;
-    __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)((const char*)base + koff), (short)0, (int)(rem > 0x7fffffff ? 0x7fffffff : rem), 0x00020000);
+    const v4i_t srd = make_srd((const char*)base + koff, total_bytes - koff);   // inline-asm DMA: gemm_common.h
     const int w = threadIdx.x >> 6;
 #pragma unroll
-    for (int j = 0; j < NI; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_t*)(img + (j * 8 + w) * 1024), 16, voff[j], 0, 0, 0);
+    for (int j = 0; j < NI; ++j) dma16_asm(img + (j * 8 + w) * 1024, srd, voff[j]);
 #endif
   }
 };
@@ -182,17 +179,9 @@ ASRX_DEV int p5_finish_tile(const GemmArgs& g, int split, int z, int m0, int n0,
   return issued;
 }
 
-// Tile sequence of one workgroup: tile(v) for v < count.  XCD-contiguous (workgroup b runs on XCD b % 8, which
-// owns a contiguous tile range swept by its G/8 workgroups together, so the column tiles of a row panel share
-// one L2) or round-robin; a grouped launch gives each workgroup one tile (count 1, base = its tile).
-struct P5Tiles {
-  int xcdm, lo8, jg, G8, b0, G, count;
-  ASRX_DEV int operator()(int v) const { return xcdm ? lo8 + jg + v * G8 : b0 + v * G; }
-};
-
 // The p5 main loop over a workgroup's tiles (ring runs across tile boundaries).  lds: NS stages.
 template <int BM, bool AT, bool BT, int EPI>
-ASRX_DEV void p5_body(const GemmArgs& g, const P5Tiles tl, int split, int z, unsigned char* lds) {
+ASRX_DEV void p5_body(const GemmArgs& g, const TileSeq tl, int split, int z, unsigned char* lds) {
   using C = P5Cfg<BM>;
   constexpr int NS = C::NS, P = C::P;
   constexpr int TM = BM / 32, TN = 4;   // 16x16 fragments per wave: (BM/2)/16 rows x 64/16 cols
@@ -312,14 +301,7 @@ __global__ __launch_bounds__(P5_THREADS) void gemm_bf16_p5_kernel(GemmArgs g, in
   __shared__ __attribute__((aligned(1024))) unsigned char lds[P5Cfg<BM>::NS * P5Cfg<BM>::STAGE];
   const int G = gridDim.x, b0 = blockIdx.x;
   if (b0 >= ntiles) return;
-  P5Tiles tl;
-  tl.xcdm = xcd && (G % 8) == 0;
-  tl.G8 = G / 8; tl.jg = b0 / 8; tl.b0 = b0; tl.G = G;
-  const int per8 = (ntiles + 7) / 8, xg = b0 % 8;
-  tl.lo8 = xg * per8;
-  const int hi8 = min(ntiles, tl.lo8 + per8);
-  tl.count = tl.xcdm ? (hi8 - tl.lo8 > tl.jg ? (hi8 - tl.lo8 - tl.jg + tl.G8 - 1) / tl.G8 : 0)
-                     : (ntiles - b0 + G - 1) / G;
+  const TileSeq tl = TileSeq::persistent(ntiles, xcd, b0, G);
   p5_body<BM, AT, BT, EPI>(g, tl, blockIdx.y, blockIdx.z, lds);
 }
 
@@ -343,7 +325,7 @@ __global__ __launch_bounds__(P5_THREADS) void gemm_bf16_p5g_kernel(float alpha, 
   g.splitk = 1; g.k_per_split = e.k; g.cvec = 1;
   g.rowsum = e.rowsum;
   g.dbg = dbg;
-  P5Tiles tl = {0, 0, 0, 0, tid - e.tile_start, 1, 1};
+  const TileSeq tl = TileSeq::single(tid - e.tile_start);
   p5_body<256, AT, BT, EPI>(g, tl, 0, 0, lds);
 }
 

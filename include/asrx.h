@@ -100,9 +100,10 @@ int asrx_gemm_grouped_table(const asrx_gemm_desc* common, const asrx_gemm_group_
 /* Same with an explicit workgroup -> tile map: block_tile[b] (device, `blocks` entries, 0xFFFF = idle) names
  * the tile workgroup b computes.  Workgroup b runs on XCD b % 8, so a host that lays the tiles of one group on
  * one XCD at the same time lets them share that XCD's L2 (the operand panels of dW = dY^T X are re-read by
- * every tile of the group).  common->tile selects the tile: 128 = register-staged 128x128 tiles (the
- * asrx_gemm_grouped_table kernel; common->relu carries its cvec flag), 256 = the 256x256 LDS-DMA ring
- * (gemm_p5.hip; fp32 C with 16-byte aligned rows, every group's n % 4 == 0, alpha 1, beta 0 or 1).
+ * every tile of the group).  common->tile selects the tile: 3 = the p3 LDS-DMA ring, 256x128 tiles (m x n;
+ * fp32 C with 16-byte aligned rows, every group's n % 4 == 0, alpha 1, beta 0 or 1), 128 = register-staged
+ * 128x128 tiles (the asrx_gemm_grouped_table kernel; common->relu carries its cvec flag), 256 = the 256x256
+ * LDS-DMA ring (gemm_p5.hip; same requirements as 3).
  * Replaces the weight/bias-gradient mm + sum of autograd for every nn.Linear (layers.py:10-12,36,48,51). */
 int asrx_gemm_grouped_xcd(const asrx_gemm_desc* common, const asrx_gemm_group_dev* groups,
                           const uint16_t* tile_group, const uint16_t* block_tile, int32_t count, int32_t tiles,

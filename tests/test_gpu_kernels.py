@@ -136,15 +136,15 @@ def test_gemm_fused_rowsum(tile, splitk, kernel_variant):
     assert relerr(bg.cpu(), 2 + dy.double().sum(0)) < 1e-5
 
 
-@pytest.mark.parametrize("wtile,xcd", [(128, False), (128, True), (256, True)])
+@pytest.mark.parametrize("wkind,xcd", [("reg", False), ("reg", True), ("p5", True), ("p3", True)])
 @pytest.mark.parametrize("ngroups", [1, 7, 60])
-def test_gemm_grouped_wgrad(ngroups, wtile, xcd, monkeypatch):
+def test_gemm_grouped_wgrad(ngroups, wkind, xcd, monkeypatch):
     """Grouped weight gradients (asrx_gemm_grouped): ragged shapes, K not a multiple of 64, fused bias-grad row
     sums, beta=1 accumulation into existing fp32 grads; > MAX_GROUPS problems split over several launches."""
     g = torch.Generator(device=dev).manual_seed(ngroups)
     shapes = [(1000, 136, 96), (4096, 512, 512), (333, 248, 64), (64, 8, 576), (2500, 1536, 512),
               (77, 40, 1216), (249, 200, 24)]
-    monkeypatch.setattr(K(), "WGRAD_TILE", wtile)
+    monkeypatch.setattr(K(), "WGRAD_KIND", wkind)
     monkeypatch.setattr(K(), "WGRAD_XCD", xcd)
     items, refs = [], []
     for i in range(ngroups):
