@@ -602,22 +602,33 @@ ASRX_DEV void p3_body(const GemmArgs& g, const TileSeq tl, int split, int z, uns
   }
   P3_ISSUE_NEXT();
   if (total > 1) P3_ISSUE_NEXT();
-  // younger-operation ledger: stage s was issued in step s - 2; younger than it are the epilogue stores of steps
-  // s - 2 and s - 1 (e2, e1: the exact store counts epilogue_tile reports, else 0) and stage s + 1 (6 pieces,
-  // 7 with a bias DMA: 6 is a lower bound).  A lower bound only over-waits.
-  int e1 = 0, e2 = 0;
+  // Epilogues that read memory (gate / residual / row-add: PRE) load those operands right after the barrier of
+  // the tile's last K-step and issue that step's stage only AFTER the epilogue, so the epilogue's wait for its
+  // loads (in-order vmcnt) covers only the stage already needed next, not a freshly issued one.
+  constexpr bool PRE = EpiPre<EPI, TN, TM>::ANY;
+  // younger-operation ledger (lower bounds; an under-count only over-waits): stage s was issued in step s - 2.
+  // Younger than it: the stores of step s - 2's epilogue if issued after that step's stage (ea2), stage s + 1
+  // (P_INST pieces), and the stores of step s - 1's epilogue (eb1 before / ea1 after its stage issue).
+  int ea1 = 0, ea2 = 0, eb1 = 0;
   int vc = 0, kk = 0, cb = 0;   // compute cursor
   for (int s = 0; s < total; ++s) {
-    wait_vmcnt_rt(e2 + (s + 1 < total ? P_INST : 0) + e1);
+    wait_vmcnt_rt(ea2 + (s + 1 < total ? P_INST : 0) + eb1 + ea1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    e2 = e1;
-    e1 = 0;
-    if (s + 2 < total) P3_ISSUE_NEXT();
+    ea2 = ea1;
+    ea1 = 0;
+    eb1 = 0;
+    const bool last = kk == nk - 1;
+    const bool defer = PRE && last && g.splitk == 1 && g.dbg != 1;
+    if (!defer && s + 2 < total) P3_ISSUE_NEXT();
     const unsigned char* la = lds + cb * P_STAGE;
     const unsigned char* lb = la + PA_BYTES;
     const int t = P3_TILE(vc);
     const bool do_rs = AT && g.rowsum != nullptr && (t % ntn) == 0 && wn == 0;
+    EpiPre<EPI, TN, TM> pre;
+    if constexpr (PRE) {
+      if (defer) epi_prefetch<EPI, TN, TM>(pre, g, (t / ntn) * P_BM, (t % ntn) * P_BN, wm, wn);
+    }
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
       s8_t fa[TM], fb[TN];
@@ -670,8 +681,12 @@ ASRX_DEV void p3_body(const GemmArgs& g, const TileSeq tl, int split, int z, uns
           keep_live(acc);
         } else {
           const int full = m0 + P_BM <= g.M && n0 + P_BN <= g.N;
-          e1 = epilogue_tile<EPI, TN, TM, use_lb>(g, z, m0, n0, wm, wn, acc, (lds_cfloat_t*)(lds + 3 * P_STAGE) + n0,
-                                                  full);
+          lds_cfloat_t* lbias = (lds_cfloat_t*)(lds + 3 * P_STAGE) + n0;
+          if (defer) {
+            eb1 = epilogue_tile<EPI, TN, TM, use_lb, PRE>(g, z, m0, n0, wm, wn, acc, lbias, full, &pre);
+          } else {
+            ea1 = epilogue_tile<EPI, TN, TM, use_lb>(g, z, m0, n0, wm, wn, acc, lbias, full);
+          }
         }
       }
 #pragma unroll
@@ -679,6 +694,7 @@ ASRX_DEV void p3_body(const GemmArgs& g, const TileSeq tl, int split, int z, uns
 #pragma unroll
         for (int j = 0; j < TM; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
     }
+    if (defer && s + 2 < total) P3_ISSUE_NEXT();
     if (++kk == nk) { kk = 0; ++vc; }
     cb = cb == 2 ? 0 : cb + 1;
   }

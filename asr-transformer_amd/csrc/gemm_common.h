@@ -131,11 +131,52 @@ enum : int {
 
 // The fused element-wise epilogue of the fast path for the 4 consecutive columns n..n+3 of row m (valid
 // m < M, n < N); gate/resid/rowadd are read here, C is not.
-template <int EPI>
-ASRX_DEV f4_t epi_vals(const GemmArgs& g, int m, int n, f4_t v, f4_t b4) {
+// Epilogue operands read from memory (gate / residual / row-add) for a whole wave tile, loaded ahead of the
+// tile's last K-step by a persistent kernel (epi_prefetch) so that their wait does not also wait for stages
+// issued after them.
+template <int EPI, int TN, int TM>
+struct EpiPre {
+  static constexpr bool G = (EPI & E_GATE) != 0, R = (EPI & (E_RESID | E_ROWADD)) != 0;
+  static constexpr bool ANY = (G || R) && EPI != E_GENERIC;
+  uint2 gt[G ? TN : 1][G ? TM : 1];
+  f4_t rr[R ? TN : 1][R ? TM : 1];
+};
+
+template <int EPI, int TN, int TM>
+ASRX_DEV void epi_prefetch(EpiPre<EPI, TN, TM>& p, const GemmArgs& g, int m0, int n0, int wm, int wn) {
+  const int l = threadIdx.x & 63, gq = l >> 4;
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int m = m0 + wm + 16 * j + (l & 15), n = n0 + wn + 16 * i + 4 * gq;
+      const bool ok = m < g.M && n < g.N;
+      if constexpr (EpiPre<EPI, TN, TM>::G) {
+        p.gt[i][j] = make_uint2(0u, 0u);
+        if (ok) p.gt[i][j] = *(const uint2*)((const bf16_t*)g.gate + (int64_t)m * g.ld_gate + n);
+      }
+      if constexpr (EpiPre<EPI, TN, TM>::R) {
+        p.rr[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+        if (ok) {
+          if constexpr ((EPI & E_RESID) != 0)
+            p.rr[i][j] = *(const f4_t*)((const float*)g.resid + (int64_t)m * g.ld_resid + n);
+          else
+            p.rr[i][j] = *(const f4_t*)(g.rowadd + (int64_t)(m % g.rowadd_mod) * g.ld_rowadd + n);
+        }
+      }
+    }
+}
+
+// pre_gt / pre_rr: the prefetched gate / residual-or-row-add values (PRE), else read here
+template <int EPI, bool PRE = false>
+ASRX_DEV f4_t epi_vals(const GemmArgs& g, int m, int n, f4_t v, f4_t b4, uint2 pre_gt = uint2{0u, 0u},
+                       f4_t pre_rr = f4_t{0.f, 0.f, 0.f, 0.f}) {
   if constexpr ((EPI & E_ALPHA) != 0) v *= g.alpha;
   if constexpr ((EPI & E_BIAS) != 0) v += b4;
-  if constexpr ((EPI & E_ROWADD) != 0) v += *(const f4_t*)(g.rowadd + (int64_t)(m % g.rowadd_mod) * g.ld_rowadd + n);
+  if constexpr ((EPI & E_ROWADD) != 0) {
+    if constexpr (PRE) v += pre_rr;
+    else v += *(const f4_t*)(g.rowadd + (int64_t)(m % g.rowadd_mod) * g.ld_rowadd + n);
+  }
   if constexpr ((EPI & E_RELU) != 0) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
@@ -149,13 +190,18 @@ ASRX_DEV f4_t epi_vals(const GemmArgs& g, int m, int n, f4_t v, f4_t b4) {
     v[3] = rng_half(h1, 1) >= g.drop_thr ? v[3] * g.drop_scale : 0.f;
   }
   if constexpr ((EPI & E_GATE) != 0) {
-    const uint2 gt = *(const uint2*)((const bf16_t*)g.gate + (int64_t)m * g.ld_gate + n);
+    uint2 gt;
+    if constexpr (PRE) gt = pre_gt;
+    else gt = *(const uint2*)((const bf16_t*)g.gate + (int64_t)m * g.ld_gate + n);
     if (!(bf2f(gt.x & 0xffff) > 0.f)) v[0] = 0.f;
     if (!(bf2f(gt.x >> 16) > 0.f)) v[1] = 0.f;
     if (!(bf2f(gt.y & 0xffff) > 0.f)) v[2] = 0.f;
     if (!(bf2f(gt.y >> 16) > 0.f)) v[3] = 0.f;
   }
-  if constexpr ((EPI & E_RESID) != 0) v += *(const f4_t*)((const float*)g.resid + (int64_t)m * g.ld_resid + n);
+  if constexpr ((EPI & E_RESID) != 0) {
+    if constexpr (PRE) v += pre_rr;
+    else v += *(const f4_t*)((const float*)g.resid + (int64_t)m * g.ld_resid + n);
+  }
   return v;
 }
 
@@ -165,9 +211,13 @@ typedef __attribute__((address_space(3))) const float lds_cfloat_t;
 // paired path; 0 elsewhere): a persistent kernel adds it to the count of operations younger than its next
 // stage, so it does not wait for these stores.  lbias (optional): the tile's bias columns [n0, n0 + BN) staged
 // in LDS (no global load in the epilogue: such a load would wait for every older LDS-DMA stage in flight).
-template <int EPI, int TN, int TM, bool LB = false>
+template <int EPI, int TN, int TM, bool LB = false, bool PRE = false>
 ASRX_DEV int epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int wn, f4_t (&acc)[TN][TM],
-                           lds_cfloat_t* lbias = nullptr, int full = 0) {
+                           lds_cfloat_t* lbias = nullptr, int full = 0,
+                           const EpiPre<EPI, TN, TM>* pre = nullptr) {
+  // (PRE requires EpiPre<EPI,TN,TM>::ANY; its members are indexed only where they exist)
+#define ASRX_PGT(i, j) (EpiPre<EPI, TN, TM>::G ? pre->gt[EpiPre<EPI, TN, TM>::G ? (i) : 0][EpiPre<EPI, TN, TM>::G ? (j) : 0] : uint2{0u, 0u})
+#define ASRX_PRR(i, j) (EpiPre<EPI, TN, TM>::R ? pre->rr[EpiPre<EPI, TN, TM>::R ? (i) : 0][EpiPre<EPI, TN, TM>::R ? (j) : 0] : f4_t{0.f, 0.f, 0.f, 0.f})
   const int l = threadIdx.x & 63, gq = l >> 4;
   if constexpr (EPI == E_GENERIC) {
 #pragma unroll
@@ -204,8 +254,13 @@ ASRX_DEV int epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int
           const int m = m0 + wm + 16 * j + (l & 15);
           f4_t va = acc[i][j], vb = acc[i + 1][j];
           if (m < g.M) {
-            if (na < g.N) va = epi_vals<EPI>(g, m, na, va, ba);
-            if (nb < g.N) vb = epi_vals<EPI>(g, m, nb, vb, bb);
+            if constexpr (PRE) {
+              if (na < g.N) va = epi_vals<EPI, true>(g, m, na, va, ba, ASRX_PGT(i, j), ASRX_PRR(i, j));
+              if (nb < g.N) vb = epi_vals<EPI, true>(g, m, nb, vb, bb, ASRX_PGT(i + 1, j), ASRX_PRR(i + 1, j));
+            } else {
+              if (na < g.N) va = epi_vals<EPI>(g, m, na, va, ba);
+              if (nb < g.N) vb = epi_vals<EPI>(g, m, nb, vb, bb);
+            }
           }
           const uint32_t ax = pack2bf(va[0], va[1]), ay = pack2bf(va[2], va[3]);
           const uint32_t bx = pack2bf(vb[0], vb[1]), by = pack2bf(vb[2], vb[3]);
@@ -233,7 +288,9 @@ ASRX_DEV int epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int
     for (int j = 0; j < TM; ++j) {
       const int m = m0 + wm + 16 * j + (l & 15);
       if (m >= g.M) continue;
-      f4_t v = epi_vals<EPI>(g, m, n, acc[i][j], b4);
+      f4_t v;
+      if constexpr (PRE) v = epi_vals<EPI, true>(g, m, n, acc[i][j], b4, ASRX_PGT(i, j), ASRX_PRR(i, j));
+      else v = epi_vals<EPI>(g, m, n, acc[i][j], b4);
       if constexpr ((EPI & E_F32) != 0) {
         f4_t* c = (f4_t*)((float*)g.c + (int64_t)m * g.ldc + n);
         if constexpr ((EPI & E_BETA) != 0) v += *c;
@@ -247,6 +304,8 @@ ASRX_DEV int epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int
     }
   }
   return 0;
+#undef ASRX_PGT
+#undef ASRX_PRR
 }
 
 // Epilogue sets instantiated per layout; anything else runs the generic epilogue.

@@ -50,18 +50,27 @@ def main():
             a = (torch.rand(M, Kd, device="cuda", generator=g) * 2 - 1).bfloat16()
         if kind == "wgrad":
             pass
-        elif kind in ("fwd", "fwdb"):
+        elif kind in ("fwd", "fwdb", "fwdr"):
             w = (torch.rand(N, Kd, device="cuda", generator=g) * 2 - 1).bfloat16()
         else:
             w = (torch.rand(Kd, N, device="cuda", generator=g) * 2 - 1).bfloat16()
         if kind != "wgrad":
             y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
 
-        bias = torch.randn(N, device="cuda", generator=g) if kind == "fwdb" else None
+        bias = torch.randn(N, device="cuda", generator=g) if kind in ("fwdb", "fwdr") else None
+        if kind == "fwdr":      # out-projection / FFN2 epilogue: bias, dropout, fp32 residual add, fp32 out
+            resid = torch.randn(M, N, device="cuda", generator=g)
+            yf = torch.empty(M, N, device="cuda")
+        if kind == "dgradg":    # FFN2 data gradient gated by the ReLU of the hidden activation
+            gate = torch.randn(M, N, device="cuda", generator=g).bfloat16()
 
         def run():
             if kind == "fwdb":
                 K.linear(a, w, y, bias=bias)
+            elif kind == "fwdr":
+                K.linear(a, w, yf, bias=bias, dropout_p=0.1, seed=3, resid=resid, ld_resid=N)
+            elif kind == "dgradg":
+                K.linear_dgrad(a, w, y, gate=gate, ld_gate=N)
             elif kind == "wgrad":
                 K.gemm(a, w, y, M, N, Kd, lda=M, ldb=N, ldc=N, a_trans=True, b_trans=True, beta=1.0, splitk=1)
             elif kind == "fwd":
