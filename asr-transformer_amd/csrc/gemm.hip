@@ -1152,7 +1152,8 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
     // auto (measured on the c3 shapes, tools/gemm_bench.py): the p3 ring wins every projection with K <= 4096
     // whose grid fills the chip; smaller grids (the decoder's 4096-row GEMMs) take the 4-stage ring kernel; the
     // register path wins the weight-gradient (A^T, reduction over B*T rows) and very long-K GEMMs.
-    else if (kvar == 0 && !d->a_trans && d->k <= 4096) {
+    // (with the inline-asm LDS-DMA, p3 also wins the long-K cross-attention K/V data gradient, K = 12 288)
+    else if (kvar == 0 && !d->a_trans) {
       if (nt_p3 * splitk * batch >= 192) pl.use = 1;
       // (64x64 tiles also win the long-K decoder GEMMs, K >= 1536: 4 x more workgroups to cover the latency)
       else pl.use = (nt_r128 * splitk * batch >= 192 && d->k < 1536) ? 6 : 5;

@@ -42,20 +42,21 @@ def main():
         kind, dims = spec.split(":")
         M, N, Kd = (int(x) for x in dims.split("x"))
         g = torch.Generator(device="cuda").manual_seed(0)
-        if kind == "wgrad":     # C[M,N] (+)= A^T B with A = dy [K][M], B = x [K][N] (reduction over K rows)
+        if kind in ("wgrad", "wgradp"):   # C[M,N] (+)= A^T B, A = dy [K][M], B = x [K][N]; wgradp: linear_wgrad plan
             a = (torch.rand(Kd, M, device="cuda", generator=g) * 2 - 1).bfloat16()
             w = (torch.rand(Kd, N, device="cuda", generator=g) * 2 - 1).bfloat16()
             y = torch.zeros(M, N, device="cuda")
         else:
             a = (torch.rand(M, Kd, device="cuda", generator=g) * 2 - 1).bfloat16()
-        if kind == "wgrad":
+        if kind in ("wgrad", "wgradp"):
             pass
         elif kind in ("fwd", "fwdb", "fwdr"):
             w = (torch.rand(N, Kd, device="cuda", generator=g) * 2 - 1).bfloat16()
         else:
             w = (torch.rand(Kd, N, device="cuda", generator=g) * 2 - 1).bfloat16()
-        if kind != "wgrad":
+        if kind not in ("wgrad", "wgradp"):
             y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        bg = torch.zeros(M, device="cuda")
 
         bias = torch.randn(N, device="cuda", generator=g) if kind in ("fwdb", "fwdr") else None
         if kind == "fwdr":      # out-projection / FFN2 epilogue: bias, dropout, fp32 residual add, fp32 out
@@ -71,6 +72,8 @@ def main():
                 K.linear(a, w, yf, bias=bias, dropout_p=0.1, seed=3, resid=resid, ld_resid=N)
             elif kind == "dgradg":
                 K.linear_dgrad(a, w, y, gate=gate, ld_gate=N)
+            elif kind == "wgradp":
+                K.linear_wgrad(a, w, y, bias_grad=bg)
             elif kind == "wgrad":
                 K.gemm(a, w, y, M, N, Kd, lda=M, ldb=N, ldc=N, a_trans=True, b_trans=True, beta=1.0, splitk=1)
             elif kind == "fwd":
