@@ -505,15 +505,22 @@ struct PStage {
     }
   }
   // base: operand start; total_bytes: one past its last valid byte; k0: first k of the stage
-  ASRX_DEV void issue(unsigned char* img, const bf16_t* base, int64_t ld, int64_t total_bytes, int k0) const {
-#if defined(__HIP_DEVICE_COMPILE__)  // the buffer-resource builtins do not exist in the host pass (which then
-                                     // silently dropped the kernel's host stubs)
+  ASRX_DEV v4i_t srd(const bf16_t* base, int64_t ld, int64_t total_bytes, int k0) const {
     const int64_t koff = KSTRIDED ? (int64_t)k0 * ld * 2 : (int64_t)k0 * 2;
-    const v4i_t srd = make_srd((const char*)base + koff, total_bytes - koff);
+    return make_srd((const char*)base + koff, total_bytes - koff);
+  }
+  // pieces [J0, J1) of this thread's NI LDS-DMA pieces
+  template <int J0, int J1>
+  ASRX_DEV void issue_part(unsigned char* img, v4i_t d) const {
+#if defined(__HIP_DEVICE_COMPILE__)  // keep device-only builtins out of the host pass (it then silently dropped
+                                     // the kernel's host stubs)
     const int w = threadIdx.x >> 6;
 #pragma unroll
-    for (int j = 0; j < NI; ++j) dma16_asm(img + (j * 8 + w) * 1024, srd, voff[j]);
+    for (int j = J0; j < J1; ++j) dma16_asm(img + (j * 8 + w) * 1024, d, voff[j]);
 #endif
+  }
+  ASRX_DEV void issue(unsigned char* img, const bf16_t* base, int64_t ld, int64_t total_bytes, int k0) const {
+    issue_part<0, NI>(img, srd(base, ld, total_bytes, k0));
   }
 };
 
@@ -606,6 +613,7 @@ ASRX_DEV void p3_body(const GemmArgs& g, const TileSeq tl, int split, int z, uns
   // the tile's last K-step and issue that step's stage only AFTER the epilogue, so the epilogue's wait for its
   // loads (in-order vmcnt) covers only the stage already needed next, not a freshly issued one.
   constexpr bool PRE = EpiPre<EPI, TN, TM>::ANY;
+  const bool sp_iss = !(g.dbg & 4);   // ASRX_GEMM_DBG=4: issue each stage in one block (A/B)
   // younger-operation ledger (lower bounds; an under-count only over-waits): stage s was issued in step s - 2.
   // Younger than it: the stores of step s - 2's epilogue if issued after that step's stage (ea2), stage s + 1
   // (P_INST pieces), and the stores of step s - 1's epilogue (eb1 before / ea1 after its stage issue).
@@ -620,7 +628,28 @@ ASRX_DEV void p3_body(const GemmArgs& g, const TileSeq tl, int split, int z, uns
     eb1 = 0;
     const bool last = kk == nk - 1;
     const bool defer = PRE && last && g.splitk == 1 && g.dbg != 1;
-    if (!defer && s + 2 < total) P3_ISSUE_NEXT();
+    // This step's stage (s + 2): issued in one block right after the barrier, or (split) in two halves, each
+    // behind the fragment reads of one 32-deep k-slice, so the DMA issue overlaps the LDS read latency instead
+    // of holding every wave's MFMAs after the barrier.
+    const bool doiss = !defer && s + 2 < total;
+    unsigned char* img_ = nullptr;
+    v4i_t srda = {0, 0, 0, 0}, srdb = {0, 0, 0, 0};
+    if (doiss) {
+      if (ik == 0) {
+        const int pt_ = P3_TILE(iv);
+        sa.set_tile((pt_ / ntn) * P_BM, g.lda);
+        sb.set_tile((pt_ % ntn) * P_BN, g.ldb);
+      }
+      img_ = lds + ib * P_STAGE;
+      srda = sa.srd(A, g.lda, a_bytes, kbeg + ik * BK);
+      srdb = sb.srd(B, g.ldb, b_bytes, kbeg + ik * BK);
+      if (!sp_iss) {
+        sa.template issue_part<0, 4>(img_, srda);
+        sb.template issue_part<0, 2>(img_ + PA_BYTES, srdb);
+      }
+      if (++ik == nk) { ik = 0; ++iv; }
+      ib = ib == 2 ? 0 : ib + 1;
+    }
     const unsigned char* la = lds + cb * P_STAGE;
     const unsigned char* lb = la + PA_BYTES;
     const int t = P3_TILE(vc);
@@ -636,6 +665,15 @@ ASRX_DEV void p3_body(const GemmArgs& g, const TileSeq tl, int split, int z, uns
       for (int j = 0; j < TM; ++j) fa[j] = p_frag<P_BM, AT>(la, wm + 16 * j, ks);
 #pragma unroll
       for (int i = 0; i < TN; ++i) fb[i] = p_frag<P_BN, BT>(lb, wn + 16 * i, ks);
+      if (sp_iss && doiss) {
+        if (ks == 0) {
+          sa.template issue_part<0, 2>(img_, srda);
+          sb.template issue_part<0, 1>(img_ + PA_BYTES, srdb);
+        } else {
+          sa.template issue_part<2, 4>(img_, srda);
+          sb.template issue_part<1, 2>(img_ + PA_BYTES, srdb);
+        }
+      }
 #pragma unroll
       for (int i = 0; i < TN; ++i)
 #pragma unroll

@@ -365,7 +365,10 @@ ASRX_DEV v4i_t make_srd(const void* base, int64_t num_bytes) {
 ASRX_DEV void dma16_asm(const void* lds_dst, v4i_t srd, uint32_t voff) {
   const uint32_t m0 = __builtin_amdgcn_readfirstlane(
       (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)lds_dst);
-  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0), "v"(voff), "s"(srd)
+  v4i_t d;   // (re-)assert uniformity: a descriptor merged across branches may otherwise sit in VGPRs
+#pragma unroll
+  for (int i = 0; i < 4; ++i) d[i] = __builtin_amdgcn_readfirstlane(srd[i]);
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0), "v"(voff), "s"(d)
                : "memory", "m0");
 }
 
