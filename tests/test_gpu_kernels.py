@@ -283,7 +283,8 @@ def attn_variant(request):
 @pytest.mark.parametrize("B,H,Lq,Lk,kind", [(2, 4, 70, 70, "decoder"), (3, 2, 64, 249, "none"),
                                            (2, 2, 249, 249, "none"), (1, 2, 100, 300, "none"),
                                            (2, 3, 33, 33, "decoder"), (1, 2, 300, 64, "none"),
-                                           (2, 2, 256, 256, "decoder"), (1, 1, 5, 17, "none")])
+                                           (2, 2, 256, 256, "decoder"), (1, 1, 5, 17, "none"),
+                                           (1, 2, 999, 999, "none"), (1, 2, 300, 300, "decoder")])
 def test_attention_fused(dh, B, H, Lq, Lk, kind, attn_variant):
     from asrx.kernels import MaskSpec
     g = torch.Generator().manual_seed(B * 100 + Lq + Lk + dh)

@@ -94,6 +94,20 @@ def test_forward_c3_bf16_vs_oracle():
     assert float((logits.cpu().argmax(-1) == ref.argmax(-1)).double().mean()) >= 0.98
 
 
+def test_forward_c5_long_utterance_bf16_vs_oracle():
+    """c5 long-utterance stress geometry (T = 4000 frames -> T' = 999 encoder positions, O(T'^2) attention on the
+    tiled LDS K/V path since T' > 256), one utterance, bf16 fused path vs the oracle on the host."""
+    m, cfg = build("c5", "bf16")
+    m.eval()
+    s, t, k = synthetic_batch(cfg, 1, 4000, 65, seed=4321)
+    P = det_params(cfg, 0)
+    with torch.no_grad():
+        ref = oracle_forward(P, s, t[:, :-1], k[:, :-1], cfg, False)
+        logits = m(s.to(dev), t[:, :-1].to(dev), k[:, :-1].to(dev))
+    assert relerr(logits, ref) < 1.5e-2
+    assert float((logits.cpu().argmax(-1) == ref.argmax(-1)).double().mean()) >= 0.98
+
+
 @pytest.mark.parametrize("precision,tol", [("fp32", 1e-3), ("bf16", 5e-2)])
 def test_train_grads_micro(golden_dir, precision, tol):
     g = golden(golden_dir, "micro")
