@@ -143,7 +143,13 @@ def check(rc, name):
         raise RuntimeError(f"asrx: {name} failed: {ERRORS.get(rc, rc)}")
 
 
+_FNS = {}
+
+
 def call(name, *args):
-    rc = getattr(lib(), name)(*args)
+    fn = _FNS.get(name)
+    if fn is None:
+        fn = _FNS[name] = getattr(lib(), name)
+    rc = fn(*args)
     if rc != 0:
         raise RuntimeError(f"asrx: {name} failed: {ERRORS.get(rc, rc)}")

@@ -36,6 +36,7 @@ class FlatParams:
                 p.data = v
                 p.grad = self._view(self.grad, p)
         self._shadow_version = None
+        self._w16c, self._gc, self._gview = {}, {}, {}   # cached views into the flat buffers (id(p) -> view)
         self.on_grad_ready = None   # optional callback(param_list) used by the DDP bucketer
 
     def _view(self, buf, p):
@@ -65,12 +66,19 @@ class FlatParams:
         o = self.offsets[id(p)]
         return buf[o:o + p.numel()]
 
-    def w16(self, p):
-        """bf16 operand copy of p in its PHYSICAL layout (as a 2-D [rows, cols] matrix)."""
+    def _phys2d(self, p, buf):
         phys = getattr(p, "_asrx_phys", None)
         shape = phys[0] if phys is not None else p.shape
-        r = self.raw(p, self.shadow)
+        r = self.raw(p, buf)
         return r.view(shape[0], -1) if len(shape) > 1 else r
+
+    def w16(self, p):
+        """bf16 operand copy of p in its PHYSICAL layout (as a 2-D [rows, cols] matrix); views cached (the flat
+        buffers never move)."""
+        c = self._w16c.get(id(p))
+        if c is None:
+            c = self._w16c[id(p)] = self._phys2d(p, self.shadow)
+        return c
 
     def w32(self, p):
         phys = getattr(p, "_asrx_phys", None)
@@ -81,10 +89,10 @@ class FlatParams:
     def g(self, p):
         """fp32 gradient region of p (physical layout, 2-D for matrices); (re)binds p.grad if needed."""
         self.ensure_grad(p)
-        phys = getattr(p, "_asrx_phys", None)
-        shape = phys[0] if phys is not None else p.shape
-        r = self.raw(p, self.grad)
-        return r.view(shape[0], -1) if len(shape) > 1 else r
+        c = self._gc.get(id(p))
+        if c is None:
+            c = self._gc[id(p)] = self._phys2d(p, self.grad)
+        return c
 
     def span(self, first, count_params, buf):
         """A contiguous view covering `count_params` consecutive parameters starting at `first`."""
@@ -100,10 +108,13 @@ class FlatParams:
         return buf[o0:o1]
 
     def ensure_grad(self, p):
-        v = self._view(self.grad, p)
+        v = self._gview.get(id(p))
+        if v is not None and p.grad is v:
+            return
+        v = self._gview[id(p)] = self._view(self.grad, p)
         if p.grad is None or p.grad.data_ptr() != v.data_ptr():
             v.zero_()
-            p.grad = v
+        p.grad = v
 
     def refresh_shadow(self, force=False):
         """Re-cast the fp32 master params into the bf16 operand buffer when any param changed."""

@@ -205,6 +205,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = trainer.step(s, t, m)
+    t_enq = time.perf_counter() - t0      # host time to enqueue the K steps (the GPU runs behind it)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -237,6 +238,7 @@ def main():
                       "model": "speech-transformer", "global_batch": B * world, "seq_len": T,
                       "parallelism": f"dp{world}"},
            "frames_per_sec_per_gpu": round(value / world, 1),
+           "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 3),
            "loss": round(float(loss), 4),
            "roofline": roof}
     if rank == 0 and not args.no_sub:
