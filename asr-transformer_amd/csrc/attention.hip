@@ -19,6 +19,7 @@
 #include <cstring>
 
 #include "common.h"
+#include "gemm_common.h"
 
 namespace {
 
@@ -52,7 +53,9 @@ struct AttnArgs {
   int dbg;   // phase timestamps of block 0 / wave 0 into g_attn_dbg (tools only; ASRX_ATTN_DBG=1)
 };
 
-__device__ unsigned long long g_attn_dbg[64];
+__device__ unsigned long long g_attn_dbg[64 + 4 * 1024];   // [64..]: per-block real-time (fwd)
+#define FWD_TS(i) do { if (a.dbg && threadIdx.x == 0) sdbg[(i)] = __builtin_amdgcn_s_memtime(); } while (0)
+#define FWD_RT(i) do { if (a.dbg && threadIdx.x == 0) sdbg[(i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define ATTN_TS(i) do { if (a.dbg && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && (i) < 64) \
                           g_attn_dbg[(i)] = __builtin_amdgcn_s_memtime(); } while (0)
 
@@ -422,6 +425,33 @@ constexpr int R_KS = 64 + 8;    // K image (forward): 144-B rows, 16-B fragment 
 constexpr int R_VS = 64 + 16;   // V image (forward) / K image (backward): 160-B rows for the transposed reads
 constexpr int R_CS = 64 + 16;   // Q / dO chunk images (backward): row and transposed reads
 
+// Forward images are written by LDS-DMA, which lays 64 lanes x 16 B down linearly (1 KiB = 8 unpadded 128-B key
+// rows), so bank spreading is an XOR swizzle of the 16-B chunk instead of row padding: chunk c of key row r sits
+// in slot c ^ (r & 7) (K, ds_read_b128 row reads) or c ^ (r & 6) (V, ds_read_b64_tr_b16 reads keep chunk pairs
+// together); both are conflict-free for the lane groups of their read instructions.
+ASRX_DEV int kslot(int r, int c) { return c ^ (r & 7); }
+ASRX_DEV int vslot(int r, int c) { return c ^ (r & 6); }
+
+// Loads written as inline asm: the compiler does not count them, the kernel waits for them itself (counted
+// vmcnt, then pin() so that no use of the value is scheduled above the wait).
+ASRX_DEV s8_t ld128_asm(const void* p) {
+  s8_t r;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p));
+  return r;
+}
+ASRX_DEV uint32_t ld32_asm(const void* p) {
+  uint32_t r;
+  asm volatile("global_load_dword %0, %1, off" : "=v"(r) : "v"(p));
+  return r;
+}
+ASRX_DEV uint32_t ldu8_asm(const void* p) {
+  uint32_t r;
+  asm volatile("global_load_ubyte %0, %1, off" : "=v"(r) : "v"(p));
+  return r;
+}
+template <typename T> ASRX_DEV void pin(T& x) { asm volatile("" : "+v"(x)); }
+ASRX_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 ASRX_DEV f4_t mfma32(s8_t a, s8_t b, f4_t c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
 ASRX_DEV s8_t cat8(s4_t x, s4_t y) { return s8_t{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]}; }
 ASRX_DEV s8_t lds_b128(const bf16_t* p) { return *(const s8_t*)p; }
@@ -482,9 +512,9 @@ __global__ __launch_bounds__(256) void attn_dropgen_kernel(AttnArgs a, uint32_t*
 // Forward grid (ceil(Lq/256), B*H), 8 waves x 32 queries (two 16-query sub-tiles per wave).  Dropout factors
 // come from the query-major keep bits (a 4-bit nibble per (sub-tile, 16-key half) -> one LDS table read).
 template <int MODE>
-__global__ __launch_bounds__(512) void attn_fwd_res_kernel(AttnArgs a, const uint32_t* qmaj) {
-  __shared__ __attribute__((aligned(16))) bf16_t sk[R_MAXK * R_KS];
-  __shared__ __attribute__((aligned(16))) bf16_t sv[R_MAXK * R_VS];
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void attn_fwd_res_kernel(AttnArgs a, const uint32_t* qmaj) {
+  __shared__ __attribute__((aligned(1024))) bf16_t sk[R_MAXK * 64];
+  __shared__ __attribute__((aligned(1024))) bf16_t sv[R_MAXK * 64];
   __shared__ __attribute__((aligned(16))) float skb[R_MAXK];   // per-key score bias: 0 or -inf
   __shared__ __attribute__((aligned(16))) f4_t slut[16];       // dropout factors of a 4-bit keep mask
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
@@ -493,55 +523,91 @@ __global__ __launch_bounds__(512) void attn_fwd_res_kernel(AttnArgs a, const uin
   const int nk = nkt * 32;
   const bf16_t* Kb = a.k + b * a.kb + h * 64;
   const bf16_t* Vb = a.v + b * a.vb + h * 64;
-  // K/V staging: every load of a batch is issued before the first LDS write (one memory latency per batch)
-  for (int c0 = threadIdx.x; c0 < nk * 8; c0 += 512 * 4) {
-    uint4 kv[4], vv[4];
+  // phase timestamps (ASRX_ATTN_DBG) go to LDS and are stored at the end: no store among the counted loads
+  __shared__ uint64_t sdbg[16];
+  if (a.dbg && threadIdx.x < 16) sdbg[threadIdx.x] = 0;
+  FWD_RT(12);
+  FWD_TS(0);
+  // Every global load of the prologue is issued up front, in this order per wave: [MODE 1: key / query
+  // validity bytes], Q fragments (4), keep words (16), then the K/V images in four 64-key pieces by LDS-DMA
+  // (piece i = key rows 64 i .. 64 i + 63; wave w moves rows 64 i + 8 w .. + 7 of K and of V).  Piece i is
+  // waited for just before key tile 2 i, so the scores of the first keys overlap the arrival of the last ones
+  // (all workgroups of a launch start together: the staging phase is HBM-bound).  Rows past Lk are outside the
+  // descriptors' range and read as zeros.
+  const int qw0 = (blockIdx.x * 8 + w) * 32;
+  const int nkw = nkt;
+  const int np = (nk + 63) >> 6;   // 64-key pieces
+  uint32_t kval = 1, qval[2] = {1, 1};
+  if (MODE == 1) {
+    const uint8_t* kvp = a.kvalid ? a.kvalid + b * a.validb + min((int)threadIdx.x, a.Lk - 1) : (const uint8_t*)a.q;
+    kval = ldu8_asm(kvp);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = c0 + i * 512, row = min(c >> 3, a.Lk - 1), dc = (c & 7) * 8;
-      kv[i] = *(const uint4*)(Kb + (int64_t)row * a.kr + dc);
-      vv[i] = *(const uint4*)(Vb + (int64_t)row * a.vr + dc);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = c0 + i * 512, row = c >> 3, dc = (c & 7) * 8;
-      if (c < nk * 8) {
-        *(uint4*)(sk + row * R_KS + dc) = row < a.Lk ? kv[i] : make_uint4(0, 0, 0, 0);
-        *(uint4*)(sv + row * R_VS + dc) = row < a.Lk ? vv[i] : make_uint4(0, 0, 0, 0);
-      }
+    for (int qs = 0; qs < 2; ++qs) {
+      const int qc = min(qw0 + 16 * qs + li, a.Lq - 1);
+      qval[qs] = ldu8_asm(a.qvalid ? a.qvalid + b * a.validb + qc : (const uint8_t*)a.q);
     }
   }
-  if (threadIdx.x < nk) {
-    const int key = threadIdx.x;
-    bool ok = key < a.Lk;
-    if (MODE == 1 && ok && a.kvalid) ok = a.kvalid[b * a.validb + key] != 0;
-    skb[key] = ok ? 0.f : -INFINITY;
+  s8_t qf[2][2];
+  uint32_t dw[2][8];   // query-major keep words of this lane's two queries (one per 32-key tile)
+#pragma unroll
+  for (int qs = 0; qs < 2; ++qs) {
+    const int qc = min(qw0 + 16 * qs + li, a.Lq - 1);
+    const bf16_t* qp = a.q + b * a.qb + (int64_t)qc * a.qr + h * 64 + 8 * g;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) qf[qs][c] = ld128_asm(qp + 32 * c);
   }
+#pragma unroll
+  for (int qs = 0; qs < 2; ++qs) {
+    const int qc = min(qw0 + 16 * qs + li, a.Lq - 1);
+    const uint32_t* dp = qmaj ? qmaj + ((int64_t)bh * a.Lq + qc) * nkw : (const uint32_t*)a.q;
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) dw[qs][kt] = ld32_asm(dp + (qmaj ? min(kt, nkw - 1) : 0));
+  }
+  {
+    const asrxg::v4i_t ksrd = asrxg::make_srd(Kb, ((int64_t)(a.Lk - 1) * a.kr + 64) * 2);
+    const asrxg::v4i_t vsrd = asrxg::make_srd(Vb, ((int64_t)(a.Lk - 1) * a.vr + 64) * 2);
+    const int rl = l >> 3, sl = l & 7;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i >= np) break;   // workgroup-uniform
+      const int r = 64 * i + 8 * w + rl;
+      asrxg::dma16_asm(sk + (64 * i + 8 * w) * 64, ksrd, (uint32_t)(r * a.kr + 8 * kslot(r, sl)) * 2u);
+      asrxg::dma16_asm(sv + (64 * i + 8 * w) * 64, vsrd, (uint32_t)(r * a.vr + 8 * vslot(r, sl)) * 2u);
+    }
+  }
+  FWD_TS(1);
+  asrxg::wait_vmcnt_bs<0, 7>(2 * (np - 1));   // everything but pieces 1 .. np-1
+#pragma unroll
+  for (int qs = 0; qs < 2; ++qs) {
+    pin(qf[qs][0]);
+    pin(qf[qs][1]);
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) pin(dw[qs][kt]);
+    if (!qmaj) {
+#pragma unroll
+      for (int kt = 0; kt < 8; ++kt) dw[qs][kt] = 0xffffffffu;
+    }
+  }
+  bool qdead[2] = {false, false};
+  if (MODE == 1) {
+    pin(kval);
+    pin(qval[0]);
+    pin(qval[1]);
+    if (!a.kvalid) kval = 1;
+#pragma unroll
+    for (int qs = 0; qs < 2; ++qs) qdead[qs] = a.qvalid && qw0 + 16 * qs + li < a.Lq && (qval[qs] & 0xff) == 0;
+  }
+  if (threadIdx.x < nk) skb[threadIdx.x] = (threadIdx.x < a.Lk && (kval & 0xff) != 0) ? 0.f : -INFINITY;
   if (threadIdx.x < 16) {
     f4_t f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) f[r] = ((threadIdx.x >> r) & 1) ? a.dscale : 0.f;
     slut[threadIdx.x] = f;
   }
-  const int qw0 = (blockIdx.x * 8 + w) * 32;
-  s8_t qf[2][2];
-  bool qdead[2];
-  uint32_t dw[2][8];   // query-major keep words of this lane's two queries (one per 32-key tile)
-  const int nkw = nkt;
-#pragma unroll
-  for (int qs = 0; qs < 2; ++qs) {
-    const int q = qw0 + 16 * qs + li;
-    const int qc = min(q, a.Lq - 1);
-    const bf16_t* qp = a.q + b * a.qb + (int64_t)qc * a.qr + h * 64 + 8 * g;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) qf[qs][c] = *(const s8_t*)(qp + 32 * c);
-    qdead[qs] = MODE == 1 && q < a.Lq && a.qvalid && !a.qvalid[b * a.validb + q];
-#pragma unroll
-    for (int kt = 0; kt < 8; ++kt)
-      dw[qs][kt] = (qmaj && kt < nkw) ? qmaj[((int64_t)bh * a.Lq + qc) * nkw + kt] : 0xffffffffu;
-  }
-  __syncthreads();
-  if (qw0 >= a.Lq) return;   // no barrier below
+  lds_barrier();
+  FWD_TS(2);
+  FWD_RT(13);
+  const bool act = qw0 < a.Lq;   // waves past the last query still stage their K/V share
 
   f4_t o[4][2];
 #pragma unroll
@@ -552,13 +618,18 @@ __global__ __launch_bounds__(512) void attn_fwd_res_kernel(AttnArgs a, const uin
 
 #pragma unroll
   for (int kt = 0; kt < 8; ++kt) {
-    if (kt >= ktn) break;
+    if (kt >= nkt) break;   // workgroup-uniform
+    if (kt > 0 && (kt & 1) == 0) {   // piece kt / 2 (< np, since kt < nkt)
+      asrxg::wait_vmcnt_bs<0, 7>(2 * (np - 1 - (kt >> 1)));
+      lds_barrier();
+    }
+    if (!act || kt >= ktn) continue;
     f4_t s[2][2];
     f4_t kb[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      const bf16_t* kr = sk + (kt * 32 + 16 * t + li) * R_KS + 8 * g;
-      const s8_t k0 = lds_b128(kr), k1 = lds_b128(kr + 32);
+      const bf16_t* kr = sk + (kt * 32 + 16 * t + li) * 64;
+      const s8_t k0 = lds_b128(kr + 8 * (g ^ (li & 7))), k1 = lds_b128(kr + 8 * ((g + 4) ^ (li & 7)));
       kb[t] = *(const f4_t*)(skb + kt * 32 + 16 * t + 4 * g);
 #pragma unroll
       for (int qs = 0; qs < 2; ++qs) s[t][qs] = mfma32(k1, qf[qs][1], mfma32(k0, qf[qs][0], f4_t{0.f, 0.f, 0.f, 0.f}));
@@ -610,13 +681,16 @@ __global__ __launch_bounds__(512) void attn_fwd_res_kernel(AttnArgs a, const uin
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const bf16_t* vp = sv + (kt * 32 + 4 * g + (li >> 2)) * R_VS + 16 * u + 4 * (li & 3);
-      const s8_t vt = cat8(lds_tr(vp), lds_tr(vp + 16 * R_VS));
+      const int vr = kt * 32 + 4 * g + (li >> 2);   // (vr + 16) & 6 == vr & 6
+      const bf16_t* vp = sv + vr * 64 + 8 * vslot(vr, 2 * u + ((li >> 1) & 1)) + 4 * (li & 1);
+      const s8_t vt = cat8(lds_tr(vp), lds_tr(vp + 16 * 64));
 #pragma unroll
       for (int qs = 0; qs < 2; ++qs) o[u][qs] = mfma32(vt, cat8(pf[0][qs], pf[1][qs]), o[u][qs]);
     }
+    FWD_TS(3 + kt);
   }
 
+  if (!act) return;
 #pragma unroll
   for (int qs = 0; qs < 2; ++qs) {
     const int q = qw0 + 16 * qs + li;
@@ -635,6 +709,15 @@ __global__ __launch_bounds__(512) void attn_fwd_res_kernel(AttnArgs a, const uin
       const float mu = m_run[qs] == -INFINITY ? 0.f : m_run[qs];
       a.lse[(int64_t)bh * a.Lq + q] = live ? mu + log2f(l_run[qs]) : INFINITY;
     }
+  }
+  FWD_TS(11);
+  if (a.dbg && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+    for (int i = 0; i < 12; ++i) g_attn_dbg[44 + i] = sdbg[i];
+  if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0 && bh < 1024) {
+    g_attn_dbg[64 + 4 * bh] = sdbg[12];
+    g_attn_dbg[65 + 4 * bh] = sdbg[13];
+    g_attn_dbg[66 + 4 * bh] = __builtin_amdgcn_s_memrealtime();
+    g_attn_dbg[67 + 4 * bh] = __smid();
   }
 }
 
@@ -1104,7 +1187,7 @@ extern "C" int asrx_attention_bwd(const asrx_attn_desc* d, void* stream) {
 
 // tools only (not part of include/asrx.h): copy the phase timestamps of the last debug launch
 extern "C" int asrx_attn_debug_read(unsigned long long* host, int n) {
-  if (!host || n < 0 || n > 64) return ASRX_ERR_ARG;
+  if (!host || n < 0 || n > 64 + 4 * 1024) return ASRX_ERR_ARG;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_attn_dbg), sizeof(unsigned long long) * n) == hipSuccess ? ASRX_OK
                                                                                                        : ASRX_ERR_LAUNCH;
 }

@@ -52,16 +52,10 @@ def case(name, Lq, Lk, causal):
 
 
 def timeit(fn, reps):
-    ts = []
-    for _ in range(reps + 3):
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        fn()
-        e.record()
-        e.synchronize()
-        ts.append(s.elapsed_time(e))
-    ts = sorted(ts[3:])
-    return ts[len(ts) // 2]
+    """ms per call: reps calls captured in a HIP graph and replayed (no host launch gaps)."""
+    sys.path.insert(0, REPO)
+    from bench import _graph_time_ms
+    return _graph_time_ms(fn, launches=reps)
 
 
 def main():
@@ -88,12 +82,30 @@ def main():
             bwd()
             torch.cuda.synchronize()
             os.environ["ASRX_ATTN_DBG"] = "1"
+            fwd()
             bwd()
             torch.cuda.synchronize()
             os.environ.pop("ASRX_ATTN_DBG")
-            buf = (ctypes.c_ulonglong * 64)()
-            lib().asrx_attn_debug_read(buf, 64)
+            nb = B * H
+            buf = (ctypes.c_ulonglong * (64 + 4 * nb))()
+            lib().asrx_attn_debug_read(buf, 64 + 4 * nb)
             ts = list(buf)
+            blk = [ts[64 + 4 * i:68 + 4 * i] for i in range(nb)]
+            t00 = min(x[0] for x in blk)
+            pc = lambda v: [int(sorted(v)[int(q * (len(v) - 1))]) for q in (0, .1, .5, .9, 1)]   # noqa: E731
+            print(name, "fwd per-block (10 ns ticks; pct 0/10/50/90/100): start", pc([x[0] - t00 for x in blk]),
+                  " staged", pc([x[1] - x[0] for x in blk]), " total", pc([x[2] - x[0] for x in blk]),
+                  " end", pc([x[2] - t00 for x in blk]), " distinct CUs", len(set(x[3] for x in blk)))
+            from collections import Counter
+            per = Counter(x[3] for x in blk)
+            late = [x for x in blk if x[0] - t00 > 200]
+            print("   blocks per CU id:", sorted(Counter(per.values()).items()), " late starters:", len(late),
+                  " late per CU count:", sorted(Counter(per[x[3]] for x in late).items()),
+                  " late bh ids:", [i for i, x in enumerate(blk) if x[0] - t00 > 200][:24])
+            f0 = ts[44]
+            if f0:
+                print(name, "fwd: staging-issued", ts[45] - f0, " barrier", ts[46] - f0,
+                      " tiles", [ts[47 + k] - f0 for k in range(8) if ts[47 + k] >= f0], " end", ts[55] - f0)
             t0 = ts[0]
             print(name, "prologue", ts[1] - t0, "cycles")
             for ch in range(8):

@@ -16,14 +16,10 @@ from asrx import kernels as K  # noqa: E402
 
 
 def timed(fn, reps):
-    fn()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(reps):
-        fn()
-    e.record()
-    e.synchronize()
-    return s.elapsed_time(e) / reps * 1e-3
+    """GPU time per call: reps calls captured in a HIP graph and replayed (no host launch gaps)."""
+    sys.path.insert(0, REPO)
+    from bench import _graph_time_ms
+    return _graph_time_ms(fn, launches=reps) * 1e-3
 
 
 def main():
