@@ -162,6 +162,8 @@ def linear_dgrad(dy, w, out, **kw):
 def wgrad_plan(n_out, k_in, rows):
     """Tile and split-K for dW = dY^T X (reduction over the B*T rows): 128x128 tiles, splits chosen so that
     ~320 workgroups fill the 256 CUs while each split keeps >= 256 rows."""
+    if n_out == 64 and k_in % 64 == 0 and k_in <= 576 and rows >= 64 * 256:
+        return 64, 256   # gemm.hip tall-K kernel (conv2 dW): one 64 x k_in partial per split, 256 splits
     tile = 128 if (n_out >= 128 and k_in >= 128) else 64
     tiles = math.ceil(n_out / tile) * math.ceil(k_in / tile)
     splitk = 1
@@ -603,7 +605,7 @@ def conv1_bwd_w(x, dy1, dw, db):
     _cuda(x, dy1, dw, db)
     B, _, F, T = x.shape
     nblocks = 512
-    part = torch.empty(nblocks * 640, device=x.device, dtype=torch.float32)
+    part = torch.empty((nblocks + 128) * 640, device=x.device, dtype=torch.float32)   # + finish pass 1 rows
     call("asrx_conv1_bwd_w", x.data_ptr(), dy1.data_ptr(), B, F, T, part.data_ptr(), nblocks, dw.data_ptr(),
          db.data_ptr(), stream())
 
@@ -613,7 +615,7 @@ def conv1_bwd_fused(dcols, y1, x, dw, db):
     _cuda(dcols, y1, x, dw, db)
     B, _, F, T = x.shape
     nblocks = (B * y1.shape[1] * 8 + 3) // 4  # 8 waves per conv1 output row (b, f1): frontend.hip CB_SEG
-    part = torch.empty(nblocks * 640, device=x.device, dtype=torch.float32)
+    part = torch.empty((nblocks + 128) * 640, device=x.device, dtype=torch.float32)   # + finish pass 1 rows
     call("asrx_conv1_bwd_fused", code(dcols), dcols.data_ptr(), code(y1), y1.data_ptr(), x.data_ptr(), B, F, T,
          part.data_ptr(), nblocks, dw.data_ptr(), db.data_ptr(), stream())
 

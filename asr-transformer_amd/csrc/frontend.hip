@@ -13,43 +13,54 @@ namespace {
 
 constexpr int C1 = 64;
 
+// One workgroup per conv1 output row (b, f1): lane = (position slot t1 % 32, channel group of 8); the lane's
+// 8 x (9 taps + bias) weights are read once into registers (16-B LDS reads) and the row is swept 32 positions
+// per step — no per-element index division, no weight reads in the loop; 16-B channels-last stores.
 template <typename OT>
-__global__ __launch_bounds__(256) void conv1_fwd_kernel(const float* __restrict__ x, int B, int F, int T, int F1,
-                                                        int T1, const float* __restrict__ w,
-                                                        const float* __restrict__ bias, OT* __restrict__ y) {
-  __shared__ float sw[C1 * 9 + C1];
+__global__ __launch_bounds__(256) void conv1_fwd_row_kernel(const float* __restrict__ x, int F, int T, int F1,
+                                                            int T1, const float* __restrict__ w,
+                                                            const float* __restrict__ bias, OT* __restrict__ y) {
+  __shared__ __attribute__((aligned(16))) float sw[C1 * 9 + C1];
   for (int i = threadIdx.x; i < C1 * 10; i += 256) sw[i] = i < C1 * 9 ? w[i] : bias[i - C1 * 9];
   __syncthreads();
-  const int64_t total = (int64_t)B * F1 * T1 * 8;
-  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
-    const int cg = (int)(t & 7);
-    const int64_t pos = t >> 3;
-    const int t1 = (int)(pos % T1);
-    const int64_t r = pos / T1;
-    const int f1 = (int)(r % F1);
-    const int b = (int)(r / F1);
-    const float* xp = x + ((int64_t)b * F + 2 * f1) * T + 2 * t1;
+  const int cg = threadIdx.x & 7, ps = threadIdx.x >> 3;
+  const int row = blockIdx.x, b = row / F1, f1 = row % F1;
+  float wr[8][9], br[8];
+#pragma unroll
+  for (int q = 0; q < 18; ++q) {   // 72 consecutive weights of channels 8 cg .. 8 cg + 7
+    const f4_t v = *(const f4_t*)(sw + cg * 72 + 4 * q);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) wr[(4 * q + e) / 9][(4 * q + e) % 9] = v[e];
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) br[i] = sw[C1 * 9 + cg * 8 + i];
+  // the row's three input lines (3 x T floats) staged in LDS once: the sweep then reads no global memory
+  extern __shared__ float sx[];   // [3][T]
+  const float* xr = x + ((int64_t)b * F + 2 * f1) * T;
+  for (int i = threadIdx.x; i < 3 * T; i += 256) sx[i] = xr[(int64_t)(i / T) * T + i % T];
+  __syncthreads();
+  OT* yr = y + (int64_t)row * T1 * C1 + cg * 8;
+  for (int t1 = ps; t1 < T1; t1 += 32) {
     float in[9];
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
-      for (int kw = 0; kw < 3; ++kw) in[kh * 3 + kw] = xp[(int64_t)kh * T + kw];
+      for (int kw = 0; kw < 3; ++kw) in[kh * 3 + kw] = sx[kh * T + 2 * t1 + kw];
     float o[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int c = cg * 8 + i;
-      float s = sw[C1 * 9 + c];
+      float s = br[i];
 #pragma unroll
-      for (int k = 0; k < 9; ++k) s += sw[c * 9 + k] * in[k];
+      for (int k = 0; k < 9; ++k) s = fmaf(wr[i][k], in[k], s);
       o[i] = fmaxf(s, 0.f);
     }
     if constexpr (sizeof(OT) == 2) {
       uint4 u;
       u.x = pack2bf(o[0], o[1]); u.y = pack2bf(o[2], o[3]); u.z = pack2bf(o[4], o[5]); u.w = pack2bf(o[6], o[7]);
-      *(uint4*)(y + pos * C1 + cg * 8) = u;
+      *(uint4*)(yr + (int64_t)t1 * C1) = u;
     } else {
-      *(f4_t*)(y + pos * C1 + cg * 8) = f4_t{o[0], o[1], o[2], o[3]};
-      *(f4_t*)(y + pos * C1 + cg * 8 + 4) = f4_t{o[4], o[5], o[6], o[7]};
+      *(f4_t*)(yr + (int64_t)t1 * C1) = f4_t{o[0], o[1], o[2], o[3]};
+      *(f4_t*)(yr + (int64_t)t1 * C1 + 4) = f4_t{o[4], o[5], o[6], o[7]};
     }
   }
 }
@@ -239,23 +250,164 @@ __global__ __launch_bounds__(256) void conv1_bwd_fused_kernel(const DT* __restri
     part[(int64_t)blockIdx.x * 640 + i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
 }
 
-// one block per output (640 = 64 channels x (9 taps + bias)); partials summed by 256 threads + LDS tree
-__global__ __launch_bounds__(256) void conv1_bwd_finish(const float* part, int nblocks, float* dw, float* db) {
-  __shared__ float red[256];
-  const int i = blockIdx.x;
-  float s = 0.f;
-  for (int p = threadIdx.x; p < nblocks; p += 256) s += part[(int64_t)p * 640 + i];
-  red[threadIdx.x] = s;
+// bf16 dcols / y1: the same sweep with 16-byte loads.  Lane = (position slot pp = l >> 3, channel group
+// cg = l & 7): a wave-step covers 8 same-parity positions of its row (t1 = t0 + 2 pp) x 64 channels, each lane
+// summing its <= 4 conv2 taps of 8 channels (one 16-B dcols load per tap), gating by y1 (one 16-B load) and
+// accumulating 8 channels x (9 x-taps + bias).  The 8 position slots are reduced by lane shuffles at the end.
+__global__ __launch_bounds__(256) void conv1_bwd_fused_v8_kernel(const bf16_t* __restrict__ dcols,
+                                                                 const bf16_t* __restrict__ y1,
+                                                                 const float* __restrict__ x, int B, int F, int T,
+                                                                 int F1, int T1, int F2, int T2,
+                                                                 float* __restrict__ part) {
+  const int l = threadIdx.x & 63, cg = l & 7, pp = l >> 3;
+  const int sub = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wid = blockIdx.x * 4 + sub;
+  const int row = wid / CB_SEG, seg = wid % CB_SEG;
+  const int tlen = ((T1 + CB_SEG - 1) / CB_SEG + 1) & ~1;
+  const int tlo = seg * tlen, thi = min(T1, tlo + tlen);
+  float acc[8][10];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int k = 0; k < 10; ++k) acc[i][k] = 0.f;
+  if (row < B * F1) {
+    const int b = row / F1, f1 = row % F1;
+    const bool fe = !(f1 & 1);
+    const int khs[2] = {fe ? 0 : 1, 2};
+    const int f2s[2] = {fe ? f1 / 2 : (f1 - 1) / 2, fe ? f1 / 2 - 1 : 0};
+    const bool hvs[2] = {f2s[0] < F2, fe && f1 >= 2 && f2s[1] < F2};
+    const float* xr = x + ((int64_t)b * F + 2 * f1) * T;
+    const bf16_t* yr = y1 + (int64_t)row * T1 * C1 + cg * 8;
+    const bf16_t* dbase = dcols + (int64_t)b * T2 * F2 * 576 + cg * 8;
+    for (int pt = 0; pt < 2; ++pt) {
+#pragma unroll 2
+      for (int t0 = tlo + pt; t0 < thi; t0 += 16) {
+        const int t1 = t0 + 2 * pp;
+        const bool tv = t1 < thi;
+        const int t1c = tv ? t1 : pt;
+        uint4 dv[2][2];
+        bool ok[2][2];
+#pragma unroll
+        for (int ih = 0; ih < 2; ++ih) {
+          const int kh = khs[ih], f2 = hvs[ih] ? f2s[ih] : 0;
+#pragma unroll
+          for (int iw = 0; iw < 2; ++iw) {
+            const int kw = pt ? 1 : 2 * iw;
+            const int td = t1c - kw;
+            const bool wv = (pt == 0 || iw == 0) && td >= 0 && (td >> 1) < T2;
+            const int t2 = wv ? (td >> 1) : 0;
+            ok[ih][iw] = hvs[ih] && wv && tv;
+            dv[ih][iw] = *(const uint4*)(dbase + ((int64_t)t2 * F2 + f2) * 576 + (kh * 3 + kw) * C1);
+          }
+        }
+        const uint4 gy = *(const uint4*)(yr + (int64_t)t1c * C1);
+        const float* xp = xr + 2 * t1c;
+        float xv[9];
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw) xv[kh * 3 + kw] = xp[(int64_t)kh * T + kw];
+        float g[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) g[i] = 0.f;
+#pragma unroll
+        for (int ih = 0; ih < 2; ++ih)
+#pragma unroll
+          for (int iw = 0; iw < 2; ++iw) {
+            if (!ok[ih][iw]) continue;
+            const uint32_t* u = (const uint32_t*)&dv[ih][iw];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              g[2 * e] += bf2f(u[e] & 0xffff);
+              g[2 * e + 1] += bf2f(u[e] >> 16);
+            }
+          }
+        const uint32_t* yu = (const uint32_t*)&gy;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (!(bf2f(yu[e] & 0xffff) > 0.f)) g[2 * e] = 0.f;
+          if (!(bf2f(yu[e] >> 16) > 0.f)) g[2 * e + 1] = 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+#pragma unroll
+          for (int k = 0; k < 9; ++k) acc[i][k] = fmaf(g[i], xv[k], acc[i][k]);
+          acc[i][9] += g[i];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      float v = acc[i][k];
+      v += __shfl_xor(v, 8, 64);
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      acc[i][k] = v;
+    }
+  __shared__ float red[4][640];
+  if (pp == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int k = 0; k < 10; ++k) red[sub][(cg * 8 + i) * 10 + k] = acc[i][k];
+  }
   __syncthreads();
-  for (int k = 128; k > 0; k >>= 1) {
-    if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
-    __syncthreads();
+  for (int i = threadIdx.x; i < 640; i += 256)
+    part[(int64_t)blockIdx.x * 640 + i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+}
+
+// Partials [nblocks][640] (640 = 64 channels x (9 taps + bias)) -> dW1 / db1 in two deterministic passes with
+// coalesced 640-wide row reads: pass 1, CF_G1 workgroups each sum a contiguous run of rows into part2[g][640];
+// pass 2, 10 workgroups of (64 columns x 4 row groups) sum part2 and add into the gradients.
+// (both passes issue all their loads before the first add: latency-bound otherwise)
+constexpr int CF_G1 = 128;
+constexpr int CF_R1 = 48;   // pass-1 rows loaded per batch
+
+__global__ __launch_bounds__(256) void conv1_bwd_reduce1(const float* __restrict__ part, int nblocks,
+                                                         float* __restrict__ part2) {
+  const int per = (nblocks + CF_G1 - 1) / CF_G1;
+  const int r0 = blockIdx.x * per, r1 = min(nblocks, r0 + per);
+  for (int c = threadIdx.x; c < 640; c += 256) {
+    float s = 0.f;
+    for (int base = r0; base < r1; base += CF_R1) {
+      float v[CF_R1];
+#pragma unroll
+      for (int j = 0; j < CF_R1; ++j) v[j] = base + j < r1 ? part[(int64_t)(base + j) * 640 + c] : 0.f;
+#pragma unroll
+      for (int j = 0; j < CF_R1; ++j) s += v[j];
+    }
+    part2[blockIdx.x * 640 + c] = s;
   }
-  if (threadIdx.x == 0) {
-    const int c = i / 10, k = i % 10;
-    if (k < 9) dw[c * 9 + k] += red[0];
-    else db[c] += red[0];
+}
+
+__global__ __launch_bounds__(256) void conv1_bwd_reduce2(const float* __restrict__ part2, float* dw, float* db) {
+  __shared__ float red[16][16];
+  const int c = blockIdx.x * 16 + (threadIdx.x & 15), rg = threadIdx.x >> 4;
+  float v[CF_G1 / 16];
+#pragma unroll
+  for (int j = 0; j < CF_G1 / 16; ++j) v[j] = part2[(rg + 16 * j) * 640 + c];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < CF_G1 / 16; ++j) s += v[j];
+  red[rg][threadIdx.x & 15] = s;
+  __syncthreads();
+  if (rg == 0) {
+    s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += red[i][threadIdx.x];
+    const int ch = c / 10, k = c % 10;
+    if (k < 9) dw[ch * 9 + k] += s;
+    else db[ch] += s;
   }
+}
+
+void conv1_bwd_finish(const float* part, int nblocks, float* dw, float* db, hipStream_t st) {
+  float* part2 = const_cast<float*>(part) + (int64_t)nblocks * 640;
+  hipLaunchKernelGGL(conv1_bwd_reduce1, dim3(CF_G1), dim3(256), 0, st, part, nblocks, part2);
+  hipLaunchKernelGGL(conv1_bwd_reduce2, dim3(40), dim3(256), 0, st, part2, dw, db);
 }
 
 __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restrict__ tok, int64_t ntok, int L,
@@ -466,13 +618,15 @@ extern "C" int asrx_conv1_fwd(const float* x, int32_t B, int32_t F, int32_t T, c
                               void* y1, int32_t y_dtype, void* stream) {
   if (!x || !w || !b || !y1 || B <= 0 || F < 3 || T < 3) return ASRX_ERR_ARG;
   const int F1 = (F - 3) / 2 + 1, T1 = (T - 3) / 2 + 1;
-  const dim3 grid(grid_for((int64_t)B * F1 * T1 * 8));
+  if (T > 5120) return ASRX_ERR_UNSUPPORTED;   // 3 input lines staged in LDS (<= 60 KiB)
+  const dim3 grid((unsigned)(B * F1));
+  const size_t shm = sizeof(float) * 3 * T;
   if (y_dtype == ASRX_F32)
-    hipLaunchKernelGGL(conv1_fwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, x, B, F, T, F1, T1, w, b,
-                       (float*)y1);
+    hipLaunchKernelGGL(conv1_fwd_row_kernel<float>, grid, dim3(256), shm, (hipStream_t)stream, x, F, T, F1, T1, w,
+                       b, (float*)y1);
   else
-    hipLaunchKernelGGL(conv1_fwd_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, x, B, F, T, F1, T1, w, b,
-                       (bf16_t*)y1);
+    hipLaunchKernelGGL(conv1_fwd_row_kernel<bf16_t>, grid, dim3(256), shm, (hipStream_t)stream, x, F, T, F1, T1, w,
+                       b, (bf16_t*)y1);
   ASRX_CHECK_LAUNCH();
   return ASRX_OK;
 }
@@ -510,7 +664,7 @@ extern "C" int asrx_conv1_bwd_w(const float* x, const float* dy1, int32_t B, int
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(conv1_bwd_w_kernel, dim3(nblocks), dim3(256), 0, st, x, dy1, B, F, T, F1, T1, part, per);
   ASRX_CHECK_LAUNCH();
-  hipLaunchKernelGGL(conv1_bwd_finish, dim3(640), dim3(256), 0, st, part, nblocks, dw, db);
+  conv1_bwd_finish(part, nblocks, dw, db, st);
   ASRX_CHECK_LAUNCH();
   return ASRX_OK;
 }
@@ -605,13 +759,15 @@ extern "C" int asrx_conv1_bwd_fused(int32_t dcols_dtype, const void* dcols, int3
   hipStream_t st = (hipStream_t)stream;
 #define ASRX_FUSED(DT, YT) hipLaunchKernelGGL((conv1_bwd_fused_kernel<DT, YT>), dim3(nblocks), dim3(256), 0, st, \
       (const DT*)dcols, (const YT*)y1, x, B, F, T, F1, T1, F2, T2, part)
-  if (dcols_dtype == ASRX_BF16 && y1_dtype == ASRX_BF16) ASRX_FUSED(bf16_t, bf16_t);
+  if (dcols_dtype == ASRX_BF16 && y1_dtype == ASRX_BF16)
+    hipLaunchKernelGGL(conv1_bwd_fused_v8_kernel, dim3(nblocks), dim3(256), 0, st, (const bf16_t*)dcols,
+                       (const bf16_t*)y1, x, B, F, T, F1, T1, F2, T2, part);
   else if (dcols_dtype == ASRX_F32 && y1_dtype == ASRX_F32) ASRX_FUSED(float, float);
   else if (dcols_dtype == ASRX_BF16 && y1_dtype == ASRX_F32) ASRX_FUSED(bf16_t, float);
   else ASRX_FUSED(float, bf16_t);
 #undef ASRX_FUSED
   ASRX_CHECK_LAUNCH();
-  hipLaunchKernelGGL(conv1_bwd_finish, dim3(640), dim3(256), 0, st, part, nblocks, dw, db);
+  conv1_bwd_finish(part, nblocks, dw, db, st);
   ASRX_CHECK_LAUNCH();
   return ASRX_OK;
 }

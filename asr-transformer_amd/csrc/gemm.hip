@@ -1114,6 +1114,138 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Tall-K weight gradient (A^T, B^T; M = 64, N <= 576, N % 16 == 0; the conv2 front-end's dW = dY^T cols with
+// K = B*T''*F'' ~ 300k rows).  One 64 x N fp32 partial per split (grid = splitk workgroups, 8 waves), the K
+// range swept in 32-row steps through a 3-stage LDS-DMA ring: stage = dY rows [32][64] (4 KiB) + B rows
+// [32][N] (N/16 KiB), both copied whole-row (the operands are contiguous row blocks) with the 16-byte chunk
+// index XOR-swizzled by (row & 6), conflict-free for the ds_read_b64_tr_b16 fragment reads.  Wave w owns
+// m-tiles 2 (w & 1) + {0, 1} and n-tiles 9 (w >> 1) + {0..8}; the bias gradient (row sums of A) rides along
+// as MFMAs against a ones operand in the waves of the first n-quarter.  Rows past the split's end read as
+// zeros (descriptor range).  Partials go to the split-K workspace; tallk_reduce_kernel finishes.
+// ------------------------------------------------------------------------------------------------
+constexpr int TK_ROWS = 32;
+constexpr int TK_MAXN = 576;
+constexpr int TK_STAGE = TK_ROWS * (64 + TK_MAXN) * 2;   // 40 KiB
+
+__global__ __launch_bounds__(512) void gemm_bf16_tallk_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[3 * TK_STAGE];
+  const int z = blockIdx.x, w = threadIdx.x >> 6, l = threadIdx.x & 63, g4 = l >> 4, li = l & 15;
+  const int N = g.N, ntt = N >> 4;
+  const int k0 = z * g.k_per_split, k1 = min(g.K, k0 + g.k_per_split);
+  const int nsteps = k1 > k0 ? (k1 - k0 + TK_ROWS - 1) / TK_ROWS : 0;
+  const bf16_t* A = (const bf16_t*)g.a + (int64_t)k0 * g.lda;
+  const bf16_t* B = (const bf16_t*)g.b + (int64_t)k0 * g.ldb;
+  const v4i_t srda = make_srd(A, (int64_t)max(0, k1 - k0) * g.lda * 2);
+  const v4i_t srdb = make_srd(B, (int64_t)max(0, k1 - k0) * g.ldb * 2);
+  const int a_bytes = TK_ROWS * 64 * 2;                  // A image [32][64]
+  const int ninst = (a_bytes + TK_ROWS * N * 2) / 1024;  // 1-KiB DMA pieces per stage
+  const int opw = (ninst - w + 7) / 8;                   // this wave's pieces per stage
+  const int cpr = N / 8;                                 // 16-B chunks per B row
+  auto issue = [&](int s) {
+    unsigned char* img = lds + (s % 3) * TK_STAGE;
+    const int r0 = s * TK_ROWS;
+    for (int j = w; j < ninst; j += 8) {
+      const int slot = j * 64 + l;   // 16-B slot of the stage image
+      if (slot < a_bytes / 16) {
+        const int row = slot >> 3, c = (slot & 7) ^ (row & 6);
+        dma16_asm(img + j * 1024, srda, (uint32_t)(((r0 + row) * g.lda + c * 8) * 2));
+      } else {
+        const int sb = slot - a_bytes / 16, row = sb / cpr, c = (sb % cpr) ^ (row & 6);
+        dma16_asm(img + j * 1024, srdb, (uint32_t)(((r0 + row) * g.ldb + c * 8) * 2));
+      }
+    }
+  };
+  const int mh = w & 1, nq = w >> 1;
+  f4_t acc[2][9], rs[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    rs[i] = f4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 9; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+  }
+  s8_t ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (short)0x3F80;
+  // fragment addressing: lane reads rows 4 g4 + (li >> 2) (+16) at 8-B column 4 (li & 3) of a 16-column tile;
+  // (row & 6) is the same for both rows
+  const int frow = 4 * g4 + (li >> 2), fsw = frow & 6, fsub = (li >> 1) & 1, fhalf = 4 * (li & 1);
+  if (nsteps > 0) issue(0);
+  if (nsteps > 1) issue(1);
+  for (int s = 0; s < nsteps; ++s) {
+    wait_vmcnt_bs<0, 15>(s + 1 < nsteps ? opw : 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + 2 < nsteps) issue(s + 2);
+    const bf16_t* ia = (const bf16_t*)(lds + (s % 3) * TK_STAGE);
+    const bf16_t* ib = ia + TK_ROWS * 64;
+    s8_t fa[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int mt = 2 * mh + i;
+      const bf16_t* p = ia + frow * 64 + 8 * ((2 * mt + fsub) ^ fsw) + fhalf;
+      const s4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4_t*)p);
+      const s4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4_t*)(p + 16 * 64));
+      fa[i] = s8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const int nt = 9 * nq + j;
+      if (nt < ntt) {   // wave-uniform
+        const bf16_t* p = ib + frow * N + 8 * ((2 * nt + fsub) ^ fsw) + fhalf;
+        const s4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4_t*)p);
+        const s4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4_t*)(p + 16 * N));
+        const s8_t fb = s8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int i = 0; i < 2; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb, acc[i][j], 0, 0, 0);
+      }
+    }
+    if (nq == 0 && g.rowsum) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) rs[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], ones, rs[i], 0, 0, 0);
+    }
+  }
+  // partial slab z: lane holds D[m = 16 mt + 4 g4 + r][n = 16 nt + li]
+  float* ws = g.ws + (int64_t)z * g.M * N;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int m0 = 16 * (2 * mh + i) + 4 * g4;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const int nt = 9 * nq + j;
+      if (nt < ntt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ws[(int64_t)(m0 + r) * N + 16 * nt + li] = acc[i][j][r];
+      }
+    }
+    if (nq == 0 && g.rowsum && li == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) g.rowsum_ws[(int64_t)z * g.M + m0 + r] = rs[i][r];
+    }
+  }
+}
+
+// Split-K finish for many splits: block = 32 output quads x 8 split groups, LDS combine, then the epilogue.
+__global__ __launch_bounds__(256) void tallk_reduce_kernel(GemmArgs g) {
+  __shared__ f4_t red[8][32];
+  const int nq = g.N / 4;
+  const int q = blockIdx.x * 32 + (threadIdx.x & 31), sg = threadIdx.x >> 5;
+  const int quads = g.M * nq;
+  f4_t s = f4_t{0.f, 0.f, 0.f, 0.f};
+  if (q < quads) {
+    const int m = q / nq, n0 = (q % nq) * 4;
+    for (int sp = sg; sp < g.splitk; sp += 8) s += *(const f4_t*)(g.ws + ((int64_t)sp * g.M + m) * g.N + n0);
+  }
+  red[sg][threadIdx.x & 31] = s;
+  __syncthreads();
+  if (sg == 0 && q < quads) {
+#pragma unroll
+    for (int i = 1; i < 8; ++i) s += red[i][threadIdx.x];
+    float v[4] = {s[0], s[1], s[2], s[3]};
+    epilogue4(g, 0, q / nq, (q % nq) * 4, v);
+  }
+}
+
 __global__ __launch_bounds__(256) void rowsum_finish_kernel(const float* ws, int splitk, int M, float* out) {
   const int m = blockIdx.x * 256 + threadIdx.x;
   if (m >= M) return;
@@ -1197,7 +1329,13 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
       else pl.use = (nt_r128 * splitk * batch >= 192 && d->k < 1536) ? 6 : 5;
     }
   }
-  if (pl.use == 1) pl.ntiles = nt_p3;
+  // tall-K weight gradient (conv2 dW: 64 x 576 outputs, ~300k-row reduction): many-split LDS-DMA kernel
+  // (ragged K is fine: rows past a split's end read as zeros)
+  if (pl.vec && kvar == 0 && d->a_trans && d->b_trans && d->m == 64 && d->n % 64 == 0 && d->n <= TK_MAXN &&
+      splitk >= 64 && batch == 1 && d->lda % 8 == 0 && d->ldb % 8 == 0)
+    pl.use = 9;
+  if (pl.use == 9) pl.ntiles = splitk;
+  else if (pl.use == 1) pl.ntiles = nt_p3;
   else if (pl.use == 7) pl.ntiles = ((d->m + 255) / 256) * ((d->n + 255) / 256);
   else if (pl.use == 8) pl.ntiles = ((d->m + 127) / 128) * ((d->n + 255) / 256);
   else if (pl.use == 5) pl.ntiles = ((d->m + 63) / 64) * ((d->n + 63) / 64);
@@ -1218,7 +1356,8 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
           (d->gate ? E_GATE : 0) | (d->resid ? E_RESID : 0) | (d->beta == 1.f ? E_BETA : 0) |
           (d->c_dtype == ASRX_F32 ? E_F32 : 0) | (d->alpha != 1.f ? E_ALPHA : 0) | (d->rowadd ? E_ROWADD : 0);
   }
-  pl.epi = ((pl.use <= 2 || pl.use >= 5) && epi_instantiated(d->a_trans, d->b_trans, epi)) ? epi : E_GENERIC;
+  pl.epi = ((pl.use <= 2 || (pl.use >= 5 && pl.use != 9)) && epi_instantiated(d->a_trans, d->b_trans, epi))
+               ? epi : E_GENERIC;
   return pl;
 }
 
@@ -1234,7 +1373,9 @@ extern "C" int asrx_gemm_kernel_name(const asrx_gemm_desc* d, char* buf, int len
     return ASRX_OK;
   }
   const GemmPlan pl = plan_bf16(d, batch, splitk);
-  if (pl.use == 1 || pl.use == 2)
+  if (pl.use == 9)
+    snprintf(buf, len, "gemm_bf16_tallk_kernel");
+  else if (pl.use == 1 || pl.use == 2)
     snprintf(buf, len, "gemm_bf16_%s_kernel<%s, %s, %d>", pl.use == 1 ? "p3" : "glds", tf[!!d->a_trans],
              tf[!!d->b_trans], pl.epi);
   else if (pl.use == 7 || pl.use == 8)
@@ -1374,6 +1515,8 @@ extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
         const int nt = ((d->m + P_BM - 1) / P_BM) * ((gc.N + P_BN - 1) / P_BN);
         dispatch_p3<false, false>(gc, epi, nt, 1, 1, st);
       }
+    } else if (pl.use == 9) {
+      hipLaunchKernelGGL(gemm_bf16_tallk_kernel, dim3(splitk), dim3(512), 0, st, g);
     } else if (pl.use == 1) {
       if (!d->a_trans && !d->b_trans) dispatch_p3<false, false>(g, epi, pl.ntiles, splitk, batch, st);
       else if (!d->a_trans && d->b_trans) dispatch_p3<false, true>(g, epi, pl.ntiles, splitk, batch, st);
@@ -1417,7 +1560,10 @@ extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
   if (splitk > 1) {
     const int64_t quads = (int64_t)d->m * ((d->n + 3) / 4);
     const int blocks = (int)std::min<int64_t>((quads + 255) / 256, 4096);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, g);
+    if (d->in_dtype == ASRX_BF16 && plan_bf16(d, batch, splitk).use == 9)
+      hipLaunchKernelGGL(tallk_reduce_kernel, dim3((unsigned)((quads + 31) / 32)), dim3(256), 0, st, g);
+    else
+      hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, g);
     ASRX_CHECK_LAUNCH();
     if (g.rowsum) {
       hipLaunchKernelGGL(rowsum_finish_kernel, dim3((d->m + 255) / 256), dim3(256), 0, st, g.rowsum_ws, splitk,

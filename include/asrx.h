@@ -223,7 +223,7 @@ int asrx_conv1_bwd_w(const float* x, const float* dy1, int32_t B, int32_t F, int
 /* Fused conv1 backward (dW1 += sum dy1 * x-taps, db1 += sum dy1) straight from the conv2 column gradient:
  * dy1 = relu'(y1) * col2im(dcols) is formed on the fly and never stored (replaces col2im + conv1_bwd_w on the
  * training path; model.py:168-169).  nblocks = ceil(B * F1 * 8 / 4) (8 waves per conv1 output row), part:
- * [nblocks][640] workspace. */
+ * [nblocks + 128][640] workspace (per-block partials, then the finish's first-pass rows). */
 int asrx_conv1_bwd_fused(int32_t dcols_dtype, const void* dcols, int32_t y1_dtype, const void* y1, const float* x,
                          int32_t B, int32_t F, int32_t T, float* part, int32_t nblocks, float* dw, float* db,
                          void* stream);

@@ -165,6 +165,31 @@ def test_gemm_grouped_wgrad(ngroups, wkind, xcd, monkeypatch):
             assert relerr(bg, rb) < 1e-5
 
 
+@pytest.mark.parametrize("rows,n", [(302784, 576), (40000, 576), (16384 + 37, 128), (70001, 512)])
+@pytest.mark.parametrize("with_bias", [True, False])
+def test_linear_wgrad_tallk(rows, n, with_bias):
+    """conv2-shaped weight gradient dW[64, n] += dy^T x over a very tall reduction (the many-split tall-K kernel,
+    plan use 9): ragged split ends, fused bias gradient, beta=1 accumulation."""
+    g = torch.Generator(device=dev).manual_seed(rows + n)
+    dy = bf(torch.randn(rows, 64, device=dev, generator=g))
+    x = bf(torch.randn(rows, n, device=dev, generator=g))
+    wg = torch.randn(64, n, device=dev, generator=g)
+    bg = torch.randn(64, device=dev, generator=g) if with_bias else None
+    ref = wg.double() + dy.double().t() @ x.double()
+    rb = None if bg is None else bg.double() + dy.double().sum(0)
+    tile, splitk = K().wgrad_plan(64, n, rows)
+    assert splitk == 256
+    from asrx._lib import GemmDesc
+    d = GemmDesc(64, n, rows, 0, dy.data_ptr(), 64, 1, x.data_ptr(), n, 1, wg.data_ptr(), n, 1)
+    d.splitk = splitk
+    assert K().kernel_name(d) == "gemm_bf16_tallk_kernel"
+    K().linear_wgrad(dy, x, wg, bias_grad=bg)
+    torch.cuda.synchronize()
+    assert relerr(wg, ref) < 1e-5
+    if bg is not None:
+        assert relerr(bg, rb) < 1e-5
+
+
 def test_gemm_batched_heads():
     """Two-level batch strides as used by the unfused attention: z = b*H + h."""
     Bn, H, L, dh = 3, 4, 37, 32
@@ -427,9 +452,10 @@ def test_softmax_masked(dtype, Lk):
 
 # ------------------------------------------------------------------------------------------------ front-end
 
+@pytest.mark.parametrize("T", [61, 1000])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_conv_frontend(dtype):
-    B, F, T = 2, 80, 61
+def test_conv_frontend(dtype, T):
+    B, F = 2, 80
     g = torch.Generator().manual_seed(5)
     x = torch.randn(B, 1, F, T, generator=g)
     w1 = torch.randn(64, 1, 3, 3, generator=g) * 0.3

@@ -3,15 +3,11 @@ set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-L=asr-transformer_amd/asrx/lib
-timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread -m gpu -k "attention or attn" > gpurun_out/pt.log 2>&1 || { tail -40 gpurun_out/pt.log; exit 1; }
-tail -1 gpurun_out/pt.log
-for i in 1 2; do
-  for v in libasrx_old.so libasrx.so; do
-    echo "== $v"
-    ASRX_LIB=$L/$v timeout -k 10 300 python tools/attn_bench.py > gpurun_out/ab.log 2>&1 || { cat gpurun_out/ab.log; exit 1; }
-    grep -v amdgpu.ids gpurun_out/ab.log
-  done
-done
-timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/pmc_l2 -o run --output-format csv -- python3 tools/gemm_probe.py --variant p3 --shapes fwd:15936x1536x512,dgrad:15936x512x1536 --rounds 1 --reps 3 > gpurun_out/pmc.log 2>&1 || { tail -5 gpurun_out/pmc.log; exit 1; }
-grep -v amdgpu.ids gpurun_out/pmc.log | grep -v "^W2026\|^E2026" | tail -3
+timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread -m gpu -k "tallk or conv_frontend or wgrad or frontend" > gpurun_out/pt.log 2>&1 || { tail -40 gpurun_out/pt.log; exit 1; }
+tail -2 gpurun_out/pt.log
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_fe -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-probe --no-sub > gpurun_out/b.log 2>&1 || { tail -5 gpurun_out/b.log; exit 1; }
+grep -o '"ms_per_step": [0-9.]*' gpurun_out/b.log
+f=$(find gpurun_out/prof_fe -name '*kernel_stats.csv' | head -1)
+grep -i "conv1\|tallk\|im2col\|reduce\|gemm_bf16_kernel<64" "$f" | cut -d, -f1-4
+timeout -k 10 600 python -u -m pytest tests/test_gpu_model.py -x -q --timeout 300 --timeout-method thread -m gpu > gpurun_out/pm.log 2>&1 || { tail -40 gpurun_out/pm.log; exit 1; }
+tail -2 gpurun_out/pm.log
