@@ -8,6 +8,7 @@ plain dict `S`.
 Reference call sites (modules/Transformer): pre-LN sublayers model.py:18-25 / 65-75; MHA layers.py:15-40;
 FeedForward layers.py:53-58; front-end model.py:168-171 + 41-47; decoder embedding model.py:117.
 """
+import bisect
 import math
 import os
 
@@ -15,6 +16,53 @@ import torch
 
 from . import kernels as K
 from .kernels import MaskSpec
+
+
+class FreshGrads:
+    """Weight-gradient regions of the flat fp32 gradient buffer that a training step leaves UNZEROED because their
+    only writer is one weight-gradient GEMM (asrx.train.Trainer): the first GEMM that covers such a region exactly
+    writes it with beta = 0 (no zero fill before, no read of C inside); any other writer first zeroes the fresh
+    regions it overlaps.  Whatever no writer claimed is zeroed by drain()."""
+
+    def __init__(self, store, params):
+        self.grad = store.grad
+        self.base = store.grad.data_ptr()
+        ent = sorted((store.offset(p), p.numel()) for p in params)
+        self.offs = [o for o, _ in ent]
+        self.live = dict(ent)
+
+    def take(self, gw):
+        """True: gw covers only fresh regions, exactly (write with beta 0); they are claimed.  False: the fresh
+        regions gw overlaps (if any) are zeroed and claimed (accumulate with beta 1)."""
+        if not self.live:
+            return False
+        a = (gw.data_ptr() - self.base) // 4
+        rows, cols = (gw.shape[0], gw.shape[1]) if gw.dim() == 2 else (1, gw.numel())
+        ld = gw.stride(0) if gw.dim() == 2 else cols
+        b = a + (rows - 1) * ld + cols
+        i = bisect.bisect_left(self.offs, a)
+        if i > 0 and self.offs[i - 1] + self.live.get(self.offs[i - 1], 0) > a:
+            i -= 1
+        hit = []
+        while i < len(self.offs) and self.offs[i] < b:
+            o = self.offs[i]
+            if o in self.live:
+                hit.append(o)
+            i += 1
+        if not hit:
+            return False
+        full = (ld == cols and (gw.dim() < 2 or gw.stride(1) == 1) and hit[0] == a
+                and sum(self.live[o] for o in hit) == b - a)
+        for o in hit:
+            n = self.live.pop(o)
+            if not full:
+                self.grad[o:o + n].zero_()
+        return full
+
+    def drain(self):
+        for o, n in self.live.items():
+            self.grad[o:o + n].zero_()
+        self.live.clear()
 
 
 class Ctx:
@@ -29,6 +77,7 @@ class Ctx:
         self.attn_impl = attn_impl
         self.wq = None                  # list -> weight gradients are queued and issued grouped (flush_wgrad)
         self.lnq = None                 # list -> LayerNorm dgamma|dbeta partials queued for one grouped reduce
+        self.fresh = None               # FreshGrads of a Trainer step (unzeroed weight-gradient regions)
 
     def W(self, p):
         return self.store.w16(p) if self.cd == torch.bfloat16 else self.store.w32(p)
@@ -51,7 +100,20 @@ class Ctx:
         if self.wq is not None and K.wgrad_groupable(dy, x, gw):
             self.wq.append((dy, x, gw, gb))
         else:
-            K.linear_wgrad(dy, x, gw, bias_grad=gb)
+            first = self.fresh is not None and self.fresh.take(gw)
+            K.linear_wgrad(dy, x, gw, bias_grad=gb, beta=0.0 if first else 1.0)
+
+    def _issue_wgrads(self, q):
+        """One grouped launch for the queued weight gradients; with fresh (unzeroed) targets the first writes go
+        in a beta = 0 launch ahead of the accumulating one."""
+        if self.fresh is None:
+            K.linear_wgrad_grouped(q)
+            return
+        q0, q1 = [], []
+        for it in q:
+            (q0 if self.fresh.take(it[2]) else q1).append(it)
+        K.linear_wgrad_grouped(q0, beta=0.0)
+        K.linear_wgrad_grouped(q1)
 
     def defer_wgrad(self):
         if self.cd == torch.bfloat16 and self.wq is None:
@@ -62,7 +124,7 @@ class Ctx:
     def flush_wgrad(self):
         q, self.wq = self.wq, None
         lq, self.lnq = self.lnq, None
-        K.linear_wgrad_grouped(q or [])
+        self._issue_wgrads(q or [])
         K.reduce_rows_grouped(lq or [])
         side = getattr(self, "_wside", None)
         if side is not None:          # weight gradients issued on the side stream are final only after it
@@ -83,7 +145,7 @@ class Ctx:
             dy.record_stream(side)
             x.record_stream(side)
         with torch.cuda.stream(side):
-            K.linear_wgrad_grouped(q)
+            self._issue_wgrads(q)
         self._wside = side
 
 

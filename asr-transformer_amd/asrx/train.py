@@ -7,11 +7,34 @@ same metrics dict) for drop-in use with any torch optimizer and loss.
 bucketed gradient all-reduce -> fused AdamW over the flat parameter buffer (which also refreshes the bf16
 operand copy).  No autograd graph, no per-parameter launches.
 """
+import os
+
 import torch
 
 from . import kernels as K
+from .blocks import FreshGrads
 from .dist import GradAllReduce
 from .functions import get_store, make_ctx, model_backward, model_forward
+
+# weight gradients whose only writer is one weight-gradient GEMM are not zeroed before the backward: that GEMM
+# writes them with beta = 0 (blocks.FreshGrads).  ASRX_FRESH_GRADS=0 zeroes the whole buffer instead (A/B).
+FRESH_GRADS = os.environ.get("ASRX_FRESH_GRADS", "1") == "1"
+
+
+def wgrad_only_params(model):
+    """Parameters written only by a weight-gradient GEMM: the Linear weights (incl. the packed Q/K/V and K/V
+    projections and the classifier).  Biases (fused row sums accumulate), LayerNorm, embedding and conv
+    parameters have accumulating writers and are zeroed each step."""
+    from .layers import MHA, _Lin
+    from .model import _Classifier
+    out = []
+    for m in model.modules():
+        if isinstance(m, (_Lin, _Classifier)):
+            out.append(m.weight)
+        elif isinstance(m, MHA):
+            out += [p for p in (getattr(m, "wq", None), getattr(m, "wkv", None), getattr(m, "wqkv", None))
+                    if p is not None]
+    return out
 
 
 def train_epoch(model, data_loader, loss_function, optimizer, device):
@@ -84,6 +107,13 @@ class Trainer:
         self.step_count = 0
         self.reducer = GradAllReduce(self.store.grad, group=group, bucket_mb=bucket_mb, allreduce_fn=allreduce_fn)
         self.store.refresh_shadow(force=True)
+        self._wonly = wgrad_only_params(model) if FRESH_GRADS else []
+        if self._wonly:   # flat indices of everything else (zeroed each step by one index_fill)
+            keep = torch.ones(self.store.grad.numel(), dtype=torch.bool)
+            for p in self._wonly:
+                o = self.store.offset(p)
+                keep[o:o + p.numel()] = False
+            self._zero_idx = keep.nonzero().squeeze(1).to(self.store.grad.device)
 
     def forward_backward(self, spectrum, text, mask):
         """text: (B, L+1) with BOS ... ; inputs text[:, :-1], targets text[:, 1:] (train.py:24,32)."""
@@ -93,9 +123,16 @@ class Trainer:
         V = model.decoder._classifier.V
         tgt = text[:, 1:].reshape(-1).contiguous()
         loss, dl, _ = K.cross_entropy(logits, V, tgt, ignore_index=self.ignore_index)
-        self.store.grad.zero_()
+        if self._wonly and C.cd == torch.bfloat16 and all(p.grad is not None for p in self.store.params):
+            self.store.grad.index_fill_(0, self._zero_idx, 0.0)
+            C.fresh = FreshGrads(self.store, self._wonly)
+        else:
+            self.store.grad.zero_()
         model_backward(C, model, S, dl.to(C.cd) if dl.dtype != C.cd else dl,
                        ready=self.reducer.ready if self.reducer.active else None)
+        if C.fresh is not None:
+            C.fresh.drain()
+            C.fresh = None
         return loss
 
     def step(self, spectrum, text, mask):

@@ -224,6 +224,31 @@ def test_submodule_grads_fp32():
     assert relerr(xd2.grad, xr2.grad) < 1e-3
 
 
+@pytest.mark.parametrize("cfgname", ["micro", "c2"])
+def test_trainer_fresh_grads_match_zeroed(cfgname):
+    """Trainer steps leave the Linear-weight gradients unzeroed and write them with beta = 0 (FreshGrads): the
+    gradients must equal, bit for bit, those of a step that zeroes the whole buffer first (dropout 0, no
+    optimizer step in between)."""
+    from asrx.train import Trainer
+    m, cfg = build(cfgname, "bf16", dropout=0.0)
+    m.train()
+    spec = CONFIGS[cfgname]
+    s, t, k = synthetic_batch(cfg, spec["batch"], spec["frames"], spec["text_len"] + 1, seed=11)
+    s, t, k = s.to(dev), t.to(dev), k.to(dev)
+    tr = Trainer(m)
+    assert tr._wonly
+    tr.store.grad.fill_(float("nan"))        # stale garbage in the unzeroed regions must never leak through
+    tr.forward_backward(s, t, k)              # first step: binds grads, zeroes everything
+    tr.store.grad.fill_(float("nan"))
+    tr.forward_backward(s, t, k)              # fresh mode
+    g_fresh = tr.store.grad.clone()
+    assert torch.isfinite(g_fresh).all()
+    tr._wonly = []
+    tr.store.grad.fill_(float("nan"))
+    tr.forward_backward(s, t, k)              # whole-buffer zero
+    assert torch.equal(g_fresh, tr.store.grad)
+
+
 def test_bf16_training_reduces_loss():
     """A few bf16 AdamW steps (dropout 0.1) on one c1 batch drive the loss down."""
     import asrx
