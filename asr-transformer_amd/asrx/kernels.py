@@ -601,6 +601,25 @@ def col2im_conv2(dcols, y1, dy1):
          stream())
 
 
+def conv2_fwd(y1, w2, bias, out):
+    """out[B*T2*F2, 64] (bf16) = relu(conv2(y1) + bias), an implicit GEMM over y1 (B, F1, T1, 64) channels-last
+    bf16; w2: [64][576] bf16 with columns (kh, kw, c)."""
+    _cuda(y1, w2, bias, out)
+    B, F1, T1, _ = y1.shape
+    call("asrx_conv2_fwd", y1.data_ptr(), w2.data_ptr(), bias.data_ptr(), out.data_ptr(), B, F1, T1, stream())
+
+
+def conv2_wgrad(dy2, y1, dw, db, splitk=256):
+    """dw[64][576] += dy2^T im2col(y1), db[64] += colsum(dy2) (fp32 grads) with the im2col rows gathered from y1
+    (B, F1, T1, 64) bf16 on the fly (tall-K kernel, `splitk` row splits)."""
+    _cuda(dy2, y1, dw, db)
+    B, F1, T1, _ = y1.shape
+    ws = torch.empty(splitk * 64 * 576, device=dy2.device, dtype=torch.float32)
+    rws = torch.empty(splitk * 64, device=dy2.device, dtype=torch.float32) if db is not None else None
+    call("asrx_conv2_wgrad", dy2.data_ptr(), y1.data_ptr(), B, F1, T1, dw.data_ptr(), _p(db), ws.data_ptr(),
+         ws.numel(), _p(rws), splitk, stream())
+
+
 def conv1_bwd_w(x, dy1, dw, db):
     _cuda(x, dy1, dw, db)
     B, _, F, T = x.shape

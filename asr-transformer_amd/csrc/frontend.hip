@@ -7,7 +7,10 @@
 //   embedding       : model.py:94-96,117 (nn.Embedding(padding_idx) + PE + dropout).
 //   cross-entropy   : train.py:32 (caller-supplied CE, mean reduction).
 //   Adam            : train.py:35 (caller-supplied optimizer; fused over the flat parameter buffer).
+#include <algorithm>
+
 #include "common.h"
+#include "gemm_common.h"
 
 namespace {
 
@@ -61,6 +64,120 @@ __global__ __launch_bounds__(256) void conv1_fwd_row_kernel(const float* __restr
     } else {
       *(f4_t*)(yr + (int64_t)t1 * C1) = f4_t{o[0], o[1], o[2], o[3]};
       *(f4_t*)(yr + (int64_t)t1 * C1 + 4) = f4_t{o[4], o[5], o[6], o[7]};
+    }
+  }
+}
+
+// conv2 as an implicit GEMM (no im2col image): out[row][co] = relu(bias[co] + sum_{tap, ci} y1[b, 2f2+kh,
+// 2t2+kw, ci] W2[co][tap*64 + ci]), rows (b, t2, f2).  Persistent workgroups (8 waves) walk 256-row tiles; the
+// K loop is the 9 taps: each stage = the tile's 256 gathered y1 rows of one tap (128 B each, one 8-lane piece
+// per row) + that tap's [64 co][64 ci] weight slice, both by LDS-DMA into 16-B-chunk XOR-swizzled images
+// (conflict-free ds_read_b128 fragment reads), 3-stage ring with counted vmcnt waits.  The MFMA computes the
+// transposed tile (weights as the A operand) so each lane ends with 4 consecutive output channels of a row:
+// 8-byte stores with bias + ReLU fused.
+constexpr int C2_ROWS = 256;
+constexpr int C2_ABYTES = C2_ROWS * 64 * 2;          // 32 KiB
+constexpr int C2_STAGE = C2_ABYTES + 64 * 64 * 2;    // + 8 KiB weight slice
+
+__global__ __launch_bounds__(512) void conv2_fwd_kernel(const bf16_t* __restrict__ y1, const bf16_t* __restrict__ w2,
+                                                        const float* __restrict__ bias, bf16_t* __restrict__ out,
+                                                        int M, int F1, int T1, int F2, int T2, int ntiles,
+                                                        int64_t y1_bytes) {
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[3 * C2_STAGE];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, li = l & 15;
+  const int G = gridDim.x;
+  const int mytiles = blockIdx.x < ntiles ? (ntiles - 1 - blockIdx.x) / G + 1 : 0;
+  const int total = mytiles * 9;
+  const asrxg::v4i_t srdy = asrxg::make_srd(y1, y1_bytes);
+  const asrxg::v4i_t srdw = asrxg::make_srd(w2, 64 * 576 * 2);
+  // issue cursor: y1 position base of this lane's row in each of its 4 pieces (rows 8 (w + 8 i) + (l >> 3))
+  int ibase[4];
+  int itile = -1;
+  auto issue = [&](int s) {
+    const int tl = s / 9, tap = s % 9, kh = tap / 3, kw = tap % 3;
+    const int tile = blockIdx.x + tl * G;
+    if (tile != itile) {
+      itile = tile;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = tile * C2_ROWS + 8 * (w + 8 * i) + (l >> 3);
+        const int f2 = row % F2, q = row / F2, t2 = q % T2, b = q / T2;
+        ibase[i] = row < M ? ((b * F1 + 2 * f2) * T1 + 2 * t2) : -1;
+      }
+    }
+    unsigned char* img = lds + (s % 3) * C2_STAGE;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = w + 8 * i, row = 8 * j + (l >> 3), c = (l & 7) ^ (row & 7);
+      const uint32_t voff = ibase[i] < 0 ? 0x80000000u
+                                         : (uint32_t)(((ibase[i] + kh * T1 + kw) * 64 + c * 8) * 2);
+      asrxg::dma16_asm(img + j * 1024, srdy, voff);
+    }
+    {   // weight slice: piece w = output channels 8 w .. 8 w + 7
+      const int co = 8 * w + (l >> 3), c = (l & 7) ^ (co & 7);
+      asrxg::dma16_asm(img + C2_ABYTES + w * 1024, srdw, (uint32_t)((co * 576 + tap * 64 + c * 8) * 2));
+    }
+  };
+  // bias through LDS: its global load completes before the first DMA is issued (a compiler-visible load used
+  // only in the epilogue would get a full vmcnt(0) there, draining the ring)
+  __shared__ __attribute__((aligned(16))) float sbias[64];
+  if (threadIdx.x < 64) sbias[threadIdx.x] = bias[threadIdx.x];
+  f4_t acc[4][2];
+  if (total > 0) issue(0);
+  if (total > 1) issue(1);
+  // younger-operation ledger: stage s was issued in iteration s - 2; after it came that iteration's epilogue
+  // stores (if any), stage s + 1 (5 pieces) and iteration s - 1's stores.  Stores are counted only where every
+  // lane of the wave stores (a lower bound over-waits, never under-waits).
+  int st1 = 0, st2 = 0;
+  for (int s = 0; s < total; ++s) {
+    asrxg::wait_vmcnt_bs<0, 31>(st2 + (s + 1 < total ? 5 : 0) + st1);
+    st2 = st1;
+    st1 = 0;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + 2 < total) issue(s + 2);
+    const int tap = s % 9;
+    if (tap == 0) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) acc[nt][0] = acc[nt][1] = f4_t{0.f, 0.f, 0.f, 0.f};
+    }
+    const bf16_t* ia = (const bf16_t*)(lds + (s % 3) * C2_STAGE);
+    const bf16_t* iw = ia + C2_ROWS * 64;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      s8_t fa[2], fw[4];
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) {
+        const int row = 32 * w + 16 * mi + li;
+        fa[mi] = *(const s8_t*)(ia + row * 64 + 8 * ((4 * kk + g) ^ (row & 7)));
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int co = 16 * nt + li;
+        fw[nt] = *(const s8_t*)(iw + co * 64 + 8 * ((4 * kk + g) ^ (co & 7)));
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+          acc[nt][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[nt], fa[mi], acc[nt][mi], 0, 0, 0);
+    }
+    if (tap == 8) {   // lane: channels 16 nt + 4 g + r of row 32 w + 16 mi + li
+      const int tile = blockIdx.x + (s / 9) * G;
+      st1 = tile * C2_ROWS + 32 * w + 31 < M ? 8 : 0;
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) {
+        const int row = tile * C2_ROWS + 32 * w + 16 * mi + li;
+        if (row >= M) continue;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          const f4_t bv = *(const f4_t*)(sbias + 16 * nt + 4 * g);
+          uint2 u;
+          u.x = pack2bf(fmaxf(acc[nt][mi][0] + bv[0], 0.f), fmaxf(acc[nt][mi][1] + bv[1], 0.f));
+          u.y = pack2bf(fmaxf(acc[nt][mi][2] + bv[2], 0.f), fmaxf(acc[nt][mi][3] + bv[3], 0.f));
+          *(uint2*)(out + (int64_t)row * 64 + 16 * nt + 4 * g) = u;
+        }
+      }
     }
   }
 }
@@ -627,6 +744,22 @@ extern "C" int asrx_conv1_fwd(const float* x, int32_t B, int32_t F, int32_t T, c
   else
     hipLaunchKernelGGL(conv1_fwd_row_kernel<bf16_t>, grid, dim3(256), shm, (hipStream_t)stream, x, F, T, F1, T1, w,
                        b, (bf16_t*)y1);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
+extern "C" int asrx_conv2_fwd(const void* y1, const void* w2, const float* bias, void* out, int32_t B, int32_t F1,
+                              int32_t T1, void* stream) {
+  if (!y1 || !w2 || !bias || !out || B <= 0 || F1 < 3 || T1 < 3) return ASRX_ERR_ARG;
+  if (((uintptr_t)y1 | (uintptr_t)w2 | (uintptr_t)out) % 16) return ASRX_ERR_ARG;
+  const int F2 = (F1 - 3) / 2 + 1, T2 = (T1 - 3) / 2 + 1;
+  const int64_t y1_bytes = (int64_t)B * F1 * T1 * 64 * 2;
+  const int64_t M = (int64_t)B * T2 * F2;
+  if (y1_bytes >= 0x80000000LL || M >= 0x7fffffffLL) return ASRX_ERR_UNSUPPORTED;   // 32-bit DMA offsets
+  const int ntiles = (int)((M + C2_ROWS - 1) / C2_ROWS);
+  hipLaunchKernelGGL(conv2_fwd_kernel, dim3(std::min(ntiles, 256)), dim3(512), 0, (hipStream_t)stream,
+                     (const bf16_t*)y1, (const bf16_t*)w2, bias, (bf16_t*)out, (int)M, F1, T1, F2, T2, ntiles,
+                     y1_bytes);
   ASRX_CHECK_LAUNCH();
   return ASRX_OK;
 }

@@ -1128,7 +1128,14 @@ constexpr int TK_ROWS = 32;
 constexpr int TK_MAXN = 576;
 constexpr int TK_STAGE = TK_ROWS * (64 + TK_MAXN) * 2;   // 40 KiB
 
-__global__ __launch_bounds__(512) void gemm_bf16_tallk_kernel(GemmArgs g) {
+// conv2 gather mode (cv.on): B rows are the conv2 im2col rows gathered straight from the channels-last conv1
+// output y1 (g.b): chunk c of row (b, t2, f2) = tap c / 8 (kh, kw), channels 8 (c % 8) .. +7.
+struct TallkConv {
+  int on, F1, T1, F2, T2;
+  int64_t y1_bytes;
+};
+
+__global__ __launch_bounds__(512) void gemm_bf16_tallk_kernel(GemmArgs g, TallkConv cv) {
   __shared__ __attribute__((aligned(1024))) unsigned char lds[3 * TK_STAGE];
   const int z = blockIdx.x, w = threadIdx.x >> 6, l = threadIdx.x & 63, g4 = l >> 4, li = l & 15;
   const int N = g.N, ntt = N >> 4;
@@ -1137,7 +1144,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tallk_kernel(GemmArgs g) {
   const bf16_t* A = (const bf16_t*)g.a + (int64_t)k0 * g.lda;
   const bf16_t* B = (const bf16_t*)g.b + (int64_t)k0 * g.ldb;
   const v4i_t srda = make_srd(A, (int64_t)max(0, k1 - k0) * g.lda * 2);
-  const v4i_t srdb = make_srd(B, (int64_t)max(0, k1 - k0) * g.ldb * 2);
+  const v4i_t srdb = cv.on ? make_srd(g.b, cv.y1_bytes) : make_srd(B, (int64_t)max(0, k1 - k0) * g.ldb * 2);
   const int a_bytes = TK_ROWS * 64 * 2;                  // A image [32][64]
   const int ninst = (a_bytes + TK_ROWS * N * 2) / 1024;  // 1-KiB DMA pieces per stage
   const int opw = (ninst - w + 7) / 8;                   // this wave's pieces per stage
@@ -1145,6 +1152,15 @@ __global__ __launch_bounds__(512) void gemm_bf16_tallk_kernel(GemmArgs g) {
   auto issue = [&](int s) {
     unsigned char* img = lds + (s % 3) * TK_STAGE;
     const int r0 = s * TK_ROWS;
+    // gather mode: (b, t2, f2) of the stage's first row once; a lane's row (first + dr, dr < 32) by carries
+    int f20 = 0, t20 = 0, b0 = 0;
+    if (cv.on) {
+      const int gr0 = k0 + r0;
+      f20 = gr0 % cv.F2;
+      const int q = gr0 / cv.F2;
+      t20 = q % cv.T2;
+      b0 = q / cv.T2;
+    }
     for (int j = w; j < ninst; j += 8) {
       const int slot = j * 64 + l;   // 16-B slot of the stage image
       if (slot < a_bytes / 16) {
@@ -1152,7 +1168,22 @@ __global__ __launch_bounds__(512) void gemm_bf16_tallk_kernel(GemmArgs g) {
         dma16_asm(img + j * 1024, srda, (uint32_t)(((r0 + row) * g.lda + c * 8) * 2));
       } else {
         const int sb = slot - a_bytes / 16, row = sb / cpr, c = (sb % cpr) ^ (row & 6);
-        dma16_asm(img + j * 1024, srdb, (uint32_t)(((r0 + row) * g.ldb + c * 8) * 2));
+        uint32_t voff;
+        if (!cv.on) {
+          voff = (uint32_t)(((r0 + row) * g.ldb + c * 8) * 2);
+        } else {
+          const int gr = k0 + r0 + row;
+          if (gr >= k1) {
+            voff = 0x80000000u;   // past the split: reads as zeros
+          } else {
+            int f2 = f20 + row, t2 = t20, b = b0;
+            while (f2 >= cv.F2) { f2 -= cv.F2; ++t2; }
+            while (t2 >= cv.T2) { t2 -= cv.T2; ++b; }
+            const int tap = c >> 3, kh = (tap * 11) >> 5, kw = tap - 3 * kh;   // tap / 3 for tap <= 8
+            voff = (uint32_t)(((((b * cv.F1 + 2 * f2 + kh) * cv.T1 + 2 * t2 + kw) * 64) + (c & 7) * 8) * 2);
+          }
+        }
+        dma16_asm(img + j * 1024, srdb, voff);
       }
     }
   };
@@ -1516,7 +1547,7 @@ extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
         dispatch_p3<false, false>(gc, epi, nt, 1, 1, st);
       }
     } else if (pl.use == 9) {
-      hipLaunchKernelGGL(gemm_bf16_tallk_kernel, dim3(splitk), dim3(512), 0, st, g);
+      hipLaunchKernelGGL(gemm_bf16_tallk_kernel, dim3(splitk), dim3(512), 0, st, g, TallkConv{0, 0, 0, 0, 0, 0});
     } else if (pl.use == 1) {
       if (!d->a_trans && !d->b_trans) dispatch_p3<false, false>(g, epi, pl.ntiles, splitk, batch, st);
       else if (!d->a_trans && d->b_trans) dispatch_p3<false, true>(g, epi, pl.ntiles, splitk, batch, st);
@@ -1596,5 +1627,35 @@ extern "C" int asrx_gemm_grouped_xcd(const asrx_gemm_desc* common, const asrx_ge
     return ASRX_ERR_UNSUPPORTED;
   }
   ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
+extern "C" int asrx_conv2_wgrad(const void* dy2, const void* y1, int32_t B, int32_t F1, int32_t T1, float* dw,
+                                float* db, float* ws, int64_t ws_elems, float* rws, int32_t splitk, void* stream) {
+  if (!dy2 || !y1 || !dw || !ws || B <= 0 || F1 < 3 || T1 < 3 || splitk < 1 || splitk > 65535) return ASRX_ERR_ARG;
+  if (((uintptr_t)dy2 | (uintptr_t)y1) % 16 || (db && !rws)) return ASRX_ERR_ARG;
+  if (ws_elems < (int64_t)splitk * 64 * 576) return ASRX_ERR_ARG;
+  const int F2 = (F1 - 3) / 2 + 1, T2 = (T1 - 3) / 2 + 1;
+  const int64_t y1_bytes = (int64_t)B * F1 * T1 * 64 * 2;
+  const int64_t rows = (int64_t)B * T2 * F2;
+  if (y1_bytes >= 0x80000000LL || rows * 128 >= 0x80000000LL) return ASRX_ERR_UNSUPPORTED;   // 32-bit offsets
+  GemmArgs g = {};
+  g.M = 64; g.N = 576; g.K = (int)rows;
+  g.a = dy2; g.lda = 64; g.b = y1; g.ldb = 576;
+  g.c = dw; g.ldc = 576; g.c_dtype = ASRX_F32;
+  g.batch_inner = 1; g.alpha = 1.f; g.beta = 1.f; g.rowadd_mod = 1; g.cvec = 1;
+  g.splitk = splitk;
+  g.k_per_split = (int)(((rows + BK - 1) / BK + splitk - 1) / splitk) * BK;
+  g.ws = ws; g.rowsum = db; g.rowsum_ws = rws;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(gemm_bf16_tallk_kernel, dim3(splitk), dim3(512), 0, st, g,
+                     TallkConv{1, F1, T1, F2, T2, y1_bytes});
+  ASRX_CHECK_LAUNCH();
+  hipLaunchKernelGGL(tallk_reduce_kernel, dim3((64 * 576 / 4 + 31) / 32), dim3(256), 0, st, g);
+  ASRX_CHECK_LAUNCH();
+  if (db) {
+    hipLaunchKernelGGL(rowsum_finish_kernel, dim3(1), dim3(256), 0, st, (const float*)rws, splitk, 64, db);
+    ASRX_CHECK_LAUNCH();
+  }
   return ASRX_OK;
 }

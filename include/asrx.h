@@ -214,6 +214,16 @@ int asrx_reduce_rows_grouped(const asrx_rowsum_group* groups, int32_t count, voi
  * ------------------------------------------------------------------------------------------------- */
 int asrx_conv1_fwd(const float* x, int32_t B, int32_t F, int32_t T, const float* w, const float* b, void* y1,
                    int32_t y_dtype, void* stream);
+/* conv2 (Conv2d(64,64,3,s2) + bias + ReLU, model.py:170-171) as an implicit GEMM over the channels-last conv1
+ * output y1 (B, F1, T1, 64) bf16, no im2col image: out[(b*T2 + t2)*F2 + f2][64] bf16 — the encoder input rows.
+ * w2: [64][576] bf16, columns (kh, kw, c); bias fp32 [64].  y1 must be < 2 GiB (32-bit DMA offsets). */
+int asrx_conv2_fwd(const void* y1, const void* w2, const float* bias, void* out, int32_t B, int32_t F1, int32_t T1,
+                   void* stream);
+/* conv2 weight/bias gradient (+=, fp32) without an im2col image: dw[64][576] += dy2^T im2col(y1), db[64] +=
+ * colsum(dy2); dy2 [B*T2*F2][64] bf16, y1 (B, F1, T1, 64) bf16.  ws: >= splitk*64*576 floats, rws: splitk*64
+ * floats (when db).  model.py:170 Conv2d backward. */
+int asrx_conv2_wgrad(const void* dy2, const void* y1, int32_t B, int32_t F1, int32_t T1, float* dw, float* db,
+                     float* ws, int64_t ws_elems, float* rws, int32_t splitk, void* stream);
 int asrx_im2col_conv2(int32_t dtype, const void* y1, int32_t B, int32_t F1, int32_t T1, void* cols, void* stream);
 int asrx_col2im_conv2(int32_t dcols_dtype, const void* dcols, int32_t y1_dtype, const void* y1, int32_t B,
                       int32_t F1, int32_t T1, float* dy1, void* stream);

@@ -477,6 +477,13 @@ def test_conv_frontend(dtype, T):
     ref2 = torch.nn.functional.conv2d(y1r, w2.to(dtype).double(), stride=2)        # (B,64,F2,T2)
     got = y2.cpu().view(B, T2, F2, 64).permute(0, 3, 2, 1)
     assert relerr(got, ref2) < tol
+    if dtype == torch.bfloat16:   # implicit-GEMM conv2 (no im2col image), bias + ReLU fused
+        b2 = torch.randn(64, generator=g) * 0.1
+        y2i = torch.full((B * T2 * F2, 64), float("nan"), device=dev, dtype=dtype)
+        K().conv2_fwd(y1, w2p, b2.to(dev), y2i)
+        refi = torch.relu(ref2 + b2.double().view(1, 64, 1, 1))
+        goti = y2i.float().cpu().view(B, T2, F2, 64).permute(0, 3, 2, 1)
+        assert relerr(goti, refi) < tol
     # backward: dcols -> col2im (ReLU gate) and conv1 weight grads
     y1g = y1r.clone().requires_grad_(True)
     out2 = torch.nn.functional.conv2d(y1g, w2.to(dtype).double(), stride=2)
@@ -485,6 +492,14 @@ def test_conv_frontend(dtype, T):
     dy2 = gy.permute(0, 3, 2, 1).reshape(B * T2 * F2, 64).to(dev, dtype)
     dcols = torch.empty(B * T2 * F2, 576, device=dev, dtype=dtype)
     K().gemm(dy2, w2p, dcols, B * T2 * F2, 576, 64, lda=64, ldb=576, ldc=576, b_trans=True)
+    if dtype == torch.bfloat16:   # conv2 weight/bias gradient with the im2col rows gathered from y1
+        dw2 = torch.randn(64, 576, device=dev)
+        db2 = torch.randn(64, device=dev)
+        rw = dw2.double() + dy2.double().t() @ cols.double()
+        rb = db2.double() + dy2.double().sum(0)
+        K().conv2_wgrad(dy2, y1, dw2, db2)
+        assert relerr(dw2, rw) < 1e-5
+        assert relerr(db2, rb) < 1e-5
     dy1 = torch.empty(B, F1, T1, 64, device=dev)
     K().col2im_conv2(dcols, y1, dy1)
     ref_dy1 = (y1g.grad * (y1r > 0)).permute(0, 2, 3, 1)

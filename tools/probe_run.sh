@@ -3,9 +3,12 @@ set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread -m gpu -k "conv_frontend or tallk" > gpurun_out/pt.log 2>&1 || { tail -40 gpurun_out/pt.log; exit 1; }
+tail -1 gpurun_out/pt.log
+timeout -k 10 300 python tools/conv2_bench.py 2>&1 | grep -v amdgpu.ids
 timeout -k 10 600 python -u -m pytest tests/test_gpu_model.py -x -q --timeout 300 --timeout-method thread -m gpu > gpurun_out/pm.log 2>&1 || { tail -40 gpurun_out/pm.log; exit 1; }
-tail -2 gpurun_out/pm.log
-for v in 0 1 0 1; do
-  ASRX_FRESH_GRADS=$v timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-probe --no-sub > gpurun_out/b.log 2>&1 || { tail -5 gpurun_out/b.log; exit 1; }
-  echo "fresh=$v $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/b.log)"
+tail -1 gpurun_out/pm.log
+for v in 1 2; do
+  timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-probe --no-sub > gpurun_out/b.log 2>&1 || { tail -5 gpurun_out/b.log; exit 1; }
+  echo "$(grep -o '"ms_per_step": [0-9.]*' gpurun_out/b.log)"
 done
