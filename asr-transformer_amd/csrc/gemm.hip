@@ -1277,12 +1277,27 @@ __global__ __launch_bounds__(256) void tallk_reduce_kernel(GemmArgs g) {
   }
 }
 
+// block = 64 rows x 4 split groups; each thread issues 16 loads before adding (a serial per-row sum over 256
+// splits was latency-bound at ~60 us)
 __global__ __launch_bounds__(256) void rowsum_finish_kernel(const float* ws, int splitk, int M, float* out) {
-  const int m = blockIdx.x * 256 + threadIdx.x;
-  if (m >= M) return;
+  __shared__ float red[4][64];
+  const int m = blockIdx.x * 64 + (threadIdx.x & 63), sg = threadIdx.x >> 6;
   float s = 0.f;
-  for (int sp = 0; sp < splitk; ++sp) s += ws[(int64_t)sp * M + m];
-  out[m] += s;
+  if (m < M) {
+    for (int sp0 = sg; sp0 < splitk; sp0 += 64) {
+      float v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int sp = sp0 + 4 * j;
+        v[j] = sp < splitk ? ws[(int64_t)sp * M + m] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 16; ++j) s += v[j];
+    }
+  }
+  red[sg][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (sg == 0 && m < M) out[m] += red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
 }
 
 template <int BM, int BN, bool AT, bool BT, bool VEC>
@@ -1597,7 +1612,7 @@ extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
       hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, g);
     ASRX_CHECK_LAUNCH();
     if (g.rowsum) {
-      hipLaunchKernelGGL(rowsum_finish_kernel, dim3((d->m + 255) / 256), dim3(256), 0, st, g.rowsum_ws, splitk,
+      hipLaunchKernelGGL(rowsum_finish_kernel, dim3((d->m + 63) / 64), dim3(256), 0, st, g.rowsum_ws, splitk,
                          d->m, g.rowsum);
       ASRX_CHECK_LAUNCH();
     }
