@@ -103,9 +103,10 @@ SIGNATURES = {
     "asrx_layernorm_bwd": [c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_f32, c_u64, c_vp,
                            c_i32, c_i64, c_i32, c_vp],
     "asrx_reduce_rows": [c_i32, c_vp, c_i64, c_i32, c_i64, c_vp, c_i32, c_vp, c_i32, c_vp],
-    "asrx_conv1_fwd": [c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp],
+    "asrx_conv1_fwd": [c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp],
     "asrx_im2col_conv2": [c_i32, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp],
     "asrx_conv2_fwd": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp],
+    "asrx_conv_bwd_implicit": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp],
     "asrx_conv2_wgrad": [c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp],
     "asrx_col2im_conv2": [c_i32, c_vp, c_i32, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp],
     "asrx_conv1_bwd_w": [c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp],

@@ -442,7 +442,8 @@ def frontend_fwd(C, spectrum, conv1, conv2):
     F2, T2 = (F1 - 3) // 2 + 1, (T1 - 3) // 2 + 1
     x = spectrum.contiguous().float()
     y1 = _empty((B, F1, T1, 64), C.cd, x)
-    K.conv1_fwd(x, conv1.weight.data.reshape(64, 9).contiguous(), conv1.bias.data, y1)
+    y1m = torch.empty((B, F1, T1, 8), dtype=torch.uint8, device=x.device) if C.cd == torch.bfloat16 else None
+    K.conv1_fwd(x, conv1.weight.data.reshape(64, 9).contiguous(), conv1.bias.data, y1, mask=y1m)
     feats = _empty((B * T2, F2 * 64), C.cd, x)
     if C.cd == torch.bfloat16:   # implicit GEMM over y1: no im2col image (forward or backward)
         K.conv2_fwd(y1, C.W(conv2.weight), conv2.bias.data, feats)
@@ -452,7 +453,7 @@ def frontend_fwd(C, spectrum, conv1, conv2):
         K.im2col_conv2(y1, cols)
         K.gemm(cols, C.W(conv2.weight), feats, B * T2 * F2, 64, 576, lda=576, ldb=576, ldc=64,
                bias=conv2.bias.data, relu=True)
-    return feats, dict(x=x, y1=y1, cols=cols, feats=feats, dims=(B, F, T, F1, T1, F2, T2))
+    return feats, dict(x=x, y1=y1, y1m=y1m, cols=cols, feats=feats, dims=(B, F, T, F1, T1, F2, T2))
 
 
 def frontend_bwd(C, S, dfeats_c, conv1, conv2):
@@ -469,6 +470,9 @@ def frontend_bwd(C, S, dfeats_c, conv1, conv2):
         K.conv2_wgrad(dy2, S["y1"], gw, G(conv2.bias))
     else:
         C.wgrad(dy2, cols, G(conv2.weight), G(conv2.bias))
+    if cols is None and T1 <= K.CONV_BWD_MAXT1:   # conv2 data gradient never materialised
+        K.conv_bwd_implicit(dy2, C.W(conv2.weight), S["y1m"], S["x"], G(conv1.weight).view(64, 9), G(conv1.bias))
+        return
     dcols = _empty((M2, 576), C.cd, dy2)
     K.linear_dgrad(dy2, C.W(conv2.weight), dcols)
     K.conv1_bwd_fused(dcols, S["y1"], S["x"], G(conv1.weight).view(64, 9), G(conv1.bias))

@@ -581,10 +581,12 @@ def dropout_mask(n, p, seed, device):
     return keep
 
 
-def conv1_fwd(x, w, b, y1):
-    _cuda(x, w, b, y1)
+def conv1_fwd(x, w, b, y1, mask=None):
+    """y1 = relu(conv1(x)) channels-last; mask (optional, uint8 (B, F1, T1, 8)): y1 > 0 sign bits."""
+    _cuda(x, w, b, y1, mask)
     B, _, F, T = x.shape
-    call("asrx_conv1_fwd", x.data_ptr(), B, F, T, w.data_ptr(), b.data_ptr(), y1.data_ptr(), code(y1), stream())
+    call("asrx_conv1_fwd", x.data_ptr(), B, F, T, w.data_ptr(), b.data_ptr(), y1.data_ptr(), code(y1), _p(mask),
+         stream())
 
 
 def im2col_conv2(y1, cols):
@@ -618,6 +620,21 @@ def conv2_wgrad(dy2, y1, dw, db, splitk=256):
     rws = torch.empty(splitk * 64, device=dy2.device, dtype=torch.float32) if db is not None else None
     call("asrx_conv2_wgrad", dy2.data_ptr(), y1.data_ptr(), B, F1, T1, dw.data_ptr(), _p(db), ws.data_ptr(),
          ws.numel(), _p(rws), splitk, stream())
+
+
+CONV_BWD_MAXT1 = 1024   # frontend.hip CB_MAXT1 (LDS: weights of 6 taps + the row's y1 sign bits + 3 x lines)
+
+
+def conv_bwd_implicit(dy2, w2, y1_mask, x, dw, db):
+    """conv1 weight/bias gradients (+=) straight from the conv2 output gradient dy2 [B*T2*F2][64] (bf16, already
+    ReLU-gated): the conv2 data gradient and col2im are formed on the fly (no dcols / dy1 in memory).
+    w2: [64][576] bf16 (columns kh, kw, c); y1_mask (B, F1, T1, 8) uint8 from conv1_fwd; x the fp32 spectrum."""
+    _cuda(dy2, w2, y1_mask, x, dw, db)
+    B, _, F, T = x.shape
+    nblocks = max(2, min(512, B * y1_mask.shape[1]))   # two persistent workgroups per CU
+    part = torch.empty((nblocks + 128) * 640, device=x.device, dtype=torch.float32)
+    call("asrx_conv_bwd_implicit", dy2.data_ptr(), w2.data_ptr(), y1_mask.data_ptr(), x.data_ptr(), B, F, T,
+         part.data_ptr(), nblocks, dw.data_ptr(), db.data_ptr(), stream())
 
 
 def conv1_bwd_w(x, dy1, dw, db):

@@ -19,10 +19,12 @@ constexpr int C1 = 64;
 // One workgroup per conv1 output row (b, f1): lane = (position slot t1 % 32, channel group of 8); the lane's
 // 8 x (9 taps + bias) weights are read once into registers (16-B LDS reads) and the row is swept 32 positions
 // per step — no per-element index division, no weight reads in the loop; 16-B channels-last stores.
+// mask (optional): the ReLU sign bits of y as stored, byte (row, t1, 8-channel group) — the backward's gate.
 template <typename OT>
 __global__ __launch_bounds__(256) void conv1_fwd_row_kernel(const float* __restrict__ x, int F, int T, int F1,
                                                             int T1, const float* __restrict__ w,
-                                                            const float* __restrict__ bias, OT* __restrict__ y) {
+                                                            const float* __restrict__ bias, OT* __restrict__ y,
+                                                            uint8_t* __restrict__ mask) {
   __shared__ __attribute__((aligned(16))) float sw[C1 * 9 + C1];
   for (int i = threadIdx.x; i < C1 * 10; i += 256) sw[i] = i < C1 * 9 ? w[i] : bias[i - C1 * 9];
   __syncthreads();
@@ -57,14 +59,24 @@ __global__ __launch_bounds__(256) void conv1_fwd_row_kernel(const float* __restr
       for (int k = 0; k < 9; ++k) s = fmaf(wr[i][k], in[k], s);
       o[i] = fmaxf(s, 0.f);
     }
+    uint32_t m = 0;
     if constexpr (sizeof(OT) == 2) {
       uint4 u;
       u.x = pack2bf(o[0], o[1]); u.y = pack2bf(o[2], o[3]); u.z = pack2bf(o[4], o[5]); u.w = pack2bf(o[6], o[7]);
       *(uint4*)(yr + (int64_t)t1 * C1) = u;
+      const uint32_t uu[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        m |= (uint32_t)(bf2f(uu[e] & 0xffff) > 0.f) << (2 * e);
+        m |= (uint32_t)(bf2f(uu[e] >> 16) > 0.f) << (2 * e + 1);
+      }
     } else {
       *(f4_t*)(yr + (int64_t)t1 * C1) = f4_t{o[0], o[1], o[2], o[3]};
       *(f4_t*)(yr + (int64_t)t1 * C1 + 4) = f4_t{o[4], o[5], o[6], o[7]};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) m |= (uint32_t)(o[i] > 0.f) << i;
     }
+    if (mask) mask[((int64_t)row * T1 + t1) * 8 + cg] = (uint8_t)m;
   }
 }
 
@@ -479,6 +491,161 @@ __global__ __launch_bounds__(256) void conv1_bwd_fused_v8_kernel(const bf16_t* _
 // Partials [nblocks][640] (640 = 64 channels x (9 taps + bias)) -> dW1 / db1 in two deterministic passes with
 // coalesced 640-wide row reads: pass 1, CF_G1 workgroups each sum a contiguous run of rows into part2[g][640];
 // pass 2, 10 workgroups of (64 columns x 4 row groups) sum part2 and add into the gradients.
+// conv2 data gradient + conv1 weight/bias gradient in one pass, with neither dcols nor dy1 in memory.
+// Persistent workgroups (8 waves) walk conv1 output rows (b, f1) of ONE f1 parity: the rows of a parity share
+// the conv2 kernel rows kh ({0, 2} for even f1, {1} for odd), so a workgroup stages only those taps'
+// transposed weights ([tap][ci][co], chunk-swizzled; 48 or 24 KiB) and two workgroups fit a CU.  Within a row
+// the positions of one t-parity share the kw set, so dy1[p][ci] = sum over the taps of dy2[(b, t2, f2)] .
+// W2_tap[co][ci] is an MFMA GEMM over 16-position chunks: A = dy2 rows gathered straight into registers (16 B
+// per lane), B = the staged weights.  A wave walks its (chunk, tap) items software-pipelined: the next item's
+// dy2 fragments are in flight while the current item's MFMAs (and, after a chunk's last tap, its epilogue)
+// run.  Epilogue: each lane holds 4 positions x 1 channel per 16-channel tile, gates them with conv1_fwd's
+// sign bits and accumulates channel x (9 x-taps + bias) in fp32 from the row's three input lines (LDS).
+// Per-workgroup partials [640] finish in conv1_bwd_finish.
+constexpr int CB_MAXT1 = 1024;
+
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void conv_bwd_implicit_kernel(
+    const bf16_t* __restrict__ dy2, const bf16_t* __restrict__ w2, const uint8_t* __restrict__ y1m,
+    const float* __restrict__ x, int B, int F, int T, int F1, int T1, int F2, int T2, int g_even,
+    float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int par = blockIdx.x < g_even ? 0 : 1;                 // f1 parity of this workgroup's rows
+  const int wi = par ? blockIdx.x - g_even : blockIdx.x, gn = par ? gridDim.x - g_even : g_even;
+  const int nkh = par ? 1 : 2;
+  bf16_t* sW = (bf16_t*)smem;                                  // [nkh * 3][64 ci][64 co]
+  uint8_t* sM = (uint8_t*)(sW + nkh * 3 * 64 * 64);            // [T1][8] sign bits of the row's y1
+  float* sX = (float*)(sM + ((T1 * 8 + 15) & ~15));            // [3][T]
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, g = l >> 4, li = l & 15;
+  for (int e = tid; e < nkh * 3 * 64 * 8; e += 512) {          // (tap slot, ci, 8-co chunk)
+    const int ts = e / 512, ci = (e / 8) % 64, c8 = e % 8;
+    const int tap = (par ? 1 : 2 * (ts / 3)) * 3 + ts % 3;
+    uint32_t u[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t lo = w2[(int64_t)(8 * c8 + 2 * i) * 576 + tap * 64 + ci];
+      const uint32_t hi = w2[(int64_t)(8 * c8 + 2 * i + 1) * 576 + tap * 64 + ci];
+      u[i] = lo | (hi << 16);
+    }
+    *(uint4*)(sW + (ts * 64 + ci) * 64 + 8 * (c8 ^ (ci & 7))) = make_uint4(u[0], u[1], u[2], u[3]);
+  }
+  float aw[4][10];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int k = 0; k < 10; ++k) aw[c][k] = 0.f;
+  const int nF = par ? F1 / 2 : (F1 + 1) / 2;                  // rows of this parity per utterance
+  const int R = B * nF;
+  const int n0 = (T1 + 1) / 2, n1 = T1 / 2;                    // positions of even / odd t1
+  const int c0 = (n0 + 15) / 16, nch = c0 + (n1 + 15) / 16;
+  for (int k = wi; k < R; k += gn) {
+    const int b = k / nF, f1 = 2 * (k % nF) + par, row = b * F1 + f1;
+    __syncthreads();   // previous row's readers are done (and sW is visible on the first pass)
+    {
+      const uint4* src = (const uint4*)(y1m + (int64_t)row * T1 * 8);
+      for (int i = tid; i < T1 / 2; i += 512) ((uint4*)sM)[i] = src[i];
+      if ((T1 & 1) && tid == 0) ((uint2*)sM)[T1 - 1] = ((const uint2*)src)[T1 - 1];
+      const float* xr = x + ((int64_t)b * F + 2 * f1) * T;
+      for (int i = tid; i < 3 * T; i += 512) sX[i] = xr[(int64_t)(i / T) * T + i % T];
+    }
+    __syncthreads();
+    // this wave's items: chunks ch = w, w + 8, ...; taps (ih < nkh, iw < nkw(ch)) of each
+    auto frag_ptr = [&](int ch, int ih, int iw, bool& ok) -> const bf16_t* {
+      const int pt = ch >= c0, jl = 16 * (pt ? ch - c0 : ch) + li, np = pt ? n1 : n0;
+      const int kh = par ? 1 : 2 * ih, kw = pt ? 1 : 2 * iw, fd = f1 - kh, td = pt + 2 * jl - kw;
+      ok = fd >= 0 && (fd >> 1) < F2 && jl < np && td >= 0 && (td >> 1) < T2;
+      return dy2 + ((int64_t)(b * T2 + (ok ? td >> 1 : 0)) * F2 + (ok ? fd >> 1 : 0)) * 64 + 8 * g;
+    };
+    int ch = w, ih = 0, iw = 0;
+    if (ch >= nch) continue;
+    bool ok;
+    const bf16_t* dp = frag_ptr(ch, ih, iw, ok);
+    s8_t cur0 = *(const s8_t*)dp, cur1 = *(const s8_t*)(dp + 32);
+    bool cok = ok;
+    f4_t acc[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[c] = f4_t{0.f, 0.f, 0.f, 0.f};
+    while (true) {
+      const int pt = ch >= c0, nkw = pt ? 1 : 2;
+      // next item
+      int nch_ = ch, nih = ih, niw = iw + 1;
+      if (niw >= nkw) { niw = 0; ++nih; }
+      if (nih >= nkh) { nih = 0; nch_ = ch + 8; }
+      const bool more = nch_ < nch;
+      s8_t nx0 = cur0, nx1 = cur1;
+      bool nok = false;
+      if (more) {
+        const bf16_t* np_ = frag_ptr(nch_, nih, niw, nok);
+        nx0 = *(const s8_t*)np_;
+        nx1 = *(const s8_t*)(np_ + 32);
+      }
+      // MFMAs of the current item
+      if (!cok) { cur0 = s8_t{0, 0, 0, 0, 0, 0, 0, 0}; cur1 = cur0; }
+      const int ts = ih * 3 + (pt ? 1 : 2 * iw);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int ci = 16 * c + li;
+        const bf16_t* wr = sW + (ts * 64 + ci) * 64;
+        const s8_t b0 = *(const s8_t*)(wr + 8 * (g ^ (ci & 7)));
+        const s8_t b1 = *(const s8_t*)(wr + 8 * ((4 + g) ^ (ci & 7)));
+        acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur0, b0, acc[c], 0, 0, 0);
+        acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur1, b1, acc[c], 0, 0, 0);
+      }
+      if (nch_ != ch) {   // chunk done: lane holds dy1 of positions j0 + 4 g + r, channels 16 c + li
+        const int j0 = 16 * (pt ? ch - c0 : ch), np = pt ? n1 : n0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int j = j0 + 4 * g + r;
+          if (j >= np) continue;
+          const int t1 = pt + 2 * j;
+          float xv[9];
+#pragma unroll
+          for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) xv[kh * 3 + kw] = sX[kh * T + 2 * t1 + kw];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const int ci = 16 * c + li;
+            const float gv = ((sM[t1 * 8 + (ci >> 3)] >> (ci & 7)) & 1) ? acc[c][r] : 0.f;
+#pragma unroll
+            for (int q = 0; q < 9; ++q) aw[c][q] = fmaf(gv, xv[q], aw[c][q]);
+            aw[c][9] += gv;
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] = f4_t{0.f, 0.f, 0.f, 0.f};
+      }
+      if (!more) break;
+      ch = nch_; ih = nih; iw = niw;
+      cur0 = nx0; cur1 = nx1; cok = nok;
+    }
+  }
+  // lanes with the same li hold the same channels: reduce over g, then over the waves (in the weight image)
+  __syncthreads();
+  float (*red)[640] = (float (*)[640])smem;
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      float v = aw[c][k];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      aw[c][k] = v;
+    }
+  if (g == 0) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int k = 0; k < 10; ++k) red[w][(16 * c + li) * 10 + k] = aw[c][k];
+  }
+  __syncthreads();
+  for (int i = tid; i < 640; i += 512) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += red[q][i];
+    part[(int64_t)blockIdx.x * 640 + i] = s;
+  }
+}
+
 // (both passes issue all their loads before the first add: latency-bound otherwise)
 constexpr int CF_G1 = 128;
 constexpr int CF_R1 = 48;   // pass-1 rows loaded per batch
@@ -732,7 +899,7 @@ inline unsigned grid_for(int64_t work, int cap = 8192) {
 extern "C" int asrx_version(void) { return 1; }
 
 extern "C" int asrx_conv1_fwd(const float* x, int32_t B, int32_t F, int32_t T, const float* w, const float* b,
-                              void* y1, int32_t y_dtype, void* stream) {
+                              void* y1, int32_t y_dtype, uint8_t* y1_mask, void* stream) {
   if (!x || !w || !b || !y1 || B <= 0 || F < 3 || T < 3) return ASRX_ERR_ARG;
   const int F1 = (F - 3) / 2 + 1, T1 = (T - 3) / 2 + 1;
   if (T > 5120) return ASRX_ERR_UNSUPPORTED;   // 3 input lines staged in LDS (<= 60 KiB)
@@ -740,10 +907,10 @@ extern "C" int asrx_conv1_fwd(const float* x, int32_t B, int32_t F, int32_t T, c
   const size_t shm = sizeof(float) * 3 * T;
   if (y_dtype == ASRX_F32)
     hipLaunchKernelGGL(conv1_fwd_row_kernel<float>, grid, dim3(256), shm, (hipStream_t)stream, x, F, T, F1, T1, w,
-                       b, (float*)y1);
+                       b, (float*)y1, y1_mask);
   else
     hipLaunchKernelGGL(conv1_fwd_row_kernel<bf16_t>, grid, dim3(256), shm, (hipStream_t)stream, x, F, T, F1, T1, w,
-                       b, (bf16_t*)y1);
+                       b, (bf16_t*)y1, y1_mask);
   ASRX_CHECK_LAUNCH();
   return ASRX_OK;
 }
@@ -877,6 +1044,27 @@ extern "C" int asrx_dropout_mask(uint8_t* keep, int64_t n, float p, uint64_t see
   hipLaunchKernelGGL(dropout_mask_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, keep, n,
                      drop_threshold(p), seed);
   ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
+extern "C" int asrx_conv_bwd_implicit(const void* dy2, const void* w2, const uint8_t* y1m, const float* x, int32_t B,
+                                      int32_t F, int32_t T, float* part, int32_t nblocks, float* dw, float* db,
+                                      void* stream) {
+  if (!dy2 || !w2 || !y1m || !x || !part || !dw || !db || B <= 0 || F < 7 || T < 7 || nblocks < 2)
+    return ASRX_ERR_ARG;
+  if (((uintptr_t)dy2 | (uintptr_t)y1m) % 16) return ASRX_ERR_ARG;
+  const int F1 = (F - 3) / 2 + 1, T1 = (T - 3) / 2 + 1;
+  const int F2 = (F1 - 3) / 2 + 1, T2 = (T1 - 3) / 2 + 1;
+  if (T1 > CB_MAXT1) return ASRX_ERR_UNSUPPORTED;
+  // even-f1 rows carry twice the taps of odd ones: ~2/3 of the workgroups take them
+  const int g_even = std::max(1, std::min(nblocks - 1, (2 * nblocks + 2) / 3));
+  const size_t shm = (size_t)6 * 64 * 64 * 2 + ((T1 * 8 + 15) & ~15) + sizeof(float) * 3 * T;
+  if (shm > 80 * 1024 || shm < 8 * 640 * 4) return ASRX_ERR_UNSUPPORTED;   // two workgroups per CU
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(conv_bwd_implicit_kernel, dim3(nblocks), dim3(512), shm, st, (const bf16_t*)dy2,
+                     (const bf16_t*)w2, y1m, x, B, F, T, F1, T1, F2, T2, g_even, part);
+  ASRX_CHECK_LAUNCH();
+  conv1_bwd_finish(part, nblocks, dw, db, st);
   return ASRX_OK;
 }
 

@@ -207,13 +207,14 @@ int asrx_reduce_rows_grouped(const asrx_rowsum_group* groups, int32_t count, voi
 
 /* ---------------------------------------------------------------------------------------------------
  * Conv2d front-end (model.py:168-171): conv(1->64,3x3,s2)+ReLU -> conv(64->64,3x3,s2)+ReLU, no padding.
- * conv1_fwd: x (B,1,F,T) fp32 -> y1 channels-last (B,F1,T1,64) in y_dtype (bf16 or fp32)
+ * conv1_fwd: x (B,1,F,T) fp32 -> y1 channels-last (B,F1,T1,64) in y_dtype (bf16 or fp32); y1_mask (optional,
+ *            (B,F1,T1,8) bytes): bit c of byte q = y1[..][8q + c] > 0 as stored (the ReLU gate of the backward)
  * im2col_conv2: y1 -> cols [(b,t2,f2)][(kh,kw,c)] (B*T2*F2, 576), same dtype: conv2 = GEMM(cols, W2p^T)
  * col2im_conv2: dcols -> dy1 (B,F1,T1,64) fp32, gated by y1 > 0 (ReLU backward)
  * conv1_bwd_w: dW1[c][kh*3+kw] += sum dy1*x, db1[c] += sum dy1 (partials in part[nblocks][64*10])
  * ------------------------------------------------------------------------------------------------- */
 int asrx_conv1_fwd(const float* x, int32_t B, int32_t F, int32_t T, const float* w, const float* b, void* y1,
-                   int32_t y_dtype, void* stream);
+                   int32_t y_dtype, uint8_t* y1_mask, void* stream);
 /* conv2 (Conv2d(64,64,3,s2) + bias + ReLU, model.py:170-171) as an implicit GEMM over the channels-last conv1
  * output y1 (B, F1, T1, 64) bf16, no im2col image: out[(b*T2 + t2)*F2 + f2][64] bf16 — the encoder input rows.
  * w2: [64][576] bf16, columns (kh, kw, c); bias fp32 [64].  y1 must be < 2 GiB (32-bit DMA offsets). */
@@ -224,6 +225,13 @@ int asrx_conv2_fwd(const void* y1, const void* w2, const float* bias, void* out,
  * floats (when db).  model.py:170 Conv2d backward. */
 int asrx_conv2_wgrad(const void* dy2, const void* y1, int32_t B, int32_t F1, int32_t T1, float* dw, float* db,
                      float* ws, int64_t ws_elems, float* rws, int32_t splitk, void* stream);
+/* conv1 weight/bias gradient (+=) straight from the conv2 output gradient: dy1 = relu'(y1) * conv2^T(dy2) is
+ * formed on the fly, neither the column gradient nor dy1 is stored (model.py:168-171 backward).  dy2
+ * [B*T2*F2][64] bf16 (ReLU-gated), w2 [64][576] bf16, y1_mask = conv1_fwd's sign bits, x (B,1,F,T) fp32; part:
+ * [nblocks + 128][640] workspace, nblocks >= 2 persistent workgroups (about 2/3 take the even-f1 rows).
+ * T1 <= 1024 and 48 KiB + T1*8 B + 12*T B of LDS <= 80 KiB. */
+int asrx_conv_bwd_implicit(const void* dy2, const void* w2, const uint8_t* y1_mask, const float* x, int32_t B, int32_t F,
+                           int32_t T, float* part, int32_t nblocks, float* dw, float* db, void* stream);
 int asrx_im2col_conv2(int32_t dtype, const void* y1, int32_t B, int32_t F1, int32_t T1, void* cols, void* stream);
 int asrx_col2im_conv2(int32_t dcols_dtype, const void* dcols, int32_t y1_dtype, const void* y1, int32_t B,
                       int32_t F1, int32_t T1, float* dy1, void* stream);

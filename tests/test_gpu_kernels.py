@@ -464,7 +464,10 @@ def test_conv_frontend(dtype, T):
     F1, T1 = (F - 3) // 2 + 1, (T - 3) // 2 + 1
     F2, T2 = (F1 - 3) // 2 + 1, (T1 - 3) // 2 + 1
     y1 = torch.empty(B, F1, T1, 64, device=dev, dtype=dtype)
-    K().conv1_fwd(x.to(dev), w1.reshape(64, 9).to(dev), b1.to(dev), y1)
+    y1m = torch.empty(B, F1, T1, 8, device=dev, dtype=torch.uint8)
+    K().conv1_fwd(x.to(dev), w1.reshape(64, 9).to(dev), b1.to(dev), y1, mask=y1m)
+    bits = torch.stack([(y1m.cpu() >> i) & 1 for i in range(8)], -1).reshape(B, F1, T1, 64)
+    assert torch.equal(bits.bool(), y1.float().cpu() > 0)
     ref1 = torch.relu(torch.nn.functional.conv2d(x.double(), w1.double(), b1.double(), stride=2))
     tol = 1e-5 if dtype == torch.float32 else 1e-2
     assert relerr(y1.float().cpu().permute(0, 3, 1, 2), ref1) < tol
@@ -520,6 +523,18 @@ def test_conv_frontend(dtype, T):
     K().conv1_bwd_fused(dcols, y1, x.to(dev), dw2, db2)
     assert relerr(dw2.cpu(), w1r.grad.reshape(64, 9)) < 1e-4
     assert relerr(db2.cpu(), b1r.grad) < 1e-4
+    if dtype == torch.bfloat16:   # implicit path: from dy2 itself, the column gradient never stored
+        gyb = dy2.double().cpu().view(B, T2, F2, 64).permute(0, 3, 2, 1)
+        y1g2 = y1r.clone().requires_grad_(True)
+        torch.nn.functional.conv2d(y1g2, w2.to(dtype).double(), stride=2).backward(gyb)
+        w1r2 = w1.double().requires_grad_(True)
+        b1r2 = b1.double().requires_grad_(True)
+        torch.nn.functional.conv2d(xr, w1r2, b1r2, stride=2).backward(y1g2.grad * (y1r > 0))
+        dw3 = torch.zeros(64, 9, device=dev)
+        db3 = torch.zeros(64, device=dev)
+        K().conv_bwd_implicit(dy2, w2p, y1m, x.to(dev), dw3, db3)
+        assert relerr(dw3.cpu(), w1r2.grad.reshape(64, 9)) < 1e-5
+        assert relerr(db3.cpu(), b1r2.grad) < 1e-5
 
 
 # ------------------------------------------------------------------------------------------------ misc
