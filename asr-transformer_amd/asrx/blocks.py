@@ -59,10 +59,12 @@ class FreshGrads:
                 self.grad[o:o + n].zero_()
         return full
 
-    def drain(self):
-        for o, n in self.live.items():
-            self.grad[o:o + n].zero_()
-        self.live.clear()
+    def drain(self, params=None, store=None):
+        """Zero the fresh regions nobody wrote (all, or those of `params` — e.g. before their ranges are handed
+        to the gradient all-reduce)."""
+        offs = list(self.live) if params is None else [store.offset(p) for p in params if store.offset(p) in self.live]
+        for o in offs:
+            self.grad[o:o + self.live.pop(o)].zero_()
 
 
 class Ctx:

@@ -141,6 +141,8 @@ def _release(C, ready, params):
     if ready is None or C.wq is None:
         return
     C.flush_wgrad()
+    if C.fresh is not None:   # unwritten (unzeroed) weight gradients must not reach the all-reduce
+        C.fresh.drain(params, C.store)
     for a, b in _spans(C, params):
         ready(a, b)
     C.defer_wgrad()

@@ -249,6 +249,39 @@ def test_trainer_fresh_grads_match_zeroed(cfgname):
     assert torch.equal(g_fresh, tr.store.grad)
 
 
+def test_trainer_release_path_fresh_grads():
+    """Multi-GPU backward structure on one GPU: an injected all-reduce (doubling every range it is handed)
+    receives decoder / upper-encoder ranges mid-backward and the rest at finish(); with unzeroed weight
+    gradients (FreshGrads) every range must already hold its final gradient when handed over."""
+    from asrx.train import Trainer
+    m, cfg = build("c2", "bf16", dropout=0.0)
+    m.train()
+    spec = CONFIGS["c2"]
+    s, t, k = synthetic_batch(cfg, 8, spec["frames"], spec["text_len"] + 1, seed=5)
+    s, t, k = s.to(dev), t.to(dev), k.to(dev)
+    ref = Trainer(m)
+    ref._wonly = []
+    ref.forward_backward(s, t, k)
+    g_ref = ref.store.grad.clone()
+    seen = []
+
+    def fake(view):
+        seen.append(view.numel())
+        view.mul_(2.0)
+
+    tr = Trainer(m, allreduce_fn=fake)
+    assert tr.reducer.active and tr._wonly
+    tr.forward_backward(s, t, k)              # binds / zeroes
+    tr.reducer.finish()
+    tr.store.grad.fill_(float("nan"))
+    seen.clear()
+    tr.forward_backward(s, t, k)              # fresh mode, ranges released mid-backward
+    tr.reducer.finish()
+    torch.cuda.synchronize()
+    assert len(seen) > 1
+    assert torch.equal(tr.store.grad, 2.0 * g_ref)
+
+
 def test_bf16_training_reduces_loss():
     """A few bf16 AdamW steps (dropout 0.1) on one c1 batch drive the loss down."""
     import asrx
