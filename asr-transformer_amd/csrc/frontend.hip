@@ -724,28 +724,75 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const int64_t* __restric
                                                         float sc, uint64_t seed, float* __restrict__ dtable) {
   const int v = blockIdx.x;
   if (v == pad_id) return;
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // Tokens are taken EB_CHUNK at a time: each wave ballots its quarter (EB_WIN windows of 64, all loads issued
+  // together), the matching rows are listed in LDS in token order, then every thread sums its columns over the
+  // list with the row loads of 4 matches in flight — the same fixed summation order as a one-by-one walk.
+  constexpr int EB_WIN = 16, EB_CHUNK = 4 * 64 * EB_WIN;
+  __shared__ int rows_[EB_CHUNK];
+  __shared__ int wcnt[4 * EB_WIN];
   float acc[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-  for (int64_t base = 0; base < ntok; base += 64) {
-    const int64_t i = base + lane;
-    const bool hit = i < ntok && tok[i] == v;
-    unsigned long long mask = __ballot(hit);
-    while (mask) {
-      const int b = __ffsll(mask) - 1;
-      mask &= mask - 1;
-      const int64_t r = base + b;
+  for (int64_t base = 0; base < ntok; base += EB_CHUNK) {
+    unsigned long long mk[EB_WIN];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int c = threadIdx.x + 256 * j;
-        if (c < d) {
-          float gv = dout[r * d + c];
-          if (thr) gv = rng_keep(seed, (uint32_t)(r * d + c), thr) ? gv * sc : 0.f;
-          acc[j] += gv;
+    for (int q = 0; q < EB_WIN; ++q) {
+      const int64_t i = base + 64 * (EB_WIN * w + q) + lane;
+      mk[q] = __ballot(i < ntok && tok[i] == v);
+    }
+    if (lane < EB_WIN) {
+      int c = 0;
+#pragma unroll
+      for (int q = 0; q < EB_WIN; ++q) c = q == lane ? __popcll(mk[q]) : c;
+      wcnt[EB_WIN * w + lane] = c;
+    }
+    __syncthreads();
+    int off = 0, n = 0;
+    for (int u = 0; u < 4 * EB_WIN; ++u) {   // windows in token order
+      const int c = wcnt[u];
+      if (u < EB_WIN * w) off += c;
+      n += c;
+    }
+#pragma unroll
+    for (int q = 0; q < EB_WIN; ++q) {
+      const unsigned long long m = mk[q];
+      if ((m >> lane) & 1ull)
+        rows_[off + __popcll(m & ((1ull << lane) - 1ull))] = (int)(64 * (EB_WIN * w + q) + lane);
+      off += __popcll(m);
+    }
+    __syncthreads();
+    for (int m0 = 0; m0 < n; m0 += 16) {   // 16 matched rows' loads in flight per column pair
+#pragma unroll
+      for (int jp = 0; jp < 4; ++jp) {
+        if (512 * jp >= d) break;
+        float gv[16][2];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int64_t r = base + rows_[min(m0 + e, n - 1)];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int c = 512 * jp + 256 * h + threadIdx.x;
+            gv[e][h] = c < d ? dout[r * d + c] : 0.f;
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          if (m0 + e >= n) break;
+          const int64_t r = base + rows_[m0 + e];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int c = 512 * jp + 256 * h + threadIdx.x;
+            if (c < d) {
+              float g = gv[e][h];
+              if (thr) g = rng_keep(seed, (uint32_t)(r * d + c), thr) ? g * sc : 0.f;
+              acc[2 * jp + h] += g;
+            }
+          }
         }
       }
     }
+    __syncthreads();   // rows_ / wcnt are rewritten by the next chunk
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
