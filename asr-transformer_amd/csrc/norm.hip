@@ -206,20 +206,25 @@ __global__ __launch_bounds__(256) void reduce_rows_grouped_kernel(RowsumTable t)
   while (gi + 1 < t.count && t.gr[gi + 1].chunk0 <= bid) ++gi;
   const RowsumGroup& G = t.gr[gi];
   const int c = (bid - G.chunk0) * 64 + (threadIdx.x & 63), sub = threadIdx.x >> 6;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  // 16 independent partial sums per thread: 16 loads in flight per trip (a 4-deep chain was latency-bound)
+  float s[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s[i] = 0.f;
   if (c < G.cols) {
     const float* p = G.in + c;
     const int64_t ld = G.cols;
     int r = sub;
-    for (; r + 12 < G.rows; r += 16) {
-      s0 += p[(int64_t)r * ld];
-      s1 += p[(int64_t)(r + 4) * ld];
-      s2 += p[(int64_t)(r + 8) * ld];
-      s3 += p[(int64_t)(r + 12) * ld];
+    for (; r + 60 < G.rows; r += 64) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[i] += p[(int64_t)(r + 4 * i) * ld];
     }
-    for (; r < G.rows; r += 4) s0 += p[(int64_t)r * ld];
+    for (int i = 0; r < G.rows; r += 4, ++i) s[i & 15] += p[(int64_t)r * ld];
   }
-  red[sub][threadIdx.x & 63] = (s0 + s1) + (s2 + s3);
+#pragma unroll
+  for (int i = 8; i > 0; i >>= 1)
+#pragma unroll
+    for (int j = 0; j < i; ++j) s[j] += s[j + i];
+  red[sub][threadIdx.x & 63] = s[0];
   __syncthreads();
   if (sub == 0 && c < G.cols) {
     const float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
