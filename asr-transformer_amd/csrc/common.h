@@ -66,10 +66,21 @@ static inline uint32_t drop_threshold(float p) {
   return (uint32_t)((double)p * 65536.0 + 0.5);
 }
 
+// Wave-wide sum without the LDS crossbar: DPP within rows of 16 (quad swaps, half-row and row mirrors), then
+// the gfx950 permlane16/32 swaps across rows.  Every step adds a lane and its partner (commutative), so all 64
+// lanes end with the same value.
+template <int CTRL> ASRX_DEV float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
 ASRX_DEV float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp_f<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);   // row_half_mirror: lane i <-> 7 - i
+  v += dpp_f<0x140>(v);   // row_mirror: lane i <-> 15 - i
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 ASRX_DEV float wave_max(float v) {
 #pragma unroll

@@ -43,14 +43,18 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int x_dtype, const void* x,
   const int l = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
-  float v[NJ][CH];
+  float v[NJ][CH], gm[NJ][CH], bt[NJ][CH];
   float s = 0.f;
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
+  for (int j = 0; j < NJ; ++j) {   // gamma / beta issued with the row: no load after the reductions
     load_ch<CH>(x, x_dtype, row * D + (j * 64 + l) * CH, v[j]);
+    load_ch<CH>(gamma, ASRX_F32, (j * 64 + l) * CH, gm[j]);
+    load_ch<CH>(beta, ASRX_F32, (j * 64 + l) * CH, bt[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
 #pragma unroll
     for (int i = 0; i < CH; ++i) s += v[j][i];
-  }
   const float mu = wave_sum(s) * (1.f / D);
   float q = 0.f;
 #pragma unroll
@@ -63,7 +67,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int x_dtype, const void* x,
     const int c0 = (j * 64 + l) * CH;
     float o[CH];
 #pragma unroll
-    for (int i = 0; i < CH; ++i) o[i] = (v[j][i] - mu) * rs * gamma[c0 + i] + beta[c0 + i];
+    for (int i = 0; i < CH; ++i) o[i] = (v[j][i] - mu) * rs * gm[j][i] + bt[j][i];
     store_ch<CH>(y, y_dtype, row * D + c0, o);
   }
   if (l == 0) { mean[row] = mu; rstd[row] = rs; }

@@ -50,7 +50,7 @@ def main():
             a = (torch.rand(M, Kd, device="cuda", generator=g) * 2 - 1).bfloat16()
         if kind in ("wgrad", "wgradp"):
             pass
-        elif kind in ("fwd", "fwdb", "fwdr"):
+        elif kind in ("fwd", "fwdb", "fwdr") or kind.startswith("fwds"):
             w = (torch.rand(N, Kd, device="cuda", generator=g) * 2 - 1).bfloat16()
         else:
             w = (torch.rand(Kd, N, device="cuda", generator=g) * 2 - 1).bfloat16()
@@ -66,7 +66,11 @@ def main():
             gate = torch.randn(M, N, device="cuda", generator=g).bfloat16()
 
         def run():
-            if kind == "fwdb":
+            if kind.startswith("dgrads"):   # dgradsN: data gradient with split-K N
+                K.linear_dgrad(a, w, y, splitk=int(kind[6:]))
+            elif kind.startswith("fwds"):   # fwdsN: forward with split-K N
+                K.linear(a, w, y, splitk=int(kind[4:]))
+            elif kind == "fwdb":
                 K.linear(a, w, y, bias=bias)
             elif kind == "fwdr":
                 K.linear(a, w, yf, bias=bias, dropout_p=0.1, seed=3, resid=resid, ld_resid=N)
