@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("ASRX_LIB", os.path.join(_HERE, "lib", "libasrx.so"))
 
 BF16 = 0
 F32 = 1
+BITS = 2  # gate operand only: 1 bit per element, uint32 words
 
 c_i32, c_i64, c_u64, c_f32, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float, ctypes.c_void_p
 
@@ -38,6 +39,7 @@ class GemmDesc(ctypes.Structure):
         ("splitk", c_i32), ("workspace", c_vp), ("workspace_elems", c_i64),
         ("tile", c_i32),
         ("rowsum_a", c_vp), ("rowsum_ws", c_vp),
+        ("mask_out", c_vp), ("ld_mask", c_i64),
     ]
 
 

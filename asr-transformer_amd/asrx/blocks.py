@@ -165,6 +165,8 @@ class Seeds:
 _SIDE = {}
 # weight gradients of each finished layer issued on the side stream, overlapping the backward chain
 WGRAD_OVERLAP = os.environ.get("ASRX_WGRAD_OVERLAP", "0") == "1"
+# FFN hidden-layer ReLU/dropout mask kept as bits for the data gradient (ASRX_GATE_BITS=0: read the bf16 f)
+GATE_BITS = os.environ.get("ASRX_GATE_BITS", "1") == "1"
 # generating the keep bits on a side stream (overlapping the LN + Q/K/V GEMM) measured SLOWER than generating
 # them in line (18.2 vs 17.75 ms/step: the VALU-heavy generator steals the GEMM's CUs): off by default
 _SIDE_DROPGEN = os.environ.get("ASRX_DROPGEN_SIDE", "0") == "1"
@@ -377,10 +379,16 @@ def ffn_fwd(C, x, ln, ff):
     nf = ff.squeeze.weight.shape[0]
     f = _empty((M, nf), C.cd, x)
     sf = C.seed()
-    K.linear(h, C.W(ff.squeeze.weight), f, bias=ff.squeeze.bias.data, relu=True, dropout_p=C.p, seed=sf)
+    # bf16: the epilogue also writes the 1-bit mask f > 0 (ReLU and dropout keep), which the data gradient
+    # reads as its gate: M*nf/8 bytes instead of the 2*M*nf of f itself
+    fb = None
+    if C.cd == torch.bfloat16 and nf % 32 == 0 and GATE_BITS:
+        fb = _empty((M, nf // 32), torch.int32, x)
+    K.linear(h, C.W(ff.squeeze.weight), f, bias=ff.squeeze.bias.data, relu=True, dropout_p=C.p, seed=sf,
+             mask_out=fb, ld_mask=nf // 32)
     y = _empty((M, d), torch.float32, x)
     K.linear(f, C.W(ff.unsqueeze.weight), y, bias=ff.unsqueeze.bias.data, resid=x, ld_resid=d)
-    return y, dict(x=x, h=h, mean=mean, rstd=rstd, f=f, ln=ln, ff=ff)
+    return y, dict(x=x, h=h, mean=mean, rstd=rstd, f=f, fb=fb, ln=ln, ff=ff)
 
 
 def ffn_bwd(C, S, dy, dy_c, dx_c_out=None, dx_c_p=0.0, dx_c_seed=0):
@@ -391,7 +399,11 @@ def ffn_bwd(C, S, dy, dy_c, dx_c_out=None, dx_c_p=0.0, dx_c_seed=0):
     dpre = _empty((M, nf), C.cd, x)
     keep_scale = 1.0 / (1.0 - C.p) if C.p > 0 else 1.0
     # f = Drop(ReLU(pre)) -> dpre = df * [f > 0] / (1-p)   (f > 0 <=> pre > 0 and kept)
-    K.linear_dgrad(dy_c, W(ff.unsqueeze.weight), dpre, alpha=keep_scale, gate=f, ld_gate=nf)
+    if S.get("fb") is not None:
+        K.linear_dgrad(dy_c, W(ff.unsqueeze.weight), dpre, alpha=keep_scale, gate=S["fb"], ld_gate=nf // 32,
+                       gate_bits=True)
+    else:
+        K.linear_dgrad(dy_c, W(ff.unsqueeze.weight), dpre, alpha=keep_scale, gate=f, ld_gate=nf)
     C.wgrad(dy_c, f, G(ff.unsqueeze.weight), G(ff.unsqueeze.bias))
     dh = _empty((M, d), C.cd, x)
     K.linear_dgrad(dpre, W(ff.squeeze.weight), dh)

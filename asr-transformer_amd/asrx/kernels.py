@@ -6,7 +6,7 @@ import math
 
 import torch
 
-from ._lib import MAX_GROUPS, MAX_ROWSUM_GROUPS, AttnDesc, BF16, F32, GemmDesc, GemmGroup, RowsumGroup, call
+from ._lib import MAX_GROUPS, MAX_ROWSUM_GROUPS, AttnDesc, BF16, BITS, F32, GemmDesc, GemmGroup, RowsumGroup, call
 
 _U64 = (1 << 64) - 1
 
@@ -93,9 +93,10 @@ def choose_tile(m, n, batch, splitk):
 def gemm(a, b, c, m, n, k, *, lda, ldb, ldc, a_trans=False, b_trans=False, alpha=1.0, beta=0.0, bias=None,
          rowadd=None, rowadd_mod=1, ld_rowadd=0, relu=False, dropout_p=0.0, seed=0, gate=None, ld_gate=0,
          resid=None, ld_resid=0, batch=1, batch_inner=1, sa=(0, 0), sb=(0, 0), sc=(0, 0), splitk=1, tile=0,
-         rowsum=None):
+         rowsum=None, gate_bits=False, mask_out=None, ld_mask=0):
     """C = epi(alpha * op(A) op(B)^T) — see asrx_gemm in include/asrx.h.  rowsum (fp32 [m], a_trans only):
-    += row sums of A (fused bias gradient)."""
+    += row sums of A (fused bias gradient).  gate_bits: gate is an int32 bit mask [m][ld_gate words]
+    (ASRX_BITS).  mask_out (int32 [m][ld_mask words]) receives the bits C > 0 (see asrx_gemm_desc)."""
     _cuda(a, b, c)
     if a.dtype != b.dtype:
         raise TypeError("asrx.gemm: A and B must share a dtype")
@@ -123,10 +124,11 @@ def gemm(a, b, c, m, n, k, *, lda, ldb, ldc, a_trans=False, b_trans=False, alpha
                  None if rowadd is None else rowadd.data_ptr(), ld_rowadd if rowadd is not None else 0,
                  rowadd_mod if rowadd is not None else 0, int(relu), dropout_p, seed & _U64,
                  None if gate is None else gate.data_ptr(), ld_gate if gate is not None else 0,
-                 code(gate) if gate is not None else 0,
+                 (BITS if gate_bits else code(gate)) if gate is not None else 0,
                  None if resid is None else resid.data_ptr(), ld_resid if resid is not None else 0,
                  code(resid) if resid is not None else 0,
-                 splitk, wsp, wse, tile, None if rowsum is None else rowsum.data_ptr(), rwsp)
+                 splitk, wsp, wse, tile, None if rowsum is None else rowsum.data_ptr(), rwsp,
+                 None if mask_out is None else mask_out.data_ptr(), ld_mask if mask_out is not None else 0)
     probe = PROBE
     if probe is not None and probe.active:
         name = kernel_name(d)

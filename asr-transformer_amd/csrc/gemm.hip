@@ -1394,12 +1394,14 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
   const bool fast = batch == 1 && splitk == 1 && d->n % 4 == 0 && cvec &&
                     (!d->bias || (uintptr_t)d->bias % 16 == 0) &&
                     (!d->rowadd || (d->ld_rowadd % 4 == 0 && (uintptr_t)d->rowadd % 16 == 0)) &&
-                    (!d->gate || (d->gate_dtype == ASRX_BF16 && d->ld_gate % 4 == 0 && (uintptr_t)d->gate % 8 == 0)) &&
+                    (!d->gate || (d->gate_dtype == ASRX_BF16 && d->ld_gate % 4 == 0 && (uintptr_t)d->gate % 8 == 0) ||
+                     (d->gate_dtype == ASRX_BITS && (uintptr_t)d->gate % 4 == 0)) &&
                     (!d->resid || (d->resid_dtype == ASRX_F32 && d->ld_resid % 4 == 0 && (uintptr_t)d->resid % 16 == 0)) &&
                     (d->beta == 0.f || (d->beta == 1.f && d->c_dtype == ASRX_F32));
   if (fast) {
     epi = (d->bias ? E_BIAS : 0) | (d->relu ? E_RELU : 0) | (drop_threshold(d->dropout_p) ? E_DROP : 0) |
-          (d->gate ? E_GATE : 0) | (d->resid ? E_RESID : 0) | (d->beta == 1.f ? E_BETA : 0) |
+          (d->gate ? (d->gate_dtype == ASRX_BITS ? E_GBITS : E_GATE) : 0) | (d->mask_out ? E_MASKOUT : 0) |
+          (d->resid ? E_RESID : 0) | (d->beta == 1.f ? E_BETA : 0) |
           (d->c_dtype == ASRX_F32 ? E_F32 : 0) | (d->alpha != 1.f ? E_ALPHA : 0) | (d->rowadd ? E_ROWADD : 0);
   }
   pl.epi = ((pl.use <= 2 || (pl.use >= 5 && pl.use != 9)) && epi_instantiated(d->a_trans, d->b_trans, epi))
@@ -1528,6 +1530,8 @@ extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
   g.drop_scale = d->dropout_p > 0.f && d->dropout_p < 1.f ? 1.f / (1.f - d->dropout_p) : 0.f;
   g.seed = d->seed;
   g.gate = d->gate; g.ld_gate = d->ld_gate; g.gate_dtype = d->gate_dtype;
+  g.mask_out = d->mask_out; g.ld_mask = d->ld_mask;
+  if (((d->gate && d->gate_dtype == ASRX_BITS) || d->mask_out) && d->in_dtype != ASRX_BF16) return ASRX_ERR_UNSUPPORTED;
   g.resid = d->resid; g.ld_resid = d->ld_resid; g.resid_dtype = d->resid_dtype;
   g.ws = d->workspace;
   g.rowsum = d->rowsum_a;
@@ -1545,6 +1549,11 @@ extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
     g.splitk = splitk;
     g.k_per_split = ((((int)d->k + BK - 1) / BK + splitk - 1) / splitk) * BK;
     const int epi = pl.epi;
+    // the bit-mask output is written only by the paired bf16 store path of the fast epilogues
+    if (d->mask_out && (!(epi != E_GENERIC && (epi & E_MASKOUT)) || !d->relu || d->c_dtype != ASRX_BF16 || d->n % 32 != 0 ||
+                        d->ldc % 8 != 0 || (uintptr_t)d->c % 16 != 0 || (uintptr_t)d->mask_out % 4 != 0 ||
+                        d->ld_mask < d->n / 32))
+      return ASRX_ERR_UNSUPPORTED;
     if (pl.use == 1 && (epi & E_BIAS) && epi != E_GENERIC && d->n > P_BIAS_BYTES / 4) {
       // the p3 bias epilogue stages the whole bias vector in LDS (16 KiB): wider outputs run as column chunks
       // (fast-path epilogues without dropout only: their element math does not depend on N)
@@ -1557,7 +1566,9 @@ extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
         gc.c = (char*)d->c + (int64_t)c0 * (d->c_dtype == ASRX_F32 ? 4 : 2);
         if (gc.rowadd) gc.rowadd = d->rowadd + c0;
         if (gc.resid) gc.resid = (const float*)d->resid + c0;
-        if (gc.gate) gc.gate = (const bf16_t*)d->gate + c0;
+        if (gc.gate) gc.gate = d->gate_dtype == ASRX_BITS ? (const void*)((const uint32_t*)d->gate + c0 / 32)
+                                                          : (const void*)((const bf16_t*)d->gate + c0);
+        if (gc.mask_out) gc.mask_out = d->mask_out + c0 / 32;
         const int nt = ((d->m + P_BM - 1) / P_BM) * ((gc.N + P_BN - 1) / P_BN);
         dispatch_p3<false, false>(gc, epi, nt, 1, 1, st);
       }

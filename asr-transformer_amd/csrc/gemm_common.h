@@ -26,10 +26,20 @@ struct GemmArgs {
   float* rowsum_ws;                // [splitk][M] partials when splitk > 1
   int dbg;                         // diagnostics only (ASRX_GEMM_DBG): 1 = skip the epilogue stores
   int exact;                       // p5: N % 256 == 0 -> store-only epilogues use exact-count buffer stores
+  uint32_t* mask_out; int64_t ld_mask;   // E_MASKOUT: stored C > 0 as bits of words [m][n / 32] (mask_bit_pos)
 };
 
 ASRX_DEV float ld_any(const void* p, int dtype, int64_t i) {
   return dtype == ASRX_BF16 ? bf2f(((const bf16_t*)p)[i]) : ((const float*)p)[i];
+}
+// ASRX_BITS mask layout: word [m][n / 32]; column c = n % 32 sits at bit 8 ((c & 15) >> 2) + 4 (c >> 4) + (c & 3)
+// (byte q holds columns 4q..4q+3 and 16+4q..16+4q+3: the 8 columns one epilogue lane owns)
+ASRX_DEV int mask_bit_pos(int n) { return 8 * ((n & 15) >> 2) + 4 * ((n >> 4) & 1) + (n & 3); }
+// gate value of element (m, n) for any gate dtype (ASRX_BITS: 1.0 / 0.0 from the bit mask)
+ASRX_DEV float gate_at(const GemmArgs& g, int m, int n) {
+  if (g.gate_dtype == ASRX_BITS)
+    return (((const uint32_t*)g.gate)[(int64_t)m * g.ld_gate + (n >> 5)] >> mask_bit_pos(n)) & 1u ? 1.f : 0.f;
+  return ld_any(g.gate, g.gate_dtype, (int64_t)m * g.ld_gate + n);
 }
 
 // Full epilogue for 4 consecutive columns n0..n0+3 of row m (batch z).
@@ -126,7 +136,7 @@ typedef const __attribute__((address_space(1))) void gbl_void_t;
 // specialising them removes the per-element runtime branches of epilogue4 (the generic fallback).
 enum : int {
   E_BIAS = 1, E_RELU = 2, E_DROP = 4, E_GATE = 8, E_RESID = 16, E_BETA = 32, E_F32 = 64, E_ALPHA = 128,
-  E_ROWADD = 256, E_GENERIC = 1 << 30
+  E_ROWADD = 256, E_GBITS = 512, E_MASKOUT = 1024, E_GENERIC = 1 << 30
 };
 
 // The fused element-wise epilogue of the fast path for the 4 consecutive columns n..n+3 of row m (valid
@@ -136,7 +146,7 @@ enum : int {
 // issued after them.
 template <int EPI, int TN, int TM>
 struct EpiPre {
-  static constexpr bool G = (EPI & E_GATE) != 0, R = (EPI & (E_RESID | E_ROWADD)) != 0;
+  static constexpr bool G = (EPI & (E_GATE | E_GBITS)) != 0, R = (EPI & (E_RESID | E_ROWADD)) != 0;
   static constexpr bool ANY = (G || R) && EPI != E_GENERIC;
   uint2 gt[G ? TN : 1][G ? TM : 1];
   f4_t rr[R ? TN : 1][R ? TM : 1];
@@ -153,7 +163,11 @@ ASRX_DEV void epi_prefetch(EpiPre<EPI, TN, TM>& p, const GemmArgs& g, int m0, in
       const bool ok = m < g.M && n < g.N;
       if constexpr (EpiPre<EPI, TN, TM>::G) {
         p.gt[i][j] = make_uint2(0u, 0u);
-        if (ok) p.gt[i][j] = *(const uint2*)((const bf16_t*)g.gate + (int64_t)m * g.ld_gate + n);
+        if constexpr ((EPI & E_GBITS) != 0) {   // the word holding columns n .. n + 3 (.x; .y unused)
+          if (ok) p.gt[i][j].x = ((const uint32_t*)g.gate)[(int64_t)m * g.ld_gate + (n >> 5)];
+        } else {
+          if (ok) p.gt[i][j] = *(const uint2*)((const bf16_t*)g.gate + (int64_t)m * g.ld_gate + n);
+        }
       }
       if constexpr (EpiPre<EPI, TN, TM>::R) {
         p.rr[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
@@ -197,6 +211,15 @@ ASRX_DEV f4_t epi_vals(const GemmArgs& g, int m, int n, f4_t v, f4_t b4, uint2 p
     if (!(bf2f(gt.x >> 16) > 0.f)) v[1] = 0.f;
     if (!(bf2f(gt.y & 0xffff) > 0.f)) v[2] = 0.f;
     if (!(bf2f(gt.y >> 16) > 0.f)) v[3] = 0.f;
+  }
+  if constexpr ((EPI & E_GBITS) != 0) {   // n % 4 == 0: the 4 bits sit in one word
+    uint32_t wd;
+    if constexpr (PRE) wd = pre_gt.x;
+    else wd = ((const uint32_t*)g.gate)[(int64_t)m * g.ld_gate + (n >> 5)];
+    const uint32_t nib = wd >> mask_bit_pos(n);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (!((nib >> e) & 1u)) v[e] = 0.f;
   }
   if constexpr ((EPI & E_RESID) != 0) {
     if constexpr (PRE) v += pre_rr;
@@ -270,9 +293,21 @@ ASRX_DEV int epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int
             v4u_t u = {sx[0], sy[0], sx[1], sy[1]};
             *(v4u_t*)((bf16_t*)g.c + (int64_t)m * g.ldc + ncol) = u;
           }
+          if constexpr ((EPI & E_MASKOUT) != 0) {
+            // ReLU outputs are >= 0, so "> 0" is "low 15 bits nonzero": adding 0x7fff to each 15-bit half sets
+            // its bit 15 exactly then (no carry across halves).  The lane's 8 bits (va cols 0-3, vb cols 0-3)
+            // form byte gq of the row's word for the 32 columns [na - 4 gq, +32): mask_bit_pos() below.
+            const uint32_t hi = 0x80008000u, lo = 0x7fff7fffu;
+            const uint32_t ma = ((ax & lo) + lo) & hi, mb = ((ay & lo) + lo) & hi;
+            const uint32_t mc = ((bx & lo) + lo) & hi, md = ((by & lo) + lo) & hi;
+            const uint32_t r = (ma >> 15) | (mb >> 13) | (mc >> 11) | (md >> 9);
+            const uint32_t byte = (r | (r >> 15)) & 0xffu;
+            if (m < g.M && na < g.N)
+              ((uint8_t*)g.mask_out)[((int64_t)m * g.ld_mask + (na >> 5)) * 4 + gq] = (uint8_t)byte;
+          }
         }
       }
-      return full ? TN * TM / 2 : 0;
+      return full ? ((EPI & E_MASKOUT) != 0 ? TN * TM : TN * TM / 2) : 0;
     }
   }
 #pragma unroll
@@ -310,8 +345,9 @@ ASRX_DEV int epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int
 
 // Epilogue sets instantiated per layout; anything else runs the generic epilogue.
 #define ASRX_EPI_NT(X) X(E_BIAS) X(E_BIAS | E_RELU) X(E_BIAS | E_RELU | E_DROP) X(E_BIAS | E_RESID | E_F32) \
-  X(E_BIAS | E_DROP | E_RESID | E_F32) X(E_F32) X(E_BIAS | E_ROWADD | E_F32) X(0)
-#define ASRX_EPI_NN(X) X(0) X(E_GATE) X(E_GATE | E_ALPHA) X(E_F32)
+  X(E_BIAS | E_DROP | E_RESID | E_F32) X(E_F32) X(E_BIAS | E_ROWADD | E_F32) X(0) \
+  X(E_BIAS | E_RELU | E_MASKOUT) X(E_BIAS | E_RELU | E_DROP | E_MASKOUT)
+#define ASRX_EPI_NN(X) X(0) X(E_GATE) X(E_GATE | E_ALPHA) X(E_F32) X(E_GBITS) X(E_GBITS | E_ALPHA)
 #define ASRX_EPI_TT(X) X(E_BETA | E_F32) X(E_F32)
 
 // s_waitcnt with only the vector-memory counter constrained (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14,

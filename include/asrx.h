@@ -29,6 +29,7 @@ extern "C" {
 
 #define ASRX_BF16 0
 #define ASRX_F32 1
+#define ASRX_BITS 2   /* gate operand only: 1 bit per element, uint32 words (ld in words; see mask_out) */
 
 /* Library version / build identification. */
 int asrx_version(void);
@@ -65,6 +66,13 @@ typedef struct asrx_gemm_desc {
    * dW = dY^T X is the row sum of its A operand dY^T — fused into the staging loads, no extra HBM pass.
    * With splitk > 1 the per-split partials use rowsum_ws[splitk*M]. */
   float* rowsum_a; float* rowsum_ws;
+  /* mask_out (optional; bf16 C with relu only): the bits C[m][n] > 0 as stored — the ReLU/dropout mask of an
+   * FFN hidden layer, read back by its data gradient as a gate_dtype = ASRX_BITS gate (1 bit instead of 2 bytes
+   * per element).  Layout (also that of ASRX_BITS gates): uint32 word [m][n / 32] (row stride ld_mask words),
+   * column c = n % 32 at bit 8*((c & 15) >> 2) + 4*(c >> 4) + (c & 3), i.e. byte q holds columns 4q..4q+3 and
+   * 16+4q..16+4q+3.  Requires N % 32 == 0, ldc % 8 == 0, 16-B aligned C and the fast fused epilogue; else
+   * ASRX_ERR_UNSUPPORTED. */
+  uint32_t* mask_out; int64_t ld_mask;
 } asrx_gemm_desc;
 
 int asrx_gemm(const asrx_gemm_desc* d, void* stream);

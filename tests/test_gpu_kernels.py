@@ -87,8 +87,65 @@ def test_gemm_epilogue(tile, kernel_variant):
     assert relerr(out.cpu(), ref) < 2e-3
 
 
+@pytest.mark.parametrize("kernel_variant", ["auto", "p3", "p5", "p5m", "glds", "ring", "ring128"], indirect=True)
+@pytest.mark.parametrize("m,n,p", [(300, 512, 0.1), (1000, 4160, 0.0), (4096, 2048, 0.1)])
+def test_gemm_relu_mask_bits(m, n, p, kernel_variant):
+    """FFN hidden layer: the ReLU/dropout epilogue also writes the 1-bit mask C > 0 (mask_out), and the data
+    gradient gated by those bits (gate_bits) equals the one gated by the bf16 C itself, bit for bit."""
+    k = 256
+    g = torch.Generator(device=dev).manual_seed(m + n)
+    x = bf(torch.randn(m, k, device=dev, generator=g))
+    w = bf(torch.randn(n, k, device=dev, generator=g) * 0.1)
+    bias = torch.randn(n, device=dev, generator=g) * 0.1
+    f = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
+    f0 = torch.empty_like(f)
+    bits = torch.full((m, n // 32 + 3), -1, device=dev, dtype=torch.int32)   # padded rows: strays would show
+    try:
+        K().linear(x, w, f, bias=bias, relu=True, dropout_p=p, seed=77, mask_out=bits, ld_mask=n // 32 + 3)
+    except RuntimeError as e:
+        # glds with 64 tiles is the register path (generic epilogue): the request is refused, never dropped
+        assert kernel_variant == "glds" and "unsupported" in str(e)
+        return
+    K().linear(x, w, f0, bias=bias, relu=True, dropout_p=p, seed=77)
+    torch.cuda.synchronize()
+    assert torch.equal(f, f0)
+    pos = (f.float() > 0).view(m, n // 32, 32).to(torch.int64)
+    c = torch.arange(32, device=dev)
+    want = (pos << (8 * ((c & 15) >> 2) + 4 * (c >> 4) + (c & 3))).sum(-1)   # include/asrx.h mask_out layout
+    got = bits[:, :n // 32].to(torch.int64) & 0xFFFFFFFF
+    assert torch.equal(got, want)
+    assert bool((bits[:, n // 32:] == -1).all())
+    dy = bf(torch.randn(m, k, device=dev, generator=g))
+    wt = w.t().contiguous()
+    for alpha in (1.0, 1.0 / 0.9):
+        d_bits = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
+        d_gate = torch.empty_like(d_bits)
+        K().linear_dgrad(dy, wt, d_bits, alpha=alpha, gate=bits, ld_gate=n // 32 + 3,
+                         gate_bits=True)
+        K().linear_dgrad(dy, wt, d_gate, alpha=alpha, gate=f, ld_gate=n)
+        torch.cuda.synchronize()
+        assert torch.equal(d_bits, d_gate)
+        ref = torch.where(f.float() > 0, alpha * (dy.float() @ wt.float()), torch.zeros((), device=dev))
+        assert relerr(d_bits.float(), ref) < 1e-2
+
+
+def test_gemm_mask_out_unsupported():
+    """mask_out needs relu and the paired bf16 store epilogue: fp32 C, N % 32 != 0 or no relu is refused, not
+    silently skipped."""
+    x = bf(torch.randn(64, 64, device=dev))
+    w = bf(torch.randn(48, 64, device=dev))
+    bits = torch.zeros(64, 2, device=dev, dtype=torch.int32)
+    with pytest.raises(Exception):
+        K().linear(x, w, torch.empty(64, 48, device=dev, dtype=torch.bfloat16), relu=True, mask_out=bits, ld_mask=2)
+    w = bf(torch.randn(64, 64, device=dev))
+    with pytest.raises(Exception):
+        K().linear(x, w, torch.empty(64, 64, device=dev), relu=True, mask_out=bits, ld_mask=2)
+    with pytest.raises(Exception):   # the bits are the ReLU mask: without relu the request is refused
+        K().linear(x, w, torch.empty(64, 64, device=dev, dtype=torch.bfloat16), mask_out=bits, ld_mask=2)
+
+
 @pytest.mark.parametrize("kernel_variant", ["p5", "p5m"], indirect=True)
-@pytest.mark.parametrize("m,n,k,bt", [(1000, 512, 256, False), (700, 768, 64, True), (1300, 256, 2048, False)])
+@pytest.mark.parametrize("m,n,k,bt",[(1000, 512, 256, False), (700, 768, 64, True), (1300, 256, 2048, False)])
 def test_gemm_exact_store_epilogue(m, n, k, bt, kernel_variant):
     """p5 store-only epilogues with exact-count buffer stores (N % 256 == 0, ragged M): persistent tiles back to
     back, bf16 and fp32 C, C rows padded (ldc > N) so a stray store would show."""
