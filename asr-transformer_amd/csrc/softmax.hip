@@ -2,6 +2,8 @@
 // Replaces layers.py:20 (scale), :22-23 (masked_fill(mask>0,-inf)), :25 (softmax + nan_to_num), :26 dropout,
 // and their autograd backward.  HBM-bound: one read + one (or two) writes of the score matrix.
 // LPR lanes per row (rows/wave = 64/LPR), V contiguous elements per lane per step (16-B accesses), NJ steps.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -59,6 +61,34 @@ ASRX_DEV void st_vec(void* p, int dtype, int64_t off, const float* v, int nvalid
     }
 }
 
+// Elements a lane may load at k0: the padding columns [lk, ld) are read with the row (one 16-B access instead of
+// a scalar tail; their values are masked afterwards), except on the last row, whose padding may not be allocated.
+ASRX_DEV int loadable(const SmArgs& a, int64_t rr, int k0, int V) {
+  const int64_t lim = rr < a.rows - 1 ? a.ld : a.lk;
+  return (int)max((int64_t)0, min((int64_t)V, lim - k0));
+}
+
+// Reduction over the LPR lanes of a row group by DPP within 16-lane rows, then the gfx950 permlane16/32 swaps
+// (no LDS round trips: the ds_bpermute chain of __shfl_xor set the per-row latency).
+template <int LPR, bool MAX>
+ASRX_DEV float group_reduce(float v) {
+  static_assert(LPR == 16 || LPR == 32 || LPR == 64, "row group must be 16, 32 or 64 lanes");
+  auto op = [](float x, float y) { return MAX ? fmaxf(x, y) : x + y; };
+  v = op(v, dpp_f<0xB1>(v));
+  v = op(v, dpp_f<0x4E>(v));
+  v = op(v, dpp_f<0x141>(v));
+  v = op(v, dpp_f<0x140>(v));
+  if constexpr (LPR >= 32) {
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = op(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  }
+  if constexpr (LPR == 64) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = op(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  }
+  return v;
+}
+
 ASRX_DEV bool is_masked(const SmArgs& a, int b, int q, int key) {
   if (a.mode == 1) {
     if (a.causal && key > q) return true;
@@ -70,119 +100,168 @@ ASRX_DEV bool is_masked(const SmArgs& a, int b, int q, int key) {
   return false;
 }
 
-template <int V, int LPR, int NJ>
+// U rows per lane group per block-wave: every row's loads are issued before the first row reduces, so a wave
+// keeps U x 16 B per lane in flight (the one-row version left HBM idle between a row's load and its store).
+template <int V, int LPR, int NJ, int U>
 __global__ __launch_bounds__(256) void softmax_fwd_kernel(SmArgs a) {
   constexpr int RPW = 64 / LPR;
   const int l = threadIdx.x & 63;
   const int sub = l / LPR, ll = l % LPR;
-  const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + sub;
-  const bool live = row < a.rows;
-  const int64_t rr = live ? row : 0;
-  const int64_t bh = rr / a.lq;
-  const int q = (int)(rr % a.lq);
-  const int b = (int)(bh / a.heads);
-  float v[NJ][V];
-  float mx = -INFINITY;
+  const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW * U + sub;
+  float v[U][NJ][V];
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int k0 = (j * LPR + ll) * V;
-    const int nv = max(0, min(V, a.lk - k0));
-    ld_vec<V>(a.s, a.dtype, rr * a.ld + k0, v[j], nv);
+  for (int u = 0; u < U; ++u) {
+    const int64_t row = row0 + (int64_t)u * RPW;
+    const int64_t rr = row < a.rows ? row : 0;
 #pragma unroll
-    for (int i = 0; i < V; ++i) {
-      const int key = k0 + i;
-      const bool m = key >= a.lk || is_masked(a, b, q, key);
-      v[j][i] = m ? -INFINITY : v[j][i] * a.scale2;
-      mx = fmaxf(mx, v[j][i]);
+    for (int j = 0; j < NJ; ++j) {
+      const int k0 = (j * LPR + ll) * V;
+      ld_vec<V>(a.s, a.dtype, rr * a.ld + k0, v[u][j], loadable(a, rr, k0, V));
     }
   }
 #pragma unroll
-  for (int o = LPR / 2; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-  const float mref = mx == -INFINITY ? 0.f : mx;
-  float sum = 0.f;
+  for (int u = 0; u < U; ++u) {
+    const int64_t row = row0 + (int64_t)u * RPW;
+    const bool live = row < a.rows;
+    const int64_t rr = live ? row : 0;
+    // 32-bit index math when the row count allows it (64-bit division is a long software sequence per row)
+    int64_t bh; int q;
+    if (a.rows < (int64_t)INT32_MAX) { bh = (int)rr / a.lq; q = (int)rr - (int)bh * a.lq; }
+    else { bh = rr / a.lq; q = (int)(rr % a.lq); }
+    const int b = (int)bh / a.heads;
+    float mx = -INFINITY;
 #pragma unroll
-  for (int j = 0; j < NJ; ++j)
+    for (int j = 0; j < NJ; ++j) {
+      const int k0 = (j * LPR + ll) * V;
 #pragma unroll
-    for (int i = 0; i < V; ++i) { v[j][i] = exp2f(v[j][i] - mref); sum += v[j][i]; }
+      for (int i = 0; i < V; ++i) v[u][j][i] = k0 + i >= a.lk ? -INFINITY : v[u][j][i] * a.scale2;
+      if (a.mode != 0) {  // uniform branch: the unmasked path stays straight-line
 #pragma unroll
-  for (int o = LPR / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
-  const float inv = sum > 0.f ? 1.f / sum : 0.f;  // all-masked row -> 0 (nan_to_num, layers.py:25)
-  if (!live) return;
+        for (int i = 0; i < V; ++i)
+          if (k0 + i < a.lk && is_masked(a, b, q, k0 + i)) v[u][j][i] = -INFINITY;
+      }
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int k0 = (j * LPR + ll) * V;
-    const int nv = max(0, min(V, a.lk - k0));
-    if (nv <= 0) continue;
-    float o[V];
+      for (int i = 0; i < V; ++i) mx = fmaxf(mx, v[u][j][i]);
+    }
+    mx = group_reduce<LPR, true>(mx);
+    const float mref = mx == -INFINITY ? 0.f : mx;
+    float sum = 0.f;
 #pragma unroll
-    for (int i = 0; i < V; ++i) o[i] = v[j][i] * inv;
-    st_vec<V>(a.p, a.dtype, rr * a.ld + k0, o, nv);
-    if (a.pd) {
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
-      for (int i = 0; i < V; ++i)
-        o[i] = (a.thr == 0u || attn_keep(a.seed, bh, a.lq, a.lk, q, k0 + i, a.thr)) ? o[i] * a.dscale : 0.f;
-      st_vec<V>(a.pd, a.dtype, rr * a.ld + k0, o, nv);
+      for (int i = 0; i < V; ++i) { v[u][j][i] = exp2f(v[u][j][i] - mref); sum += v[u][j][i]; }
+    sum = group_reduce<LPR, false>(sum);
+    const float inv = sum > 0.f ? 1.f / sum : 0.f;  // all-masked row -> 0 (nan_to_num, layers.py:25)
+    if (!live) continue;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int k0 = (j * LPR + ll) * V;
+      const int nv = max(0, min(V, a.lk - k0));
+      if (nv <= 0) continue;
+      float o[V];
+#pragma unroll
+      for (int i = 0; i < V; ++i) o[i] = v[u][j][i] * inv;
+      st_vec<V>(a.p, a.dtype, rr * a.ld + k0, o, nv);
+      if (a.pd) {
+#pragma unroll
+        for (int i = 0; i < V; ++i)
+          o[i] = (a.thr == 0u || attn_keep(a.seed, bh, a.lq, a.lk, q, k0 + i, a.thr)) ? o[i] * a.dscale : 0.f;
+        st_vec<V>(a.pd, a.dtype, rr * a.ld + k0, o, nv);
+      }
     }
   }
 }
 
-template <int V, int LPR, int NJ>
+template <int V, int LPR, int NJ, int U>
 __global__ __launch_bounds__(256) void softmax_bwd_kernel(SmArgs a, void* ds) {
   constexpr int RPW = 64 / LPR;
   const int l = threadIdx.x & 63;
   const int sub = l / LPR, ll = l % LPR;
-  const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + sub;
-  const bool live = row < a.rows;
-  const int64_t rr = live ? row : 0;
-  float pv[NJ][V], gv[NJ][V];
-  float dot = 0.f;
+  const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW * U + sub;
+  float pv[U][NJ][V], gv[U][NJ][V];
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int k0 = (j * LPR + ll) * V;
-    const int nv = max(0, min(V, a.lk - k0));
-    ld_vec<V>(a.p, a.dtype, rr * a.ld + k0, pv[j], nv);
-    ld_vec<V>(a.pd, a.dtype, rr * a.ld + k0, gv[j], nv);
+  for (int u = 0; u < U; ++u) {
+    const int64_t row = row0 + (int64_t)u * RPW;
+    const int64_t rr = row < a.rows ? row : 0;
 #pragma unroll
-    for (int i = 0; i < V; ++i) {
-      if (a.thr) gv[j][i] = attn_keep(a.seed, rr / a.lq, a.lq, a.lk, (int)(rr % a.lq), k0 + i, a.thr) ? gv[j][i] * a.dscale : 0.f;
-      dot += pv[j][i] * gv[j][i];
+    for (int j = 0; j < NJ; ++j) {
+      const int k0 = (j * LPR + ll) * V;
+      const int nv = loadable(a, rr, k0, V);
+      ld_vec<V>(a.p, a.dtype, rr * a.ld + k0, pv[u][j], nv);
+      ld_vec<V>(a.pd, a.dtype, rr * a.ld + k0, gv[u][j], nv);
     }
   }
 #pragma unroll
-  for (int o = LPR / 2; o > 0; o >>= 1) dot += __shfl_xor(dot, o, 64);
-  if (!live) return;
+  for (int u = 0; u < U; ++u) {
+    const int64_t row = row0 + (int64_t)u * RPW;
+    const bool live = row < a.rows;
+    const int64_t rr = live ? row : 0;
+    float dot = 0.f;
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int k0 = (j * LPR + ll) * V;
-    const int nv = max(0, min(V, a.lk - k0));
-    if (nv <= 0) continue;
-    float o[V];
+    for (int j = 0; j < NJ; ++j) {
+      const int k0 = (j * LPR + ll) * V;
 #pragma unroll
-    for (int i = 0; i < V; ++i) o[i] = pv[j][i] * (gv[j][i] - dot) * a.scale2;
-    st_vec<V>(ds, a.dtype, rr * a.ld + k0, o, nv);
+      for (int i = 0; i < V; ++i) {
+        if (k0 + i >= a.lk) { pv[u][j][i] = 0.f; gv[u][j][i] = 0.f; }
+        if (a.thr)
+          gv[u][j][i] = attn_keep(a.seed, rr / a.lq, a.lq, a.lk, (int)(rr % a.lq), k0 + i, a.thr) ? gv[u][j][i] * a.dscale : 0.f;
+        dot += pv[u][j][i] * gv[u][j][i];
+      }
+    }
+    dot = group_reduce<LPR, false>(dot);
+    if (!live) continue;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int k0 = (j * LPR + ll) * V;
+      const int nv = max(0, min(V, a.lk - k0));
+      if (nv <= 0) continue;
+      float o[V];
+#pragma unroll
+      for (int i = 0; i < V; ++i) o[i] = pv[u][j][i] * (gv[u][j][i] - dot) * a.scale2;
+      st_vec<V>(ds, a.dtype, rr * a.ld + k0, o, nv);
+    }
   }
 }
 
-template <int V, int LPR, int NJ>
+template <int V, int LPR, int NJ, int U>
 bool try_launch(const SmArgs& a, bool bwd, void* ds, hipStream_t st) {
   if ((int64_t)a.lk > (int64_t)NJ * LPR * V) return false;
   constexpr int RPW = 64 / LPR;
-  const int64_t waves = (a.rows + RPW - 1) / RPW;
+  const int64_t waves = (a.rows + RPW * U - 1) / (RPW * U);
   const unsigned blocks = (unsigned)((waves + 3) / 4);
-  if (bwd) hipLaunchKernelGGL((softmax_bwd_kernel<V, LPR, NJ>), dim3(blocks), dim3(256), 0, st, a, ds);
-  else hipLaunchKernelGGL((softmax_fwd_kernel<V, LPR, NJ>), dim3(blocks), dim3(256), 0, st, a);
+  if (bwd) hipLaunchKernelGGL((softmax_bwd_kernel<V, LPR, NJ, U>), dim3(blocks), dim3(256), 0, st, a, ds);
+  else hipLaunchKernelGGL((softmax_fwd_kernel<V, LPR, NJ, U>), dim3(blocks), dim3(256), 0, st, a);
   return true;
+}
+
+// Short rows (one step per lane) may batch U rows per lane group (ASRX_SOFTMAX_U = 1, 2 or 4; default 1);
+// long rows already keep NJ loads in flight.
+template <int V, int U>
+bool dispatch_u(const SmArgs& a, bool bwd, void* ds, hipStream_t st) {
+  return try_launch<V, 16, 1, U>(a, bwd, ds, st) || try_launch<V, 32, 1, U>(a, bwd, ds, st) ||
+         try_launch<V, 64, 1, U>(a, bwd, ds, st);
+}
+
+int softmax_u() {
+  static const int u = [] {
+    const char* e = getenv("ASRX_SOFTMAX_U");
+    const int v = e ? atoi(e) : 1;
+    return (v == 2 || v == 4) ? v : 1;
+  }();
+  return u;
 }
 
 template <int V>
 bool dispatch(const SmArgs& a, bool bwd, void* ds, hipStream_t st) {
-  return try_launch<V, 16, 1>(a, bwd, ds, st) || try_launch<V, 32, 1>(a, bwd, ds, st) ||
-         try_launch<V, 64, 1>(a, bwd, ds, st) || try_launch<V, 64, 2>(a, bwd, ds, st) ||
-         try_launch<V, 64, 4>(a, bwd, ds, st) || try_launch<V, 64, 8>(a, bwd, ds, st) ||
-         try_launch<V, 64, 16>(a, bwd, ds, st);
+  const int u = softmax_u();
+  const bool shortrow = u == 4 ? dispatch_u<V, 4>(a, bwd, ds, st)
+                      : u == 2 ? dispatch_u<V, 2>(a, bwd, ds, st) : dispatch_u<V, 1>(a, bwd, ds, st);
+  return shortrow || try_launch<V, 64, 2, 1>(a, bwd, ds, st) ||
+         try_launch<V, 64, 4, 1>(a, bwd, ds, st) || try_launch<V, 64, 8, 1>(a, bwd, ds, st) ||
+         try_launch<V, 64, 16, 1>(a, bwd, ds, st);
 }
 
-int run(const SmArgs& a, bool bwd, void* ds, hipStream_t st) {
+int run(SmArgs a, bool bwd, void* ds, hipStream_t st) {
   bool ok;
   const bool al = a.dtype == ASRX_F32 ? (a.ld % 4 == 0) : (a.ld % 8 == 0);
   if (al && a.dtype == ASRX_F32) ok = dispatch<4>(a, bwd, ds, st);
