@@ -1,6 +1,8 @@
 // LayerNorm forward/backward and deterministic row reductions (HBM-bound kernels).
 // Replaces nn.LayerNorm (model.py:14,16,33,59,61,63,101) = aten::native_layer_norm(+_backward).
 // One wave per row, CH contiguous elements per lane per step (16-B fp32 / 8-B bf16 accesses), NJ steps.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -35,42 +37,53 @@ ASRX_DEV void store_ch(void* p, int dtype, int64_t off, const float* v) {
   }
 }
 
-template <int CH, int NJ>
+// RW rows per wave: gamma/beta are loaded once per wave (RW = 1 re-read them from L2 with every row) and row r+1's
+// loads are issued before row r reduces.
+template <int CH, int NJ, int RW>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(int x_dtype, const void* x, int y_dtype, void* y,
                                                      const float* gamma, const float* beta, float* mean,
                                                      float* rstd, int64_t rows, float eps) {
   constexpr int D = CH * NJ * 64;
   const int l = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  float v[NJ][CH], gm[NJ][CH], bt[NJ][CH];
-  float s = 0.f;
+  const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RW;
+  if (row0 >= rows) return;
+  float v[RW][NJ][CH], gm[NJ][CH], bt[NJ][CH];
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {   // gamma / beta issued with the row: no load after the reductions
-    load_ch<CH>(x, x_dtype, row * D + (j * 64 + l) * CH, v[j]);
+  for (int j = 0; j < NJ; ++j) {   // gamma / beta issued with the first row: no load after the reductions
+    load_ch<CH>(x, x_dtype, row0 * D + (j * 64 + l) * CH, v[0][j]);
     load_ch<CH>(gamma, ASRX_F32, (j * 64 + l) * CH, gm[j]);
     load_ch<CH>(beta, ASRX_F32, (j * 64 + l) * CH, bt[j]);
   }
 #pragma unroll
-  for (int j = 0; j < NJ; ++j)
+  for (int r = 0; r < RW; ++r) {
+    const int64_t row = row0 + r;
+    if (row >= rows) break;  // wave-uniform
+    if (r + 1 < RW && row + 1 < rows) {
 #pragma unroll
-    for (int i = 0; i < CH; ++i) s += v[j][i];
-  const float mu = wave_sum(s) * (1.f / D);
-  float q = 0.f;
+      for (int j = 0; j < NJ; ++j) load_ch<CH>(x, x_dtype, (row + 1) * D + (j * 64 + l) * CH, v[r + 1 < RW ? r + 1 : r][j]);
+    }
+    float s = 0.f;
 #pragma unroll
-  for (int j = 0; j < NJ; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
-    for (int i = 0; i < CH; ++i) { const float t = v[j][i] - mu; q += t * t; }
-  const float rs = rsqrtf(wave_sum(q) * (1.f / D) + eps);
+      for (int i = 0; i < CH; ++i) s += v[r][j][i];
+    const float mu = wave_sum(s) * (1.f / D);
+    float q = 0.f;
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int c0 = (j * 64 + l) * CH;
-    float o[CH];
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
-    for (int i = 0; i < CH; ++i) o[i] = (v[j][i] - mu) * rs * gm[j][i] + bt[j][i];
-    store_ch<CH>(y, y_dtype, row * D + c0, o);
+      for (int i = 0; i < CH; ++i) { const float t = v[r][j][i] - mu; q += t * t; }
+    const float rs = rsqrtf(wave_sum(q) * (1.f / D) + eps);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c0 = (j * 64 + l) * CH;
+      float o[CH];
+#pragma unroll
+      for (int i = 0; i < CH; ++i) o[i] = (v[r][j][i] - mu) * rs * gm[j][i] + bt[j][i];
+      store_ch<CH>(y, y_dtype, row * D + c0, o);
+    }
+    if (l == 0) { mean[row] = mu; rstd[row] = rs; }
   }
-  if (l == 0) { mean[row] = mu; rstd[row] = rs; }
 }
 
 // Backward. Each block: 4 waves, grid-stride over rows (one row per wave per iteration); the NEXT row's
@@ -240,8 +253,21 @@ template <int CH, int NJ>
 bool ln_fwd_launch(int x_dtype, const void* x, int y_dtype, void* y, const float* gamma, const float* beta,
                    float* mean, float* rstd, int64_t rows, int d, float eps, hipStream_t st) {
   if (d != CH * NJ * 64) return false;
-  hipLaunchKernelGGL((ln_fwd_kernel<CH, NJ>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, x_dtype, x,
-                     y_dtype, y, gamma, beta, mean, rstd, rows, eps);
+  static const int rw = [] {   // rows per wave (ASRX_LN_RW = 1, 2 or 4; default 2: 9.4 -> 8.6 us at 15936 x 512)
+    const char* e = getenv("ASRX_LN_RW");
+    const int v = e ? atoi(e) : 2;
+    return (v == 1 || v == 4) ? v : 2;
+  }();
+  const unsigned blocks = (unsigned)((rows + 4 * rw - 1) / (4 * rw));
+  if (rw == 4)
+    hipLaunchKernelGGL((ln_fwd_kernel<CH, NJ, 4>), dim3(blocks), dim3(256), 0, st, x_dtype, x, y_dtype, y, gamma, beta,
+                       mean, rstd, rows, eps);
+  else if (rw == 2)
+    hipLaunchKernelGGL((ln_fwd_kernel<CH, NJ, 2>), dim3(blocks), dim3(256), 0, st, x_dtype, x, y_dtype, y, gamma, beta,
+                       mean, rstd, rows, eps);
+  else
+    hipLaunchKernelGGL((ln_fwd_kernel<CH, NJ, 1>), dim3(blocks), dim3(256), 0, st, x_dtype, x, y_dtype, y, gamma, beta,
+                       mean, rstd, rows, eps);
   return true;
 }
 
