@@ -201,12 +201,17 @@ __global__ __launch_bounds__(256) void softmax_bwd_kernel(SmArgs a, void* ds) {
     for (int j = 0; j < NJ; ++j) {
       const int k0 = (j * LPR + ll) * V;
 #pragma unroll
-      for (int i = 0; i < V; ++i) {
+      for (int i = 0; i < V; ++i)
         if (k0 + i >= a.lk) { pv[u][j][i] = 0.f; gv[u][j][i] = 0.f; }
-        if (a.thr)
-          gv[u][j][i] = attn_keep(a.seed, rr / a.lq, a.lq, a.lk, (int)(rr % a.lq), k0 + i, a.thr) ? gv[u][j][i] * a.dscale : 0.f;
-        dot += pv[u][j][i] * gv[u][j][i];
+      if (a.thr) {  // uniform branch: the no-dropout path stays straight-line
+        const int64_t bh = rr / a.lq;
+        const int q = (int)(rr - bh * a.lq);
+#pragma unroll
+        for (int i = 0; i < V; ++i)
+          gv[u][j][i] = attn_keep(a.seed, bh, a.lq, a.lk, q, k0 + i, a.thr) ? gv[u][j][i] * a.dscale : 0.f;
       }
+#pragma unroll
+      for (int i = 0; i < V; ++i) dot += pv[u][j][i] * gv[u][j][i];
     }
     dot = group_reduce<LPR, false>(dot);
     if (!live) continue;

@@ -157,6 +157,10 @@ def sub_rooflines(B, T2, d, H, ff, p_drop):
     hbm("softmax_fwd", 2 * nbh * T2 * T2 * 2, lambda: K.softmax_fwd(sc, pr, None, nbh, H, T2, T2, ld, d ** -0.5,
                                                                     MaskSpec()),
         f"unfused path (attention=\"unfused\"): {nbh}x{T2}x{T2} bf16 scores -> probabilities")
+    dpd = torch.randn(nbh, T2, ld, device="cuda", generator=gen).bfloat16()
+    dsc = torch.empty_like(sc)
+    hbm("softmax_bwd", 3 * nbh * T2 * T2 * 2, lambda: K.softmax_bwd(pr, dpd, dsc, nbh, T2, T2, ld, d ** -0.5),
+        f"unfused path: {nbh}x{T2}x{T2} bf16 probabilities + their gradient -> score gradient")
     return out
 
 
