@@ -40,20 +40,17 @@ class GemmDesc(ctypes.Structure):
         ("tile", c_i32),
         ("rowsum_a", c_vp), ("rowsum_ws", c_vp),
         ("mask_out", c_vp), ("ld_mask", c_i64),
+        ("kernel", c_i32),
     ]
 
 
-class GemmGroup(ctypes.Structure):
+class GemmGroupDev(ctypes.Structure):
+    """asrx_gemm_group_dev: one 64-byte entry of a grouped launch's device table."""
     _fields_ = [
-        ("m", c_i32), ("n", c_i32), ("k", c_i32),
-        ("a", c_vp), ("lda", c_i64),
-        ("b", c_vp), ("ldb", c_i64),
-        ("c", c_vp), ("ldc", c_i64),
-        ("rowsum_a", c_vp),
+        ("a", c_vp), ("b", c_vp), ("c", c_vp), ("rowsum_a", c_vp),
+        ("lda", c_i32), ("ldb", c_i32), ("ldc", c_i32), ("m", c_i32), ("n", c_i32), ("k", c_i32),
+        ("tile_start", c_i32), ("reserved", c_i32),
     ]
-
-
-MAX_GROUPS = 48   # gemm.hip MAX_GROUPS (kernel-argument table)
 
 
 class RowsumGroup(ctypes.Structure):
@@ -82,16 +79,16 @@ class AttnDesc(ctypes.Structure):
         ("dv", c_vp), ("dv_rstride", c_i64), ("dv_bstride", c_i64),
         ("delta", c_vp), ("dq_acc", c_vp),
         ("dropmask", c_vp), ("dropmask_ready", c_i32),
+        ("o_lo", c_vp),
     ]
 
 
 # name -> argtypes (restype is int for all)
 SIGNATURES = {
     "asrx_version": [],
+    "asrx_struct_sizes": [ctypes.POINTER(c_i64), c_i32],
     "asrx_gemm": [ctypes.POINTER(GemmDesc), c_vp],
     "asrx_gemm_kernel_name": [ctypes.POINTER(GemmDesc), ctypes.c_char_p, c_i32],
-    "asrx_gemm_grouped": [ctypes.POINTER(GemmDesc), ctypes.POINTER(GemmGroup), c_i32, c_vp],
-    "asrx_gemm_grouped_table": [ctypes.POINTER(GemmDesc), c_vp, c_vp, c_i32, c_i32, c_i32, c_vp],
     "asrx_gemm_grouped_xcd": [ctypes.POINTER(GemmDesc), c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp],
     "asrx_reduce_rows_grouped": [ctypes.POINTER(RowsumGroup), c_i32, c_vp],
     "asrx_attention_fwd": [ctypes.POINTER(AttnDesc), c_vp],
@@ -118,7 +115,9 @@ SIGNATURES = {
     "asrx_cross_entropy": [c_vp, c_i64, c_i32, c_i64, c_vp, c_i64, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp],
     "asrx_cast": [c_i32, c_vp, c_i32, c_vp, c_i64, c_vp],
     "asrx_adam": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32, c_i32,
-                  c_vp],
+                  c_vp, c_vp],
+    "asrx_upload": [c_vp, c_vp, c_i64, c_vp],
+    "asrx_set_seed_offset": [c_u64, c_vp],
     "asrx_dropout_mask": [c_vp, c_i64, c_f32, c_u64, c_vp],
 }
 

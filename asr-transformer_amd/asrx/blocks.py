@@ -247,8 +247,10 @@ def attn_fwd(C, q, k, v, o, B, H, Lq, Lk, dh, strides, scale, spec, prep=None):
         else:
             dm = K.dropmask_buffer(B, H, Lq, Lk, dh, C.p, q.device)
         S["dropmask"] = dm
+        # training: the O rounding residual keeps the backward's delta exact (see include/asrx.h o_lo)
+        S["o_lo"] = torch.empty_like(o) if C.train else None
         S["lse"] = K.attention_fwd(q, k, v, o, B, H, Lq, Lk, dh, strides, scale, spec, C.p, seed,
-                                   dropmask=dm, dropmask_ready=ready)
+                                   dropmask=dm, dropmask_ready=ready, o_lo=S["o_lo"])
         S["impl"] = "fused"
         return S
     S["impl"] = "unfused"
@@ -273,7 +275,7 @@ def attn_bwd(C, S, q, k, v, o, do, dq, dk, dv, gstrides):
     strides, scale, spec, seed = S["strides"], S["scale"], S["spec"], S["seed"]
     if S["impl"] == "fused":
         K.attention_bwd(q, k, v, o, S["lse"], do, dq, dk, dv, B, H, Lq, Lk, dh, strides, gstrides, scale, spec,
-                        C.p, seed, dropmask=S["dropmask"])
+                        C.p, seed, dropmask=S["dropmask"], o_lo=S["o_lo"])
         return
     (qr, qb), (kr, kb), (vr, vb), _ = strides
     (dor, dob), (dqr, dqb), (dkr, dkb), (dvr, dvb) = gstrides

@@ -4,16 +4,12 @@ flat gradient buffer that `p.grad` views (asrx.params); the Functions return Non
 
 `model_forward` / `model_backward` are also used directly (no autograd) by the fused trainer (asrx.train).
 """
-import random
-
 import torch
 
 from . import blocks as Bk
 from . import kernels as K
 from .kernels import MaskSpec
 from .params import FlatParams
-
-_SEED_BASE = random.SystemRandom().randrange(1 << 62)
 
 
 # ------------------------------------------------------------------------------------------- store / context
@@ -57,6 +53,12 @@ def get_store(m):
     return st
 
 
+def draw_seed():
+    """Dropout seed base of one call, drawn from torch's default CPU generator: runs are reproducible under
+    torch.manual_seed, as the reference's nn.Dropout is (its masks come from torch's RNG)."""
+    return int(torch.randint(0, 1 << 62, (1,), dtype=torch.int64))
+
+
 def make_ctx(m, p_drop):
     root = root_of(m)
     st = get_store(m)
@@ -65,9 +67,7 @@ def make_ctx(m, p_drop):
     if cd == torch.bfloat16:
         st.refresh_shadow()
     train = m.training
-    n = root.__dict__.get("_asrx_calls", 0) + 1
-    root.__dict__["_asrx_calls"] = n
-    seeds = Bk.Seeds(_SEED_BASE + n * 1000003)
+    seeds = Bk.Seeds(draw_seed())
     return Bk.Ctx(st, cd, train, p_drop, seeds, getattr(root, "attention", "fused"))
 
 
@@ -145,6 +145,9 @@ def _release(C, ready, params):
         C.fresh.drain(params, C.store)
     for a, b in _spans(C, params):
         ready(a, b)
+    boundary = getattr(ready, "boundary", None)   # graph capture: the released ranges end a captured segment
+    if boundary is not None:
+        boundary()
     C.defer_wgrad()
 
 

@@ -5,7 +5,12 @@ same metrics dict) for drop-in use with any torch optimizer and loss.
 
 `Trainer` is the MI355X-native step: forward -> fused cross-entropy kernel -> explicit backward -> RCCL
 bucketed gradient all-reduce -> fused AdamW over the flat parameter buffer (which also refreshes the bf16
-operand copy).  No autograd graph, no per-parameter launches.
+operand copy).  No autograd graph, no per-parameter launches.  After two eager steps the step is captured as
+HIP graph(s) and replayed (about 700 launches otherwise cost ~13 ms of Python/ctypes enqueue per step, as much as
+the GPU work): per-step values reach the replay through device memory (dropout seed offset, Adam lr / bias
+corrections), new batches are copied into the captured input buffers.  With a multi-GPU reducer the backward
+is captured in segments that end where gradient ranges become final; the RCCL all-reduce of each range is
+issued between segment replays, so it still overlaps the rest of the backward.
 """
 import os
 
@@ -19,6 +24,65 @@ from .functions import get_store, make_ctx, model_backward, model_forward
 # weight gradients whose only writer is one weight-gradient GEMM are not zeroed before the backward: that GEMM
 # writes them with beta = 0 (blocks.FreshGrads).  ASRX_FRESH_GRADS=0 zeroes the whole buffer instead (A/B).
 FRESH_GRADS = os.environ.get("ASRX_FRESH_GRADS", "1") == "1"
+# capture the training step as HIP graph(s) after the eager warm-up steps (ASRX_GRAPH=0: eager steps, A/B)
+GRAPH = os.environ.get("ASRX_GRAPH", "1") == "1"
+GRAPH_WARMUP = 2
+
+
+class _Segments:
+    """A training step captured as a sequence of HIP graphs sharing one memory pool, replayed in order.
+
+    A new segment starts where (a) the backward hands finished gradient ranges to the all-reduce (`ready` +
+    `boundary`: the replay issues their RCCL all-reduce between segment replays, overlapping the rest of the
+    backward) or (b) the bench's kernel probe times one kernel (`split`: that kernel gets a segment of its own,
+    bracketed by HIP events at replay)."""
+
+    def __init__(self, pool):
+        self.pool = pool
+        self.graphs, self.after, self.timed = [], [], []
+        self._pending = []
+        self._begin(None)
+
+    def _begin(self, timed):
+        g = torch.cuda.CUDAGraph()
+        g.capture_begin(pool=self.pool)
+        self.graphs.append(g)
+        self.timed.append(timed)
+
+    def _end(self):
+        self.graphs[-1].capture_end()
+        self.after.append(self._pending)
+        self._pending = []
+
+    def __call__(self, a, b):
+        self._pending.append((a, b))
+
+    def boundary(self):
+        self._end()
+        self._begin(None)
+
+    def split(self, timed):
+        self._end()
+        self._begin(timed)
+
+    def close(self):
+        self._end()
+
+    def replay(self, reducer):
+        probe = K.PROBE
+        for g, spans, timed in zip(self.graphs, self.after, self.timed):
+            if timed is not None and probe is not None and probe.record(timed[0]):
+                name, flops = timed
+                s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s0.record()
+                g.replay()
+                s1.record()
+                probe.events.setdefault(name, []).append((s0, s1))
+                probe.flops[name] = probe.flops.get(name, 0) + flops
+            else:
+                g.replay()
+            for a, b in spans:
+                reducer.ready(a, b)
 
 
 def wgrad_only_params(model):
@@ -97,7 +161,7 @@ class Trainer:
     """Native data-parallel training step for an asrx.Transformer."""
 
     def __init__(self, model, lr=1e-4, betas=(0.9, 0.98), eps=1e-9, weight_decay=0.0, decoupled=True,
-                 ignore_index=-100, group=None, bucket_mb=64, allreduce_fn=None):
+                 ignore_index=-100, group=None, bucket_mb=64, allreduce_fn=None, graph=None):
         self.model = model
         self.store = get_store(model)
         self.m = torch.zeros_like(self.store.flat)
@@ -108,6 +172,9 @@ class Trainer:
         self.reducer = GradAllReduce(self.store.grad, group=group, bucket_mb=bucket_mb, allreduce_fn=allreduce_fn)
         self.store.refresh_shadow(force=True)
         self._wonly = wgrad_only_params(model) if FRESH_GRADS else []
+        self.graph = GRAPH if graph is None else bool(graph)
+        self._cap = None        # captured step: (segments, static inputs, loss)
+        self._hyp = torch.zeros(3, dtype=torch.float32, device=self.store.flat.device)
         if self._wonly:   # flat indices of everything else (zeroed each step by one index_fill)
             keep = torch.ones(self.store.grad.numel(), dtype=torch.bool)
             for p in self._wonly:
@@ -115,8 +182,9 @@ class Trainer:
                 keep[o:o + p.numel()] = False
             self._zero_idx = keep.nonzero().squeeze(1).to(self.store.grad.device)
 
-    def forward_backward(self, spectrum, text, mask):
-        """text: (B, L+1) with BOS ... ; inputs text[:, :-1], targets text[:, 1:] (train.py:24,32)."""
+    def forward_backward(self, spectrum, text, mask, ready=None, capture=False):
+        """text: (B, L+1) with BOS ... ; inputs text[:, :-1], targets text[:, 1:] (train.py:24,32).
+        ready: gradient-range hook (default: the reducer's, when multi-GPU); capture: building a HIP graph."""
         model = self.model
         C = make_ctx(model, model.decoder.p)
         logits, S = model_forward(C, model, spectrum, text[:, :-1], mask[:, :-1])
@@ -128,19 +196,73 @@ class Trainer:
             C.fresh = FreshGrads(self.store, self._wonly)
         else:
             self.store.grad.zero_()
-        model_backward(C, model, S, dl.to(C.cd) if dl.dtype != C.cd else dl,
-                       ready=self.reducer.ready if self.reducer.active else None)
+        if ready is None and not capture and self.reducer.active:
+            ready = self.reducer.ready
+        model_backward(C, model, S, dl.to(C.cd) if dl.dtype != C.cd else dl, ready=ready)
         if C.fresh is not None:
             C.fresh.drain()
             C.fresh = None
         return loss
 
+    def _adam(self, hyp=None):
+        K.adam(self.store.flat, self.store.grad, self.m, self.v, self.store.shadow, self.lr, self.betas[0],
+               self.betas[1], self.eps, self.wd, max(1, self.step_count), grad_scale=1.0 / self.reducer.world,
+               decoupled=self.decoupled, hyp=hyp)
+
     def step(self, spectrum, text, mask):
+        """One training step (forward, CE, backward, all-reduce, AdamW).  Returns the loss as a device scalar; in
+        graph mode it is the captured output tensor, overwritten by the next step."""
+        if self.graph and self.model.precision == "bf16":
+            if self._cap is not None and not self._matches(spectrum, text, mask):
+                self._cap = None            # new input shapes: recapture
+            if self._cap is None and self.step_count >= GRAPH_WARMUP:
+                self._capture(spectrum, text, mask)
+            if self._cap is not None:
+                return self._replay(spectrum, text, mask)
         loss = self.forward_backward(spectrum, text, mask)
         self.reducer.finish()
         self.step_count += 1
-        K.adam(self.store.flat, self.store.grad, self.m, self.v, self.store.shadow, self.lr, self.betas[0],
-               self.betas[1], self.eps, self.wd, self.step_count, grad_scale=1.0 / self.reducer.world,
-               decoupled=self.decoupled)
+        self._adam()
+        self.store.mark_shadow_fresh()
+        return loss
+
+    # ---- HIP graph mode
+    def _matches(self, spectrum, text, mask):
+        ins = self._cap[1]
+        return all(a.shape == b.shape and a.dtype == b.dtype for a, b in zip(ins, (spectrum, text, mask)))
+
+    def _capture(self, spectrum, text, mask):
+        dev = self.store.flat.device
+        ins = tuple(x.to(dev).clone() for x in (spectrum, text, mask))
+        torch.cuda.synchronize(dev)
+        pool = torch.cuda.graph_pool_handle()
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            seg = _Segments(pool)
+            K.CAPTURE = seg
+            try:
+                loss = self.forward_backward(*ins, ready=seg if self.reducer.active else None, capture=True)
+                if not self.reducer.active:
+                    self._adam(self._hyp)
+            finally:
+                K.CAPTURE = None
+                seg.close()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize(dev)
+        self._cap = (seg, ins, loss)
+
+    def _replay(self, spectrum, text, mask):
+        seg, ins, loss = self._cap
+        for dst, src in zip(ins, (spectrum, text, mask)):
+            if dst.data_ptr() != src.data_ptr():
+                dst.copy_(src, non_blocking=True)
+        self.step_count += 1
+        K.set_seed_offset(self.step_count)
+        K.adam_hyper(self._hyp, self.lr, self.betas[0], self.betas[1], self.step_count)
+        seg.replay(self.reducer)
+        if self.reducer.active:
+            self.reducer.finish()
+            self._adam(self._hyp)
         self.store.mark_shadow_fresh()
         return loss

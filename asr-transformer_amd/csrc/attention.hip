@@ -30,6 +30,24 @@ ASRX_DEV s4_t lds_b64(const bf16_t* p) { return *(const s4_t*)p; }
 ASRX_DEV f4_t mfma16(s4_t a, s4_t b, f4_t c) { return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0); }
 
 typedef uint32_t u2_t __attribute__((ext_vector_type(2)));
+
+// Store 4 output values as bf16 at p and, with lo != nullptr, their rounding residuals v - bf16(v) as bf16 at lo.
+// The backward's delta = rowsum(dO * O) must equal sum_key P * dP to fp32 accuracy: with the scale d_model^-1/2
+// the softmax rows are flat, dS = P (dP - delta) is a small difference, and the bf16 rounding of O alone would
+// leave an error of about 2^-9 |O| in delta, multiplied by the mean key in dQ (the K bias gradient, zero in exact
+// arithmetic, grew 30-40x over the reference's bf16 path without it).
+ASRX_DEV void store_o4(bf16_t* p, bf16_t* lo, float v0, float v1, float v2, float v3) {
+  uint2 st;
+  st.x = pack2bf(v0, v1);
+  st.y = pack2bf(v2, v3);
+  *(uint2*)p = st;
+  if (lo) {
+    uint2 r;
+    r.x = pack2bf(v0 - bf2f(st.x & 0xffff), v1 - bf2f(st.x >> 16));
+    r.y = pack2bf(v2 - bf2f(st.y & 0xffff), v3 - bf2f(st.y >> 16));
+    *(uint2*)lo = r;
+  }
+}
 ASRX_DEV s4_t to_bf4(f4_t v) { return __builtin_bit_cast(s4_t, (u2_t){pack2bf(v[0], v[1]), pack2bf(v[2], v[3])}); }
 
 struct AttnArgs {
@@ -50,6 +68,7 @@ struct AttnArgs {
   bf16_t* dv; int64_t dvr, dvb;
   float* delta; float* dq_acc;
   uint32_t* dropmask;
+  bf16_t* o_lo;   // optional: O - bf16(O) (bf16), written by the forward, added to O in the backward's delta
   int dbg;   // phase timestamps of block 0 / wave 0 into g_attn_dbg (tools only; ASRX_ATTN_DBG=1)
 };
 
@@ -76,6 +95,7 @@ ASRX_DEV bool masked(const AttnArgs& a, int b, int q, int key) {
 // ---------------------------------------------------------------------------------------------------------
 template <int DH>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
+  a.seed = seed_eff(a.seed);
   constexpr int KS = DH + 4;   // K image row stride (elements): conflict-free ds_read_b64 row reads
   constexpr int VS = DH + 16;  // V image row stride: conflict-free ds_read_b64_tr_b16
   constexpr int NU = DH / 16;
@@ -195,14 +215,11 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
 
   if (!qlive) return;
   const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
-  bf16_t* op = a.o + b * a.ob + (int64_t)q * a.orr + h * DH + 4 * g;
+  const int64_t oo = b * a.ob + (int64_t)q * a.orr + h * DH + 4 * g;
 #pragma unroll
-  for (int u = 0; u < NU; ++u) {
-    uint2 st;
-    st.x = pack2bf(oacc[u][0] * inv, oacc[u][1] * inv);
-    st.y = pack2bf(oacc[u][2] * inv, oacc[u][3] * inv);
-    *(uint2*)(op + 16 * u) = st;
-  }
+  for (int u = 0; u < NU; ++u)
+    store_o4(a.o + oo + 16 * u, a.o_lo ? a.o_lo + oo + 16 * u : nullptr, oacc[u][0] * inv, oacc[u][1] * inv,
+             oacc[u][2] * inv, oacc[u][3] * inv);
   if (g == 0 && a.lse) {
     const float mu = m_run == -INFINITY ? 0.f : m_run;
     a.lse[(int64_t)bh * a.Lq + q] = l_run > 0.f ? mu + log2f(l_run) : INFINITY;
@@ -223,10 +240,11 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(AttnArgs a) {
     const int q = (int)(row % a.Lq);
     const int64_t bh = row / a.Lq;
     const int b = (int)(bh / a.H), h = (int)(bh % a.H);
-    const bf16_t* op = a.o + b * a.ob + (int64_t)q * a.orr + h * DH + li * PER;
+    const int64_t oo = b * a.ob + (int64_t)q * a.orr + h * DH + li * PER;
     const bf16_t* dp = a.dout + b * a.dob + (int64_t)q * a.dor + h * DH + li * PER;
 #pragma unroll
-    for (int i = 0; i < PER; ++i) s += bf2f(op[i]) * bf2f(dp[i]);
+    for (int i = 0; i < PER; ++i)
+      s += (bf2f(a.o[oo + i]) + (a.o_lo ? bf2f(a.o_lo[oo + i]) : 0.f)) * bf2f(dp[i]);
   }
 #pragma unroll
   for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
@@ -238,6 +256,7 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(AttnArgs a) {
 // ---------------------------------------------------------------------------------------------------------
 template <int DH>
 __global__ __launch_bounds__(512) void attn_bwd_kernel(AttnArgs a, int nw, int single) {
+  a.seed = seed_eff(a.seed);
   constexpr int NU = DH / 16;
   constexpr int KST = DH + 16;   // K image (tr reads for dQ)
   constexpr int CS = DH + 16;    // Q / dO chunk images (row reads + tr reads)
@@ -481,6 +500,7 @@ ASRX_DEV float xsum4(float v) {
 //   query-major qmaj[(bh * Lq + q) * nkw + kw],   bit j = keep(q, key 32 kw + j)            (forward)
 // grid (nqc, B*H), 256 threads: thread = key (32 queries -> 16 pair hashes), LDS transpose for qmaj.
 __global__ __launch_bounds__(256) void attn_dropgen_kernel(AttnArgs a, uint32_t* kmaj, uint32_t* qmaj) {
+  a.seed = seed_eff(a.seed);
   __shared__ uint32_t sw[R_MAXK];
   const int qc = blockIdx.x, bh = blockIdx.y, tid = threadIdx.x;
   const int nqc = gridDim.x, nkw = (a.Lk + 31) >> 5, q0 = qc * 32;
@@ -513,6 +533,7 @@ __global__ __launch_bounds__(256) void attn_dropgen_kernel(AttnArgs a, uint32_t*
 // come from the query-major keep bits (a 4-bit nibble per (sub-tile, 16-key half) -> one LDS table read).
 template <int MODE>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void attn_fwd_res_kernel(AttnArgs a, const uint32_t* qmaj) {
+  a.seed = seed_eff(a.seed);
   __shared__ __attribute__((aligned(1024))) bf16_t sk[R_MAXK * 64];
   __shared__ __attribute__((aligned(1024))) bf16_t sv[R_MAXK * 64];
   __shared__ __attribute__((aligned(16))) float skb[R_MAXK];   // per-key score bias: 0 or -inf
@@ -697,14 +718,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
     if (q >= a.Lq) continue;
     const bool live = !qdead[qs] && l_run[qs] > 0.f;
     const float inv = live ? 1.f / l_run[qs] : 0.f;
-    bf16_t* op = a.o + b * a.ob + (int64_t)q * a.orr + h * 64 + 4 * g;
+    const int64_t oo = b * a.ob + (int64_t)q * a.orr + h * 64 + 4 * g;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      uint2 st;
-      st.x = pack2bf(o[u][qs][0] * inv, o[u][qs][1] * inv);
-      st.y = pack2bf(o[u][qs][2] * inv, o[u][qs][3] * inv);
-      *(uint2*)(op + 16 * u) = st;
-    }
+    for (int u = 0; u < 4; ++u)
+      store_o4(a.o + oo + 16 * u, a.o_lo ? a.o_lo + oo + 16 * u : nullptr, o[u][qs][0] * inv, o[u][qs][1] * inv,
+               o[u][qs][2] * inv, o[u][qs][3] * inv);
     if (g == 0 && a.lse) {
       const float mu = m_run[qs] == -INFINITY ? 0.f : m_run[qs];
       a.lse[(int64_t)bh * a.Lq + q] = live ? mu + log2f(l_run[qs]) : INFINITY;
@@ -730,6 +748,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
 // compare only in blocks that reach above the diagonal.
 template <int MODE, int NKT>
 __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
+  a.seed = seed_eff(a.seed);
   // NKT 32-key blocks (= waves); keys past Lk are zero rows with a -inf score bias
   constexpr int NK = NKT * 32, NTHR = NKT * 64;
   constexpr int RDT = 32 + 8;                                     // dS^T image [key][32 queries] row stride
@@ -808,7 +827,8 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
   // delta = rowsum(dO * O) is formed here too: the threads that stage a dO piece also load the matching O
   // piece, dot the 8 elements and reduce over the row's 8 pieces (adjacent lanes) — no separate delta pass.
   const bf16_t* Ob = a.o + b * a.ob + h * 64;
-  uint4 preo[PRE];
+  const bf16_t* Olb = a.o_lo ? a.o_lo + b * a.ob + h * 64 : nullptr;
+  uint4 preo[PRE], prel[PRE];
   auto fetch = [&](int ch) {
     const int q0 = ch * 32;
     if (usebits) {
@@ -821,7 +841,10 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
       const int which = c >> 8, row = (c >> 3) & 31, dc = (c & 7) * 8;
       const int q = min(q0 + row, a.Lq - 1);
       pre[i] = *(const uint4*)((which ? Db + (int64_t)q * a.dor : Qb + (int64_t)q * a.qr) + dc);
-      if (which) preo[i] = *(const uint4*)(Ob + (int64_t)q * a.orr + dc);
+      if (which) {
+        preo[i] = *(const uint4*)(Ob + (int64_t)q * a.orr + dc);
+        if (Olb) prel[i] = *(const uint4*)(Olb + (int64_t)q * a.orr + dc);
+      }
     }
     if (tid < 32) praw = lseb[min(q0 + tid, a.Lq - 1)];
   };
@@ -836,10 +859,18 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
       if (which) {   // wave-uniform: a wave's 64 pieces are all Q or all dO
         const uint32_t* dd = (const uint32_t*)&pre[i];
         const uint32_t* oo = (const uint32_t*)&preo[i];
+        const uint32_t* ol = (const uint32_t*)&prel[i];
         float dot = 0.f;
+        if (Olb) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          dot += bf2f(dd[e] & 0xffff) * bf2f(oo[e] & 0xffff) + bf2f(dd[e] >> 16) * bf2f(oo[e] >> 16);
+          for (int e = 0; e < 4; ++e)
+            dot += bf2f(dd[e] & 0xffff) * (bf2f(oo[e] & 0xffff) + bf2f(ol[e] & 0xffff)) +
+                   bf2f(dd[e] >> 16) * (bf2f(oo[e] >> 16) + bf2f(ol[e] >> 16));
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            dot += bf2f(dd[e] & 0xffff) * bf2f(oo[e] & 0xffff) + bf2f(dd[e] >> 16) * bf2f(oo[e] >> 16);
+        }
         dot += __shfl_xor(dot, 1, 64);
         dot += __shfl_xor(dot, 2, 64);
         dot += __shfl_xor(dot, 4, 64);
@@ -1061,15 +1092,17 @@ int fill_args(const asrx_attn_desc* d, AttnArgs& a) {
   a.dv = (bf16_t*)d->dv; a.dvr = d->dv_rstride; a.dvb = d->dv_bstride;
   a.delta = d->delta; a.dq_acc = d->dq_acc;
   a.dropmask = d->dropmask;
-  const char* dbg = getenv("ASRX_ATTN_DBG");
-  a.dbg = dbg && dbg[0] == '1';
+  a.o_lo = (bf16_t*)d->o_lo;
+  if (a.o_lo && (uintptr_t)a.o_lo % 8) return ASRX_ERR_UNSUPPORTED;
+  static const int dbg = [] { const char* e = getenv("ASRX_ATTN_DBG"); return e && e[0] == '1'; }();
+  a.dbg = dbg;
   return ASRX_OK;
 }
 
 // Lk <= 256 and dh = 64 -> resident-K/V kernels (ASRX_ATTN_KERNEL=tiled forces the general tiled kernels)
 bool resident_ok(const asrx_attn_desc* d, const AttnArgs& a) {
-  const char* e = getenv("ASRX_ATTN_KERNEL");
-  if (e && !strcmp(e, "tiled")) return false;
+  static const bool tiled = [] { const char* e = getenv("ASRX_ATTN_KERNEL"); return e && !strcmp(e, "tiled"); }();
+  if (tiled) return false;
   return d->dh == 64 && a.Lk <= R_MAXK && (a.orr % 4) == 0 && (a.ob % 4) == 0;
 }
 
@@ -1079,6 +1112,8 @@ size_t bwd_smem(int nw, int dh) {
 }
 
 }  // namespace
+
+ASRX_SEED_OFFSET_SETTER(attention)
 
 extern "C" int asrx_attn_dropgen(const asrx_attn_desc* d, void* stream) {
   AttnArgs a;

@@ -8,6 +8,7 @@
 //   cross-entropy   : train.py:32 (caller-supplied CE, mean reduction).
 //   Adam            : train.py:35 (caller-supplied optimizer; fused over the flat parameter buffer).
 #include <algorithm>
+#include <cstring>
 
 #include "common.h"
 #include "gemm_common.h"
@@ -698,6 +699,7 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
                                                         const float* __restrict__ table, int d,
                                                         const float* __restrict__ pe, uint32_t thr, float sc,
                                                         uint64_t seed, float* __restrict__ out) {
+  seed = seed_eff(seed);
   const int dq = d / 4;
   const int64_t total = ntok * dq;
   for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
@@ -722,6 +724,7 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
 __global__ __launch_bounds__(256) void embed_bwd_kernel(const int64_t* __restrict__ tok, int64_t ntok, int d,
                                                         const float* __restrict__ dout, int pad_id, uint32_t thr,
                                                         float sc, uint64_t seed, float* __restrict__ dtable) {
+  seed = seed_eff(seed);
   const int v = blockIdx.x;
   if (v == pad_id) return;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -888,7 +891,12 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    bf16_t* __restrict__ pb, int64_t n, float lr, float b1, float b2,
                                                    float eps, float wd, float bc1, float rbc2, float gs,
-                                                   int decoupled) {
+                                                   int decoupled, const float* __restrict__ hyp) {
+  if (hyp) {   // device-resident step hyper-parameters (a replayed HIP graph): lr, bias corrections 1 and 2
+    lr = hyp[0];
+    bc1 = hyp[1];
+    rbc2 = 1.f / sqrtf(hyp[2]);
+  }
   const int64_t n4 = n / 4;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
     f4_t pp = ((f4_t*)p)[i], gg = ((const f4_t*)g)[i], mm = ((f4_t*)m)[i], vv = ((f4_t*)v)[i];
@@ -930,6 +938,7 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
 }
 
 __global__ __launch_bounds__(256) void dropout_mask_kernel(uint8_t* keep, int64_t n, uint32_t thr, uint64_t seed) {
+  seed = seed_eff(seed);
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
     keep[i] = rng_keep(seed, (uint32_t)i, thr) ? 1 : 0;
 }
@@ -943,7 +952,18 @@ inline unsigned grid_for(int64_t work, int cap = 8192) {
 
 }  // namespace
 
-extern "C" int asrx_version(void) { return 1; }
+ASRX_SEED_OFFSET_SETTER(frontend)
+
+extern "C" int asrx_version(void) { return 2; }
+
+extern "C" int asrx_struct_sizes(int64_t* out, int32_t n) {
+  if (!out || n < 0) return ASRX_ERR_ARG;
+  const int64_t s[4] = {(int64_t)sizeof(asrx_gemm_desc), (int64_t)sizeof(asrx_attn_desc),
+                        (int64_t)sizeof(asrx_gemm_group_dev), (int64_t)sizeof(asrx_rowsum_group)};
+  const int k = n < 4 ? n : 4;
+  for (int i = 0; i < k; ++i) out[i] = s[i];
+  return k;
+}
 
 extern "C" int asrx_conv1_fwd(const float* x, int32_t B, int32_t F, int32_t T, const float* w, const float* b,
                               void* y1, int32_t y_dtype, uint8_t* y1_mask, void* stream) {
@@ -1073,14 +1093,14 @@ extern "C" int asrx_cast(int32_t src_dtype, const void* src, int32_t dst_dtype, 
 
 extern "C" int asrx_adam(float* p, const float* g, float* m, float* v, void* p_bf16, int64_t n, float lr, float beta1,
                          float beta2, float eps, float weight_decay, float bias_corr1, float bias_corr2,
-                         float grad_scale, int32_t decoupled, void* stream) {
-  if (!p || !g || !m || !v || n < 0 || bias_corr1 <= 0.f || bias_corr2 <= 0.f) return ASRX_ERR_ARG;
+                         float grad_scale, int32_t decoupled, const float* hyp, void* stream) {
+  if (!p || !g || !m || !v || n < 0 || (!hyp && (bias_corr1 <= 0.f || bias_corr2 <= 0.f))) return ASRX_ERR_ARG;
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16) return ASRX_ERR_ARG;
   if (p_bf16 && (uintptr_t)p_bf16 % 8) return ASRX_ERR_ARG;
   if (n == 0) return ASRX_OK;
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1)), dim3(256), 0, (hipStream_t)stream, p, g, m, v,
                      (bf16_t*)p_bf16, n, lr, beta1, beta2, eps, weight_decay, bias_corr1, 1.f / sqrtf(bias_corr2),
-                     grad_scale, decoupled);
+                     grad_scale, decoupled, hyp);
   ASRX_CHECK_LAUNCH();
   return ASRX_OK;
 }
@@ -1137,5 +1157,42 @@ extern "C" int asrx_conv1_bwd_fused(int32_t dcols_dtype, const void* dcols, int3
   ASRX_CHECK_LAUNCH();
   conv1_bwd_finish(part, nblocks, dw, db, st);
   ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Host bytes -> device through kernel arguments: the launch records the bytes, so the copy needs no pinned host
+// buffer and is capturable in a HIP graph (a replay re-writes the same bytes).  Used for per-launch tables
+// (grouped weight-gradient groups / tile maps) and per-step scalars (Adam hyper-parameters).
+namespace {
+constexpr int UPLOAD_CHUNK = 2048;
+struct UploadChunk {
+  uint32_t w[UPLOAD_CHUNK / 4];
+};
+__global__ __launch_bounds__(256) void upload_kernel(UploadChunk c, uint32_t* __restrict__ dst, int nwords) {
+  for (int i = threadIdx.x; i < nwords; i += 256) dst[i] = c.w[i];
+}
+}  // namespace
+
+extern "C" int asrx_upload(void* dst, const void* src, int64_t nbytes, void* stream) {
+  if (!dst || (!src && nbytes > 0) || nbytes < 0 || nbytes % 4 || (uintptr_t)dst % 4) return ASRX_ERR_ARG;
+  const unsigned char* s = (const unsigned char*)src;
+  for (int64_t off = 0; off < nbytes; off += UPLOAD_CHUNK) {
+    const int n = (int)std::min<int64_t>(UPLOAD_CHUNK, nbytes - off);
+    UploadChunk c;
+    std::memcpy(c.w, s + off, n);
+    hipLaunchKernelGGL(upload_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, c, (uint32_t*)((char*)dst + off),
+                       n / 4);
+    ASRX_CHECK_LAUNCH();
+  }
+  return ASRX_OK;
+}
+
+extern "C" int asrx_set_seed_offset(uint64_t offset, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (asrx_seed_offset_gemm(offset, st) || asrx_seed_offset_attention(offset, st) ||
+      asrx_seed_offset_norm(offset, st) || asrx_seed_offset_softmax(offset, st) ||
+      asrx_seed_offset_frontend(offset, st))
+    return ASRX_ERR_LAUNCH;
   return ASRX_OK;
 }

@@ -214,41 +214,13 @@ ASRX_DEV void gemm_bf16_tile(const GemmArgs& g, int tile, int split, int z, bf16
 
 template <int BM, int BN, bool AT, bool BT, bool VEC>
 __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs g) {
+  g.seed = seed_eff(g.seed);
   __shared__ __attribute__((aligned(16))) bf16_t lds[reg_lds_elems<BM, BN, AT, BT>()];
   gemm_bf16_tile<BM, BN, AT, BT, VEC>(g, blockIdx.x, blockIdx.y, blockIdx.z, lds);
 }
 
-// ------------------------------------------------------------------------------------------------
-// Grouped GEMM: many independent problems (same layouts/epilogue, own shapes and pointers) in ONE launch.
-// The weight gradients of every layer (dW = dY^T X, reduction over the B*T rows) are independent of each
-// other, so the backward queues them and issues them together: enough 128x128 tiles to fill 256 CUs
-// several times over with no split-K (no fp32 partials, no reduce pass), long-K groups first.
-// The table travels in the kernel arguments (MAX_GROUPS entries, < 4 KiB).
-// ------------------------------------------------------------------------------------------------
-constexpr int MAX_GROUPS = 48;
-struct GroupTable {
-  float alpha, beta;
-  int c_dtype, count, cvec;
-  GroupEnt e[MAX_GROUPS];
-};
-
-template <bool AT, bool BT>
-__global__ __launch_bounds__(256) void gemm_bf16_grouped_kernel(GroupTable t) {
-  __shared__ __attribute__((aligned(16))) bf16_t lds[reg_lds_elems<128, 128, AT, BT>()];
-  const int tid = blockIdx.x;
-  int gi = 0;
-  while (gi + 1 < t.count && t.e[gi + 1].tile_start <= tid) ++gi;   // wave-uniform scan of the kernarg table
-  const GroupEnt& e = t.e[gi];
-  GemmArgs g = {};
-  g.M = e.m; g.N = e.n; g.K = e.k;
-  g.a = e.a; g.lda = e.lda; g.b = e.b; g.ldb = e.ldb; g.c = e.c; g.ldc = e.ldc; g.c_dtype = t.c_dtype;
-  g.batch_inner = 1; g.alpha = t.alpha; g.beta = t.beta; g.rowadd_mod = 1;
-  g.splitk = 1; g.k_per_split = ((e.k + BK - 1) / BK) * BK; g.cvec = t.cvec;
-  g.rowsum = e.rowsum;
-  gemm_bf16_tile<128, 128, AT, BT, true>(g, tid - e.tile_start, 0, 0, lds);
-}
-
-// Same, table in device memory (any number of groups, one launch): entry i = asrx_gemm_group_dev of the
+// Grouped GEMM: many independent problems (dW = dY^T X of every layer) in ONE launch, register-staged 128x128
+// tiles (fallback of asrx_gemm_grouped_xcd for tables the LDS-DMA ring cannot take); table in device memory: entry i = asrx_gemm_group_dev of the
 // C-ABI (64 B, layout-identical to GroupEnt), tile_group[tile] = its group.
 template <bool AT, bool BT>
 __global__ __launch_bounds__(256) void gemm_bf16_grouped_dev_kernel(float alpha, float beta, int c_dtype, int cvec,
@@ -273,200 +245,6 @@ __global__ __launch_bounds__(256) void gemm_bf16_grouped_dev_kernel(float alpha,
   g.splitk = 1; g.k_per_split = ((e.k + BK - 1) / BK) * BK; g.cvec = cvec;
   g.rowsum = e.rowsum;
   gemm_bf16_tile<128, 128, AT, BT, true>(g, tid - e.tile_start, 0, 0, lds);
-}
-
-// ------------------------------------------------------------------------------------------------
-// bf16 kernel, direct-to-LDS staging (global_load_lds_dwordx4): 128x128x64 tiles, 4 waves (64x64 each),
-// two LDS buffers, one barrier per K-step.  Each wave-instruction writes 1 KiB of LDS lane-linearly, so the
-// bank-conflict swizzles live on the per-lane SOURCE addresses and are undone on the fragment reads:
-//   k-contiguous image [128 rows][64 k] (128-B rows): 16-B chunk c of row r stored at c ^ ((r >> 1) & 7)
-//     -> the ds_read_b128 fragment reads of a 16-lane group hit 16 distinct 16-B slots (conflict-free);
-//   k-strided image [64 k][128 cols] (256-B rows): 32-B chunk XOR ks_swz<128>(k) as in the register path.
-// Rows past M/N are clamped to the last valid row (their results are never stored); K must be a multiple
-// of 64 per split (host-checked).
-// ------------------------------------------------------------------------------------------------
-constexpr int GT = 128;                       // tile edge
-constexpr int GTILE_BYTES = GT * BK * 2;      // 16 KiB per operand per stage
-constexpr int G_INST = GTILE_BYTES / 4096;    // glds instructions per thread per operand per stage (4)
-
-
-template <bool KSTRIDED>
-ASRX_DEV void glds_stage(unsigned char* lds_tile, const bf16_t* base, int64_t ld, int r0, int rmax, int k0) {
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-#pragma unroll
-  for (int j = 0; j < G_INST; ++j) {
-    const int q = j * 4 + w;             // 1-KiB piece of the image written by this wave-instruction
-    const int o = q * 1024 + l * 16;     // image byte offset of this lane's 16 B
-    const bf16_t* src;
-    if constexpr (!KSTRIDED) {
-      const int r = o >> 7, cp = (o >> 4) & 7;
-      const int c = cp ^ ((r >> 1) & 7);
-      const int gr = min(r0 + r, rmax - 1);
-      src = base + (int64_t)gr * ld + k0 + c * 8;
-    } else {
-      const int kr = o >> 8, c16 = (o >> 4) & 15;
-      const int c32 = (c16 >> 1) ^ ks_swz<GT>(kr);
-      const int col = min(r0 + c32 * 16 + (c16 & 1) * 8, rmax - 8);
-      src = base + (int64_t)(k0 + kr) * ld + col;
-    }
-    __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(lds_tile + q * 1024), 16, 0, 0);
-  }
-}
-
-template <bool KSTRIDED>
-ASRX_DEV s8_t glds_frag(const unsigned char* lds_tile, int i0, int ks) {
-  const int l = threadIdx.x & 63, g = l >> 4;
-  if constexpr (!KSTRIDED) {
-    const int r = i0 + (l & 15);
-    const int c = (ks * 4 + g) ^ ((r >> 1) & 7);
-    return *(const s8_t*)(lds_tile + r * 128 + c * 16);
-  } else {
-    const bf16_t* t = (const bf16_t*)lds_tile;
-    const int i = l & 15, q = i >> 2, p = i & 3;
-    const int k1 = ks * 32 + 8 * g + q;
-    const int k2 = k1 + 4;
-    const bf16_t* a1 = t + k1 * GT + (((i0 >> 4) ^ ks_swz<GT>(k1)) << 4) + 4 * p;
-    const bf16_t* a2 = t + k2 * GT + (((i0 >> 4) ^ ks_swz<GT>(k2)) << 4) + 4 * p;
-    s4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4_t*)a1);
-    s4_t v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4_t*)a2);
-    return s8_t{v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
-  }
-}
-
-
-// Persistent over output tiles: each workgroup walks tiles blockIdx.x, +gridDim.x, ... and issues the NEXT
-// (tile, k-step) stage — across tile boundaries too — before computing the current one, so the first stage
-// of a tile loads while the previous tile's epilogue runs.
-template <bool AT, bool BT, int EPI>
-__global__ __launch_bounds__(256) void gemm_bf16_glds_kernel(GemmArgs g, int ntiles) {
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * 2 * GTILE_BYTES];
-  constexpr int TM = 4, TN = 4;
-  const int ntn = (g.N + GT - 1) / GT;
-  const int split = blockIdx.y;
-  const int z = blockIdx.z;
-  const int zo = z / g.batch_inner, zi = z % g.batch_inner;
-  const bf16_t* A = (const bf16_t*)g.a + zo * g.sa_o + zi * g.sa_i;
-  const bf16_t* B = (const bf16_t*)g.b + zo * g.sb_o + zi * g.sb_i;
-  const int kbeg = split * g.k_per_split;
-  const int kend = min(g.K, kbeg + g.k_per_split);
-  const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
-  int t = blockIdx.x;
-  if (t >= ntiles || nk == 0) return;
-  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
-
-  auto stage = [&](int buf, int tt, int kk) {
-    unsigned char* base = lds + buf * 2 * GTILE_BYTES;
-    glds_stage<AT>(base, A, g.lda, (tt / ntn) * GT, g.M, kbeg + kk * BK);
-    glds_stage<BT>(base + GTILE_BYTES, B, g.ldb, (tt % ntn) * GT, g.N, kbeg + kk * BK);
-  };
-
-  f4_t acc[TN][TM];
-#pragma unroll
-  for (int i = 0; i < TN; ++i)
-#pragma unroll
-    for (int j = 0; j < TM; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
-  float rs[TM];
-#pragma unroll
-  for (int j = 0; j < TM; ++j) rs[j] = 0.f;
-
-  stage(0, t, 0);
-  __syncthreads();
-  int kt = 0, cur = 0;
-  while (true) {
-    int nt = t, nkt = kt + 1;
-    if (nkt == nk) { nt = t + gridDim.x; nkt = 0; }
-    const bool has_next = nt < ntiles;
-    if (has_next) stage(cur ^ 1, nt, nkt);
-    const unsigned char* la = lds + cur * 2 * GTILE_BYTES;
-    const unsigned char* lb = la + GTILE_BYTES;
-    const bool do_rs = AT && g.rowsum != nullptr && (t % ntn) == 0 && wn == 0;
-#pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
-      s8_t fa[TM], fb[TN];
-#pragma unroll
-      for (int j = 0; j < TM; ++j) fa[j] = glds_frag<AT>(la, wm + 16 * j, ks);
-#pragma unroll
-      for (int i = 0; i < TN; ++i) fb[i] = glds_frag<BT>(lb, wn + 16 * i, ks);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < TN; ++i)
-#pragma unroll
-        for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[i], fa[j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      if constexpr (AT) {
-        if (do_rs) {
-#pragma unroll
-          for (int j = 0; j < TM; ++j)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) rs[j] += bf2f((bf16_t)fa[j][e]);
-        }
-      }
-    }
-    if (kt == nk - 1) {
-      const int m0 = (t / ntn) * GT, n0 = (t % ntn) * GT;
-      if constexpr (AT) {
-        if (do_rs) {
-#pragma unroll
-          for (int j = 0; j < TM; ++j) {
-            float v = rs[j];
-            v += __shfl_xor(v, 16, 64);
-            v += __shfl_xor(v, 32, 64);
-            const int m = m0 + wm + 16 * j + l;
-            if (l < 16 && m < g.M) {
-              if (g.splitk > 1) g.rowsum_ws[(int64_t)split * g.M + m] = v;
-              else g.rowsum[m] += v;
-            }
-            rs[j] = 0.f;
-          }
-        }
-      }
-      if (g.splitk > 1) {
-        const int gq = l >> 4;
-#pragma unroll
-        for (int i = 0; i < TN; ++i)
-#pragma unroll
-          for (int j = 0; j < TM; ++j) {
-            float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-            store_partial4(g, split, m0 + wm + 16 * j + (l & 15), n0 + wn + 16 * i + 4 * gq, v);
-          }
-      } else {
-        epilogue_tile<EPI>(g, z, m0, n0, wm, wn, acc);
-      }
-#pragma unroll
-      for (int i = 0; i < TN; ++i)
-#pragma unroll
-        for (int j = 0; j < TM; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
-    }
-    __syncthreads();
-    if (!has_next) break;
-    t = nt;
-    kt = nkt;
-    cur ^= 1;
-  }
-}
-
-template <bool AT, bool BT, int EPI>
-void launch_glds(const GemmArgs& g, int ntiles, int splitk, int batch, hipStream_t st) {
-  const int per = splitk * batch;
-  const int gx = std::max(1, std::min(ntiles, std::max(1, 512 / per)));
-  hipLaunchKernelGGL((gemm_bf16_glds_kernel<AT, BT, EPI>), dim3(gx, splitk, batch), dim3(256), 0, st, g, ntiles);
-}
-
-
-template <bool AT, bool BT>
-void dispatch_glds(const GemmArgs& g, int epi, int ntiles, int splitk, int batch, hipStream_t st) {
-#define ASRX_CASE(E) \
-  case (E): launch_glds<AT, BT, (E)>(g, ntiles, splitk, batch, st); return;
-  if constexpr (!AT && !BT) {
-    switch (epi) { ASRX_EPI_NT(ASRX_CASE) default: break; }
-  } else if constexpr (!AT && BT) {
-    switch (epi) { ASRX_EPI_NN(ASRX_CASE) default: break; }
-  } else if constexpr (AT && BT) {
-    switch (epi) { ASRX_EPI_TT(ASRX_CASE) default: break; }
-  }
-#undef ASRX_CASE
-  launch_glds<AT, BT, E_GENERIC>(g, ntiles, splitk, batch, st);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -741,6 +519,7 @@ ASRX_DEV void p3_body(const GemmArgs& g, const TileSeq tl, int split, int z, uns
 
 template <bool AT, bool BT, int EPI>
 __global__ __launch_bounds__(512) void gemm_bf16_p3_kernel(GemmArgs g, int ntiles, int xcd) {
+  g.seed = seed_eff(g.seed);
   __shared__ __attribute__((aligned(1024))) unsigned char lds[3 * P_STAGE + P_BIAS_BYTES];
   const int G = gridDim.x, b0 = blockIdx.x;
   if (b0 >= ntiles) return;
@@ -786,8 +565,8 @@ template <bool AT, bool BT, int EPI>
 void launch_p3(const GemmArgs& g, int ntiles, int splitk, int batch, hipStream_t st) {
   const int per = splitk * batch;
   const int gx = std::max(1, std::min(ntiles, std::max(1, 256 / per)));
-  const char* e = getenv("ASRX_P3_XCD");   // XCD-contiguous tile order: measured 1-7% faster on the c3 shapes
-  const int xcd = e ? atoi(e) : 1;
+  // XCD-contiguous tile order: measured 1-7% faster on the c3 shapes (ASRX_P3_XCD=0: round-robin, A/B)
+  static const int xcd = [] { const char* e = getenv("ASRX_P3_XCD"); return e ? atoi(e) : 1; }();
   hipLaunchKernelGGL((gemm_bf16_p3_kernel<AT, BT, EPI>), dim3(gx, splitk, batch), dim3(P_THREADS), 0, st, g, ntiles,
                      xcd);
 }
@@ -879,6 +658,7 @@ template <int BM, int BN> constexpr int ring_stages() { return 4; }
 
 template <int BM, int BN, bool AT, bool BT, int EPI>
 __global__ __launch_bounds__(256) void gemm_bf16_ring_kernel(GemmArgs g, int ntiles, int xcd) {
+  g.seed = seed_eff(g.seed);
   constexpr int R_STAGES = ring_stages<BM, BN>();
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int P = RStage<BM, AT>::NI + RStage<BN, BT>::NI;   // LDS-DMA instructions per thread per stage
@@ -961,8 +741,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_ring_kernel(GemmArgs g, int nti
 template <int BM, int BN, bool AT, bool BT>
 void dispatch_ring(const GemmArgs& g, int epi, int splitk, int batch, hipStream_t st) {
   const int ntiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
-  const char* e = getenv("ASRX_RING_XCD");
-  const int xcd = e ? atoi(e) : 1;
+  static const int xcd = [] { const char* e = getenv("ASRX_RING_XCD"); return e ? atoi(e) : 1; }();
   dim3 grid(xcd ? 8 * ((ntiles + 7) / 8) : ntiles, splitk, batch);
 #define ASRX_CASE(E) \
   case (E): hipLaunchKernelGGL((gemm_bf16_ring_kernel<BM, BN, AT, BT, (E)>), grid, dim3(R_THREADS), 0, st, g, ntiles, xcd); return;
@@ -1024,6 +803,7 @@ ASRX_DEV void f32_store(float* lds, const float* regs) {
 
 template <bool AT, bool BT>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g, int vec) {
+  g.seed = seed_eff(g.seed);
   __shared__ __attribute__((aligned(16))) float lds[2][2][FBK * FSTRIDE];
   const int ntn = (g.N + FBN - 1) / FBN;
   const int tile = blockIdx.x;
@@ -1093,6 +873,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g, int vec) {
 
 // Split-K finish: sum partial slabs in fixed order, then the full epilogue.
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g) {
+  g.seed = seed_eff(g.seed);
   const int64_t quads = (int64_t)g.M * ((g.N + 3) / 4);
   const int nq = (g.N + 3) / 4;
   for (int64_t t = blockIdx.x * 256 + threadIdx.x; t < quads; t += (int64_t)gridDim.x * 256) {
@@ -1323,8 +1104,8 @@ void dispatch_bf16(const GemmArgs& g, bool at, bool bt, bool vec, int batch, hip
 // ------------------------------------------------------------------------------------------------
 // Kernel selection (shared by asrx_gemm and asrx_gemm_kernel_name so profiling can name the launch).
 struct GemmPlan {
-  int use;     // 1 = p3 (256x128 LDS-DMA ring), 2 = glds (128x128), 3 = register path 128, 4 = register path 64,
-               // 5 = ring 64x64, 6 = ring 128x64 (4-stage LDS-DMA, small grids)
+  int use;     // 1 = p3 (256x128 LDS-DMA ring), 3 = register path 128, 4 = register path 64,
+               // 5 = ring 64x64, 6 = ring 128x64 (4-stage LDS-DMA, small grids), 9 = tall-K (conv2 dW)
   bool vec;    // 16-byte aligned operands
   int epi;     // instantiated epilogue flags (E_GENERIC when the fast-path set has no match)
   int ntiles;  // output tiles of the chosen kernel
@@ -1348,11 +1129,7 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
     const long t128 = (long)((d->m + 127) / 128) * ((d->n + 127) / 128) * batch * splitk;
     tile = t128 >= 400 ? 128 : 64;
   }
-  // kernel family: ASRX_GEMM_KERNEL = auto | p3 | glds | reg  (A/B switch for benchmarking)
-  const char* kenv = getenv("ASRX_GEMM_KERNEL");
-  const int kvar = !kenv ? 0 : (!strcmp(kenv, "p3") ? 1 : (!strcmp(kenv, "glds") ? 2 : (!strcmp(kenv, "reg") ? 3 :
-                   (!strcmp(kenv, "ring") ? 4 : (!strcmp(kenv, "ring128") ? 5 : (!strcmp(kenv, "p5") ? 6 :
-                   (!strcmp(kenv, "p5m") ? 7 : 0)))))));
+  const int kvar = d->kernel == 1 ? 1 : d->kernel == 3 ? 3 : d->kernel == 4 ? 4 : d->kernel == 5 ? 5 : 0;
   const bool dma_ok = pl.vec && d->k % BK == 0 && (!d->a_trans || d->m % 8 == 0) && (!d->b_trans || d->n % 8 == 0) &&
                       d->m >= 8 && d->n >= 8;
   const int nt_p3 = ((d->m + P_BM - 1) / P_BM) * ((d->n + P_BN - 1) / P_BN);
@@ -1360,11 +1137,8 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
   const int nt_r128 = ((d->m + 127) / 128) * ((d->n + 63) / 64);
   if (dma_ok) {
     if (kvar == 1) pl.use = 1;
-    else if (kvar == 2) pl.use = tile == 128 ? 2 : pl.use;
     else if (kvar == 4 && !d->a_trans) pl.use = 5;
     else if (kvar == 5 && !d->a_trans) pl.use = 6;
-    else if (kvar == 6) pl.use = 7;
-    else if (kvar == 7) pl.use = 8;
     // auto (measured on the c3 shapes, tools/gemm_bench.py): the p3 ring wins every projection with K <= 4096
     // whose grid fills the chip; smaller grids (the decoder's 4096-row GEMMs) take the 4-stage ring kernel; the
     // register path wins the weight-gradient (A^T, reduction over B*T rows) and very long-K GEMMs.
@@ -1382,8 +1156,6 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
     pl.use = 9;
   if (pl.use == 9) pl.ntiles = splitk;
   else if (pl.use == 1) pl.ntiles = nt_p3;
-  else if (pl.use == 7) pl.ntiles = ((d->m + 255) / 256) * ((d->n + 255) / 256);
-  else if (pl.use == 8) pl.ntiles = ((d->m + 127) / 128) * ((d->n + 255) / 256);
   else if (pl.use == 5) pl.ntiles = ((d->m + 63) / 64) * ((d->n + 63) / 64);
   else if (pl.use == 6) pl.ntiles = nt_r128;
   else pl.ntiles = ((d->m + tile - 1) / tile) * ((d->n + tile - 1) / tile);
@@ -1404,12 +1176,14 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
           (d->resid ? E_RESID : 0) | (d->beta == 1.f ? E_BETA : 0) |
           (d->c_dtype == ASRX_F32 ? E_F32 : 0) | (d->alpha != 1.f ? E_ALPHA : 0) | (d->rowadd ? E_ROWADD : 0);
   }
-  pl.epi = ((pl.use <= 2 || (pl.use >= 5 && pl.use != 9)) && epi_instantiated(d->a_trans, d->b_trans, epi))
+  pl.epi = ((pl.use == 1 || pl.use == 5 || pl.use == 6) && epi_instantiated(d->a_trans, d->b_trans, epi))
                ? epi : E_GENERIC;
   return pl;
 }
 
 }  // namespace
+
+ASRX_SEED_OFFSET_SETTER(gemm)
 
 extern "C" int asrx_gemm_kernel_name(const asrx_gemm_desc* d, char* buf, int len) {
   if (!d || !buf || len < 8) return ASRX_ERR_ARG;
@@ -1423,12 +1197,8 @@ extern "C" int asrx_gemm_kernel_name(const asrx_gemm_desc* d, char* buf, int len
   const GemmPlan pl = plan_bf16(d, batch, splitk);
   if (pl.use == 9)
     snprintf(buf, len, "gemm_bf16_tallk_kernel");
-  else if (pl.use == 1 || pl.use == 2)
-    snprintf(buf, len, "gemm_bf16_%s_kernel<%s, %s, %d>", pl.use == 1 ? "p3" : "glds", tf[!!d->a_trans],
-             tf[!!d->b_trans], pl.epi);
-  else if (pl.use == 7 || pl.use == 8)
-    snprintf(buf, len, "gemm_bf16_p5_kernel<%d, %s, %s, %d>", pl.use == 7 ? 256 : 128, tf[!!d->a_trans],
-             tf[!!d->b_trans], pl.epi);
+  else if (pl.use == 1)
+    snprintf(buf, len, "gemm_bf16_p3_kernel<%s, %s, %d>", tf[!!d->a_trans], tf[!!d->b_trans], pl.epi);
   else if (pl.use >= 5)
     snprintf(buf, len, "gemm_bf16_ring_kernel<%d, 64, %s, %s, %d>", pl.use == 6 ? 128 : 64, tf[!!d->a_trans],
              tf[!!d->b_trans], pl.epi);
@@ -1438,69 +1208,7 @@ extern "C" int asrx_gemm_kernel_name(const asrx_gemm_desc* d, char* buf, int len
   return ASRX_OK;
 }
 
-extern "C" int asrx_gemm_grouped(const asrx_gemm_desc* common, const asrx_gemm_group* groups, int32_t count,
-                                 void* stream) {
-  if (!common || !groups || count < 0) return ASRX_ERR_ARG;
-  if (count == 0) return ASRX_OK;
-  if (count > MAX_GROUPS) return ASRX_ERR_ARG;
-  if (common->in_dtype != ASRX_BF16 || !common->a_trans || !common->b_trans) return ASRX_ERR_UNSUPPORTED;
-  if (common->c_dtype != ASRX_BF16 && common->c_dtype != ASRX_F32) return ASRX_ERR_ARG;
-  GroupTable t;
-  memset(&t, 0, sizeof(t));
-  t.alpha = common->alpha; t.beta = common->beta; t.c_dtype = common->c_dtype; t.count = count;
-  t.cvec = 1;
-  const int esz = common->c_dtype == ASRX_F32 ? 16 : 8;
-  int64_t tiles = 0;
-  for (int i = 0; i < count; ++i) {
-    const asrx_gemm_group& q = groups[i];
-    if (q.m <= 0 || q.n <= 0 || q.k < 0 || !q.a || !q.b || !q.c) return ASRX_ERR_ARG;
-    // 16-byte vector staging: k-strided operands need 8-element aligned rows/pointers
-    if (q.lda % 8 || q.ldb % 8 || (uintptr_t)q.a % 16 || (uintptr_t)q.b % 16) return ASRX_ERR_UNSUPPORTED;
-    if (q.lda > INT32_MAX || q.ldb > INT32_MAX || q.ldc > INT32_MAX) return ASRX_ERR_ARG;
-    if (q.ldc % 4 || (uintptr_t)q.c % esz) t.cvec = 0;
-    GroupEnt& e = t.e[i];
-    e.a = q.a; e.b = q.b; e.c = q.c; e.rowsum = q.rowsum_a;
-    e.lda = (int)q.lda; e.ldb = (int)q.ldb; e.ldc = (int)q.ldc;
-    e.m = q.m; e.n = q.n; e.k = q.k;
-    e.tile_start = (int)tiles;
-    tiles += (int64_t)((q.m + 127) / 128) * ((q.n + 127) / 128);
-  }
-  if (tiles > INT32_MAX) return ASRX_ERR_ARG;
-  hipLaunchKernelGGL((gemm_bf16_grouped_kernel<true, true>), dim3((unsigned)tiles), dim3(256), 0,
-                     (hipStream_t)stream, t);
-  ASRX_CHECK_LAUNCH();
-  return ASRX_OK;
-}
-
 static_assert(sizeof(GroupEnt) == sizeof(asrx_gemm_group_dev), "device group table layout");
-
-extern "C" int asrx_gemm_grouped_table(const asrx_gemm_desc* common, const asrx_gemm_group_dev* groups,
-                                       const uint16_t* tile_group, int32_t count, int32_t tiles, int32_t cvec,
-                                       void* stream) {
-  if (!common || !groups || !tile_group || count <= 0 || count > 65535 || tiles < 0) return ASRX_ERR_ARG;
-  if (tiles == 0) return ASRX_OK;
-  if (common->in_dtype != ASRX_BF16 || !common->a_trans || !common->b_trans) return ASRX_ERR_UNSUPPORTED;
-  if (common->c_dtype != ASRX_BF16 && common->c_dtype != ASRX_F32) return ASRX_ERR_ARG;
-  // 256x256 p5 tiles (host numbered the tiles for that size): every group's N % 4 == 0, 16-B aligned fp32 C rows
-  if (common->tile == 256) {
-    if (!cvec || common->c_dtype != ASRX_F32) return ASRX_ERR_ARG;
-    if (launch_p5_grouped(common->alpha, common->beta, common->c_dtype, (const GroupEnt*)groups, tile_group, nullptr,
-                          tiles, tiles, (hipStream_t)stream) != 0)
-      return ASRX_ERR_UNSUPPORTED;
-    ASRX_CHECK_LAUNCH();
-    return ASRX_OK;
-  }
-  // XCD-contiguous tiles measured 1.5x SLOWER here (every workgroup of an XCD sweeping the same operand panel in
-  // lockstep concentrates the L2 traffic); round-robin is the default
-  const char* e = getenv("ASRX_GROUPED_XCD");
-  const int xcd = e ? atoi(e) : 0;
-  const unsigned grid = xcd ? 8u * (unsigned)((tiles + 7) / 8) : (unsigned)tiles;
-  hipLaunchKernelGGL((gemm_bf16_grouped_dev_kernel<true, true>), dim3(grid), dim3(256), 0,
-                     (hipStream_t)stream, common->alpha, common->beta, common->c_dtype, cvec ? 1 : 0,
-                     (const GroupEnt*)groups, tile_group, (int)tiles, xcd, nullptr);
-  ASRX_CHECK_LAUNCH();
-  return ASRX_OK;
-}
 
 extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
   if (!d || d->m < 0 || d->n < 0 || d->k < 0 || !d->a || !d->b || !d->c) return ASRX_ERR_ARG;
@@ -1536,9 +1244,8 @@ extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
   g.ws = d->workspace;
   g.rowsum = d->rowsum_a;
   g.rowsum_ws = d->rowsum_ws;
-  { const char* e = getenv("ASRX_GEMM_DBG"); g.dbg = e ? atoi(e) : 0; }
-  { const char* e = getenv("ASRX_P5_EXACT"); g.exact = (d->n % 256 == 0) && batch == 1 && (!e || atoi(e) != 0) &&
-                ((uintptr_t)d->c % 16 == 0) && (d->ldc % (d->c_dtype == ASRX_F32 ? 4 : 8) == 0); }
+  static const int dbg_env = [] { const char* e = getenv("ASRX_GEMM_DBG"); return e ? atoi(e) : 0; }();
+  g.dbg = dbg_env;
   if (g.rowsum && (!d->a_trans || d->in_dtype != ASRX_BF16 || batch != 1)) return ASRX_ERR_UNSUPPORTED;
   if (g.rowsum && splitk > 1 && !g.rowsum_ws) return ASRX_ERR_ARG;
   const int esz = d->c_dtype == ASRX_F32 ? 16 : 8;
@@ -1579,13 +1286,6 @@ extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
       else if (!d->a_trans && d->b_trans) dispatch_p3<false, true>(g, epi, pl.ntiles, splitk, batch, st);
       else if (d->a_trans && !d->b_trans) dispatch_p3<true, false>(g, epi, pl.ntiles, splitk, batch, st);
       else dispatch_p3<true, true>(g, epi, pl.ntiles, splitk, batch, st);
-    } else if (pl.use == 2) {
-      if (!d->a_trans && !d->b_trans) dispatch_glds<false, false>(g, epi, pl.ntiles, splitk, batch, st);
-      else if (!d->a_trans && d->b_trans) dispatch_glds<false, true>(g, epi, pl.ntiles, splitk, batch, st);
-      else if (d->a_trans && !d->b_trans) dispatch_glds<true, false>(g, epi, pl.ntiles, splitk, batch, st);
-      else dispatch_glds<true, true>(g, epi, pl.ntiles, splitk, batch, st);
-    } else if (pl.use == 7 || pl.use == 8) {
-      dispatch_p5(g, pl.use == 7 ? 256 : 128, d->a_trans, d->b_trans, epi, pl.ntiles, splitk, batch, st);
     } else if (pl.use >= 5) {
       if (!d->b_trans) {
         if (pl.use == 6) dispatch_ring<128, 64, false, false>(g, epi, splitk, batch, st);
@@ -1648,9 +1348,8 @@ extern "C" int asrx_gemm_grouped_xcd(const asrx_gemm_desc* common, const asrx_ge
     hipLaunchKernelGGL((gemm_bf16_grouped_dev_kernel<true, true>), dim3(blocks), dim3(256), 0, (hipStream_t)stream,
                        common->alpha, common->beta, common->c_dtype, common->relu ? 1 : 0, (const GroupEnt*)groups,
                        tile_group, (int)tiles, 0, block_tile);
-  } else if (launch_p5_grouped(common->alpha, common->beta, common->c_dtype, (const GroupEnt*)groups, tile_group,
-                               block_tile, tiles, blocks, (hipStream_t)stream) != 0) {
-    return ASRX_ERR_UNSUPPORTED;
+  } else {
+    return ASRX_ERR_ARG;
   }
   ASRX_CHECK_LAUNCH();
   return ASRX_OK;

@@ -1,4 +1,4 @@
-// Shared pieces of the bf16/f32 GEMM kernels (gemm.hip, gemm_p5.hip): kernel arguments, the fused
+// Shared pieces of the bf16/f32 GEMM kernels (gemm.hip): kernel arguments, the fused
 // epilogues, LDS image helpers and counted-vmcnt waits.
 #pragma once
 #include "common.h"
@@ -25,7 +25,6 @@ struct GemmArgs {
   float* rowsum;                   // fused bias gradient: rowsum[m] += sum_k A(m,k)   (A k-strided only)
   float* rowsum_ws;                // [splitk][M] partials when splitk > 1
   int dbg;                         // diagnostics only (ASRX_GEMM_DBG): 1 = skip the epilogue stores
-  int exact;                       // p5: N % 256 == 0 -> store-only epilogues use exact-count buffer stores
   uint32_t* mask_out; int64_t ld_mask;   // E_MASKOUT: stored C > 0 as bits of words [m][n / 32] (mask_bit_pos)
 };
 
@@ -437,10 +436,6 @@ struct GroupEnt {
   int pad;
 };
 
-// p5 family (gemm_p5.hip): BM x 256 x 32 tiles, BM = 256 or 128
-void dispatch_p5(const GemmArgs& g, int bm, bool at, bool bt, int epi, int ntiles, int splitk, int batch,
-                 hipStream_t st);
-
 template <int TN, int TM>
 ASRX_DEV void keep_live(f4_t (&acc)[TN][TM]) {
 #pragma unroll
@@ -448,10 +443,5 @@ ASRX_DEV void keep_live(f4_t (&acc)[TN][TM]) {
 #pragma unroll
     for (int j = 0; j < TM; ++j) asm volatile("" ::"v"(acc[i][j]));
 }
-
-// grouped weight gradients on 256x256 p5 tiles (A^T, B^T operands, fp32 C, alpha 1, beta 0 or 1); 0 = launched
-// block_tile: workgroup -> tile map (nullptr: identity, blocks == ntiles)
-int launch_p5_grouped(float alpha, float beta, int c_dtype, const GroupEnt* ents, const uint16_t* tile_group,
-                      const uint16_t* block_tile, int ntiles, int blocks, hipStream_t st);
 
 }  // namespace asrxg

@@ -97,6 +97,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int x_dtype, const void* x,
                                                      const float* dres, float* dx_out, void* dx_drop,
                                                      int drop_dtype, uint32_t thr, float dscale, uint64_t seed, float* part,
                                                      int64_t rows) {
+  seed = seed_eff(seed);
   constexpr int D = CH * NJ * 64;
   __shared__ float red[4][2 * D];
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -284,6 +285,8 @@ bool ln_bwd_launch(int x_dtype, const void* x, int dy_dtype, const void* dy, con
 }
 
 }  // namespace
+
+ASRX_SEED_OFFSET_SETTER(norm)
 
 extern "C" int asrx_layernorm_fwd(int32_t x_dtype, const void* x, int32_t y_dtype, void* y, const float* gamma,
                                   const float* beta, float* mean, float* rstd, int64_t rows, int32_t d, float eps,

@@ -104,6 +104,7 @@ ASRX_DEV bool is_masked(const SmArgs& a, int b, int q, int key) {
 // keeps U x 16 B per lane in flight (the one-row version left HBM idle between a row's load and its store).
 template <int V, int LPR, int NJ, int U>
 __global__ __launch_bounds__(256) void softmax_fwd_kernel(SmArgs a) {
+  a.seed = seed_eff(a.seed);
   constexpr int RPW = 64 / LPR;
   const int l = threadIdx.x & 63;
   const int sub = l / LPR, ll = l % LPR;
@@ -174,6 +175,7 @@ __global__ __launch_bounds__(256) void softmax_fwd_kernel(SmArgs a) {
 
 template <int V, int LPR, int NJ, int U>
 __global__ __launch_bounds__(256) void softmax_bwd_kernel(SmArgs a, void* ds) {
+  a.seed = seed_eff(a.seed);
   constexpr int RPW = 64 / LPR;
   const int l = threadIdx.x & 63;
   const int sub = l / LPR, ll = l % LPR;
@@ -278,6 +280,8 @@ int run(SmArgs a, bool bwd, void* ds, hipStream_t st) {
 }
 
 }  // namespace
+
+ASRX_SEED_OFFSET_SETTER(softmax)
 
 extern "C" int asrx_softmax_fwd(int32_t dtype, const void* s, void* p, void* pd, int64_t nbh, int32_t heads,
                                 int32_t lq, int32_t lk, int64_t ld, float scale, int32_t mask_mode, int32_t causal,

@@ -17,6 +17,7 @@ N=1 only.
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -39,17 +40,37 @@ def parse():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-batch", type=int, default=4)
-    ap.add_argument("--cpu-steps", type=int, default=10)
+    ap.add_argument("--cpu-batch", type=int, default=8)
+    ap.add_argument("--cpu-steps", type=int, default=4)
+    ap.add_argument("--no-graph", action="store_true", help="eager steps (no HIP graph capture)")
     ap.add_argument("--no-probe", action="store_true")
     ap.add_argument("--no-sub", action="store_true", help="skip the per-kernel sub-rooflines")
     return ap.parse_args()
 
 
-def cpu_baseline(cfg, frames, text_len, batch, steps):
-    """Oracle train step (fp32 eager CPU restatement of the reference, per-head loop) on the host cores."""
-    from oracle.ref_model import det_params, synthetic_batch, train_step_grads
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+def host_cpu():
+    """(model name, logical CPUs in this process's affinity set, threads to use).  The threads are the CPU share
+    the box grants this job (OMP_NUM_THREADS, 16 per GPU on the pool), at most the affinity set."""
+    model = "unknown"
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    aff = len(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS") or aff)
+    return model, aff, max(1, min(aff, share))
+
+
+def cpu_baseline(cfg, frames, text_len, batch, steps, extra=True):
+    """The reference's CPU PyTorch path on the host cores: the oracle (fp32 eager restatement of the
+    reference, per-head loop, nan_to_num) timed on a bounded sample of the headline workload — the c3 train
+    step at B=8 — plus, with `extra`, the forward of every GPU config (c2 at full batch, c3 at
+    B=64, c5 at B=2) normalised to frames/s."""
+    from oracle.ref_model import CONFIGS, det_params, forward, synthetic_batch, train_step_grads
+    model, aff, threads = host_cpu()
     torch.set_num_threads(threads)
     P = {k: v.clone().requires_grad_(True) for k, v in det_params(cfg, 0).items()}
     s, t, m = synthetic_batch(cfg, batch, frames, text_len + 1, seed=99)
@@ -60,10 +81,26 @@ def cpu_baseline(cfg, frames, text_len, batch, steps):
             v.grad = None
         train_step_grads(P, s, t, m, cfg, training=True)
     dt = time.perf_counter() - t0
-    return {"value": round(batch * frames * steps / dt, 1), "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"oracle fp32 train step (fwd+CE+bwd, dropout {cfg.dropout}) {cfg.n_enc}+{cfg.n_dec} layers "
-                      f"d{cfg.d_model}, B={batch}, T={frames}, L={text_len}, {steps} steps after 1 warmup, "
-                      f"{dt:.1f}s"}
+    out = {"value": round(batch * frames * steps / dt, 1), "unit": "frames/s", "cores": threads, "kind": "port",
+           "sample": f"oracle fp32 train step (fwd+CE+bwd, dropout {cfg.dropout}) {cfg.n_enc}+{cfg.n_dec} layers "
+                     f"d{cfg.d_model}, B={batch}, T={frames}, L={text_len}, {steps} steps after 1 warmup, "
+                     f"{dt:.1f}s",
+           "cpu_model": model, "affinity_cpus": aff, "threads": threads}
+    if extra:
+        fw = {}
+        for name, b in (("c2", CONFIGS["c2"]["batch"]), ("c3", 64), ("c5", 2)):
+            sp = CONFIGS[name]
+            c = sp["cfg"]
+            Pn = det_params(c, 0)
+            sx, tx, mx = synthetic_batch(c, b, sp["frames"], sp["text_len"] + 1, seed=99)
+            with torch.no_grad():
+                t0 = time.perf_counter()
+                forward(Pn, sx, tx[:, :-1], mx[:, :-1], c, False)
+                d1 = time.perf_counter() - t0
+            fw[name] = {"frames_per_s": round(b * sp["frames"] / d1, 1), "batch": b, "frames": sp["frames"],
+                        "s": round(d1, 2), "mode": "fp32 forward (eval)"}
+        out["forward"] = fw
+    return out
 
 
 def pmc_traffic(kernel, config):
@@ -78,15 +115,17 @@ def pmc_traffic(kernel, config):
     return None if rec is None else rec["hbm_bytes_per_launch"]
 
 
-def _graph_time_ms(fn, launches=20, rounds=5):
-    """GPU time of one fn() call: `launches` calls captured in a HIP graph, replayed between HIP events on the
-    capturing stream (no host launch gaps inside the timed region); median over rounds."""
-    fn()
+def _graph_time_ms(fns, launches=24, rounds=5):
+    """GPU time of one launch: `launches` calls (cycling through the closures `fns`) captured in a HIP graph,
+    replayed between HIP events on the capturing stream (no host launch gaps inside the timed region); median
+    over rounds."""
+    for fn in fns:
+        fn()
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
-        for _ in range(launches):
-            fn()
+        for i in range(launches):
+            fns[i % len(fns)]()
     g.replay()
     torch.cuda.synchronize()
     ts = []
@@ -100,66 +139,102 @@ def _graph_time_ms(fn, launches=20, rounds=5):
     return sorted(ts)[len(ts) // 2]
 
 
+COLD_BYTES = 768 << 20    # > the 256 MiB Infinity Cache: rotating buffer sets this large read from HBM
+
+
 def sub_rooflines(B, T2, d, H, ff, p_drop):
     """The north_star's per-kernel sub-rooflines at the workload's encoder shapes (rows = B*T'): MFMA
     utilisation of the attention projection GEMM and the fused attention forward, HBM fraction of LayerNorm
     fwd/bwd and of the (unfused-path) masked softmax.  Algorithmic bytes: every operand read once, every
-    output written once."""
+    output written once.
+
+    Cache state: `us` / `frac` rotate through independent buffer sets totalling > 768 MiB, so every launch
+    reads operands the previous launches evicted from the 256 MiB Infinity Cache (cold, HBM-sourced);
+    `us_warm` / `frac_warm` repeat one buffer set (its working set stays cache-resident)."""
     from asrx import kernels as K
     from asrx.kernels import MaskSpec
     rows, dh = B * T2, d // H
     gen = torch.Generator(device="cuda").manual_seed(7)
     out = {}
 
-    def mfma(name, flops, fn, note):
-        t = _graph_time_ms(fn)
-        tf = flops / (t * 1e-3) / 1e12
+    def timed(make, set_bytes):
+        nsets = max(2, -(-COLD_BYTES // set_bytes))
+        fns = [make() for _ in range(nsets)]
+        t_cold = _graph_time_ms(fns)
+        t_warm = _graph_time_ms(fns[:1])
+        del fns
+        torch.cuda.empty_cache()
+        return t_cold, t_warm, nsets
+
+    def mfma(name, flops, make, set_bytes, note):
+        t, tw, n = timed(make, set_bytes)
+        tf, tfw = flops / (t * 1e-3) / 1e12, flops / (tw * 1e-3) / 1e12
         out[name] = {"bound": "mfma", "achieved": round(tf, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(tf / PEAK_BF16_TFLOPS, 4), "us": round(t * 1e3, 2), "shape": note}
+                     "frac": round(tf / PEAK_BF16_TFLOPS, 4), "us": round(t * 1e3, 2),
+                     "frac_warm": round(tfw / PEAK_BF16_TFLOPS, 4), "us_warm": round(tw * 1e3, 2),
+                     "buffer_sets": n, "shape": note}
 
-    def hbm(name, nbytes, fn, note):
-        t = _graph_time_ms(fn)
-        gbs = nbytes / (t * 1e-3) / 1e9
+    def hbm(name, nbytes, make, note):
+        t, tw, n = timed(make, nbytes)
+        gbs, gbw = nbytes / (t * 1e-3) / 1e9, nbytes / (tw * 1e-3) / 1e9
         out[name] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": round(gbs / PEAK_HBM_GBS, 4), "us": round(t * 1e3, 2), "shape": note}
+                     "frac": round(gbs / PEAK_HBM_GBS, 4), "us": round(t * 1e3, 2),
+                     "frac_warm": round(gbw / PEAK_HBM_GBS, 4), "us_warm": round(tw * 1e3, 2),
+                     "buffer_sets": n, "shape": note}
 
-    x = (torch.randn(rows, d, device="cuda", generator=gen) * 0.5).bfloat16()
-    wqkv = (torch.randn(3 * d, d, device="cuda", generator=gen) * 0.05).bfloat16()
-    bqkv = torch.randn(3 * d, device="cuda", generator=gen) * 0.1
-    qkv = torch.empty(rows, 3 * d, device="cuda", dtype=torch.bfloat16)
-    mfma("qkv_projection_gemm", 2.0 * rows * 3 * d * d, lambda: K.linear(x, wqkv, qkv, bias=bqkv),
+    def rnd(*shape, dtype=torch.float32, scale=1.0):
+        return (torch.randn(*shape, device="cuda", generator=gen) * scale).to(dtype)
+
+    wqkv = rnd(3 * d, d, dtype=torch.bfloat16, scale=0.05)
+    bqkv = rnd(3 * d, scale=0.1)
+
+    def make_qkv():
+        x, qkv = rnd(rows, d, dtype=torch.bfloat16, scale=0.5), torch.empty(rows, 3 * d, device="cuda",
+                                                                              dtype=torch.bfloat16)
+        return lambda: K.linear(x, wqkv, qkv, bias=bqkv)
+    mfma("qkv_projection_gemm", 2.0 * rows * 3 * d * d, make_qkv, rows * d * 8,
          f"[{rows}x{d}] x [{d}x{3 * d}] + bias, bf16 out")
-    o = torch.empty(rows, d, device="cuda", dtype=torch.bfloat16)
     st = ((3 * d, T2 * 3 * d),) * 3 + ((d, T2 * d),)
-    dm = K.dropmask_buffer(B, H, T2, T2, dh, p_drop, x.device)
-    mfma("attention_fwd", 4.0 * B * H * T2 * T2 * dh,
-         lambda: K.attention_fwd(qkv, qkv[:, d:], qkv[:, 2 * d:], o, B, H, T2, T2, dh, st, d ** -0.5,
-                                 MaskSpec(), p_drop, 11, dropmask=dm),
+
+    def make_attn():
+        qkv = rnd(rows, 3 * d, dtype=torch.bfloat16, scale=0.5)
+        o = torch.empty(rows, d, device="cuda", dtype=torch.bfloat16)
+        dm = K.dropmask_buffer(B, H, T2, T2, dh, p_drop, qkv.device)
+        return lambda: K.attention_fwd(qkv, qkv[:, d:], qkv[:, 2 * d:], o, B, H, T2, T2, dh, st, d ** -0.5,
+                                       MaskSpec(), p_drop, 11, dropmask=dm)
+    mfma("attention_fwd", 4.0 * B * H * T2 * T2 * dh, make_attn, rows * d * 8,
          f"B*H={B * H} Lq=Lk={T2} dh={dh}, dropout {p_drop} (incl. the keep-bit generation kernel)")
-    xr = torch.randn(rows, d, device="cuda", generator=gen)
     gam = torch.rand(d, device="cuda", generator=gen) + 0.5
-    bet = torch.randn(d, device="cuda", generator=gen)
-    y = torch.empty(rows, d, device="cuda", dtype=torch.bfloat16)
-    mean, rstd = K.layernorm_fwd(xr, gam, bet, y)
-    hbm("layernorm_fwd", rows * d * (4 + 2) + rows * 8, lambda: K.layernorm_fwd(xr, gam, bet, y),
-        f"[{rows}x{d}] fp32 in, bf16 out, fp32 mean/rstd")
-    dy = torch.randn(rows, d, device="cuda", generator=gen).bfloat16()
-    dres = torch.randn(rows, d, device="cuda", generator=gen)
-    dxd = torch.empty(rows, d, device="cuda", dtype=torch.bfloat16)
-    dgb = torch.zeros(2 * d, device="cuda")
-    hbm("layernorm_bwd", rows * d * (4 + 2 + 4 + 4 + 2) + rows * 8,
-        lambda: K.layernorm_bwd(xr, dy, gam, mean, rstd, dgb, dres=dres, dx_drop=dxd, dropout_p=p_drop, seed=5,
-                                defer=[]),
+    bet = rnd(d)
+
+    def make_lnf():
+        xr, y = rnd(rows, d), torch.empty(rows, d, device="cuda", dtype=torch.bfloat16)
+        return lambda: K.layernorm_fwd(xr, gam, bet, y)
+    hbm("layernorm_fwd", rows * d * (4 + 2) + rows * 8, make_lnf, f"[{rows}x{d}] fp32 in, bf16 out, fp32 mean/rstd")
+
+    def make_lnb():
+        xr = rnd(rows, d)
+        mean, rstd = K.layernorm_fwd(xr, gam, bet, torch.empty(rows, d, device="cuda", dtype=torch.bfloat16))
+        dy, dres = rnd(rows, d, dtype=torch.bfloat16), rnd(rows, d)
+        dxd, dgb = torch.empty(rows, d, device="cuda", dtype=torch.bfloat16), torch.zeros(2 * d, device="cuda")
+        return lambda: K.layernorm_bwd(xr, dy, gam, mean, rstd, dgb, dres=dres, dx_drop=dxd, dropout_p=p_drop,
+                                       seed=5, defer=[])
+    hbm("layernorm_bwd", rows * d * (4 + 2 + 4 + 4 + 2) + rows * 8, make_lnb,
         f"[{rows}x{d}]: x fp32, dy bf16, dres fp32 in; dx fp32, dropout(dx) bf16 out")
     nbh, ld = B * H, (T2 + 7) // 8 * 8
-    sc = torch.randn(nbh, T2, ld, device="cuda", generator=gen).bfloat16()
-    pr = torch.empty_like(sc)
-    hbm("softmax_fwd", 2 * nbh * T2 * T2 * 2, lambda: K.softmax_fwd(sc, pr, None, nbh, H, T2, T2, ld, d ** -0.5,
-                                                                    MaskSpec()),
+
+    def make_smf():
+        sc = rnd(nbh, T2, ld, dtype=torch.bfloat16)
+        pr = torch.empty_like(sc)
+        return lambda: K.softmax_fwd(sc, pr, None, nbh, H, T2, T2, ld, d ** -0.5, MaskSpec())
+    hbm("softmax_fwd", 2 * nbh * T2 * T2 * 2, make_smf,
         f"unfused path (attention=\"unfused\"): {nbh}x{T2}x{T2} bf16 scores -> probabilities")
-    dpd = torch.randn(nbh, T2, ld, device="cuda", generator=gen).bfloat16()
-    dsc = torch.empty_like(sc)
-    hbm("softmax_bwd", 3 * nbh * T2 * T2 * 2, lambda: K.softmax_bwd(pr, dpd, dsc, nbh, T2, T2, ld, d ** -0.5),
+
+    def make_smb():
+        pr, dpd = rnd(nbh, T2, ld, dtype=torch.bfloat16), rnd(nbh, T2, ld, dtype=torch.bfloat16)
+        dsc = torch.empty_like(pr)
+        return lambda: K.softmax_bwd(pr, dpd, dsc, nbh, T2, T2, ld, d ** -0.5)
+    hbm("softmax_bwd", 3 * nbh * T2 * T2 * 2, make_smb,
         f"unfused path: {nbh}x{T2}x{T2} bf16 probabilities + their gradient -> score gradient")
     return out
 
@@ -174,7 +249,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import asrx
     from asrx import kernels as K
-    from asrx.train import Trainer
+    from asrx.train import GRAPH_WARMUP, Trainer
     from oracle.ref_model import CONFIGS, synthetic_batch
 
     spec = CONFIGS[args.config]
@@ -187,22 +262,32 @@ def main():
     if world > 1:   # identical initial weights on every rank
         for p in model.parameters():
             dist.broadcast(p.data, 0)
-    trainer = Trainer(model, lr=1e-4)
+    trainer = Trainer(model, lr=1e-4, graph=not args.no_graph)
     s, t, m = synthetic_batch(cfg, B, T, L + 1, seed=1234 + rank)
     s, t, m = s.cuda(), t.cuda(), m.cuda()
 
-    for i in range(args.warmup):
-        survey = not args.no_probe and i == args.warmup - 1
-        if survey:      # last warmup step: time every GEMM launch to find the dominant kernel instantiation
+    # Warm-up.  The last eager step (steady state: gradients bound, unzeroed Linear-weight gradients) times every
+    # GEMM launch to find the dominant kernel instantiation; from then on the probe times only that kernel (in
+    # graph mode the capture gives it a graph segment of its own, bracketed by HIP events at every replay).  The
+    # step is captured as HIP graph(s) at step GRAPH_WARMUP; if the requested warm-up is shorter, the missing
+    # steps run untimed as setup (reported as setup_steps).
+    probe = None
+    setup = 0 if args.no_graph else max(0, GRAPH_WARMUP + 1 - args.warmup)
+    survey = args.warmup - 1 if args.no_graph else GRAPH_WARMUP - 1
+    for i in range(args.warmup + setup):
+        if not args.no_probe and i == survey:
             K.PROBE = K.KernelProbe()
             K.PROBE.active = True
         loss = trainer.step(s, t, m)
+        if not args.no_probe and i == survey:
+            torch.cuda.synchronize()
+            probe = K.KernelProbe(K.PROBE.dominant())
+            probe.active = True
+            K.PROBE = probe
     torch.cuda.synchronize()
-    probe = None
-    if K.PROBE is not None:
-        probe = K.KernelProbe(K.PROBE.dominant())
-        probe.active = True
-        K.PROBE = probe
+    if probe is not None:
+        probe.events = {}
+        probe.flops = {}
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -243,6 +328,7 @@ def main():
                       "parallelism": f"dp{world}"},
            "frames_per_sec_per_gpu": round(value / world, 1),
            "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 3),
+           "graph": trainer._cap is not None, "setup_steps": setup,
            "loss": round(float(loss), 4),
            "roofline": roof}
     if rank == 0 and not args.no_sub:

@@ -34,6 +34,11 @@ extern "C" {
 /* Library version / build identification. */
 int asrx_version(void);
 
+/* sizeof of the descriptor structs as this library was compiled (binding check: a ctypes / cgo mirror of a
+ * struct must have the same size): out[0] = asrx_gemm_desc, out[1] = asrx_attn_desc, out[2] =
+ * asrx_gemm_group_dev, out[3] = asrx_rowsum_group.  Returns the number of entries written (<= n). */
+int asrx_struct_sizes(int64_t* out, int32_t n);
+
 /* ---------------------------------------------------------------------------------------------------
  * GEMM with fused epilogue:   C[z][m][n] = epi( alpha * sum_k A(z,m,k) * B(z,n,k) )
  *   A(m,k) = a_trans ? A[k*lda + m] : A[m*lda + k]
@@ -73,45 +78,31 @@ typedef struct asrx_gemm_desc {
    * 16+4q..16+4q+3.  Requires N % 32 == 0, ldc % 8 == 0, 16-B aligned C and the fast fused epilogue; else
    * ASRX_ERR_UNSUPPORTED. */
   uint32_t* mask_out; int64_t ld_mask;
+  /* kernel family (tests / A-B; 0 = auto): 1 = 256x128 LDS-DMA ring (p3), 3 = register-staged tiles, 4 = 64x64
+   * LDS-DMA ring, 5 = 128x64 LDS-DMA ring — honoured where the family's preconditions hold, else auto. */
+  int32_t kernel;
 } asrx_gemm_desc;
 
 int asrx_gemm(const asrx_gemm_desc* d, void* stream);
 
-/* Grouped GEMM: `count` independent problems C_i = epi(alpha * op(A_i) op(B_i)^T) in ONE launch (no split-K).
- * Layout flags, dtypes, alpha/beta come from `common` (its pointers/shapes are ignored); each group has its own
- * shape, operands, output and optional fused row-sum (bias gradient).  Supported: bf16 in, a_trans = b_trans
- * = 1 (weight gradients dW = dY^T X), count <= 48, 16-byte aligned operand rows.
+/* Grouped GEMM: `count` independent problems C_i = epi(alpha * op(A_i) op(B_i)^T) in ONE launch (no split-K),
+ * the group table in DEVICE memory: entries of 64 B; group i's output tiles are numbered consecutively from
+ * tile_start; tile_group[t] (device) = the group of tile t.  Layout flags, dtypes, alpha/beta come from
+ * `common` (its pointers/shapes are ignored).  Supported: bf16 in, a_trans = b_trans = 1 (weight gradients
+ * dW = dY^T X), 16-byte aligned operand rows (the table is not inspected on the host).
  * Replaces: the per-layer weight-gradient aten::mm + bias-gradient sum of autograd's nn.Linear backward
  * (layers.py:10-12,36,48,51; model.py:32) — issued together once the backward has produced every dY. */
-typedef struct asrx_gemm_group {
-  int32_t m, n, k;
-  const void* a; int64_t lda;
-  const void* b; int64_t ldb;
-  void* c; int64_t ldc;
-  float* rowsum_a;
-} asrx_gemm_group;
-
-int asrx_gemm_grouped(const asrx_gemm_desc* common, const asrx_gemm_group* groups, int32_t count, void* stream);
-
-/* Same with the group table in DEVICE memory (any count, one launch): entries of 64 B, 128x128 output tiles
- * numbered consecutively per group from tile_start; tile_group[t] (device) = the group of tile t.  The caller
- * guarantees the same alignment preconditions as asrx_gemm_grouped (the table is not inspected on the host);
- * cvec: every C row start is 16-byte aligned. */
 typedef struct asrx_gemm_group_dev {
   const void* a; const void* b; void* c; float* rowsum_a;
   int32_t lda, ldb, ldc, m, n, k, tile_start, reserved;
 } asrx_gemm_group_dev;
 
-int asrx_gemm_grouped_table(const asrx_gemm_desc* common, const asrx_gemm_group_dev* groups,
-                            const uint16_t* tile_group, int32_t count, int32_t tiles, int32_t cvec, void* stream);
-
-/* Same with an explicit workgroup -> tile map: block_tile[b] (device, `blocks` entries, 0xFFFF = idle) names
+/* Launch with an explicit workgroup -> tile map: block_tile[b] (device, `blocks` entries, 0xFFFF = idle) names
  * the tile workgroup b computes.  Workgroup b runs on XCD b % 8, so a host that lays the tiles of one group on
  * one XCD at the same time lets them share that XCD's L2 (the operand panels of dW = dY^T X are re-read by
  * every tile of the group).  common->tile selects the tile: 3 = the p3 LDS-DMA ring, 256x128 tiles (m x n;
  * fp32 C with 16-byte aligned rows, every group's n % 4 == 0, alpha 1, beta 0 or 1), 128 = register-staged
- * 128x128 tiles (the asrx_gemm_grouped_table kernel; common->relu carries its cvec flag), 256 = the 256x256
- * LDS-DMA ring (gemm_p5.hip; same requirements as 3).
+ * 128x128 tiles (any alignment-checked table; common->relu carries its "every C row 16-byte aligned" flag).
  * Replaces the weight/bias-gradient mm + sum of autograd for every nn.Linear (layers.py:10-12,36,48,51). */
 int asrx_gemm_grouped_xcd(const asrx_gemm_desc* common, const asrx_gemm_group_dev* groups,
                           const uint16_t* tile_group, const uint16_t* block_tile, int32_t count, int32_t tiles,
@@ -161,6 +152,11 @@ typedef struct asrx_attn_desc {
    * without it the forward uses the tiled kernel. */
   uint32_t* dropmask;
   int32_t dropmask_ready;       /* nonzero: the forward finds the bits already generated (asrx_attn_dropgen) */
+  /* optional (training): bf16 buffer with o's strides; the forward writes the rounding residual O - bf16(O)
+   * there and the backward forms delta = rowsum(dO * (O + residual)), i.e. sum_key P dP to fp32 accuracy.
+   * (With the d_model^-1/2 scale the softmax rows are flat and dS = P (dP - delta) is a small difference: the
+   * bf16 rounding of O alone perturbs dQ by delta's error times the mean key.) */
+  void* o_lo;
 } asrx_attn_desc;
 
 int asrx_attention_fwd(const asrx_attn_desc* d, void* stream);
@@ -277,14 +273,28 @@ int asrx_cross_entropy(const float* logits, int64_t rows, int32_t V, int64_t ld,
  * Elementwise utilities.
  * ------------------------------------------------------------------------------------------------- */
 int asrx_cast(int32_t src_dtype, const void* src, int32_t dst_dtype, void* dst, int64_t n, void* stream);
-/* Fused Adam/AdamW over flat fp32 buffers; optionally refreshes the bf16 shadow copy of the params. */
+/* Fused Adam/AdamW over flat fp32 buffers; optionally refreshes the bf16 shadow copy of the params.
+ * Replaces optimizer.step() (train.py:35).  hyp (optional, device): {lr, bias_corr1, bias_corr2} read at run
+ * time instead of the scalar arguments, so a captured step (HIP graph) takes the current step's values. */
 int asrx_adam(float* p, const float* g, float* m, float* v, void* p_bf16, int64_t n, float lr, float beta1,
               float beta2, float eps, float weight_decay, float bias_corr1, float bias_corr2, float grad_scale,
-              int32_t decoupled, void* stream);
+              int32_t decoupled, const float* hyp, void* stream);
 /* delta[(b*heads+h)*lq+q] = sum_d dO*O (attention backward prologue). */
 int asrx_attn_delta(const asrx_attn_desc* d, void* stream);
 /* y = dropout(x) with the library RNG (idx = element index); used for tests of the RNG stream. */
 int asrx_dropout_mask(uint8_t* keep, int64_t n, float p, uint64_t seed, void* stream);
+
+/* ---------------------------------------------------------------------------------------------------
+ * HIP-graph support.  A captured training step replays every launch with the arguments recorded at capture.
+ * ------------------------------------------------------------------------------------------------- */
+/* Copy nbytes (multiple of 4) of HOST memory to dst (device, 4-byte aligned) through kernel arguments, ordered
+ * on `stream`; the host buffer may be reused as soon as the call returns, and the copy is capturable (a replay
+ * writes the same bytes again).  Used for grouped-launch tables and per-step scalars. */
+int asrx_upload(void* dst, const void* src, int64_t nbytes, void* stream);
+/* Device-resident dropout seed offset folded into the seed of every dropout-drawing kernel at its start
+ * (offset 0 = seeds used as given).  Set once per training step, BEFORE the step's forward: a replayed graph
+ * then draws fresh masks each step while forward and backward of one step still agree. */
+int asrx_set_seed_offset(uint64_t offset, void* stream);
 
 #ifdef __cplusplus
 }

@@ -301,4 +301,10 @@ CONFIGS = {
                batch=64, frames=1000, text_len=64),
     "c5": dict(cfg=OracleConfig(d_model=512, dec_len=256, enc_len=4000, n_enc=12, n_dec=12, n_heads=8, ff_dim=2048),
                batch=16, frames=4000, text_len=256),
+    # d_head = 64 gradient fixtures (tests/golden/make_golden.py): the bf16 training path's resident-K/V attention
+    # kernels (T' = 49 <= 256) and the tiled long-sequence kernels (T' = 274 > 256) pinned to the reference
+    "g64": dict(cfg=OracleConfig(d_model=128, dec_len=16, enc_len=64, n_enc=1, n_dec=1, n_heads=2, ff_dim=256),
+                batch=2, frames=200, text_len=16),
+    "g64l": dict(cfg=OracleConfig(d_model=128, dec_len=16, enc_len=300, n_enc=1, n_dec=1, n_heads=2, ff_dim=256),
+                 batch=1, frames=1100, text_len=16),
 }

@@ -122,6 +122,34 @@ def gen_model(name, train_grads_full):
     np.savez_compressed(os.path.join(OUT, f"model_{name}.npz"), **out)
 
 
+def gen_grads(name, full_filter=None):
+    """dropout=0 training step of the reference at a d_head = 64 config (train.py:28-34: forward, CE over
+    text[:, 1:], backward): loss, logits, every parameter gradient (full tensors for keys passing
+    `full_filter`, norms for all)."""
+    spec = CONFIGS[name]
+    cfg = spec["cfg"]
+    spectrum, text, mask = synthetic_batch(cfg, spec["batch"], spec["frames"], spec["text_len"] + 1, seed=4242)
+    out = dict(spectrum=np32(spectrum), text=text.numpy().astype(np.int64), mask=np32(mask))
+    mt = build_ref(cfg, dropout=0.0).train()
+    lt = mt(spectrum, text[:, :-1], mask[:, :-1])
+    loss = torch.nn.functional.cross_entropy(lt.transpose(1, 2), text[:, 1:])
+    loss.backward()
+    out["logits"] = np32(lt)
+    out["loss"] = np.float32(loss.item())
+    names, norms = [], []
+    for k, p in mt.named_parameters():
+        if p.grad is None:
+            continue
+        names.append(k)
+        norms.append(float(p.grad.norm()))
+        if full_filter is None or full_filter(k):
+            out["grad/" + k] = np32(p.grad)
+    out["grad_names"] = np.array(names)
+    out["grad_norms"] = np.array(norms, dtype=np.float64)
+    out["nograd_names"] = np.array([k for k, p in mt.named_parameters() if p.grad is None])
+    np.savez_compressed(os.path.join(OUT, f"grads_{name}.npz"), **out)
+
+
 def gen_schema():
     """Reference state_dict key order and shapes (drop-in schema check without the reference present)."""
     import json
@@ -144,6 +172,9 @@ if __name__ == "__main__":
     gen_ops()
     gen_model("micro", train_grads_full=True)
     gen_model("c1", train_grads_full=False)
+    gen_grads("g64")
+    # long sequence: full tensors for the attention parameters (the tiled kernels' gradients), norms elsewhere
+    gen_grads("g64l", lambda k: "_attention" in k or "_norm" in k)
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

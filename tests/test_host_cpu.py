@@ -41,6 +41,27 @@ def test_abi_rejects_bad_arguments_without_gpu():
     assert lib.asrx_cast(0, None, 0, None, 10, None) == -1
 
 
+def test_ctypes_struct_sizes_match_the_library():
+    """Every descriptor struct mirrored in the ctypes binding has the size the library was compiled with
+    (asrx_struct_sizes): a stale mirror would make the library read past the caller's struct."""
+    import ctypes
+    import asrx
+    from asrx._lib import AttnDesc, GemmDesc, GemmGroupDev, RowsumGroup
+    lib = asrx.native()
+    out = (ctypes.c_int64 * 4)()
+    assert lib.asrx_struct_sizes(out, 4) == 4
+    assert list(out) == [ctypes.sizeof(GemmDesc), ctypes.sizeof(AttnDesc), ctypes.sizeof(GemmGroupDev),
+                         ctypes.sizeof(RowsumGroup)]
+    assert ctypes.sizeof(GemmGroupDev) == 64
+
+
+def test_abi_upload_and_seed_offset_validate_arguments_without_gpu():
+    import asrx
+    lib = asrx.native()
+    assert lib.asrx_upload(None, None, 16, None) == -1
+    assert lib.asrx_upload(4096, None, 6, None) == -1      # nbytes not a multiple of 4
+
+
 def _build(name, **kw):
     import asrx
     cfg = CONFIGS[name]["cfg"]
@@ -139,18 +160,15 @@ def test_gemm_kernel_plan_names_without_gpu():
             d.bias = 4 << 20
         return d
 
-    os.environ.pop("ASRX_GEMM_KERNEL", None)
     assert kernel_name(desc(15936, 1536, 512, bias=True)) == "gemm_bf16_p3_kernel<false, false, 1>"
     assert kernel_name(desc(15936, 512, 2048, bt=1)) == "gemm_bf16_p3_kernel<false, true, 0>"
     wg = desc(2048, 512, 15936, at=1, bt=1, c_dtype=F32)
     wg.tile = 128                     # as kernels.wgrad_plan sets it
     assert kernel_name(wg) == "gemm_bf16_kernel<128, 128, true, true, true>"
     assert kernel_name(desc(64, 64, 64, in_dtype=F32, c_dtype=F32)) == "gemm_f32_kernel<false, false>"
-    os.environ["ASRX_GEMM_KERNEL"] = "reg"
-    try:
-        assert kernel_name(desc(15936, 1536, 512)).startswith("gemm_bf16_kernel<128, 128, false, false, true>")
-    finally:
-        os.environ.pop("ASRX_GEMM_KERNEL")
+    forced = desc(15936, 1536, 512)
+    forced.kernel = 3                 # asrx_gemm_desc.kernel: register-staged family
+    assert kernel_name(forced).startswith("gemm_bf16_kernel<128, 128, false, false, true>")
 
 
 def test_rng_restatement_statistics():

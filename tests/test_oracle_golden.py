@@ -96,6 +96,29 @@ def test_train_step_grads(golden_dir, name):
         assert grads[k] is None or float(grads[k].abs().max()) == 0.0, k
 
 
+@pytest.mark.parametrize("name", ["g64", "g64l"])
+def test_train_step_grads_dh64(golden_dir, name):
+    """d_head = 64 fixtures (the bf16 path's resident / tiled attention kernels): oracle loss, logits and every
+    gradient vs the reference's own training step."""
+    g = load(golden_dir, f"grads_{name}.npz")
+    spec = CONFIGS[name]
+    cfg = spec["cfg"]
+    P = {k: v.clone().requires_grad_(True) for k, v in det_params(cfg).items()}
+    s, t, m = synthetic_batch(cfg, spec["batch"], spec["frames"], spec["text_len"] + 1, seed=4242)
+    np.testing.assert_array_equal(s.numpy(), g["spectrum"])
+    np.testing.assert_array_equal(t.numpy(), g["text"])
+    logits = forward(P, s, t[:, :-1], m[:, :-1], cfg, False)
+    assert rel(logits.detach(), g["logits"]) < 1e-5
+    loss = torch.nn.functional.cross_entropy(logits.transpose(1, 2), t[:, 1:])
+    loss.backward()
+    assert abs(float(loss) - float(g["loss"])) < 1e-5 * abs(float(g["loss"]))
+    for k, n in zip(g["grad_names"], g["grad_norms"]):
+        gk = P[k].grad
+        assert abs(float(gk.norm()) - n) <= 1e-4 * n + 1e-7, k
+        if "grad/" + k in g.files:
+            assert rel(gk, g["grad/" + k]) < 1e-4, k
+
+
 def test_greedy_decode(golden_dir):
     g = load(golden_dir, "model_c1.npz")
     spec = CONFIGS["c1"]
