@@ -115,6 +115,21 @@ def pmc_traffic(kernel, config):
     return None if rec is None else rec["hbm_bytes_per_launch"]
 
 
+def pmc_mfma(kernel, config):
+    """MFMA busy fraction of `kernel` from the committed counter pass (profiles/<config>_pmc_mfma.json, written by
+    tools/pmc_mfma.py from rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE),
+    or None."""
+    path = os.path.join(REPO, "profiles", f"{config}_pmc_mfma.json")
+    try:
+        with open(path) as f:
+            rec = json.load(f)["kernels"].get(kernel)
+    except (OSError, ValueError, KeyError):
+        return None
+    if rec is None:
+        return None
+    return {k: rec.get(k) for k in ("mfma_busy_frac", "mfma_tflops", "clock_ghz", "mfma_flop_per_launch")}
+
+
 def _graph_time_ms(fns, launches=24, rounds=5):
     """GPU time of one launch: `launches` calls (cycling through the closures `fns`) captured in a HIP graph,
     replayed between HIP events on the capturing stream (no host launch gaps inside the timed region); median
@@ -315,7 +330,8 @@ def main():
                 "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": pmc_traffic(probe.target, args.config),
                 "kernel": probe.target, "launches_per_step": len(durs) // args.steps,
                 "avg_launch_us": round(avg_ms * 1e3, 2),
-                "flop_per_launch_avg": probe.flops[probe.target] // len(durs)}
+                "flop_per_launch_avg": probe.flops[probe.target] // len(durs),
+                "pmc_mfma": pmc_mfma(probe.target, args.config)}
     out = {"metric": "encoder+decoder frames/sec/GPU at d_model=512 T=1000; 1->8 GPU scaling",
            "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
