@@ -109,7 +109,7 @@ def kernel_name(d):
 PROBE = None
 
 # asrx_gemm_desc.kernel: forced kernel family (0 = auto).  ASRX_GEMM_KERNEL picks a process-wide default (A/B).
-KERNEL_CODES = {"auto": 0, "p3": 1, "reg": 3, "ring": 4, "ring128": 5}
+KERNEL_CODES = {"auto": 0, "p3": 1, "reg": 3, "ring": 4, "ring128": 5, "p4": 6}
 GEMM_KERNEL = KERNEL_CODES.get(os.environ.get("ASRX_GEMM_KERNEL", "auto"), 0)
 
 
@@ -217,6 +217,7 @@ def linear_wgrad(dy, x, wgrad, *, beta=1.0, bias_grad=None, **kw):
 GROUPED_TABLE_KERNEL = "gemm_bf16_grouped_dev_kernel<true, true>"
 # (beta != 1, beta == 1) instantiations (96 = E_BETA | E_F32: accumulate into the fp32 grads)
 GROUPED_P3_KERNELS = ("gemm_bf16_p3g_kernel<64>", "gemm_bf16_p3g_kernel<96>")
+GROUPED_P4_KERNELS = ("gemm_bf16_p4g_kernel<64>", "gemm_bf16_p4g_kernel<96>")
 
 
 def wgrad_groupable(dy, x, wgrad):
@@ -227,14 +228,15 @@ def wgrad_groupable(dy, x, wgrad):
             and x.data_ptr() % 16 == 0 and dy.shape[0] <= 65536)
 
 
-# Weight-gradient kernel: "p3" = the 256x128 LDS-DMA ring (gemm.hip p3_body, measured fastest), "reg" = the
-# register-staged 128x128 tiles (also the fallback for tables the ring cannot take).  ASRX_WGRAD_KIND overrides.
-WGRAD_KIND = os.environ.get("ASRX_WGRAD_KIND", "p3")
+# Weight-gradient kernel: "p4" = 256x256 tiles on the software-pipelined LDS-DMA ring (gemm.hip p4_body; c3 step
+# 14.11 -> 13.80 ms against "p3", the 256x128 ring), "reg" = the register-staged 128x128 tiles (also the fallback
+# for tables the ring cannot take).  ASRX_WGRAD_KIND overrides.
+WGRAD_KIND = os.environ.get("ASRX_WGRAD_KIND", "p4")
 
 
 def _grouped_p3_ok(items, beta):
     """Can the LDS-DMA ring kernel take these weight gradients (fp32 C rows 16-byte aligned, beta 0 or 1)?"""
-    return WGRAD_KIND == "p3" and beta in (0.0, 1.0) and all(
+    return WGRAD_KIND in ("p3", "p4") and beta in (0.0, 1.0) and all(
         x.shape[1] % 4 == 0 and wgrad.stride(0) % 4 == 0 and wgrad.data_ptr() % 16 == 0
         for (_, x, wgrad, _) in items)
 
@@ -277,7 +279,7 @@ def xcd_plan(shapes, tile=256, nxcd=8):
     return plan
 
 
-_TILE_CODE = {"p3": ((256, 128), 3), "reg": ((128, 128), 128)}
+_TILE_CODE = {"p3": ((256, 128), 3), "p4": ((256, 256), 4), "reg": ((128, 128), 128)}
 
 
 def upload(dst, host_bytes):
@@ -336,7 +338,7 @@ def _grouped_xcd(items, common, kind="p3"):
 WGRAD_XCD = os.environ.get("ASRX_WGRAD_XCD", "1") != "0"
 
 
-def linear_wgrad_grouped(items, *, beta=1.0):
+def linear_wgrad_grouped(items, *, beta=1.0, kind=None):
     """Issue many independent weight gradients wgrad[N,K] (+)= dy[M,N]^T . x[M,K] (+ bias_grad[N] += colsum dy)
     as ONE grouped launch (longest reductions first, tiles of a group on one XCD)."""
     if not items:
@@ -346,13 +348,15 @@ def linear_wgrad_grouped(items, *, beta=1.0):
     common.in_dtype, common.a_trans, common.b_trans, common.c_dtype = BF16, 1, 1, F32
     common.alpha, common.beta = 1.0, beta
     p3 = _grouped_p3_ok(items, beta)
-    kname = GROUPED_P3_KERNELS[beta == 1.0] if p3 else GROUPED_TABLE_KERNEL
+    kind = kind or WGRAD_KIND
+    kname = ((GROUPED_P4_KERNELS if kind == "p4" else GROUPED_P3_KERNELS)[beta == 1.0] if p3
+             else GROUPED_TABLE_KERNEL)
     probe = PROBE
     if probe is not None and probe.active and probe.log is not None:
         probe.log.append((kname, len(items), 0,
                           sum(it[0].shape[0] * it[0].shape[1] * it[1].shape[1] for it in items), 1, 1))
     # the table upload is issued first, so a timed bracket holds the grouped GEMM alone
-    flops, launch, _ = _grouped_xcd(items, common, "p3" if p3 else "reg")
+    flops, launch, _ = _grouped_xcd(items, common, kind if p3 else "reg")
     if probe is not None and probe.active:
         timed_launch(kname, flops, launch)
     else:

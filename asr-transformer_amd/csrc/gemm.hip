@@ -247,6 +247,14 @@ __global__ __launch_bounds__(256) void gemm_bf16_grouped_dev_kernel(float alpha,
   gemm_bf16_tile<128, 128, AT, BT, true>(g, tid - e.tile_start, 0, 0, lds);
 }
 
+// diagnostics switch (ASRX_GEMM_DBG, or asrx_gemm_set_debug for interleaved A/B in one process): 1 = skip the
+// epilogue stores, 4 = issue each LDS-DMA stage in one block, 8 = no operand loads (compute on stale LDS)
+int g_gemm_dbg = -1;
+int gemm_dbg() {
+  if (g_gemm_dbg < 0) { const char* e = getenv("ASRX_GEMM_DBG"); g_gemm_dbg = e ? atoi(e) : 0; }
+  return g_gemm_dbg;
+}
+
 // ------------------------------------------------------------------------------------------------
 // bf16 "p3" kernel: 256x128x64 tiles, 8 waves (4x2, 64x64 each), persistent, a 3-stage LDS-DMA ring
 // (3 x 48 KiB): stage s+2 is issued while stage s is computed, the wait before each K-step is a counted
@@ -325,13 +333,29 @@ ASRX_DEV s8_t p_frag(const unsigned char* img, int i0, int ks) {
 // (An XCD-owned ROW order — row-block tm served by the workgroups with b % 8 == tm % 8 — was measured 10-50%
 // slower on every c3 shape; the XCD-contiguous TILE ranges of gemm_bf16_p3_kernel's `xcd` mode are 1-7% faster.)
 
-// The p3 main loop over a workgroup's tile sequence tl (the ring runs across tile boundaries).
-// lds: 3 ring stages + P_BIAS_BYTES (the bias vector of bias epilogues, N <= 4096: it is loaded once before the
+// The p3 / p4 main loop over a workgroup's tile sequence tl (the ring runs across tile boundaries).
+//   BN = 128 ("p3"): 256x128 tiles, 8 waves as 4x2 of 64x64, a 3-stage ring of 48 KiB stages (two in flight).
+//   BN = 256 ("p4"): 256x256 tiles, 8 waves as 2x4 of 128x64, a 2-stage ring of 64 KiB stages (one in flight
+//                    while the other is computed): half the operand ingest per FLOP of p3 and 25% fewer LDS
+//                    fragment reads per MFMA (a 128x64 wave tile re-uses each A fragment 4x, each B fragment 8x).
+// lds: NST ring stages + P_BIAS_BYTES (the bias vector of bias epilogues, N <= 4096: it is loaded once before the
 // ring starts, so the epilogues issue no global load, which would wait for every LDS-DMA stage in flight).
-template <bool AT, bool BT, int EPI>
+template <int BN> struct PGeo {
+  static constexpr int NST = BN == 256 ? 2 : 3;        // ring stages
+  static constexpr int TM = BN == 256 ? 8 : 4;         // 16-row fragments per wave
+  static constexpr int TN = 4;                         // 16-column fragments per wave
+  static constexpr int PB = BN * BK * 2, STAGE = PA_BYTES + PB;
+  static constexpr int INST = STAGE / (P_THREADS * 16);   // LDS-DMA instructions per thread per stage
+  static constexpr int NIA = PA_BYTES / (P_THREADS * 16), NIB = PB / (P_THREADS * 16);
+  static constexpr int LDS = NST * STAGE + P_BIAS_BYTES;
+};
+
+template <bool AT, bool BT, int EPI, int BN = P_BN>
 ASRX_DEV void p3_body(const GemmArgs& g, const TileSeq tl, int split, int z, unsigned char* lds) {
-  constexpr int TM = 4, TN = 4;
-  const int ntn = (g.N + P_BN - 1) / P_BN;
+  using G_ = PGeo<BN>;
+  constexpr int TM = G_::TM, TN = G_::TN, NST = G_::NST, STAGE = G_::STAGE, INST = G_::INST;
+  constexpr int NIA = G_::NIA, NIB = G_::NIB;
+  const int ntn = (g.N + BN - 1) / BN;
   const int zo = z / g.batch_inner, zi = z % g.batch_inner;
   const bf16_t* A = (const bf16_t*)g.a + zo * g.sa_o + zi * g.sa_i;
   const bf16_t* B = (const bf16_t*)g.b + zo * g.sb_o + zi * g.sb_i;
@@ -347,11 +371,13 @@ ASRX_DEV void p3_body(const GemmArgs& g, const TileSeq tl, int split, int z, uns
   const int ntl = tl.count;
   const int total = ntl * nk;
   const int wave = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int wm = BN == 256 ? (wave >> 2) * 128 : (wave >> 1) * 64;
+  const int wn = BN == 256 ? (wave & 3) * 64 : (wave & 1) * 64;
 
   PStage<P_BM, AT> sa;
-  PStage<P_BN, BT> sb;
-  // issue cursor (runs two steps ahead of the compute cursor)
+  PStage<BN, BT> sb;
+  const bool noload = (g.dbg & 8) != 0;   // diagnostics (ASRX_GEMM_DBG & 8): no operand loads, compute on stale LDS
+  // issue cursor (runs NST - 1 steps ahead of the compute cursor)
   int iv = 0, ik = 0, ib = 0;
   // (a macro rather than a lambda: hipcc/ROCm 7.2 dropped the host device-stubs of most instantiations of this
   //  kernel when the issue step was a capturing lambda)
@@ -360,13 +386,15 @@ ASRX_DEV void p3_body(const GemmArgs& g, const TileSeq tl, int split, int z, uns
     if (ik == 0) {                                                           \
       const int pt_ = P3_TILE(iv);                                           \
       sa.set_tile((pt_ / ntn) * P_BM, g.lda);                                \
-      sb.set_tile((pt_ % ntn) * P_BN, g.ldb);                                \
+      sb.set_tile((pt_ % ntn) * BN, g.ldb);                                  \
     }                                                                        \
-    unsigned char* img_ = lds + ib * P_STAGE;                                \
-    sa.issue(img_, A, g.lda, a_bytes, kbeg + ik * BK);                       \
-    sb.issue(img_ + PA_BYTES, B, g.ldb, b_bytes, kbeg + ik * BK);            \
+    unsigned char* img_ = lds + ib * STAGE;                                  \
+    if (!noload) {                                                           \
+      sa.issue(img_, A, g.lda, a_bytes, kbeg + ik * BK);                     \
+      sb.issue(img_ + PA_BYTES, B, g.ldb, b_bytes, kbeg + ik * BK);          \
+    }                                                                        \
     if (++ik == nk) { ik = 0; ++iv; }                                        \
-    ib = ib == 2 ? 0 : ib + 1;                                               \
+    ib = ib == NST - 1 ? 0 : ib + 1;                                         \
   } while (0)
 
   f4_t acc[TN][TM];
@@ -381,60 +409,63 @@ ASRX_DEV void p3_body(const GemmArgs& g, const TileSeq tl, int split, int z, uns
   // bias epilogues: the host splits N > 4096 into column chunks, so the whole bias fits the LDS region
   constexpr bool use_lb = (EPI & E_BIAS) != 0;
   if constexpr (use_lb) {
-    float* lb = (float*)(lds + 3 * P_STAGE);
+    float* lb = (float*)(lds + NST * STAGE);
     for (int c = threadIdx.x * 4; c < g.N; c += P_THREADS * 4) *(f4_t*)(lb + c) = *(const f4_t*)(g.bias + c);
     __syncthreads();
   }
   P3_ISSUE_NEXT();
-  if (total > 1) P3_ISSUE_NEXT();
+  if (NST == 3 && total > 1) P3_ISSUE_NEXT();
   // Epilogues that read memory (gate / residual / row-add: PRE) load those operands right after the barrier of
   // the tile's last K-step and issue that step's stage only AFTER the epilogue, so the epilogue's wait for its
   // loads (in-order vmcnt) covers only the stage already needed next, not a freshly issued one.
   constexpr bool PRE = EpiPre<EPI, TN, TM>::ANY;
   const bool sp_iss = !(g.dbg & 4);   // ASRX_GEMM_DBG=4: issue each stage in one block (A/B)
-  // younger-operation ledger (lower bounds; an under-count only over-waits): stage s was issued in step s - 2.
-  // Younger than it: the stores of step s - 2's epilogue if issued after that step's stage (ea2), stage s + 1
-  // (P_INST pieces), and the stores of step s - 1's epilogue (eb1 before / ea1 after its stage issue).
+  // younger-operation ledger (lower bounds; an under-count only over-waits).  NST = 3: stage s was issued in step
+  // s - 2; younger than it: the stores of step s - 2's epilogue if issued after that step's stage (ea2), stage
+  // s + 1 (INST pieces), and the stores of step s - 1's epilogue (eb1 before / ea1 after its stage issue).
+  // NST = 2: stage s was issued in step s - 1; younger than it: that step's epilogue stores issued after it (ea1).
   int ea1 = 0, ea2 = 0, eb1 = 0;
   int vc = 0, kk = 0, cb = 0;   // compute cursor
   for (int s = 0; s < total; ++s) {
-    wait_vmcnt_rt(ea2 + (s + 1 < total ? P_INST : 0) + eb1 + ea1);
+    if constexpr (NST == 3) wait_vmcnt_rt(ea2 + (s + 1 < total ? INST : 0) + eb1 + ea1);
+    else wait_vmcnt_rt(ea1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     ea2 = ea1;
     ea1 = 0;
     eb1 = 0;
     const bool last = kk == nk - 1;
-    const bool defer = PRE && last && g.splitk == 1 && g.dbg != 1;
-    // This step's stage (s + 2): issued in one block right after the barrier, or (split) in two halves, each
-    // behind the fragment reads of one 32-deep k-slice, so the DMA issue overlaps the LDS read latency instead
-    // of holding every wave's MFMAs after the barrier.
-    const bool doiss = !defer && s + 2 < total;
+    const bool defer = PRE && last && g.splitk == 1 && !(g.dbg & 1);
+    // This step's stage (s + NST - 1): issued in one block right after the barrier, or (split) in two halves,
+    // each behind the fragment reads of one 32-deep k-slice, so the DMA issue overlaps the LDS read latency
+    // instead of holding every wave's MFMAs after the barrier.
+    const bool doiss = !defer && s + NST - 1 < total;
+    const bool dodma = doiss && !noload;
     unsigned char* img_ = nullptr;
     v4i_t srda = {0, 0, 0, 0}, srdb = {0, 0, 0, 0};
     if (doiss) {
       if (ik == 0) {
         const int pt_ = P3_TILE(iv);
         sa.set_tile((pt_ / ntn) * P_BM, g.lda);
-        sb.set_tile((pt_ % ntn) * P_BN, g.ldb);
+        sb.set_tile((pt_ % ntn) * BN, g.ldb);
       }
-      img_ = lds + ib * P_STAGE;
+      img_ = lds + ib * STAGE;
       srda = sa.srd(A, g.lda, a_bytes, kbeg + ik * BK);
       srdb = sb.srd(B, g.ldb, b_bytes, kbeg + ik * BK);
-      if (!sp_iss) {
-        sa.template issue_part<0, 4>(img_, srda);
-        sb.template issue_part<0, 2>(img_ + PA_BYTES, srdb);
+      if (!sp_iss && dodma) {
+        sa.template issue_part<0, NIA>(img_, srda);
+        sb.template issue_part<0, NIB>(img_ + PA_BYTES, srdb);
       }
       if (++ik == nk) { ik = 0; ++iv; }
-      ib = ib == 2 ? 0 : ib + 1;
+      ib = ib == NST - 1 ? 0 : ib + 1;
     }
-    const unsigned char* la = lds + cb * P_STAGE;
+    const unsigned char* la = lds + cb * STAGE;
     const unsigned char* lb = la + PA_BYTES;
     const int t = P3_TILE(vc);
     const bool do_rs = AT && g.rowsum != nullptr && (t % ntn) == 0 && wn == 0;
     EpiPre<EPI, TN, TM> pre;
     if constexpr (PRE) {
-      if (defer) epi_prefetch<EPI, TN, TM>(pre, g, (t / ntn) * P_BM, (t % ntn) * P_BN, wm, wn);
+      if (defer) epi_prefetch<EPI, TN, TM>(pre, g, (t / ntn) * P_BM, (t % ntn) * BN, wm, wn);
     }
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
@@ -442,14 +473,14 @@ ASRX_DEV void p3_body(const GemmArgs& g, const TileSeq tl, int split, int z, uns
 #pragma unroll
       for (int j = 0; j < TM; ++j) fa[j] = p_frag<P_BM, AT>(la, wm + 16 * j, ks);
 #pragma unroll
-      for (int i = 0; i < TN; ++i) fb[i] = p_frag<P_BN, BT>(lb, wn + 16 * i, ks);
-      if (sp_iss && doiss) {
+      for (int i = 0; i < TN; ++i) fb[i] = p_frag<BN, BT>(lb, wn + 16 * i, ks);
+      if (sp_iss && dodma) {
         if (ks == 0) {
-          sa.template issue_part<0, 2>(img_, srda);
-          sb.template issue_part<0, 1>(img_ + PA_BYTES, srdb);
+          sa.template issue_part<0, NIA / 2>(img_, srda);
+          sb.template issue_part<0, NIB / 2>(img_ + PA_BYTES, srdb);
         } else {
-          sa.template issue_part<2, 4>(img_, srda);
-          sb.template issue_part<1, 2>(img_ + PA_BYTES, srdb);
+          sa.template issue_part<NIA / 2, NIA>(img_, srda);
+          sb.template issue_part<NIB / 2, NIB>(img_ + PA_BYTES, srdb);
         }
       }
 #pragma unroll
@@ -466,7 +497,7 @@ ASRX_DEV void p3_body(const GemmArgs& g, const TileSeq tl, int split, int z, uns
       }
     }
     if (kk == nk - 1) {
-      const int m0 = (t / ntn) * P_BM, n0 = (t % ntn) * P_BN;
+      const int m0 = (t / ntn) * P_BM, n0 = (t % ntn) * BN;
       if constexpr (AT) {
         if (do_rs) {
 #pragma unroll
@@ -493,11 +524,11 @@ ASRX_DEV void p3_body(const GemmArgs& g, const TileSeq tl, int split, int z, uns
             store_partial4(g, split, m0 + wm + 16 * j + (l & 15), n0 + wn + 16 * i + 4 * gq, v);
           }
       } else {
-        if (g.dbg == 1) {
+        if (g.dbg & 1) {
           keep_live(acc);
         } else {
-          const int full = m0 + P_BM <= g.M && n0 + P_BN <= g.N;
-          lds_cfloat_t* lbias = (lds_cfloat_t*)(lds + 3 * P_STAGE) + n0;
+          const int full = m0 + P_BM <= g.M && n0 + BN <= g.N;
+          lds_cfloat_t* lbias = (lds_cfloat_t*)(lds + NST * STAGE) + n0;
           if (defer) {
             eb1 = epilogue_tile<EPI, TN, TM, use_lb, PRE>(g, z, m0, n0, wm, wn, acc, lbias, full, &pre);
           } else {
@@ -510,30 +541,319 @@ ASRX_DEV void p3_body(const GemmArgs& g, const TileSeq tl, int split, int z, uns
 #pragma unroll
         for (int j = 0; j < TM; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
     }
-    if (defer && s + 2 < total) P3_ISSUE_NEXT();
+    if (defer && s + NST - 1 < total) P3_ISSUE_NEXT();
     if (++kk == nk) { kk = 0; ++vc; }
-    cb = cb == 2 ? 0 : cb + 1;
+    cb = cb == NST - 1 ? 0 : cb + 1;
   }
 #undef P3_TILE
+}
+
+// p4 main loop (256x256 tiles, 8 waves as 2x4 of 128x64, 2 ring stages of 64 KiB), software-pipelined ACROSS
+// K-steps: one barrier per K-step, placed between its two 32-deep k-slices.
+//   phase A (step s): read the k-slice-1 fragments of step s (buffer s % 2) | MFMAs of k-slice 0
+//   wait for stage s + 1, lgkmcnt(0) (k-slice-1 reads done), barrier: buffer s % 2 is dead, stage s + 1 visible
+//   issue stage s + 2 into buffer s % 2
+//   phase B: read the k-slice-0 fragments of step s + 1 (buffer (s + 1) % 2) | MFMAs of k-slice 1
+//   (last K-step of a tile: epilogue)
+// so every fragment read overlaps the MFMAs of the previous k-slice (the barrier no longer separates the reads
+// of a K-step from its MFMAs), and a stage is in flight from the middle of step s - 1 to the middle of step s.
+// p4 LDS-DMA staging: one per-lane byte offset per operand (the lane's row/column within the piece pattern of
+// its wave, plus the tile origin; recomputed at every tile), the piece j's offset added next to its issue (the
+// PStage voff[] array of p3 held 4 VGPRs per operand across the loop: spilled beside the 128x64 accumulators,
+// its reloads then waited on vmcnt in the middle of the DMA issue).
+template <int R, bool KSTRIDED>
+struct P4Stage {
+  static constexpr int NI = R * BK * 2 / (P_THREADS * 16);
+  uint32_t vlane;
+  uint32_t jstep;   // bytes between piece j and j + 1 (wave-uniform)
+  ASRX_DEV void set_tile(int r0, int64_t ld) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int o = w * 1024 + l * 16;   // piece 0
+    if constexpr (!KSTRIDED) {
+      const int r = o >> 7, c = ((o >> 4) & 7) ^ ((r >> 1) & 7);   // (r >> 1) & 7 is the same for every piece j
+      vlane = (uint32_t)(((int64_t)(r0 + r) * ld + c * 8) * 2);
+      jstep = (uint32_t)(64 * ld * 2);                             // piece j: rows + 64 j
+    } else {
+      constexpr int RB = R * 2;
+      const int kr = o / RB, c16 = (o % RB) >> 4;
+      const int c32 = (c16 >> 1) ^ ks_swz<128>(kr);                // ks_swz of kr + 16 j == ks_swz of kr
+      vlane = (uint32_t)(((int64_t)kr * ld + r0 + c32 * 16 + (c16 & 1) * 8) * 2);
+      jstep = (uint32_t)(8192 / RB * ld * 2);                      // piece j: k-rows + 8192 j / RB
+    }
+    jstep = __builtin_amdgcn_readfirstlane(jstep);
+  }
+  ASRX_DEV v4i_t srd(const bf16_t* base, int64_t ld, int64_t total_bytes, int k0) const {
+    const int64_t koff = KSTRIDED ? (int64_t)k0 * ld * 2 : (int64_t)k0 * 2;
+    return make_srd((const char*)base + koff, total_bytes - koff);
+  }
+  ASRX_DEV void issue(unsigned char* img, v4i_t d) {
+#pragma unroll
+    for (int j = 0; j < NI; ++j) issue_piece(img, d, j);
+  }
+  ASRX_DEV void issue_piece(unsigned char* img, v4i_t d, int j) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const int w = threadIdx.x >> 6;
+    uint32_t v = vlane;
+    asm volatile("" : "+v"(v));   // keep the per-piece sum next to its issue
+    dma16_asm(img + (j * 8 + w) * 1024, d, v + j * jstep);
+#endif
+  }
+};
+
+// p4 fragment read: as p_frag, but the k-strided image's 32-byte-chunk XOR is taken as a per-lane byte offset S
+// (ks_swz<128> of the lane's k-rows: the same for both k-row halves and both k-slices), so a fragment's address
+// is base + ((j * 32) ^ S) computed next to its read.  S is re-laundered at every phase (p4_body), which keeps
+// the compiler from hoisting 8 x 4 such addresses out of the K loop (they spilled the k-strided instantiations).
+ASRX_DEV uint32_t p4_swz_bytes() {
+  const int l = threadIdx.x & 63;
+  return (uint32_t)(ks_swz<128>(8 * (l >> 4) + ((l & 15) >> 2)) * 32);
+}
+template <int R, bool KSTRIDED>
+ASRX_DEV s8_t p4_frag(const unsigned char* img, int i0, int ks, uint32_t S) {
+  if constexpr (!KSTRIDED) {
+    return p_frag<R, false>(img, i0, ks);
+  } else {
+    const int l = threadIdx.x & 63, g = l >> 4, i = l & 15, q = i >> 2, p = i & 3;
+    const int k1 = ks * 32 + 8 * g + q;
+    // (i0 >> 4) * 32 ^ S == (i0 & ~255) * 2 + (((i0 & 255) * 2) ^ S): the row block's window, then the XOR
+    const unsigned char* a1 = img + k1 * R * 2 + 8 * p + (i0 & ~127) * 2 + (((uint32_t)(i0 & 127) * 2) ^ S);
+    const unsigned char* a2 = a1 + 4 * R * 2;
+    s4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4_t*)a1);
+    s4_t v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4_t*)a2);
+    return s8_t{v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
+  }
+}
+
+template <bool AT, bool BT, int EPI, int BN>
+ASRX_DEV void p4_body(const GemmArgs& g, const TileSeq tl, int split, int z, unsigned char* lds) {
+  using G_ = PGeo<BN>;
+  constexpr int TM = G_::TM, TN = G_::TN, NST = G_::NST, STAGE = G_::STAGE, INST = G_::INST;
+  const int ntn = (g.N + BN - 1) / BN;
+  const int zo = z / g.batch_inner, zi = z % g.batch_inner;
+  const bf16_t* A = (const bf16_t*)g.a + zo * g.sa_o + zi * g.sa_i;
+  const bf16_t* B = (const bf16_t*)g.b + zo * g.sb_o + zi * g.sb_i;
+  const int64_t a_bytes = AT ? ((int64_t)(g.K - 1) * g.lda + g.M) * 2 : ((int64_t)(g.M - 1) * g.lda + g.K) * 2;
+  const int64_t b_bytes = BT ? ((int64_t)(g.K - 1) * g.ldb + g.N) * 2 : ((int64_t)(g.N - 1) * g.ldb + g.K) * 2;
+  const int kbeg = split * g.k_per_split;
+  const int kend = min(g.K, kbeg + g.k_per_split);
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  if (nk == 0 || tl.count == 0) return;
+  const int total = tl.count * nk;
+  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int wm = BN == 256 ? (wave >> 2) * 128 : (wave >> 1) * 64;
+  const int wn = BN == 256 ? (wave & 3) * 64 : (wave & 1) * 64;
+  const bool noload = (g.dbg & 8) != 0;
+
+  P4Stage<P_BM, AT> sa;
+  P4Stage<BN, BT> sb;
+  int iv = 0, ik = 0, ib = 0;   // issue cursor
+#define P4_ISSUE_NEXT()                                                      \
+  do {                                                                       \
+    if (ik == 0) {                                                           \
+      const int pt_ = tl(iv);                                                \
+      sa.set_tile((pt_ / ntn) * P_BM, g.lda);                                \
+      sb.set_tile((pt_ % ntn) * BN, g.ldb);                                  \
+    }                                                                        \
+    if (!noload) {                                                           \
+      unsigned char* img_ = lds + ib * STAGE;                                \
+      sa.issue(img_, sa.srd(A, g.lda, a_bytes, kbeg + ik * BK));             \
+      sb.issue(img_ + PA_BYTES, sb.srd(B, g.ldb, b_bytes, kbeg + ik * BK));  \
+    }                                                                        \
+    if (++ik == nk) { ik = 0; ++iv; }                                        \
+    ib = ib == NST - 1 ? 0 : ib + 1;                                         \
+  } while (0)
+
+  // Keep the rolling order in the schedule (the compiler otherwise hoists every read of a phase in front of its
+  // MFMAs: both fragment sets live at once, which spilled the k-strided instantiations into scratch, whose
+  // reloads then drained the LDS-DMA ring through vmcnt): the B-fragment reads, then per A row fragment its 4
+  // MFMAs followed by that fragment's read for the next k-slice.
+#define P4_ROLL_ORDER()                                                                       \
+  do {                                                                                        \
+    __builtin_amdgcn_sched_group_barrier(0x100, TN * (BT ? 2 : 1), 0);                        \
+    _Pragma("unroll") for (int j_ = 0; j_ < TM; ++j_) {                                       \
+      __builtin_amdgcn_sched_group_barrier(0x008, TN, 0);                                     \
+      __builtin_amdgcn_sched_group_barrier(0x100, AT ? 2 : 1, 0);                             \
+    }                                                                                         \
+  } while (0)
+  f4_t acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+  float rs[TM];
+#pragma unroll
+  for (int j = 0; j < TM; ++j) rs[j] = 0.f;
+
+  constexpr bool use_lb = (EPI & E_BIAS) != 0;
+  if constexpr (use_lb) {
+    float* lb = (float*)(lds + NST * STAGE);
+    for (int c = threadIdx.x * 4; c < g.N; c += P_THREADS * 4) *(f4_t*)(lb + c) = *(const f4_t*)(g.bias + c);
+    __syncthreads();
+  }
+  constexpr bool PRE = EpiPre<EPI, TN, TM>::ANY;
+  // prologue: stages 0 .. NST - 1 (stage s + NST is issued in the middle of step s), wait for stage 0
+  P4_ISSUE_NEXT();
+  if (total > 1) P4_ISSUE_NEXT();
+  if (NST == 3 && total > 2) P4_ISSUE_NEXT();
+  if (noload) wait_vmcnt<0>();
+  else wait_stages<INST, NST - 1>(min(total, NST) - 1);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  uint32_t S = p4_swz_bytes();
+  s8_t fa0[TM], fb0[TN], fa1[TM], fb1[TN];
+#pragma unroll
+  for (int j = 0; j < TM; ++j) fa0[j] = p4_frag<P_BM, AT>(lds, wm + 16 * j, 0, S);
+#pragma unroll
+  for (int i = 0; i < TN; ++i) fb0[i] = p4_frag<BN, BT>(lds + PA_BYTES, wn + 16 * i, 0, S);
+
+  // younger-operation ledger for the mid-step wait of step s (stage s + 1; lower bounds, an under-count only
+  // over-waits): e1 = stores of step s - 1's epilogue younger than stage s + 1 (NST = 2: those issued after stage
+  // s + 1, i.e. not deferred; NST = 3: all of them), e2 = stores of step s - 2's epilogue (NST = 3), and for NST = 3
+  // stage s + 2 (issued in the middle of step s - 1, or in the prologue)
+  int e1 = 0, e2 = 0;
+  int vc = 0, kk = 0, cb = 0;   // compute cursor
+  for (int s = 0; s < total; ++s) {
+    const unsigned char* la = lds + cb * STAGE;
+    const int t = tl(vc);
+    const bool last = kk == nk - 1;
+    const bool do_rs = AT && g.rowsum != nullptr && (t % ntn) == 0 && wn == 0;
+    asm volatile("" : "+v"(S));
+    // ---- phase A: k-slice 0 MFMAs, row fragment j's k-slice-1 read issued right after its last use (the
+    // fragments roll through one register set: ~32 VGPRs of A fragments live, not 64)
+#pragma unroll
+    for (int i = 0; i < TN; ++i) fb1[i] = p4_frag<BN, BT>(la + PA_BYTES, wn + 16 * i, 1, S);
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+#pragma unroll
+      for (int i = 0; i < TN; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[i], fa0[j], acc[i][j], 0, 0, 0);
+      if constexpr (AT) {
+        if (do_rs) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) rs[j] += bf2f((bf16_t)fa0[j][e]);
+        }
+      }
+      fa1[j] = p4_frag<P_BM, AT>(la, wm + 16 * j, 1, S);
+    }
+    P4_ROLL_ORDER();
+    // ---- mid-step barrier: stage s + 1 landed and visible; buffer cb dead
+    if (s + 1 < total) {
+      if (noload) wait_vmcnt_rt(e1 + e2);
+      else wait_vmcnt_rt(e1 + e2 + (NST == 3 && s + 2 < total ? INST : 0));
+    }
+    e2 = NST == 3 ? e1 : 0;
+    e1 = 0;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const bool defer = PRE && last && g.splitk == 1 && !(g.dbg & 1);
+    EpiPre<EPI, TN, TM> pre;
+    if constexpr (PRE) {
+      if (defer) epi_prefetch<EPI, TN, TM>(pre, g, (t / ntn) * P_BM, (t % ntn) * BN, wm, wn);
+    }
+    if (!defer && s + NST < total) P4_ISSUE_NEXT();
+    // ---- phase B: k-slice 1 MFMAs | the next step's k-slice-0 reads (buffer cb + 1), rolling as in phase A
+    // (issuing the stage's LDS-DMA pieces one or two at a time between phase B's MFMA groups instead measured
+    //  no faster with loads and slower without)
+    const unsigned char* ln = lds + (cb == NST - 1 ? 0 : cb + 1) * STAGE;
+    asm volatile("" : "+v"(S));
+    const bool more = s + 1 < total;
+    if (more) {
+#pragma unroll
+      for (int i = 0; i < TN; ++i) fb0[i] = p4_frag<BN, BT>(ln + PA_BYTES, wn + 16 * i, 0, S);
+    }
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+#pragma unroll
+      for (int i = 0; i < TN; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[i], fa1[j], acc[i][j], 0, 0, 0);
+      if constexpr (AT) {
+        if (do_rs) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) rs[j] += bf2f((bf16_t)fa1[j][e]);
+        }
+      }
+      if (more) fa0[j] = p4_frag<P_BM, AT>(ln, wm + 16 * j, 0, S);
+    }
+    P4_ROLL_ORDER();
+    if (last) {
+      const int m0 = (t / ntn) * P_BM, n0 = (t % ntn) * BN;
+      if constexpr (AT) {
+        if (do_rs) {
+#pragma unroll
+          for (int j = 0; j < TM; ++j) {
+            float v = rs[j];
+            v += __shfl_xor(v, 16, 64);
+            v += __shfl_xor(v, 32, 64);
+            const int m = m0 + wm + 16 * j + l;
+            if (l < 16 && m < g.M) {
+              if (g.splitk > 1) g.rowsum_ws[(int64_t)split * g.M + m] = v;
+              else g.rowsum[m] += v;
+            }
+            rs[j] = 0.f;
+          }
+        }
+      }
+      if (g.splitk > 1) {
+        const int gq = l >> 4;
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int j = 0; j < TM; ++j) {
+            float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+            store_partial4(g, split, m0 + wm + 16 * j + (l & 15), n0 + wn + 16 * i + 4 * gq, v);
+          }
+      } else if (g.dbg & 1) {
+        keep_live(acc);
+      } else {
+        const int full = m0 + P_BM <= g.M && n0 + BN <= g.N;
+        lds_cfloat_t* lbias = (lds_cfloat_t*)(lds + NST * STAGE) + n0;
+        if (defer) {
+          const int e = epilogue_tile<EPI, TN, TM, use_lb, PRE>(g, z, m0, n0, wm, wn, acc, lbias, full, &pre);
+          if (NST == 3) e1 = e;   // (NST = 2: the deferred stage is issued after these stores)
+        } else {
+          e1 = epilogue_tile<EPI, TN, TM, use_lb>(g, z, m0, n0, wm, wn, acc, lbias, full);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+    }
+    if (defer && s + NST < total) P4_ISSUE_NEXT();
+    if (++kk == nk) { kk = 0; ++vc; }
+    cb = cb == NST - 1 ? 0 : cb + 1;
+  }
+#undef P4_ISSUE_NEXT
+#undef P4_ROLL_ORDER
 }
 
 template <bool AT, bool BT, int EPI>
 __global__ __launch_bounds__(512) void gemm_bf16_p3_kernel(GemmArgs g, int ntiles, int xcd) {
   g.seed = seed_eff(g.seed);
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[3 * P_STAGE + P_BIAS_BYTES];
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[PGeo<128>::LDS];
   const int G = gridDim.x, b0 = blockIdx.x;
   if (b0 >= ntiles) return;
-  p3_body<AT, BT, EPI>(g, TileSeq::persistent(ntiles, xcd, b0, G), blockIdx.y, blockIdx.z, lds);
+  if (g.dbg & 16) p4_body<AT, BT, EPI, 128>(g, TileSeq::persistent(ntiles, xcd, b0, G), blockIdx.y, blockIdx.z, lds);
+  else p3_body<AT, BT, EPI, 128>(g, TileSeq::persistent(ntiles, xcd, b0, G), blockIdx.y, blockIdx.z, lds);
 }
 
-// Grouped weight gradients (dW (+)= dY^T X of every layer in one launch) on p3 tiles: one 256x128 tile per
+template <bool AT, bool BT, int EPI>
+__global__ __launch_bounds__(512) void gemm_bf16_p4_kernel(GemmArgs g, int ntiles, int xcd) {
+  g.seed = seed_eff(g.seed);
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[PGeo<256>::LDS];
+  const int G = gridDim.x, b0 = blockIdx.x;
+  if (b0 >= ntiles) return;
+  p4_body<AT, BT, EPI, 256>(g, TileSeq::persistent(ntiles, xcd, b0, G), blockIdx.y, blockIdx.z, lds);
+}
+
+// Grouped weight gradients (dW (+)= dY^T X of every layer in one launch) on p3 / p4 tiles: one tile per
 // workgroup, block -> tile through block_tile (XCD-aware host layout) and tile -> group through tile_group.
+// rocprofv3 names: the p3 grouped launch keeps its round-1 name
 template <int EPI>
 __global__ __launch_bounds__(512) void gemm_bf16_p3g_kernel(float alpha, float beta, int c_dtype,
                                                             const GroupEnt* __restrict__ ents,
                                                             const uint16_t* __restrict__ tile_group,
-                                                            const uint16_t* __restrict__ block_tile, int ntiles) {
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[3 * P_STAGE + P_BIAS_BYTES];
+                                                            const uint16_t* __restrict__ block_tile, int ntiles,
+                                                            int dbg) {
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[PGeo<128>::LDS];
   const int tid = block_tile ? (int)block_tile[blockIdx.x] : (int)blockIdx.x;
   if (tid >= ntiles) return;
   const int gi = __builtin_amdgcn_readfirstlane((int)tile_group[tid]);
@@ -544,38 +864,93 @@ __global__ __launch_bounds__(512) void gemm_bf16_p3g_kernel(float alpha, float b
   g.batch_inner = 1; g.alpha = alpha; g.beta = beta; g.rowadd_mod = 1;
   g.splitk = 1; g.k_per_split = e.k; g.cvec = 1;
   g.rowsum = e.rowsum;
-  p3_body<true, true, EPI>(g, TileSeq::single(tid - e.tile_start), 0, 0, lds);
+  g.dbg = dbg & 9;
+  if (dbg & 16) p4_body<true, true, EPI, 128>(g, TileSeq::single(tid - e.tile_start), 0, 0, lds);
+  else p3_body<true, true, EPI, 128>(g, TileSeq::single(tid - e.tile_start), 0, 0, lds);
+}
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_bf16_p4g_kernel(float alpha, float beta, int c_dtype,
+                                                            const GroupEnt* __restrict__ ents,
+                                                            const uint16_t* __restrict__ tile_group,
+                                                            const uint16_t* __restrict__ block_tile, int ntiles,
+                                                            int dbg) {
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[PGeo<256>::LDS];
+  const int tid = block_tile ? (int)block_tile[blockIdx.x] : (int)blockIdx.x;
+  if (tid >= ntiles) return;
+  const int gi = __builtin_amdgcn_readfirstlane((int)tile_group[tid]);
+  const GroupEnt e = ents[gi];
+  GemmArgs g = {};
+  g.M = e.m; g.N = e.n; g.K = e.k;
+  g.a = e.a; g.lda = e.lda; g.b = e.b; g.ldb = e.ldb; g.c = e.c; g.ldc = e.ldc; g.c_dtype = c_dtype;
+  g.batch_inner = 1; g.alpha = alpha; g.beta = beta; g.rowadd_mod = 1;
+  g.splitk = 1; g.k_per_split = e.k; g.cvec = 1;
+  g.rowsum = e.rowsum;
+  g.dbg = dbg & 9;
+  p4_body<true, true, EPI, 256>(g, TileSeq::single(tid - e.tile_start), 0, 0, lds);
 }
 
 int launch_p3_grouped(const asrx_gemm_desc* common, const GroupEnt* ents, const uint16_t* tile_group,
-                      const uint16_t* block_tile, int ntiles, int blocks, hipStream_t st) {
+                      const uint16_t* block_tile, int ntiles, int blocks, bool p4, hipStream_t st) {
   if (common->c_dtype != ASRX_F32 || common->alpha != 1.f) return -1;
-  if (common->beta == 1.f)
-    hipLaunchKernelGGL((gemm_bf16_p3g_kernel<E_BETA | E_F32>), dim3(blocks), dim3(P_THREADS), 0, st, common->alpha,
-                       common->beta, common->c_dtype, ents, tile_group, block_tile, ntiles);
-  else if (common->beta == 0.f)
-    hipLaunchKernelGGL((gemm_bf16_p3g_kernel<E_F32>), dim3(blocks), dim3(P_THREADS), 0, st, common->alpha,
-                       common->beta, common->c_dtype, ents, tile_group, block_tile, ntiles);
-  else
-    return -1;
+  if (common->beta != 1.f && common->beta != 0.f) return -1;
+#define ASRX_G(KER, E) hipLaunchKernelGGL((KER<E>), dim3(blocks), dim3(P_THREADS), 0, st, common->alpha, common->beta, \
+                                          common->c_dtype, ents, tile_group, block_tile, ntiles, gemm_dbg())
+  if (p4) {
+    if (common->beta == 1.f) ASRX_G(gemm_bf16_p4g_kernel, E_BETA | E_F32);
+    else ASRX_G(gemm_bf16_p4g_kernel, E_F32);
+  } else {
+    if (common->beta == 1.f) ASRX_G(gemm_bf16_p3g_kernel, E_BETA | E_F32);
+    else ASRX_G(gemm_bf16_p3g_kernel, E_F32);
+  }
+#undef ASRX_G
   return 0;
 }
 
-template <bool AT, bool BT, int EPI>
+template <bool AT, bool BT, int EPI, bool P4>
 void launch_p3(const GemmArgs& g, int ntiles, int splitk, int batch, hipStream_t st) {
   const int per = splitk * batch;
   const int gx = std::max(1, std::min(ntiles, std::max(1, 256 / per)));
   // XCD-contiguous tile order: measured 1-7% faster on the c3 shapes (ASRX_P3_XCD=0: round-robin, A/B)
   static const int xcd = [] { const char* e = getenv("ASRX_P3_XCD"); return e ? atoi(e) : 1; }();
-  hipLaunchKernelGGL((gemm_bf16_p3_kernel<AT, BT, EPI>), dim3(gx, splitk, batch), dim3(P_THREADS), 0, st, g, ntiles,
-                     xcd);
+  if constexpr (P4)
+    hipLaunchKernelGGL((gemm_bf16_p4_kernel<AT, BT, EPI>), dim3(gx, splitk, batch), dim3(P_THREADS), 0, st, g, ntiles,
+                       xcd);
+  else
+    hipLaunchKernelGGL((gemm_bf16_p3_kernel<AT, BT, EPI>), dim3(gx, splitk, batch), dim3(P_THREADS), 0, st, g,
+                       ntiles, xcd);
 }
 
-template <bool AT, bool BT>
+// p4 (256x256 tiles) instantiations: the epilogues of the wide projection GEMMs it is planned for (the
+// residual epilogues of the N = 512 GEMMs, whose prefetched operands would not fit the registers beside the
+// 128x64 accumulator tile, stay on p3)
+#define ASRX_EPI4_NT(X) X(E_BIAS) X(E_BIAS | E_RELU) X(E_BIAS | E_RELU | E_DROP) X(E_F32) X(0) \
+  X(E_BIAS | E_RELU | E_MASKOUT) X(E_BIAS | E_RELU | E_DROP | E_MASKOUT)
+#define ASRX_EPI4_NN(X) X(0) X(E_F32) X(E_GBITS) X(E_GBITS | E_ALPHA)
+#define ASRX_EPI4_TT(X) X(E_BETA | E_F32) X(E_F32)
+
+bool p4_instantiated(bool at, bool bt, int epi) {
+#define ASRX_HAS(E) if (epi == (E)) return true;
+  if (!at && !bt) { ASRX_EPI4_NT(ASRX_HAS) }
+  else if (!at && bt) { ASRX_EPI4_NN(ASRX_HAS) }
+  else if (at && bt) { ASRX_EPI4_TT(ASRX_HAS) }
+#undef ASRX_HAS
+  return false;
+}
+
+template <bool AT, bool BT, bool P4 = false>
 void dispatch_p3(const GemmArgs& g, int epi, int ntiles, int splitk, int batch, hipStream_t st) {
 #define ASRX_CASE(E) \
-  case (E): launch_p3<AT, BT, (E)>(g, ntiles, splitk, batch, st); return;
-  if constexpr (!AT && !BT) {
+  case (E): launch_p3<AT, BT, (E), P4>(g, ntiles, splitk, batch, st); return;
+  if constexpr (P4) {
+    if constexpr (!AT && !BT) {
+      switch (epi) { ASRX_EPI4_NT(ASRX_CASE) default: break; }
+    } else if constexpr (!AT && BT) {
+      switch (epi) { ASRX_EPI4_NN(ASRX_CASE) default: break; }
+    } else if constexpr (AT && BT) {
+      switch (epi) { ASRX_EPI4_TT(ASRX_CASE) default: break; }
+    }
+    return;   // (the planner only picks p4 for an instantiated epilogue)
+  } else if constexpr (!AT && !BT) {
     switch (epi) { ASRX_EPI_NT(ASRX_CASE) default: break; }
   } else if constexpr (!AT && BT) {
     switch (epi) { ASRX_EPI_NN(ASRX_CASE) default: break; }
@@ -583,7 +958,7 @@ void dispatch_p3(const GemmArgs& g, int epi, int ntiles, int splitk, int batch, 
     switch (epi) { ASRX_EPI_TT(ASRX_CASE) default: break; }
   }
 #undef ASRX_CASE
-  launch_p3<AT, BT, E_GENERIC>(g, ntiles, splitk, batch, st);
+  if constexpr (!P4) launch_p3<AT, BT, E_GENERIC, false>(g, ntiles, splitk, batch, st);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1104,7 +1479,7 @@ void dispatch_bf16(const GemmArgs& g, bool at, bool bt, bool vec, int batch, hip
 // ------------------------------------------------------------------------------------------------
 // Kernel selection (shared by asrx_gemm and asrx_gemm_kernel_name so profiling can name the launch).
 struct GemmPlan {
-  int use;     // 1 = p3 (256x128 LDS-DMA ring), 3 = register path 128, 4 = register path 64,
+  int use;     // 1 = p3 (256x128 LDS-DMA ring), 2 = p4 (256x256), 3 = register path 128, 4 = register path 64,
                // 5 = ring 64x64, 6 = ring 128x64 (4-stage LDS-DMA, small grids), 9 = tall-K (conv2 dW)
   bool vec;    // 16-byte aligned operands
   int epi;     // instantiated epilogue flags (E_GENERIC when the fast-path set has no match)
@@ -1129,14 +1504,17 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
     const long t128 = (long)((d->m + 127) / 128) * ((d->n + 127) / 128) * batch * splitk;
     tile = t128 >= 400 ? 128 : 64;
   }
-  const int kvar = d->kernel == 1 ? 1 : d->kernel == 3 ? 3 : d->kernel == 4 ? 4 : d->kernel == 5 ? 5 : 0;
+  const int kvar = d->kernel == 1 ? 1 : d->kernel == 3 ? 3 : d->kernel == 4 ? 4 : d->kernel == 5 ? 5 :
+                   d->kernel == 6 ? 6 : 0;
   const bool dma_ok = pl.vec && d->k % BK == 0 && (!d->a_trans || d->m % 8 == 0) && (!d->b_trans || d->n % 8 == 0) &&
                       d->m >= 8 && d->n >= 8;
   const int nt_p3 = ((d->m + P_BM - 1) / P_BM) * ((d->n + P_BN - 1) / P_BN);
+  const int nt_p4 = ((d->m + P_BM - 1) / P_BM) * ((d->n + 255) / 256);
   pl.use = tile == 128 ? 3 : 4;
   const int nt_r128 = ((d->m + 127) / 128) * ((d->n + 63) / 64);
   if (dma_ok) {
     if (kvar == 1) pl.use = 1;
+    else if (kvar == 6) pl.use = 2;
     else if (kvar == 4 && !d->a_trans) pl.use = 5;
     else if (kvar == 5 && !d->a_trans) pl.use = 6;
     // auto (measured on the c3 shapes, tools/gemm_bench.py): the p3 ring wins every projection with K <= 4096
@@ -1144,7 +1522,12 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
     // register path wins the weight-gradient (A^T, reduction over B*T rows) and very long-K GEMMs.
     // (with the inline-asm LDS-DMA, p3 also wins the long-K cross-attention K/V data gradient, K = 12 288)
     else if (kvar == 0 && !d->a_trans) {
-      if (nt_p3 * splitk * batch >= 192) pl.use = 1;
+      // wide outputs whose 256x256 tiles still fill the chip (>= 1.25 tiles per CU; the c3 FFN1 forward, the gated
+      // FFN2 data gradient, the Q/K/V and cross K/V projections) take p4: half the operand ingest per FLOP
+      // (tools/blas_ref.py: FFN1 forward 47 -> 39 us, FFN2 data gradient 52 -> 41 us); the N = 512 outputs (126
+      // such tiles) stay on p3
+      if (nt_p4 * splitk * batch >= 320 && splitk == 1 && batch == 1) pl.use = 2;
+      else if (nt_p3 * splitk * batch >= 192) pl.use = 1;
       // (64x64 tiles also win the long-K decoder GEMMs, K >= 1536: 4 x more workgroups to cover the latency)
       else pl.use = (nt_r128 * splitk * batch >= 192 && d->k < 1536) ? 6 : 5;
     }
@@ -1156,6 +1539,7 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
     pl.use = 9;
   if (pl.use == 9) pl.ntiles = splitk;
   else if (pl.use == 1) pl.ntiles = nt_p3;
+  else if (pl.use == 2) pl.ntiles = nt_p4;
   else if (pl.use == 5) pl.ntiles = ((d->m + 63) / 64) * ((d->n + 63) / 64);
   else if (pl.use == 6) pl.ntiles = nt_r128;
   else pl.ntiles = ((d->m + tile - 1) / tile) * ((d->n + tile - 1) / tile);
@@ -1176,14 +1560,23 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
           (d->resid ? E_RESID : 0) | (d->beta == 1.f ? E_BETA : 0) |
           (d->c_dtype == ASRX_F32 ? E_F32 : 0) | (d->alpha != 1.f ? E_ALPHA : 0) | (d->rowadd ? E_ROWADD : 0);
   }
-  pl.epi = ((pl.use == 1 || pl.use == 5 || pl.use == 6) && epi_instantiated(d->a_trans, d->b_trans, epi))
+  pl.epi = ((pl.use == 1 || pl.use == 2 || pl.use == 5 || pl.use == 6) && epi_instantiated(d->a_trans, d->b_trans, epi))
                ? epi : E_GENERIC;
+  if (pl.use == 2 && (splitk != 1 || batch != 1 || !p4_instantiated(d->a_trans, d->b_trans, pl.epi))) {
+    pl.use = 1;   // p4 takes single, unsplit GEMMs with its instantiated epilogues; the rest stays on p3
+    pl.ntiles = nt_p3;
+  }
   return pl;
 }
 
 }  // namespace
 
 ASRX_SEED_OFFSET_SETTER(gemm)
+
+extern "C" int asrx_gemm_set_debug(int32_t flags) {
+  g_gemm_dbg = flags < 0 ? 0 : flags;
+  return ASRX_OK;
+}
 
 extern "C" int asrx_gemm_kernel_name(const asrx_gemm_desc* d, char* buf, int len) {
   if (!d || !buf || len < 8) return ASRX_ERR_ARG;
@@ -1197,8 +1590,9 @@ extern "C" int asrx_gemm_kernel_name(const asrx_gemm_desc* d, char* buf, int len
   const GemmPlan pl = plan_bf16(d, batch, splitk);
   if (pl.use == 9)
     snprintf(buf, len, "gemm_bf16_tallk_kernel");
-  else if (pl.use == 1)
-    snprintf(buf, len, "gemm_bf16_p3_kernel<%s, %s, %d>", tf[!!d->a_trans], tf[!!d->b_trans], pl.epi);
+  else if (pl.use == 1 || pl.use == 2)
+    snprintf(buf, len, "gemm_bf16_p%d_kernel<%s, %s, %d>", pl.use == 2 ? 4 : 3, tf[!!d->a_trans], tf[!!d->b_trans],
+             pl.epi);
   else if (pl.use >= 5)
     snprintf(buf, len, "gemm_bf16_ring_kernel<%d, 64, %s, %s, %d>", pl.use == 6 ? 128 : 64, tf[!!d->a_trans],
              tf[!!d->b_trans], pl.epi);
@@ -1244,8 +1638,7 @@ extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
   g.ws = d->workspace;
   g.rowsum = d->rowsum_a;
   g.rowsum_ws = d->rowsum_ws;
-  static const int dbg_env = [] { const char* e = getenv("ASRX_GEMM_DBG"); return e ? atoi(e) : 0; }();
-  g.dbg = dbg_env;
+  g.dbg = gemm_dbg();
   if (g.rowsum && (!d->a_trans || d->in_dtype != ASRX_BF16 || batch != 1)) return ASRX_ERR_UNSUPPORTED;
   if (g.rowsum && splitk > 1 && !g.rowsum_ws) return ASRX_ERR_ARG;
   const int esz = d->c_dtype == ASRX_F32 ? 16 : 8;
@@ -1261,7 +1654,7 @@ extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
                         d->ldc % 8 != 0 || (uintptr_t)d->c % 16 != 0 || (uintptr_t)d->mask_out % 4 != 0 ||
                         d->ld_mask < d->n / 32))
       return ASRX_ERR_UNSUPPORTED;
-    if (pl.use == 1 && (epi & E_BIAS) && epi != E_GENERIC && d->n > P_BIAS_BYTES / 4) {
+    if ((pl.use == 1 || pl.use == 2) && (epi & E_BIAS) && epi != E_GENERIC && d->n > P_BIAS_BYTES / 4) {
       // the p3 bias epilogue stages the whole bias vector in LDS (16 KiB): wider outputs run as column chunks
       // (fast-path epilogues without dropout only: their element math does not depend on N)
       if ((epi & E_DROP) || d->a_trans || d->b_trans || batch != 1 || splitk != 1) return ASRX_ERR_UNSUPPORTED;
@@ -1276,11 +1669,18 @@ extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
         if (gc.gate) gc.gate = d->gate_dtype == ASRX_BITS ? (const void*)((const uint32_t*)d->gate + c0 / 32)
                                                           : (const void*)((const bf16_t*)d->gate + c0);
         if (gc.mask_out) gc.mask_out = d->mask_out + c0 / 32;
-        const int nt = ((d->m + P_BM - 1) / P_BM) * ((gc.N + P_BN - 1) / P_BN);
-        dispatch_p3<false, false>(gc, epi, nt, 1, 1, st);
+        const int bn = pl.use == 2 ? 256 : P_BN;
+        const int nt = ((d->m + P_BM - 1) / P_BM) * ((gc.N + bn - 1) / bn);
+        if (pl.use == 2) dispatch_p3<false, false, true>(gc, epi, nt, 1, 1, st);
+        else dispatch_p3<false, false>(gc, epi, nt, 1, 1, st);
       }
     } else if (pl.use == 9) {
       hipLaunchKernelGGL(gemm_bf16_tallk_kernel, dim3(splitk), dim3(512), 0, st, g, TallkConv{0, 0, 0, 0, 0, 0});
+    } else if (pl.use == 2) {
+      if (!d->a_trans && !d->b_trans) dispatch_p3<false, false, true>(g, epi, pl.ntiles, splitk, batch, st);
+      else if (!d->a_trans && d->b_trans) dispatch_p3<false, true, true>(g, epi, pl.ntiles, splitk, batch, st);
+      else if (d->a_trans && !d->b_trans) dispatch_p3<true, false, true>(g, epi, pl.ntiles, splitk, batch, st);
+      else dispatch_p3<true, true, true>(g, epi, pl.ntiles, splitk, batch, st);
     } else if (pl.use == 1) {
       if (!d->a_trans && !d->b_trans) dispatch_p3<false, false>(g, epi, pl.ntiles, splitk, batch, st);
       else if (!d->a_trans && d->b_trans) dispatch_p3<false, true>(g, epi, pl.ntiles, splitk, batch, st);
@@ -1340,8 +1740,9 @@ extern "C" int asrx_gemm_grouped_xcd(const asrx_gemm_desc* common, const asrx_ge
   if (tiles == 0 || blocks == 0) return ASRX_OK;
   if (common->in_dtype != ASRX_BF16 || !common->a_trans || !common->b_trans) return ASRX_ERR_UNSUPPORTED;
   if (common->c_dtype != ASRX_BF16 && common->c_dtype != ASRX_F32) return ASRX_ERR_ARG;
-  if (common->tile == 3) {     // p3 LDS-DMA ring tiles, 256x128 (fp32 C, 16-B rows, n % 4 == 0, alpha 1, beta 0|1)
-    if (launch_p3_grouped(common, (const GroupEnt*)groups, tile_group, block_tile, tiles, blocks,
+  if (common->tile == 3 || common->tile == 4) {   // p3 / p4 LDS-DMA ring tiles, 256x128 / 256x256 (fp32 C, 16-B
+                                                  // rows, n % 4 == 0, alpha 1, beta 0|1)
+    if (launch_p3_grouped(common, (const GroupEnt*)groups, tile_group, block_tile, tiles, blocks, common->tile == 4,
                           (hipStream_t)stream) != 0)
       return ASRX_ERR_UNSUPPORTED;
   } else if (common->tile == 128) {   // register-staged 128x128 tiles (gemm_bf16_tile): any alignment-checked table

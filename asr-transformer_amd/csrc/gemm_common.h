@@ -145,9 +145,11 @@ enum : int {
 // issued after them.
 template <int EPI, int TN, int TM>
 struct EpiPre {
-  static constexpr bool G = (EPI & (E_GATE | E_GBITS)) != 0, R = (EPI & (E_RESID | E_ROWADD)) != 0;
-  static constexpr bool ANY = (G || R) && EPI != E_GENERIC;
-  uint2 gt[G ? TN : 1][G ? TM : 1];
+  static constexpr bool G = (EPI & E_GATE) != 0, GB = (EPI & E_GBITS) != 0, R = (EPI & (E_RESID | E_ROWADD)) != 0;
+  static constexpr bool ANY = (G || GB || R) && EPI != E_GENERIC;
+  uint2 gt[G ? TN : 1][G ? TM : 1];        // bf16 gate: 4 values
+  uint32_t gw[GB ? (TN + 1) / 2 : 1][GB ? TM : 1];   // bit-mask gate: the word holding the 32 columns of the
+                                                     // fragment pair 2i, 2i + 1 (wn and n0 are 32-aligned)
   f4_t rr[R ? TN : 1][R ? TM : 1];
 };
 
@@ -162,10 +164,12 @@ ASRX_DEV void epi_prefetch(EpiPre<EPI, TN, TM>& p, const GemmArgs& g, int m0, in
       const bool ok = m < g.M && n < g.N;
       if constexpr (EpiPre<EPI, TN, TM>::G) {
         p.gt[i][j] = make_uint2(0u, 0u);
-        if constexpr ((EPI & E_GBITS) != 0) {   // the word holding columns n .. n + 3 (.x; .y unused)
-          if (ok) p.gt[i][j].x = ((const uint32_t*)g.gate)[(int64_t)m * g.ld_gate + (n >> 5)];
-        } else {
-          if (ok) p.gt[i][j] = *(const uint2*)((const bf16_t*)g.gate + (int64_t)m * g.ld_gate + n);
+        if (ok) p.gt[i][j] = *(const uint2*)((const bf16_t*)g.gate + (int64_t)m * g.ld_gate + n);
+      }
+      if constexpr (EpiPre<EPI, TN, TM>::GB) {   // the word holding columns n .. n + 3 (and those of fragment i + 1)
+        if (i % 2 == 0) {
+          p.gw[i / 2][j] = 0u;
+          if (ok) p.gw[i / 2][j] = ((const uint32_t*)g.gate)[(int64_t)m * g.ld_gate + (n >> 5)];
         }
       }
       if constexpr (EpiPre<EPI, TN, TM>::R) {
@@ -238,7 +242,9 @@ ASRX_DEV int epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int
                            lds_cfloat_t* lbias = nullptr, int full = 0,
                            const EpiPre<EPI, TN, TM>* pre = nullptr) {
   // (PRE requires EpiPre<EPI,TN,TM>::ANY; its members are indexed only where they exist)
-#define ASRX_PGT(i, j) (EpiPre<EPI, TN, TM>::G ? pre->gt[EpiPre<EPI, TN, TM>::G ? (i) : 0][EpiPre<EPI, TN, TM>::G ? (j) : 0] : uint2{0u, 0u})
+#define ASRX_PGT(i, j) (EpiPre<EPI, TN, TM>::G ? pre->gt[EpiPre<EPI, TN, TM>::G ? (i) : 0][EpiPre<EPI, TN, TM>::G ? (j) : 0] \
+                       : EpiPre<EPI, TN, TM>::GB ? uint2{pre->gw[EpiPre<EPI, TN, TM>::GB ? (i) / 2 : 0][EpiPre<EPI, TN, TM>::GB ? (j) : 0], 0u} \
+                       : uint2{0u, 0u})
 #define ASRX_PRR(i, j) (EpiPre<EPI, TN, TM>::R ? pre->rr[EpiPre<EPI, TN, TM>::R ? (i) : 0][EpiPre<EPI, TN, TM>::R ? (j) : 0] : f4_t{0.f, 0.f, 0.f, 0.f})
   const int l = threadIdx.x & 63, gq = l >> 4;
   if constexpr (EPI == E_GENERIC) {

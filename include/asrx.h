@@ -79,7 +79,8 @@ typedef struct asrx_gemm_desc {
    * ASRX_ERR_UNSUPPORTED. */
   uint32_t* mask_out; int64_t ld_mask;
   /* kernel family (tests / A-B; 0 = auto): 1 = 256x128 LDS-DMA ring (p3), 3 = register-staged tiles, 4 = 64x64
-   * LDS-DMA ring, 5 = 128x64 LDS-DMA ring — honoured where the family's preconditions hold, else auto. */
+   * LDS-DMA ring, 5 = 128x64 LDS-DMA ring, 6 = 256x256 LDS-DMA ring (p4) — honoured where the family's
+   * preconditions hold, else auto. */
   int32_t kernel;
 } asrx_gemm_desc;
 
@@ -101,7 +102,8 @@ typedef struct asrx_gemm_group_dev {
  * the tile workgroup b computes.  Workgroup b runs on XCD b % 8, so a host that lays the tiles of one group on
  * one XCD at the same time lets them share that XCD's L2 (the operand panels of dW = dY^T X are re-read by
  * every tile of the group).  common->tile selects the tile: 3 = the p3 LDS-DMA ring, 256x128 tiles (m x n;
- * fp32 C with 16-byte aligned rows, every group's n % 4 == 0, alpha 1, beta 0 or 1), 128 = register-staged
+ * fp32 C with 16-byte aligned rows, every group's n % 4 == 0, alpha 1, beta 0 or 1), 4 = the p4 ring, 256x256
+ * tiles (same conditions), 128 = register-staged
  * 128x128 tiles (any alignment-checked table; common->relu carries its "every C row 16-byte aligned" flag).
  * Replaces the weight/bias-gradient mm + sum of autograd for every nn.Linear (layers.py:10-12,36,48,51). */
 int asrx_gemm_grouped_xcd(const asrx_gemm_desc* common, const asrx_gemm_group_dev* groups,
@@ -112,6 +114,11 @@ int asrx_gemm_grouped_xcd(const asrx_gemm_desc* common, const asrx_gemm_group_de
  * namespace/argument list), e.g. "gemm_bf16_p3_kernel<false, false, 1>".  Host-only: no launch, no GPU
  * needed.  Used by bench.py to time exactly the kernel the roofline names. */
 int asrx_gemm_kernel_name(const asrx_gemm_desc* d, char* buf, int32_t len);
+
+/* Diagnostics only (tools/, never the product path): process-wide GEMM debug flags, overriding the ASRX_GEMM_DBG
+ * environment variable — 1 = skip the epilogue stores, 4 = issue each LDS-DMA stage in one block, 8 = skip the
+ * operand loads (compute on stale LDS); 0 = normal.  Results are garbage while any flag is set. */
+int asrx_gemm_set_debug(int32_t flags);
 
 /* ---------------------------------------------------------------------------------------------------
  * Fused multi-head attention (bf16 in/out, fp32 softmax): per (batch b, head h)

@@ -35,7 +35,7 @@ def bf(x):
 
 # ------------------------------------------------------------------------------------------------ GEMM
 
-VARIANTS = ["auto", "p3", "reg", "ring", "ring128"]   # kernel families the auto plan can select (gemm.hip plan_bf16)
+VARIANTS = ["auto", "p3", "p4", "reg", "ring", "ring128"]   # kernel families the auto plan can select (gemm.hip plan_bf16)
 
 
 @pytest.fixture
@@ -84,7 +84,7 @@ def test_gemm_epilogue(tile, kernel_variant):
     assert relerr(out.cpu(), ref) < 2e-3
 
 
-@pytest.mark.parametrize("kernel_variant", ["auto", "p3", "ring", "ring128"], indirect=True)
+@pytest.mark.parametrize("kernel_variant", ["auto", "p3", "p4", "ring", "ring128"], indirect=True)
 @pytest.mark.parametrize("m,n,p", [(300, 512, 0.1), (1000, 4160, 0.0), (4096, 2048, 0.1)])
 def test_gemm_relu_mask_bits(m, n, p, kernel_variant):
     """FFN hidden layer: the ReLU/dropout epilogue also writes the 1-bit mask C > 0 (mask_out), and the data
@@ -168,7 +168,8 @@ def test_gemm_fused_rowsum(tile, splitk, kernel_variant):
     assert relerr(bg.cpu(), 2 + dy.double().sum(0)) < 1e-5
 
 
-@pytest.mark.parametrize("wkind,xcd", [("reg", False), ("reg", True), ("p3", False), ("p3", True)])
+@pytest.mark.parametrize("wkind,xcd", [("reg", False), ("reg", True), ("p3", False), ("p3", True), ("p4", False),
+                                       ("p4", True)])
 @pytest.mark.parametrize("ngroups", [1, 7, 60])
 def test_gemm_grouped_wgrad(ngroups, wkind, xcd, monkeypatch):
     """Grouped weight gradients (asrx_gemm_grouped_xcd): ragged shapes, K not a multiple of 64, fused bias-grad

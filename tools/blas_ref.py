@@ -51,33 +51,82 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--variants", default="p3,p4")
+    ap.add_argument("--dbg", default="0", help="comma list of asrx_gemm_set_debug flags to time (diagnostics)")
+    ap.add_argument("--only", default="", help="comma list of shape names")
+    ap.add_argument("--nobias", action="store_true")
+    ap.add_argument("--nogrouped", action="store_true")
+    ap.add_argument("--noblas", action="store_true")
     args = ap.parse_args()
     g = torch.Generator(device="cuda").manual_seed(0)
 
     def rnd(*s):
         return (torch.rand(*s, device="cuda", generator=g) * 2 - 1).bfloat16()
+    variants = args.variants.split(",")
+    dbg = [int(x) for x in args.dbg.split(",")]
+
+    def dbg_runs(res, key, fn, base=0):
+        for f in dbg:
+            K.call("asrx_gemm_set_debug", f | base)
+            res[key + ("" if f == 0 else f"/d{f}")] = timeit(fn, args.reps, args.rounds)
+        K.call("asrx_gemm_set_debug", 0)
+
+    def kb(v):   # "p3+16": kernel family p3 with debug flags 16 (diagnostic A/B variants of one family)
+        k, _, f = v.partition("+")
+        return k, int(f or 0)
     for name, kind, M, N, Kd in SHAPES:
+        if args.only and name not in args.only.split(","):
+            continue
+        res = {}
+        flops = 2.0 * M * N * Kd
         if kind == "fwd":
             x, w = rnd(M, Kd), rnd(N, Kd)
+            bias = torch.randn(N, device="cuda", generator=g)
             y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-            flops = 2.0 * M * N * Kd
-            tb = timeit(lambda: torch.mm(x, w.t(), out=y), args.reps, args.rounds)
-            ta = timeit(lambda: K.linear(x, w, y), args.reps, args.rounds)
+            if not args.noblas:
+                res["hipBLASLt"] = timeit(lambda: torch.mm(x, w.t(), out=y), args.reps, args.rounds)
+            for v in variants:
+                kk, fb = kb(v)
+                dbg_runs(res, v, lambda: K.linear(x, w, y, kernel=kk), fb)
+                if not args.nobias:
+                    K.call("asrx_gemm_set_debug", fb)
+                    res[v + "+bias"] = timeit(lambda: K.linear(x, w, y, bias=bias, kernel=kk), args.reps, args.rounds)
+                    K.call("asrx_gemm_set_debug", 0)
         elif kind == "dgrad":
             dy, w = rnd(M, N), rnd(N, Kd)
             y = torch.empty(M, Kd, device="cuda", dtype=torch.bfloat16)
-            flops = 2.0 * M * N * Kd
-            tb = timeit(lambda: torch.mm(dy, w, out=y), args.reps, args.rounds)
-            ta = timeit(lambda: K.linear_dgrad(dy, w, y), args.reps, args.rounds)
+            res["hipBLASLt"] = timeit(lambda: torch.mm(dy, w, out=y), args.reps, args.rounds)
+            for v in variants:
+                kk, fb = kb(v)
+                dbg_runs(res, v, lambda: K.linear_dgrad(dy, w, y, kernel=kk), fb)
         else:   # wgrad: C[M=N_out, N=K_in] over the Kd rows
             dy, x = rnd(Kd, M), rnd(Kd, N)
-            c32 = torch.zeros(M, N, device="cuda")
             cb = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-            flops = 2.0 * M * N * Kd
-            tb = timeit(lambda: torch.mm(dy.t(), x, out=cb), args.reps, args.rounds)
-            ta = timeit(lambda: K.linear_wgrad_grouped([(dy, x, c32, None)], beta=0.0), args.reps, args.rounds)
-        print(f"{name:11s} M={M:6d} N={N:6d} K={Kd:6d} | hipBLASLt {tb * 1e6:7.1f}us {flops / tb / 1e12:6.0f}TF"
-              f" | asrx {ta * 1e6:7.1f}us {flops / ta / 1e12:6.0f}TF", flush=True)
+            res["hipBLASLt"] = timeit(lambda: torch.mm(dy.t(), x, out=cb), args.reps, args.rounds)
+        line = f"{name:11s} M={M:6d} N={N:6d} K={Kd:6d}"
+        for v, t in res.items():
+            line += f" | {v} {t * 1e6:7.1f}us {flops / t / 1e12:5.0f}TF"
+        print(line, flush=True)
+    if args.nogrouped:
+        return
+    # the step's grouped weight-gradient launch over the 12 encoder layers (distinct buffers per layer)
+    rows, d, ff = 15936, 512, 2048
+    items = []
+    for _ in range(12):
+        xs, xf = rnd(rows, d), rnd(rows, ff)
+        for (n_out, k_in, x) in ((3 * d, d, xs), (d, d, xs), (ff, d, xs), (d, ff, xf)):
+            items.append((rnd(rows, n_out), x, torch.zeros(n_out, k_in, device="cuda"),
+                          torch.zeros(n_out, device="cuda")))
+    flops = sum(2.0 * rows * it[0].shape[1] * it[1].shape[1] for it in items)
+    line = f"grouped wgrad, 12 encoder layers ({flops / 1e12:.3f} TFLOP)"
+    for v in ("p3", "p3+16", "p4"):
+        kk, fb = kb(v)
+        for f in dbg:
+            K.call("asrx_gemm_set_debug", f | fb)
+            t = timeit(lambda: K.linear_wgrad_grouped(items, beta=0.0, kind=kk), 3, args.rounds)
+            line += f" | {v}{'' if f == 0 else f'/d{f}'} {t * 1e6:8.1f}us {flops / t / 1e12:5.0f}TF"
+        K.call("asrx_gemm_set_debug", 0)
+    print(line, flush=True)
 
 
 if __name__ == "__main__":
