@@ -160,8 +160,11 @@ def test_gemm_kernel_plan_names_without_gpu():
             d.bias = 4 << 20
         return d
 
-    assert kernel_name(desc(15936, 1536, 512, bias=True)) == "gemm_bf16_p3_kernel<false, false, 1>"
+    # wide outputs (>= 320 256x256 tiles) take p4, the N = 512 outputs p3
+    assert kernel_name(desc(15936, 1536, 512, bias=True)) == "gemm_bf16_p4_kernel<false, false, 1>"
+    assert kernel_name(desc(15936, 2048, 512, bt=1)) == "gemm_bf16_p4_kernel<false, true, 0>"
     assert kernel_name(desc(15936, 512, 2048, bt=1)) == "gemm_bf16_p3_kernel<false, true, 0>"
+    assert kernel_name(desc(15936, 512, 512, bias=True)) == "gemm_bf16_p3_kernel<false, false, 1>"
     wg = desc(2048, 512, 15936, at=1, bt=1, c_dtype=F32)
     wg.tile = 128                     # as kernels.wgrad_plan sets it
     assert kernel_name(wg) == "gemm_bf16_kernel<128, 128, true, true, true>"
