@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--no-graph", action="store_true", help="eager steps (no HIP graph capture)")
     ap.add_argument("--no-probe", action="store_true")
     ap.add_argument("--no-sub", action="store_true", help="skip the per-kernel sub-rooflines")
+    ap.add_argument("--no-other", action="store_true", help="skip the c2 / c5 forward configs")
     return ap.parse_args()
 
 
@@ -254,6 +255,80 @@ def sub_rooflines(B, T2, d, H, ff, p_drop):
     return out
 
 
+# algorithmic FLOP per input frame of the teacher-forced forward (FlopCounterMode over the reference)
+FWD_MFLOP_PER_FRAME = {"c2": 4.21, "c5": 36.44}
+PEAK_F32_TFLOPS = 157.3   # MI355X fp32 matrix (= vector) peak (MI355X_MICROARCH.md)
+
+
+def other_configs(names=("c2", "c5"), reps=5):
+    """The BASELINE.json forward configs beside the headline step, timed after it: c2 (configs[1]: fp32 forward,
+    B=32, T=512, 6+6 layers d256) against the fp32 matrix peak and c5 (configs[4]: bf16 forward, B=16, T=4000 ->
+    T'=999, the tiled attention path of the long utterances) against the bf16 MFMA peak, as frames/s of the
+    teacher-forced forward (model.eval(), no_grad; HIP events around `reps` forwards after 2 warm-up ones), plus the
+    c5 encoder self-attention forward kernel alone (B*H=128, 999x999, dh=64; graph replay, cold buffers)."""
+    import asrx
+    from asrx import kernels as K
+    from asrx.kernels import MaskSpec
+    from oracle.ref_model import CONFIGS, synthetic_batch
+    out = {}
+    for name in names:
+        spec = CONFIGS[name]
+        cfg = spec["cfg"]
+        B, T, L = spec["batch"], spec["frames"], spec["text_len"]
+        prec = "fp32" if name == "c2" else "bf16"
+        torch.manual_seed(0)
+        model = asrx.Transformer(cfg.vocab_size, cfg.input_dim, cfg.d_model, cfg.dec_len, cfg.enc_len, cfg.n_enc,
+                                 cfg.n_dec, cfg.n_heads, cfg.ff_dim, dropout=cfg.dropout,
+                                 precision=prec).cuda().eval()
+        s, t, m = synthetic_batch(cfg, B, T, L + 1, seed=4321)
+        s, t, m = s.cuda(), t[:, :-1].cuda(), m[:, :-1].cuda()
+        with torch.no_grad():
+            for _ in range(2):
+                model(s, t, m)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                model(s, t, m)
+            e1.record()
+            e1.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        fps = B * T / (ms * 1e-3)
+        tf = FWD_MFLOP_PER_FRAME[name] * 1e6 * B * T / (ms * 1e-3) / 1e12
+        peak = PEAK_F32_TFLOPS if prec == "fp32" else PEAK_BF16_TFLOPS
+        out[name] = {"metric": "frames/s (teacher-forced forward)", "value": round(fps, 1), "ms_per_forward": round(ms, 3),
+                     "dtype": "f32" if prec == "fp32" else "bf16", "batch": B, "frames": T, "text_len": L,
+                     "achieved_tflops": round(tf, 1), "peak_tflops": peak, "frac": round(tf / peak, 4),
+                     "flop_basis": f"{FWD_MFLOP_PER_FRAME[name]} MFLOP/frame (SURVEY 8(d))"}
+        del model
+        torch.cuda.empty_cache()
+    if "c5" in names:   # the tiled (Lk > 256) attention forward alone at the c5 encoder shape
+        cfg = CONFIGS["c5"]["cfg"]
+        B, H, d = CONFIGS["c5"]["batch"], cfg.n_heads, cfg.d_model
+        T2, dh = asrx.subsampled(CONFIGS["c5"]["frames"]), d // cfg.n_heads
+        gen = torch.Generator(device="cuda").manual_seed(5)
+        rows = B * T2
+        st = ((3 * d, T2 * 3 * d),) * 3 + ((d, T2 * d),)
+
+        def make():
+            qkv = (torch.randn(rows, 3 * d, device="cuda", generator=gen) * 0.5).bfloat16()
+            o = torch.empty(rows, d, device="cuda", dtype=torch.bfloat16)
+            return lambda: K.attention_fwd(qkv, qkv[:, d:], qkv[:, 2 * d:], o, B, H, T2, T2, dh, st, d ** -0.5,
+                                           MaskSpec())
+        nsets = max(2, -(-COLD_BYTES // (rows * d * 8)))
+        fns = [make() for _ in range(nsets)]
+        t_ms = _graph_time_ms(fns)
+        flops = 4.0 * B * H * T2 * T2 * dh
+        tf = flops / (t_ms * 1e-3) / 1e12
+        out["c5"]["attention_fwd"] = {"bound": "mfma", "achieved": round(tf, 1), "peak": PEAK_BF16_TFLOPS,
+                                      "unit": "TFLOP/s", "frac": round(tf / PEAK_BF16_TFLOPS, 4),
+                                      "us": round(t_ms * 1e3, 2),
+                                      "shape": f"B*H={B * H} Lq=Lk={T2} dh={dh}, no mask, eval (no dropout)"}
+        del fns
+        torch.cuda.empty_cache()
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -350,6 +425,8 @@ def main():
     if rank == 0 and not args.no_sub:
         out["sub_rooflines"] = sub_rooflines(B, asrx.subsampled(T), cfg.d_model, cfg.n_heads, cfg.ff_dim,
                                              cfg.dropout)
+    if rank == 0 and world == 1 and not args.no_other:
+        out["other_configs"] = other_configs()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, T, L, args.cpu_batch, args.cpu_steps)
     if rank == 0:
