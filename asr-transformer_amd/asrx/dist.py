@@ -2,11 +2,33 @@
 RCCL (torch.distributed backend "nccl" on ROCm; xGMI between the GPUs of a node).  No per-parameter copies:
 buckets are views of the flat buffer.  The 1/world average is folded into the optimizer's grad scale.
 
+Wire formats (ASRX_DP_WIRE or GradAllReduce(wire=...)):
+  "fp32" — dist.all_reduce of the fp32 bucket (RCCL ring/tree, sums in fp32).
+  "bf16" — half the bytes on xGMI with the sum still in fp32: the bucket is cast to bf16 and split into `world`
+           chunks; an all-to-all hands rank r every peer's copy of chunk r; asrx_sum_chunks_bf16 sums them in fp32
+           and rounds once; an all-gather of the reduced bf16 chunks and a cast back fill the fp32 bucket.  (RCCL's
+           own bf16 all-reduce would round after every one of its world - 1 additions.)  Per-element error: one
+           bf16 rounding of each rank's gradient and one of the sum (relative ~2^-8).
+
 The reference has no multi-device code; the step semantics it defines are train.py:16-35
 per batch — DP averages per-shard mean losses, which equals the global mean for equal token counts per shard.
 """
+import os
+
 import torch
 import torch.distributed as dist
+
+WIRE = os.environ.get("ASRX_DP_WIRE", "fp32")
+
+
+def _cast(src, dst):
+    """dtype conversion of a bucket: the native kernel for device tensors (the product: flat grads live on the GPU);
+    torch's copy only for the CPU tensors of the gloo tests of this host logic."""
+    if src.is_cuda:
+        from . import kernels as K
+        K.cast(src, dst)
+    else:
+        dst.copy_(src)
 
 
 def bucket_views(flat, bucket_elems):
@@ -28,14 +50,20 @@ class GradAllReduce:
     all-reduced asynchronously (RCCL runs on its own stream, ordered after the compute already queued) while
     the backward continues.  `finish()` / `__call__()` reduces every range not yet issued and waits for all."""
 
-    def __init__(self, flat_grad, group=None, bucket_mb=64, allreduce_fn=None):
+    def __init__(self, flat_grad, group=None, bucket_mb=64, allreduce_fn=None, wire=None, chunk_sum=None):
         self.group = group
         self.flat = flat_grad
         self.bucket_elems = max(1, int(bucket_mb * 2 ** 20) // 4)
         self.buckets = bucket_views(flat_grad, self.bucket_elems)
         self.allreduce_fn = allreduce_fn  # injectable for CPU tests (fake backend)
+        self.wire = WIRE if wire is None else wire
+        if self.wire not in ("fp32", "bf16"):
+            raise ValueError(f"asrx.dist: unknown gradient wire format {self.wire!r}")
+        # the fp32 sum of the bf16 wire: the native kernel; injectable for the CPU (gloo) tests of this host logic
+        self.chunk_sum = chunk_sum
         self._issued = []                 # (start, end) ranges already issued this step
         self._works = []
+        self._post = []                   # bf16 wire: (bucket view, gathered bf16, work) to copy back after wait
 
     @property
     def world(self):
@@ -50,8 +78,31 @@ class GradAllReduce:
     def _issue(self, view):
         if self.allreduce_fn is not None:
             self.allreduce_fn(view)
+        elif self.wire == "bf16":
+            self._issue_bf16(view)
         else:
             self._works.append(dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+
+    def _issue_bf16(self, view):
+        """Reduce-scatter by all-to-all on bf16 chunks, fp32 sum of the W copies, all-gather of the bf16 sums.
+        The all-to-all must finish before the sum: its wait is a stream dependency (no host sync), on the stream
+        the caller issues from (the Trainer's compute stream, between captured backward segments)."""
+        W = dist.get_world_size(self.group)
+        n = view.numel()
+        c = -(-n // W)
+        send = torch.zeros(W * c, dtype=torch.bfloat16, device=view.device)
+        _cast(view, send[:n])
+        recv = torch.empty_like(send)
+        dist.all_to_all_single(recv, send, group=self.group, async_op=True).wait()
+        mine = torch.empty(c, dtype=torch.bfloat16, device=view.device)
+        if self.chunk_sum is not None:
+            self.chunk_sum(recv, W, c, mine)
+        else:
+            from . import kernels as K
+            K.sum_chunks_bf16(recv, W, c, mine)
+        full = torch.empty(W * c, dtype=torch.bfloat16, device=view.device)
+        work = dist.all_gather_into_tensor(full, mine, group=self.group, async_op=True)
+        self._post.append((view, full, work))
 
     def ready(self, start, end):
         """Gradients in flat[start:end] are final: start their all-reduce now (in buckets)."""
@@ -78,7 +129,11 @@ class GradAllReduce:
                 self._issue(v)
         for w in self._works:
             w.wait()
+        for view, full, work in self._post:
+            work.wait()
+            _cast(full[:view.numel()], view)
         self._works = []
+        self._post = []
         self._issued = []
 
     def __call__(self):

@@ -4,6 +4,8 @@ flat gradient buffer that `p.grad` views (asrx.params); the Functions return Non
 
 `model_forward` / `model_backward` are also used directly (no autograd) by the fused trainer (asrx.train).
 """
+import os
+
 import torch
 
 from . import blocks as Bk
@@ -151,21 +153,40 @@ def _release(C, ready, params):
     C.defer_wgrad()
 
 
-def encoder_bwd(C, enc, S, dy, gate_feats, ready=None):
-    """dy: grad of the encoder output (fp32 or compute dtype). Returns dfeats (compute dtype).  With `ready`,
-    the upper half of the layers (and _norm_out) is released to the gradient all-reduce once done."""
+# encoder layers per gradient release of the multi-GPU backward (ASRX_DP_RELEASE_LAYERS; 0 = half the stack).  Every
+# release ends a grouped weight-gradient launch, so finer releases trade all-reduce overlap for fuller launches.
+RELEASE_LAYERS = int(os.environ.get("ASRX_DP_RELEASE_LAYERS", "0"))
+
+
+def release_groups(n, every=None):
+    """The encoder layer ranges [lo, hi) released together, in backward order: groups of `every` layers from the
+    top; the lowest group (with _lin_in and the front-end) is left to the reducer's finish()."""
+    every = RELEASE_LAYERS if every is None else every
+    k = every if every > 0 else max(1, n // 2)
+    out, hi = [], n
+    while hi - k > 0:
+        out.append((hi - k, hi))
+        hi -= k
+    return out
+
+
+def encoder_bwd(C, enc, S, dy, gate_feats, ready=None, release_every=None):
+    """dy: grad of the encoder output (fp32 or compute dtype). Returns dfeats (compute dtype).  With `ready`, the
+    layers are released to the gradient all-reduce in groups (release_groups; the first with _norm_out) as soon as
+    their gradients are final."""
     x = S["x"]
     dx_c = torch.empty(x.shape, dtype=C.cd, device=x.device)
     dx = Bk.ln_bwd(C, x, dy, enc._norm_out, S["mean"], S["rstd"], drop_out=dx_c)
     n = len(S["layers"])
+    groups = {lo: hi for lo, hi in release_groups(n, release_every)}
     for i, layer_S in reversed(list(enumerate(S["layers"]))):
         nxt = torch.empty(x.shape, dtype=C.cd, device=x.device)
         dx = Bk.enc_layer_bwd(C, layer_S, dx, dx_c, nxt)
         dx_c = nxt
         C.flush_wgrad_side()
-        if i == n // 2 and n > 1:
-            _release(C, ready, [p for l in enc._layers[n // 2:] for p in l.parameters()] +
-                     list(enc._norm_out.parameters()))
+        if i in groups:
+            extra = list(enc._norm_out.parameters()) if groups[i] == n else []
+            _release(C, ready, [p for l in enc._layers[i:groups[i]] for p in l.parameters()] + extra)
     feats = S["feats"]
     dfeats = torch.empty(feats.shape, dtype=C.cd, device=x.device)
     w = enc._lin_in.weight

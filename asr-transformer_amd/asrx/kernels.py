@@ -547,6 +547,12 @@ def cast(src, dst):
     call("asrx_cast", code(src), src.data_ptr(), code(dst), dst.data_ptr(), src.numel(), stream())
 
 
+def sum_chunks_bf16(recv, world, chunk, out):
+    """out[i] = bf16(sum_w recv[w * chunk + i]) with an fp32 sum (bf16-wire gradient exchange, asrx.dist)."""
+    _cuda(recv, out)
+    call("asrx_sum_chunks_bf16", recv.data_ptr(), world, chunk, out.data_ptr(), stream())
+
+
 def dropout_mask(n, p, seed, device):
     keep = torch.empty(n, dtype=torch.uint8, device=device)
     call("asrx_dropout_mask", keep.data_ptr(), n, p, seed & _U64, stream())

@@ -161,7 +161,7 @@ class Trainer:
     """Native data-parallel training step for an asrx.Transformer."""
 
     def __init__(self, model, lr=1e-4, betas=(0.9, 0.98), eps=1e-9, weight_decay=0.0, decoupled=True,
-                 ignore_index=-100, group=None, bucket_mb=64, allreduce_fn=None, graph=None):
+                 ignore_index=-100, group=None, bucket_mb=64, allreduce_fn=None, graph=None, wire=None):
         self.model = model
         self.store = get_store(model)
         self.m = torch.zeros_like(self.store.flat)
@@ -169,12 +169,14 @@ class Trainer:
         self.lr, self.betas, self.eps, self.wd, self.decoupled = lr, betas, eps, weight_decay, decoupled
         self.ignore_index = ignore_index
         self.step_count = 0
-        self.reducer = GradAllReduce(self.store.grad, group=group, bucket_mb=bucket_mb, allreduce_fn=allreduce_fn)
+        self.reducer = GradAllReduce(self.store.grad, group=group, bucket_mb=bucket_mb, allreduce_fn=allreduce_fn,
+                                     wire=wire)
         self.store.refresh_shadow(force=True)
         self._wonly = wgrad_only_params(model) if FRESH_GRADS else []
         self.graph = GRAPH if graph is None else bool(graph)
         self._cap = None        # captured step: (segments, static inputs, loss)
         self._hyp = torch.zeros(3, dtype=torch.float32, device=self.store.flat.device)
+        self.ar_events = None   # list -> record the exposed all-reduce time of each step (_finish)
         if self._wonly:   # flat indices of everything else (zeroed each step by one index_fill)
             keep = torch.ones(self.store.grad.numel(), dtype=torch.bool)
             for p in self._wonly:
@@ -220,11 +222,24 @@ class Trainer:
             if self._cap is not None:
                 return self._replay(spectrum, text, mask)
         loss = self.forward_backward(spectrum, text, mask)
-        self.reducer.finish()
+        self._finish()
         self.step_count += 1
         self._adam()
         self.store.mark_shadow_fresh()
         return loss
+
+    def _finish(self):
+        """The all-reduce of whatever the backward did not release, waited for on the compute stream.  With
+        `ar_events` set to a list (bench.py), HIP events bracket it on that stream: their elapsed time is the
+        all-reduce time the backward did not hide (exposed), per step and rank."""
+        if self.ar_events is not None and self.reducer.active:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            self.reducer.finish()
+            e1.record()
+            self.ar_events.append((e0, e1))
+        else:
+            self.reducer.finish()
 
     # ---- HIP graph mode
     def _matches(self, spectrum, text, mask):
@@ -262,7 +277,7 @@ class Trainer:
         K.adam_hyper(self._hyp, self.lr, self.betas[0], self.betas[1], self.step_count)
         seg.replay(self.reducer)
         if self.reducer.active:
-            self.reducer.finish()
+            self._finish()
             self._adam(self._hyp)
         self.store.mark_shadow_fresh()
         return loss

@@ -1082,6 +1082,26 @@ extern "C" int asrx_cross_entropy(const float* logits, int64_t rows, int32_t V, 
   return ASRX_OK;
 }
 
+// Data-parallel gradient exchange on a bf16 wire (asrx.dist, wire="bf16"): after the all-to-all, rank r holds the W
+// peers' bf16 copies of its chunk, [W][c]; out[i] = bf16(sum_w in[w][i]) with the sum kept in fp32 (one rounding).
+__global__ __launch_bounds__(256) void sum_chunks_bf16_kernel(const bf16_t* __restrict__ in, int W, int64_t c,
+                                                               bf16_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < c; i += (int64_t)gridDim.x * 256) {
+    float acc = 0.f;
+    for (int w = 0; w < W; ++w) acc += bf2f(in[(int64_t)w * c + i]);
+    out[i] = f2bf(acc);
+  }
+}
+
+extern "C" int asrx_sum_chunks_bf16(const void* in, int32_t world, int64_t chunk, void* out, void* stream) {
+  if (!in || !out || world < 1 || chunk < 0) return ASRX_ERR_ARG;
+  if (chunk == 0) return ASRX_OK;
+  hipLaunchKernelGGL(sum_chunks_bf16_kernel, dim3(grid_for(chunk)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)in, (int)world, chunk, (bf16_t*)out);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
 extern "C" int asrx_cast(int32_t src_dtype, const void* src, int32_t dst_dtype, void* dst, int64_t n, void* stream) {
   if (!src || !dst || n < 0) return ASRX_ERR_ARG;
   if (n == 0) return ASRX_OK;

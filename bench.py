@@ -381,6 +381,8 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if world > 1:
+        trainer.ar_events = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = trainer.step(s, t, m)
@@ -394,6 +396,13 @@ def main():
         x = torch.tensor([dt], device="cuda", dtype=torch.float64)
         dist.all_reduce(x, op=dist.ReduceOp.MAX)
         dt = float(x)
+    exposed = None
+    if world > 1 and trainer.ar_events:
+        mine = sum(a.elapsed_time(b) for a, b in trainer.ar_events) / len(trainer.ar_events)
+        x = torch.tensor([mine], device="cuda", dtype=torch.float64)
+        allv = [torch.zeros_like(x) for _ in range(world)]
+        dist.all_gather(allv, x)
+        exposed = [round(float(v), 3) for v in allv]
     frames = B * T * args.steps * world
     value = frames / dt
     roof = None
@@ -420,6 +429,7 @@ def main():
            "frames_per_sec_per_gpu": round(value / world, 1),
            "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 3),
            "graph": trainer._cap is not None, "setup_steps": setup,
+           "allreduce_exposed_ms_per_rank": exposed, "grad_wire": trainer.reducer.wire if world > 1 else None,
            "loss": round(float(loss), 4),
            "roofline": roof}
     if rank == 0 and not args.no_sub:

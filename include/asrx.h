@@ -280,6 +280,11 @@ int asrx_cross_entropy(const float* logits, int64_t rows, int32_t V, int64_t ld,
  * Elementwise utilities.
  * ------------------------------------------------------------------------------------------------- */
 int asrx_cast(int32_t src_dtype, const void* src, int32_t dst_dtype, void* dst, int64_t n, void* stream);
+
+/* Data-parallel gradient exchange on a bf16 wire (asrx.dist.GradAllReduce, wire="bf16"; the reference trains on one
+ * device, train.py:16-35, so this is the build's own DDP step): in = the W peers' bf16 copies of one chunk of c
+ * elements, [world][chunk]; out[i] = bf16(sum over w of in[w][i]) with the sum in fp32 and one final rounding. */
+int asrx_sum_chunks_bf16(const void* in, int32_t world, int64_t chunk, void* out, void* stream);
 /* Fused Adam/AdamW over flat fp32 buffers; optionally refreshes the bf16 shadow copy of the params.
  * Replaces optimizer.step() (train.py:35).  hyp (optional, device): {lr, bias_corr1, bias_corr2} read at run
  * time instead of the scalar arguments, so a captured step (HIP graph) takes the current step's values. */

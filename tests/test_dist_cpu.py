@@ -146,3 +146,87 @@ def test_gloo_ws2_ready_ranges():
         assert p.exitcode == 0
     want = torch.arange(5000, dtype=torch.float32) * 3
     assert torch.equal(res[0], want) and torch.equal(res[1], want)
+
+
+def _torch_chunk_sum(recv, W, c, out):
+    """Test double of asrx_sum_chunks_bf16 (CPU tensors): fp32 sum of the W bf16 copies, one rounding."""
+    out.copy_(recv.view(W, c).float().sum(0).to(torch.bfloat16))
+
+
+def _bf16_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from asrx.dist import GradAllReduce
+    g = torch.Generator().manual_seed(100 + rank)
+    flat = torch.randn(5003, generator=g)
+    r = GradAllReduce(flat, bucket_mb=0.004, wire="bf16", chunk_sum=_torch_chunk_sum)   # ragged buckets
+    assert len(r.buckets) > 3
+    r.ready(2000, 5003)
+    r.finish()
+    q.put((rank, flat))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_ws3_bf16_wire_fp32_sum():
+    """bf16 wire: every rank ends with bf16(sum_r bf16(g_r)) — the sum in fp32, one rounding of each rank's
+    gradient and one of the sum — identical on all ranks; world 3 (chunks do not divide the buckets)."""
+    world, port = 3, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bf16_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    parts = [torch.randn(5003, generator=torch.Generator().manual_seed(100 + r)) for r in range(world)]
+    want = sum(p.to(torch.bfloat16).float() for p in parts).to(torch.bfloat16).float()
+    exact = sum(parts)
+    for r in range(world):
+        assert torch.equal(res[r], want)
+    assert float((res[0] - exact).abs().max() / exact.abs().max()) < 2 ** -7
+
+
+def test_release_groups_cover_each_parameter_once():
+    """The multi-GPU backward's release schedule (functions.release_groups + _spans over the flat store) followed
+    by the reducer's finish() reduces every gradient element exactly once, for every release granularity."""
+    import asrx
+    from asrx.dist import GradAllReduce
+    from asrx.functions import _spans, param_order, release_groups
+    from asrx.params import FlatParams
+    cfg = CONFIGS["c2"]["cfg"]
+    model = asrx.Transformer(cfg.vocab_size, cfg.input_dim, cfg.d_model, cfg.dec_len, cfg.enc_len, cfg.n_enc,
+                             cfg.n_dec, cfg.n_heads, cfg.ff_dim, dropout=0.0, precision="bf16")
+    store = FlatParams(param_order(model), torch.device("cpu"))   # the product's flat layout (built on the host)
+
+    class _C:
+        pass
+    C = _C()
+    C.store = store
+    enc, n = model.encoder, len(model.encoder._layers)
+    for every in (0, 1, 2, 4, 5, n, n + 3):
+        flat = store.grad
+        counts = torch.zeros(flat.numel())
+        base = flat.data_ptr()
+
+        def fake(b):
+            o = (b.data_ptr() - base) // 4
+            counts[o:o + b.numel()] += 1
+        fake.world = 2
+        r = GradAllReduce(flat, bucket_mb=0.25, allreduce_fn=fake)
+        released = list(model.decoder.parameters())
+        for a, b in _spans(C, released):
+            r.ready(a, b)
+        groups = release_groups(n, every)
+        assert groups == sorted(groups, reverse=True) and all(lo > 0 for lo, _ in groups)
+        for lo, hi in groups:
+            ps = [p for l in enc._layers[lo:hi] for p in l.parameters()]
+            if hi == n:
+                ps += list(enc._norm_out.parameters())
+            for a, b in _spans(C, ps):
+                r.ready(a, b)
+        r.finish()
+        assert counts.eq(1).all(), every

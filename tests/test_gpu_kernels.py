@@ -617,3 +617,14 @@ def test_embedding_and_ce_and_adam():
         K().adam(pd, (gr * step).to(dev), md, vd, pb, 1e-3, 0.9, 0.98, 1e-9, 0.01, step, decoupled=True)
     assert relerr(pd.cpu(), pt.detach()) < 1e-6
     assert relerr(pb.float().cpu(), pt.detach()) < 1e-2
+
+
+@pytest.mark.parametrize("world,chunk", [(1, 7), (2, 1000), (8, 12345), (3, 0)])
+def test_sum_chunks_bf16(world, chunk):
+    """bf16-wire gradient exchange (asrx.dist wire="bf16"): the W peers' bf16 chunks summed in fp32, rounded once."""
+    g = torch.Generator(device=dev).manual_seed(world * 7 + chunk)
+    recv = bf(torch.randn(world * chunk, device=dev, generator=g) * 3)
+    out = torch.empty(chunk, device=dev, dtype=torch.bfloat16)
+    K().sum_chunks_bf16(recv, world, chunk, out)
+    want = recv.view(world, chunk).float().sum(0).to(torch.bfloat16) if chunk else out
+    assert torch.equal(out, want)
