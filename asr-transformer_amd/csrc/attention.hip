@@ -739,6 +739,155 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
   }
 }
 
+// Long key ranges without mask or dropout (Lk > 256, eval / inference: the c5 encoder self-attention at T' = 999 and
+// the decoder's cross-attention over it; training keeps attn_fwd_kernel): the resident kernel's 8 waves x 32
+// queries and key-tile body, with K/V streamed through LDS in 128-key chunks, double-buffered — chunk c + 2 is
+// issued by LDS-DMA as soon as every wave has finished chunk c, and waited for (counted vmcnt + barrier) just
+// before chunk c + 1 is used.  Keys past Lk read as zero rows (descriptor range) and get a -inf score.
+constexpr int S_CK = 128;
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void attn_fwd_stream_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(1024))) bf16_t sk[2 * S_CK * 64];
+  __shared__ __attribute__((aligned(1024))) bf16_t sv[2 * S_CK * 64];
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, li = l & 15;
+  const int nch = (a.Lk + S_CK - 1) / S_CK;
+  const bf16_t* Kb = a.k + b * a.kb + h * 64;
+  const bf16_t* Vb = a.v + b * a.vb + h * 64;
+  const int qw0 = (blockIdx.x * 8 + w) * 32;
+  s8_t qf[2][2];
+#pragma unroll
+  for (int qs = 0; qs < 2; ++qs) {
+    const int qc = min(qw0 + 16 * qs + li, a.Lq - 1);
+    const bf16_t* qp = a.q + b * a.qb + (int64_t)qc * a.qr + h * 64 + 8 * g;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) qf[qs][c] = ld128_asm(qp + 32 * c);
+  }
+  const asrxg::v4i_t ksrd = asrxg::make_srd(Kb, ((int64_t)(a.Lk - 1) * a.kr + 64) * 2);
+  const asrxg::v4i_t vsrd = asrxg::make_srd(Vb, ((int64_t)(a.Lk - 1) * a.vr + 64) * 2);
+  const int rl = l >> 3, sl = l & 7;
+  // chunk c -> buffer c & 1: two 64-key pieces, wave w moves key rows 64 i + 8 w .. + 7 of K and of V
+#define STREAM_ISSUE(c)                                                                                    \
+  do {                                                                                                     \
+    _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                                        \
+      const int lr = ((c) & 1) * S_CK + 64 * i + 8 * w, r = (c) * S_CK + 64 * i + 8 * w + rl;            \
+      asrxg::dma16_asm(sk + lr * 64, ksrd, (uint32_t)(r * a.kr + 8 * kslot(r, sl)) * 2u);                 \
+      asrxg::dma16_asm(sv + lr * 64, vsrd, (uint32_t)(r * a.vr + 8 * vslot(r, sl)) * 2u);                 \
+    }                                                                                                      \
+  } while (0)
+  STREAM_ISSUE(0);
+  if (nch > 1) {
+    STREAM_ISSUE(1);
+    asrxg::wait_vmcnt<4>();   // Q and chunk 0 (chunk 1 may still be in flight)
+  } else {
+    asrxg::wait_vmcnt<0>();
+  }
+#pragma unroll
+  for (int qs = 0; qs < 2; ++qs) {
+    pin(qf[qs][0]);
+    pin(qf[qs][1]);
+  }
+  lds_barrier();
+  const bool act = qw0 < a.Lq;
+
+  f4_t o[4][2];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) o[u][0] = o[u][1] = f4_t{0.f, 0.f, 0.f, 0.f};
+  float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
+  for (int c = 0; c < nch; ++c) {
+    const bf16_t* skc = sk + (c & 1) * S_CK * 64;
+    const bf16_t* svc = sv + (c & 1) * S_CK * 64;
+    if (act) {
+#pragma unroll
+      for (int kt = 0; kt < S_CK / 32; ++kt) {
+        const int key0 = c * S_CK + kt * 32;
+        if (key0 >= a.Lk) break;   // workgroup-uniform
+        f4_t s[2][2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const bf16_t* kr = skc + (kt * 32 + 16 * t + li) * 64;
+          const s8_t k0 = lds_b128(kr + 8 * (g ^ (li & 7))), k1 = lds_b128(kr + 8 * ((g + 4) ^ (li & 7)));
+#pragma unroll
+          for (int qs = 0; qs < 2; ++qs) s[t][qs] = mfma32(k1, qf[qs][1], mfma32(k0, qf[qs][0], f4_t{0.f, 0.f, 0.f, 0.f}));
+        }
+        const bool tail = key0 + 32 > a.Lk;
+        s4_t pf[2][2];
+#pragma unroll
+        for (int qs = 0; qs < 2; ++qs) {
+          float mt = -INFINITY;
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float x = s[t][qs][r] * a.scale2;
+              if (tail && key0 + 16 * t + 4 * g + r >= a.Lk) x = -INFINITY;
+              s[t][qs][r] = x;
+              mt = fmaxf(mt, x);
+            }
+          mt = xmax4(mt);
+          const float m_new = fmaxf(m_run[qs], mt);
+          const float m_use = m_new == -INFINITY ? 0.f : m_new;
+          if (__ballot(m_new != m_run[qs])) {   // rescale only when some row's max grew (exact, wave-uniform)
+            const float alpha = exp2_raw(m_run[qs] - m_use);
+            l_run[qs] *= alpha;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) o[u][qs] *= alpha;
+            m_run[qs] = m_new;
+          }
+          float rs = 0.f;
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            f4_t pv;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float e = exp2_raw(s[t][qs][r] - m_use);
+              rs += e;
+              pv[r] = e;
+            }
+            pf[t][qs] = to_bf4(pv);
+          }
+          l_run[qs] += xsum4(rs);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int vr = kt * 32 + 4 * g + (li >> 2);   // (vr + 16) & 6 == vr & 6
+          const bf16_t* vp = svc + vr * 64 + 8 * vslot(vr, 2 * u + ((li >> 1) & 1)) + 4 * (li & 1);
+          const s8_t vt = cat8(lds_tr(vp), lds_tr(vp + 16 * 64));
+#pragma unroll
+          for (int qs = 0; qs < 2; ++qs) o[u][qs] = mfma32(vt, cat8(pf[0][qs], pf[1][qs]), o[u][qs]);
+        }
+      }
+    }
+    if (c + 1 < nch) {
+      lds_barrier();                 // every wave is done with buffer c & 1
+      if (c + 2 < nch) {
+        STREAM_ISSUE(c + 2);
+        asrxg::wait_vmcnt<4>();      // chunk c + 1 landed (chunk c + 2 may still be in flight)
+      } else {
+        asrxg::wait_vmcnt<0>();
+      }
+      lds_barrier();                 // ... and visible to every wave
+    }
+  }
+#undef STREAM_ISSUE
+  if (!act) return;
+#pragma unroll
+  for (int qs = 0; qs < 2; ++qs) {
+    const int q = qw0 + 16 * qs + li;
+    if (q >= a.Lq) continue;
+    const bool live = l_run[qs] > 0.f;
+    const float inv = live ? 1.f / l_run[qs] : 0.f;
+    const int64_t oo = b * a.ob + (int64_t)q * a.orr + h * 64 + 4 * g;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      store_o4(a.o + oo + 16 * u, a.o_lo ? a.o_lo + oo + 16 * u : nullptr, o[u][qs][0] * inv, o[u][qs][1] * inv,
+               o[u][qs][2] * inv, o[u][qs][3] * inv);
+    if (g == 0 && a.lse) {
+      const float mu = m_run[qs] == -INFINITY ? 0.f : m_run[qs];
+      a.lse[(int64_t)bh * a.Lq + q] = live ? mu + log2f(l_run[qs]) : INFINITY;
+    }
+  }
+}
+
 // Backward: grid (B*H), nw = max(2, ceil(Lk/32)) waves; wave w owns keys [32w, 32w+32) (dK, dV in registers)
 // and the workgroup sweeps the queries in chunks of 32: S and dP are recomputed with the query on the accumulator
 // row; Pd / dS feed dV^T / dK^T as B operands directly; dS (bf16) is published in LDS and, after the chunk's only
@@ -1151,6 +1300,14 @@ extern "C" int asrx_attention_fwd(const asrx_attn_desc* d, void* stream) {
     if (a.mode == 0) hipLaunchKernelGGL(attn_fwd_res_kernel<0>, grid, dim3(512), 0, st, a, qmaj);
     else if (a.mode == 1) hipLaunchKernelGGL(attn_fwd_res_kernel<1>, grid, dim3(512), 0, st, a, qmaj);
     else hipLaunchKernelGGL(attn_fwd_res_kernel<2>, grid, dim3(512), 0, st, a, qmaj);
+    ASRX_CHECK_LAUNCH();
+    return ASRX_OK;
+  }
+  static const bool tiled = [] { const char* e = getenv("ASRX_ATTN_KERNEL"); return e && !strcmp(e, "tiled"); }();
+  if (!tiled && d->dh == 64 && a.mode == 0 && !a.thr && a.Lk > R_MAXK && a.orr % 4 == 0 && a.ob % 4 == 0 &&
+      a.kr % 8 == 0 && a.vr % 8 == 0 && ((uintptr_t)a.k % 16) == 0 && ((uintptr_t)a.v % 16) == 0 &&
+      (int64_t)a.Lk * std::max(a.kr, a.vr) * 2 < 0x7fffffffLL) {
+    hipLaunchKernelGGL(attn_fwd_stream_kernel, dim3((a.Lq + 255) / 256, a.B * a.H), dim3(512), 0, st, a);
     ASRX_CHECK_LAUNCH();
     return ASRX_OK;
   }

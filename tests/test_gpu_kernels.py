@@ -343,7 +343,8 @@ def attn_variant(request):
                                            (2, 2, 249, 249, "none"), (1, 2, 100, 300, "none"),
                                            (2, 3, 33, 33, "decoder"), (1, 2, 300, 64, "none"),
                                            (2, 2, 256, 256, "decoder"), (1, 1, 5, 17, "none"),
-                                           (1, 2, 999, 999, "none"), (1, 2, 300, 300, "decoder")])
+                                           (1, 2, 999, 999, "none"), (1, 2, 300, 300, "decoder"),
+                                           (1, 2, 64, 257, "none"), (2, 2, 513, 1031, "none")])
 def test_attention_fused(dh, B, H, Lq, Lk, kind, attn_variant):
     from asrx.kernels import MaskSpec
     g = torch.Generator().manual_seed(B * 100 + Lq + Lk + dh)

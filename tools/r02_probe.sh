@@ -15,6 +15,7 @@ for s in "$@"; do
     parity) step parity 600 python -u -m pytest tests/test_gpu_train_parity.py tests/test_gpu_graph.py -x -q --timeout 300 --timeout-method thread -m gpu ;;
     benchab) for k in p3 p4 p3 p4; do ASRX_WGRAD_KIND=$k step bench_$k 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-sub; grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench_$k.log; done ;;
     other) step other 400 python -c "import bench, json; print(json.dumps(bench.other_configs()))" ;;
+    attnt) step attnt 600 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 300 --timeout-method thread -m gpu -k "attention" ;;
     counters) step counters 120 rocprofv3 -L ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 3 --no-cpu-baseline --no-probe --no-sub ;;
     pmcm) step pmcm 300 timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/pmcm -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-graph --no-cpu-baseline --no-probe --no-sub && python3 tools/pmc_mfma.py gpurun_out/pmcm/run_counter_collection.csv --out gpurun_out/c3_pmc_mfma.json ;;
