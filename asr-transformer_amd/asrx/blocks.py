@@ -384,7 +384,7 @@ def ffn_fwd(C, x, ln, ff):
     # bf16: the epilogue also writes the 1-bit mask f > 0 (ReLU and dropout keep), which the data gradient
     # reads as its gate: M*nf/8 bytes instead of the 2*M*nf of f itself
     fb = None
-    if C.cd == torch.bfloat16 and nf % 32 == 0 and GATE_BITS:
+    if C.train and C.cd == torch.bfloat16 and nf % 32 == 0 and GATE_BITS:   # (only the backward reads them)
         fb = _empty((M, nf // 32), torch.int32, x)
     K.linear(h, C.W(ff.squeeze.weight), f, bias=ff.squeeze.bias.data, relu=True, dropout_p=C.p, seed=sf,
              mask_out=fb, ld_mask=nf // 32)

@@ -416,11 +416,22 @@ def decoder(dec, x, mask, enc_x):
 
 @torch.no_grad()
 def decoder_evaluate(dec, x, enc_x):
-    """Decoder.evaluate (model.py:125-151) with its quirks: per-sample loop, whole prefix recomputed each
-    step, causal-only mask, NO final LayerNorm before the classifier, no break on EOS; returns the last
-    sample's token row and the list of logits snapshots (one per EOS hit or final step)."""
-    C = make_ctx(dec, 0.0)
-    C.train, C.p = False, 0.0
+    """Decoder.evaluate (model.py:125-151) with its quirks: causal-only mask, NO final LayerNorm before the
+    classifier, no break on EOS (every sample runs seq_len steps), returns the LAST sample's token row and the list
+    of logits snapshots `prob[:, :-1].squeeze()` (one per EOS hit or final step, samples in order).
+
+    Eval mode: the whole batch decodes together with per-layer K/V caches (one position per step: causality makes
+    the reference's full-prefix recomputation redundant), the cross-attention K/V of all layers projected once, and
+    the next tokens chosen on the GPU (asrx_greedy_argmax) — no host round trip until the end.  Train mode with
+    dropout (model.py:137 applies self._dropout, and every layer's dropouts are live): the reference's
+    per-sample prefix recomputation, whose fresh masks a cache cannot reproduce."""
+    if dec.training and dec.p > 0:
+        return _decoder_evaluate_recompute(dec, x, enc_x)
+    return _decoder_evaluate_cached(dec, x, enc_x)
+
+
+def _decoder_evaluate_recompute(dec, x, enc_x):
+    C = make_ctx(dec, dec.p)
     B, Te, d = enc_x.shape
     V = dec._classifier.V
     probs = []
@@ -438,6 +449,80 @@ def decoder_evaluate(dec, x, enc_x):
             if next_word.item() == dec._eos_token_id or i == dec._seq_len:
                 probs.append(prob[:, :-1].squeeze())
     return decoder_input, probs
+
+
+def _decoder_evaluate_cached(dec, x, enc_x):
+    C = make_ctx(dec, 0.0)
+    C.train, C.p = False, 0.0
+    dev = enc_x.device
+    B, Te, d = enc_x.shape
+    n, H, steps = len(dec._layers), dec.num_heads, dec._seq_len
+    dh = d // H
+    cls = dec._classifier
+    V, Vp = cls.V, cls.Vp
+    L0 = x.shape[1]
+    P = L0 - 1 + steps                      # positions processed (the last input has L0 + steps - 1 tokens)
+    pe = dec._pe.pe[0]
+    if P > pe.shape[0]:
+        raise ValueError(f"decoder length {P} exceeds the PE table ({pe.shape[0]}) as in layers.py:73")
+    if B == 0 or steps == 0:
+        return x[-1:].to(dev) if B else x.to(dev), []
+    enc_c = torch.empty(B * Te, d, dtype=C.cd, device=dev)
+    K.cast(enc_x.reshape(B * Te, d).contiguous(), enc_c)
+    Wkv, bkv, _, _ = _kv_block(C, dec)
+    kvx = torch.empty(B * Te, n * 2 * d, dtype=C.cd, device=dev)      # every layer's cross-attention K/V
+    K.linear(enc_c, Wkv, kvx, bias=bkv)
+    kvs = torch.empty(n, B, P, 2 * d, dtype=C.cd, device=dev)          # self-attention K/V caches
+    logits = torch.empty(B, P, Vp, dtype=torch.float32, device=dev)
+    tokens = torch.empty(B, L0 + steps, dtype=torch.int64, device=dev)
+    tokens[:, :L0] = x.to(device=dev, dtype=torch.int64)
+    cur = tokens[:, 0].contiguous()
+    scale = d ** -0.5
+    for t in range(P):
+        xs = torch.empty(B, d, dtype=torch.float32, device=dev)
+        K.embed_fwd(cur, dec._embedding.weight.data, pe[t:t + 1], xs, 1)
+        for l, layer in enumerate(dec._layers):
+            mha, cr = layer._mask_attention, layer._cross_attention
+            # masked self-attention: the new position's K/V join the cache, its query attends to positions 0..t
+            h, _, _ = Bk.ln_fwd(C, xs, layer._norm1)
+            q = torch.empty(B, d, dtype=C.cd, device=dev)
+            wqkv, bqkv = C.W(mha.wqkv), mha.bqkv.data
+            K.linear(h, wqkv[:d], q, bias=bqkv[:d])
+            cache = kvs[l]
+            K.gemm(h, wqkv[d:], cache[:, t], B, 2 * d, d, lda=d, ldb=d, ldc=P * 2 * d, bias=bqkv[d:])
+            o = torch.empty(B, d, dtype=C.cd, device=dev)
+            st = ((d, d), (2 * d, P * 2 * d), (2 * d, P * 2 * d), (d, d))
+            Bk.attn_fwd(C, q, cache, cache[:, :, d:], o, B, H, 1, t + 1, dh, st, scale, MaskSpec())
+            x1 = torch.empty(B, d, dtype=torch.float32, device=dev)
+            K.linear(o, C.W(mha._out_linear.weight), x1, bias=mha._out_linear.bias.data, resid=xs, ld_resid=d)
+            # cross-attention over the encoder output (no mask, model.py:71)
+            h2, _, _ = Bk.ln_fwd(C, x1, layer._norm2)
+            q2 = torch.empty(B, d, dtype=C.cd, device=dev)
+            K.linear(h2, C.W(cr.wq), q2, bias=cr.bq.data)
+            o2 = torch.empty(B, d, dtype=C.cd, device=dev)
+            kv_l = kvx[:, l * 2 * d:]
+            st2 = ((d, d), (n * 2 * d, Te * n * 2 * d), (n * 2 * d, Te * n * 2 * d), (d, d))
+            Bk.attn_fwd(C, q2, kv_l, kv_l[:, d:], o2, B, H, 1, Te, dh, st2, scale, MaskSpec())
+            x2 = torch.empty(B, d, dtype=torch.float32, device=dev)
+            K.linear(o2, C.W(cr._out_linear.weight), x2, bias=cr._out_linear.bias.data, resid=x1, ld_resid=d)
+            xs, _ = Bk.ffn_fwd(C, x2, layer._norm3, layer._feedforward)
+        hc = torch.empty(B, d, dtype=C.cd, device=dev)       # no final LayerNorm in evaluate (model.py:142)
+        K.cast(xs, hc)
+        lg = logits[:, t]
+        K.gemm(hc, C.W(cls.weight), lg, B, Vp, d, lda=d, ldb=d, ldc=P * Vp)
+        if t + 1 >= L0:
+            K.greedy_argmax(lg, V, tokens[:, t + 1], cur)
+        else:
+            cur = tokens[:, t + 1].contiguous()
+    tok = tokens.cpu()
+    eos = dec._eos_token_id
+    probs = []
+    for s in range(B):
+        for i in range(1, steps + 1):
+            Li = L0 + i - 1                                  # input length at step i
+            if int(tok[s, Li]) == eos or i == steps:
+                probs.append(logits[s:s + 1, :Li - 1, :V].squeeze())
+    return tokens[B - 1:B].to(x.dtype), probs
 
 
 @torch.no_grad()

@@ -547,6 +547,14 @@ def cast(src, dst):
     call("asrx_cast", code(src), src.data_ptr(), code(dst), dst.data_ptr(), src.numel(), stream())
 
 
+def greedy_argmax(logits, V, tok_col, cur=None):
+    """tok_col[r] (a strided int64 column view) = cur[r] = first argmax of logits[r, :V] (fp32 [rows, ld])."""
+    _cuda(logits, tok_col, cur)
+    rows = logits.shape[0]
+    call("asrx_greedy_argmax", logits.data_ptr(), rows, V, logits.stride(0), tok_col.data_ptr(),
+         tok_col.stride(0), _p(cur), stream())
+
+
 def sum_chunks_bf16(recv, world, chunk, out):
     """out[i] = bf16(sum_w recv[w * chunk + i]) with an fp32 sum (bf16-wire gradient exchange, asrx.dist)."""
     _cuda(recv, out)

@@ -1082,6 +1082,45 @@ extern "C" int asrx_cross_entropy(const float* logits, int64_t rows, int32_t V, 
   return ASRX_OK;
 }
 
+// Greedy decode (Decoder.evaluate, model.py:144: prob.argmax(dim=-1)[:, -1]): the next token of every row of the
+// step's logits, first index of the maximum (torch.argmax's tie rule), written into the token matrix column
+// (tok[r * tok_stride]) and into the next step's input vector cur[r].  One wave per row.
+__global__ __launch_bounds__(256) void greedy_argmax_kernel(const float* __restrict__ logits, int64_t rows, int V,
+                                                            int64_t ld, int64_t* __restrict__ tok,
+                                                            int64_t tok_stride, int64_t* __restrict__ cur) {
+  const int l = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const float* x = logits + r * ld;
+  float mx = -INFINITY;
+  int am = V;   // (a row of NaN / -inf only: index 0, as below)
+  for (int c = l; c < V; c += 64) {
+    const float v = x[c];
+    if (v > mx || (am == V && !(v < mx))) { mx = v; am = c; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(mx, o, 64);
+    const int oa = __shfl_xor(am, o, 64);
+    if (om > mx || (om == mx && oa < am)) { mx = om; am = oa; }
+  }
+  if (l == 0) {
+    const int64_t t = am < V ? am : 0;
+    tok[r * tok_stride] = t;
+    if (cur) cur[r] = t;
+  }
+}
+
+extern "C" int asrx_greedy_argmax(const float* logits, int64_t rows, int32_t V, int64_t ld, int64_t* tok,
+                                  int64_t tok_stride, int64_t* cur, void* stream) {
+  if (!logits || !tok || V <= 0 || ld < V || rows < 0) return ASRX_ERR_ARG;
+  if (rows == 0) return ASRX_OK;
+  hipLaunchKernelGGL(greedy_argmax_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+                     logits, rows, (int)V, ld, tok, tok_stride, cur);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
 // Data-parallel gradient exchange on a bf16 wire (asrx.dist, wire="bf16"): after the all-to-all, rank r holds the W
 // peers' bf16 copies of its chunk, [W][c]; out[i] = bf16(sum_w in[w][i]) with the sum kept in fp32 (one rounding).
 __global__ __launch_bounds__(256) void sum_chunks_bf16_kernel(const bf16_t* __restrict__ in, int W, int64_t c,

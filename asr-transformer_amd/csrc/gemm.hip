@@ -690,7 +690,10 @@ ASRX_DEV void p4_body(const GemmArgs& g, const TileSeq tl, int split, int z, uns
     for (int c = threadIdx.x * 4; c < g.N; c += P_THREADS * 4) *(f4_t*)(lb + c) = *(const f4_t*)(g.bias + c);
     __syncthreads();
   }
-  constexpr bool PRE = EpiPre<EPI, TN, TM>::ANY;
+  // the 256x256 tiles read their epilogue's memory operands (gate bits) in place instead of prefetching them at
+  // the last K-step: the prefetch held 16+ VGPRs beside the 128 accumulators (scratch spills) and, with two ring
+  // stages, deferring the next stage behind the epilogue left no load in flight across it
+  constexpr bool PRE = BN == 256 ? false : EpiPre<EPI, TN, TM>::ANY;
   // prologue: stages 0 .. NST - 1 (stage s + NST is issued in the middle of step s), wait for stage 0
   P4_ISSUE_NEXT();
   if (total > 1) P4_ISSUE_NEXT();

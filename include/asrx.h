@@ -281,6 +281,12 @@ int asrx_cross_entropy(const float* logits, int64_t rows, int32_t V, int64_t ld,
  * ------------------------------------------------------------------------------------------------- */
 int asrx_cast(int32_t src_dtype, const void* src, int32_t dst_dtype, void* dst, int64_t n, void* stream);
 
+/* Greedy decode step (Decoder.evaluate, model.py:144 `prob.argmax(dim=-1)[:, -1]`): for each of `rows` logit rows
+ * (fp32, row stride ld, V used columns) the first index of the maximum, stored as int64 at tok[r * tok_stride] and,
+ * if cur != NULL, at cur[r] (the next step's embedding input). */
+int asrx_greedy_argmax(const float* logits, int64_t rows, int32_t V, int64_t ld, int64_t* tok, int64_t tok_stride,
+                       int64_t* cur, void* stream);
+
 /* Data-parallel gradient exchange on a bf16 wire (asrx.dist.GradAllReduce, wire="bf16"; the reference trains on one
  * device, train.py:16-35, so this is the build's own DDP step): in = the W peers' bf16 copies of one chunk of c
  * elements, [world][chunk]; out[i] = bf16(sum over w of in[w][i]) with the sum in fp32 and one final rounding. */

@@ -173,6 +173,39 @@ def test_greedy_decode_c1(golden_dir):
     assert relerr(probs[-1], g["greedy_last_probs"]) < 1e-4
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("prefix", [1, 3])
+def test_greedy_decode_cache_equals_recompute(precision, prefix):
+    """The KV-cached batched decode (eval) returns what the reference's per-sample full-prefix recomputation
+    returns (model.py:125-151, restated as functions._decoder_evaluate_recompute): the same last-sample token row,
+    the same number of EOS/final-step logits snapshots, each of the same shape and value; also with a multi-token
+    prompt (prefill through the cache)."""
+    from asrx.functions import _decoder_evaluate_cached, _decoder_evaluate_recompute
+    m, cfg = build("c1", precision, seed=3)
+    m.eval()
+    g = torch.Generator().manual_seed(5)
+    B, Te, d = 3, 24, cfg.d_model
+    enc = (torch.randn(B, Te, d, generator=g)).to(dev)
+    x = torch.randint(5, cfg.vocab_size, (B, prefix), generator=g, dtype=torch.int64)
+    x[:, 0] = 1
+    x = x.to(torch.int32).to(dev)
+    dec = m.decoder
+    dec._eos_token_id = int(torch.randint(5, cfg.vocab_size, (1,), generator=g))   # EOS hits do occur
+    # the last input holds prefix + seq_len - 1 tokens; the PE table (layers.py:73) bounds it, as in the reference
+    dec._seq_len = min(dec._seq_len, dec._pe.pe.shape[1] - prefix + 1)
+    with torch.no_grad():
+        row_c, probs_c = _decoder_evaluate_cached(dec, x, enc)
+        row_r, probs_r = _decoder_evaluate_recompute(dec, x, enc)
+    assert row_c.dtype == row_r.dtype and row_c.shape == row_r.shape
+    assert torch.equal(row_c.cpu(), row_r.cpu())
+    assert len(probs_c) == len(probs_r)
+    tol = 1e-5 if precision == "fp32" else 2e-2
+    for a, b in zip(probs_c, probs_r):
+        assert a.shape == b.shape
+        if a.numel():
+            assert relerr(a, b) < tol
+
+
 @pytest.mark.parametrize("precision,tol", [("fp32", 1e-4), ("bf16", 2e-2)])
 def test_submodules_golden(golden_dir, precision, tol):
     """Standalone drop-in MHA / FeedForward / LayerNorm / EncoderLayer / DecoderLayer (micro config)."""

@@ -30,6 +30,10 @@ SHAPES = [
     ("ffn1 wgrad", "wgrad", 2048, 512, 15936),
     ("ffn2 wgrad", "wgrad", 512, 2048, 15936),
     ("xkv wgrad", "wgrad", 12288, 512, 15936),
+    # the step's fused epilogues: FFN1 forward (bias, ReLU, dropout 0.1, 1-bit ReLU mask out) and the FFN2 data
+    # gradient gated by those bits (alpha = 1/0.9)
+    ("ffn1 fwd epi", "fwdepi", 15936, 2048, 512),
+    ("ffn2 dgrad gated", "dgradg", 15936, 512, 2048),
 ]
 
 
@@ -99,6 +103,31 @@ def main():
             for v in variants:
                 kk, fb = kb(v)
                 dbg_runs(res, v, lambda: K.linear_dgrad(dy, w, y, kernel=kk), fb)
+        elif kind == "fwdepi":
+            x, w = rnd(M, Kd), rnd(N, Kd)
+            bias = torch.randn(N, device="cuda", generator=g)
+            y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            bits = torch.empty(M, N // 32, device="cuda", dtype=torch.int32)
+            for v in variants:
+                kk, fb = kb(v)
+                dbg_runs(res, v, lambda: K.linear(x, w, y, bias=bias, relu=True, dropout_p=0.1, seed=5,
+                                                  mask_out=bits, ld_mask=N // 32, kernel=kk), fb)
+                K.call("asrx_gemm_set_debug", fb)
+                res[v + ":relu"] = timeit(lambda: K.linear(x, w, y, bias=bias, relu=True, kernel=kk), args.reps,
+                                          args.rounds)
+                res[v + ":relu+drop"] = timeit(lambda: K.linear(x, w, y, bias=bias, relu=True, dropout_p=0.1, seed=5,
+                                                                kernel=kk), args.reps, args.rounds)
+                res[v + ":relu+mask"] = timeit(lambda: K.linear(x, w, y, bias=bias, relu=True, mask_out=bits,
+                                                                ld_mask=N // 32, kernel=kk), args.reps, args.rounds)
+                K.call("asrx_gemm_set_debug", 0)
+        elif kind == "dgradg":   # out [M, Kd] = dy [M, N] . w [N, Kd], gated by bits of [M, Kd]
+            dy, w = rnd(M, N), rnd(N, Kd)
+            y = torch.empty(M, Kd, device="cuda", dtype=torch.bfloat16)
+            bits = torch.randint(-2 ** 31, 2 ** 31 - 1, (M, Kd // 32), device="cuda", dtype=torch.int32)
+            for v in variants:
+                kk, fb = kb(v)
+                dbg_runs(res, v, lambda: K.linear_dgrad(dy, w, y, alpha=1 / 0.9, gate=bits, ld_gate=Kd // 32,
+                                                        gate_bits=True, kernel=kk), fb)
         else:   # wgrad: C[M=N_out, N=K_in] over the Kd rows
             dy, x = rnd(Kd, M), rnd(Kd, N)
             cb = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)

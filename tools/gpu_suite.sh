@@ -29,9 +29,9 @@ for step in "$@"; do
     smoke)   run smoke 300 python __graft_entry__.py smoke ;;
     bench)   run bench 900 python bench.py --steps 10 --warmup 3 ;;
     benchq)  run benchq 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
-    prof)    run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-probe --no-sub ;;
-    pmcf)    run pmcf 900 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcf -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-probe --no-sub ;;
-    pmcw)    run pmcw 900 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmcw -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-probe --no-sub ;;
+    prof)    run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-probe --no-sub --no-other ;;
+    pmcf)    run pmcf 900 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcf -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-probe --no-sub --no-other ;;
+    pmcw)    run pmcw 900 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmcw -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-probe --no-sub --no-other ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

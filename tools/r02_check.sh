@@ -23,7 +23,7 @@ for step in "$@"; do
     benchq) run benchq 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     bench)  run bench 900 python bench.py --steps 20 --warmup 5 ;;
     eager)  run eager 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-sub --no-graph ;;
-    prof)   run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 3 --no-cpu-baseline --no-probe --no-sub ;;
+    prof)   run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 3 --no-cpu-baseline --no-probe --no-sub --no-other ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

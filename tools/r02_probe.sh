@@ -13,12 +13,14 @@ for s in "$@"; do
     pmcg) for f in 0 9; do step pmcg$f 120 timeout -s KILL 100 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS GRBM_GUI_ACTIVE -d gpurun_out/pmcg$f -o run --output-format csv -- python3 tools/blas_ref.py --dbg $f --only "ffn1 fwd" --variants p4 --nobias --nogrouped --noblas --reps 5 --rounds 2; done ;;
     gemmt16) ASRX_GEMM_DBG=16 step gemmt16 600 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 300 --timeout-method thread -m gpu -k "gemm" ;;
     parity) step parity 600 python -u -m pytest tests/test_gpu_train_parity.py tests/test_gpu_graph.py -x -q --timeout 300 --timeout-method thread -m gpu ;;
-    benchab) for k in p3 p4 p3 p4; do ASRX_WGRAD_KIND=$k step bench_$k 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-sub; grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench_$k.log; done ;;
+    benchab) for k in p3 p4 p3 p4; do ASRX_WGRAD_KIND=$k step bench_$k 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-sub --no-other; grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench_$k.log; done ;;
     other) step other 400 python -c "import bench, json; print(json.dumps(bench.other_configs()))" ;;
     attnt) step attnt 600 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 300 --timeout-method thread -m gpu -k "attention" ;;
+    blasepi) step blasepi 300 python tools/blas_ref.py --dbg 0,1 --variants p3,p4 --nobias --nogrouped --only "ffn1 fwd epi,ffn2 dgrad gated,ffn1 fwd,qkv fwd" ;;
+    decode) step decode 600 python -u -m pytest tests/test_gpu_model.py -x -v --timeout 300 --timeout-method thread -m gpu -k "greedy" ;;
     counters) step counters 120 rocprofv3 -L ;;
-    prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 3 --no-cpu-baseline --no-probe --no-sub ;;
-    pmcm) step pmcm 300 timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/pmcm -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-graph --no-cpu-baseline --no-probe --no-sub && python3 tools/pmc_mfma.py gpurun_out/pmcm/run_counter_collection.csv --out gpurun_out/c3_pmc_mfma.json ;;
+    prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 3 --no-cpu-baseline --no-probe --no-sub --no-other ;;
+    pmcm) step pmcm 300 timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/pmcm -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-graph --no-cpu-baseline --no-probe --no-sub --no-other && python3 tools/pmc_mfma.py gpurun_out/pmcm/run_counter_collection.csv --out gpurun_out/c3_pmc_mfma.json ;;
     *) echo "unknown $s"; exit 2 ;;
   esac
 done
