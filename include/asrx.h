@@ -281,6 +281,18 @@ int asrx_cross_entropy(const float* logits, int64_t rows, int32_t V, int64_t ld,
  * ------------------------------------------------------------------------------------------------- */
 int asrx_cast(int32_t src_dtype, const void* src, int32_t dst_dtype, void* dst, int64_t n, void* stream);
 
+/* Power spectrogram of a batch of waveforms (the featuriser of modules/dataset.py:34-55:
+ * torchaudio.transforms.Spectrogram(n_fft, center=False) -> |STFT|^power):
+ *   audio  fp32 [batch][samples] (row stride batch_stride), frames = (samples - n_fft) / hop + 1
+ *   basis  fp32 [2 nbins][n_fft]: rows 2n / 2n+1 = window[k] * cos / -sin(2 pi n k / n_fft) (the caller's window,
+ *          zero-padded to n_fft as torch.stft does; see asrx.features)
+ *   out    fp32 [batch][nbins][frames] = scale * (re^2 + im^2)^(power/2), power 1 or 2
+ *   ws     fp32 workspace of >= batch * frames * 2 nbins elements (the DFT GEMM's output)
+ * One fp32 MFMA GEMM (frames as overlapping rows of the waveform, lda = hop) plus a square/transpose pass. */
+int asrx_spectrogram(const float* audio, int64_t batch, int64_t samples, int64_t batch_stride, const float* basis,
+                     int32_t n_fft, int32_t hop, int32_t nbins, int32_t power, float scale, float* ws,
+                     int64_t ws_elems, float* out, void* stream);
+
 /* Greedy decode step (Decoder.evaluate, model.py:144 `prob.argmax(dim=-1)[:, -1]`): for each of `rows` logit rows
  * (fp32, row stride ld, V used columns) the first index of the maximum, stored as int64 at tok[r * tok_stride] and,
  * if cur != NULL, at cur[r] (the next step's embedding input). */
