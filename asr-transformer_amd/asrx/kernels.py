@@ -349,7 +349,7 @@ def linear_wgrad_grouped(items, *, beta=1.0, kind=None):
     common.alpha, common.beta = 1.0, beta
     p3 = _grouped_p3_ok(items, beta)
     kind = kind or WGRAD_KIND
-    kname = ((GROUPED_P4_KERNELS if kind == "p4" else GROUPED_P3_KERNELS)[beta == 1.0] if p3
+    kname = ({"p4": GROUPED_P4_KERNELS}.get(kind, GROUPED_P3_KERNELS)[beta == 1.0] if p3
              else GROUPED_TABLE_KERNEL)
     probe = PROBE
     if probe is not None and probe.active and probe.log is not None:

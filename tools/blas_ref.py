@@ -59,6 +59,7 @@ def main():
     ap.add_argument("--dbg", default="0", help="comma list of asrx_gemm_set_debug flags to time (diagnostics)")
     ap.add_argument("--only", default="", help="comma list of shape names")
     ap.add_argument("--nobias", action="store_true")
+    ap.add_argument("--wgrad", default="p3,p4,p5", help="grouped weight-gradient kinds to time")
     ap.add_argument("--nogrouped", action="store_true")
     ap.add_argument("--noblas", action="store_true")
     args = ap.parse_args()
@@ -148,7 +149,7 @@ def main():
                           torch.zeros(n_out, device="cuda")))
     flops = sum(2.0 * rows * it[0].shape[1] * it[1].shape[1] for it in items)
     line = f"grouped wgrad, 12 encoder layers ({flops / 1e12:.3f} TFLOP)"
-    for v in ("p3", "p3+16", "p4"):
+    for v in args.wgrad.split(","):
         kk, fb = kb(v)
         for f in dbg:
             K.call("asrx_gemm_set_debug", f | fb)
