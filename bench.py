@@ -264,10 +264,12 @@ def other_configs(names=("c2", "c5"), reps=5):
     """The BASELINE.json forward configs beside the headline step, timed after it: c2 (configs[1]: fp32 forward,
     B=32, T=512, 6+6 layers d256) against the fp32 matrix peak and c5 (configs[4]: bf16 forward, B=16, T=4000 ->
     T'=999, the tiled attention path of the long utterances) against the bf16 MFMA peak, as frames/s of the
-    teacher-forced forward (model.eval(), no_grad; HIP events around `reps` forwards after 2 warm-up ones), plus the
+    teacher-forced forward (model.eval(), no_grad, replayed from a HIP graph by asrx.infer.GraphedForward; HIP
+    events around `reps` forwards after 2 warm-up ones; the eager time is reported beside it), plus the
     c5 encoder self-attention forward kernel alone (B*H=128, 999x999, dh=64; graph replay, cold buffers)."""
     import asrx
     from asrx import kernels as K
+    from asrx.infer import GraphedForward
     from asrx.kernels import MaskSpec
     from oracle.ref_model import CONFIGS, synthetic_batch
     out = {}
@@ -282,6 +284,7 @@ def other_configs(names=("c2", "c5"), reps=5):
                                  precision=prec).cuda().eval()
         s, t, m = synthetic_batch(cfg, B, T, L + 1, seed=4321)
         s, t, m = s.cuda(), t[:, :-1].cuda(), m[:, :-1].cuda()
+        fwd = GraphedForward(model)           # HIP-graph replay (asrx.infer): no per-launch host cost
         with torch.no_grad():
             for _ in range(2):
                 model(s, t, m)
@@ -292,6 +295,15 @@ def other_configs(names=("c2", "c5"), reps=5):
                 model(s, t, m)
             e1.record()
             e1.synchronize()
+            ms_eager = e0.elapsed_time(e1) / reps
+            fwd(s, t, m)
+            fwd(s, t, m)
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(reps):
+                fwd(s, t, m)
+            e1.record()
+            e1.synchronize()
         ms = e0.elapsed_time(e1) / reps
         fps = B * T / (ms * 1e-3)
         tf = FWD_MFLOP_PER_FRAME[name] * 1e6 * B * T / (ms * 1e-3) / 1e12
@@ -299,7 +311,8 @@ def other_configs(names=("c2", "c5"), reps=5):
         out[name] = {"metric": "frames/s (teacher-forced forward)", "value": round(fps, 1), "ms_per_forward": round(ms, 3),
                      "dtype": "f32" if prec == "fp32" else "bf16", "batch": B, "frames": T, "text_len": L,
                      "achieved_tflops": round(tf, 1), "peak_tflops": peak, "frac": round(tf / peak, 4),
-                     "flop_basis": f"{FWD_MFLOP_PER_FRAME[name]} MFLOP/frame (SURVEY 8(d))"}
+                     "flop_basis": f"{FWD_MFLOP_PER_FRAME[name]} MFLOP/frame (SURVEY 8(d))",
+                     "ms_per_forward_eager": round(ms_eager, 3), "graph": True}
         del model
         torch.cuda.empty_cache()
     if "c5" in names:   # the tiled (Lk > 256) attention forward alone at the c5 encoder shape

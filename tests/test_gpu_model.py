@@ -333,3 +333,21 @@ def test_bf16_training_reduces_loss():
         opt.step()
         losses.append(float(loss))
     assert losses[-1] < 0.7 * losses[0], losses
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_graphed_forward_equals_eager(precision):
+    """asrx.infer.GraphedForward: replayed forwards equal the eager forward bit for bit, for new inputs of the
+    captured shape, and a new shape captures a new graph."""
+    from asrx.infer import GraphedForward
+    m, cfg = build("c1", precision, seed=2)
+    m.eval()
+    fwd = GraphedForward(m)
+    for seed, B in ((1, 2), (2, 2), (3, 3)):
+        s, t, k = synthetic_batch(cfg, B, CONFIGS["c1"]["frames"], CONFIGS["c1"]["text_len"] + 1, seed=seed)
+        s, t, k = s.to(dev), t[:, :-1].to(dev), k[:, :-1].to(dev)
+        with torch.no_grad():
+            ref = m(s, t, k).clone()
+        got = fwd(s, t, k)
+        assert torch.equal(got, ref)
+    assert len(fwd._graphs) == 2
