@@ -17,6 +17,19 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: longer CPU test")
 
 
+@pytest.fixture(autouse=True)
+def _reset_dropout_seed_offset(request):
+    """A Trainer step leaves the device-resident dropout seed offset at its step count (asrx_set_seed_offset);
+    kernel tests compare keep bits with rng_ref at offset 0, so every GPU test starts from offset 0."""
+    if request.node.get_closest_marker("gpu") is not None:
+        import torch
+        if torch.cuda.is_available():
+            from asrx import kernels as K
+            K.set_seed_offset(0)
+            torch.cuda.synchronize()
+    yield
+
+
 @pytest.fixture(scope="session")
 def golden_dir():
     return GOLDEN
