@@ -1133,8 +1133,9 @@ __global__ __launch_bounds__(256) void sum_chunks_bf16_kernel(const bf16_t* __re
 }
 
 extern "C" int asrx_sum_chunks_bf16(const void* in, int32_t world, int64_t chunk, void* out, void* stream) {
-  if (!in || !out || world < 1 || chunk < 0) return ASRX_ERR_ARG;
-  if (chunk == 0) return ASRX_OK;
+  if (world < 1 || chunk < 0) return ASRX_ERR_ARG;
+  if (chunk == 0) return ASRX_OK;   // empty buckets may carry null pointers
+  if (!in || !out) return ASRX_ERR_ARG;
   hipLaunchKernelGGL(sum_chunks_bf16_kernel, dim3(grid_for(chunk)), dim3(256), 0, (hipStream_t)stream,
                      (const bf16_t*)in, (int)world, chunk, (bf16_t*)out);
   ASRX_CHECK_LAUNCH();
