@@ -90,6 +90,7 @@ SIGNATURES = {
     "asrx_gemm": [ctypes.POINTER(GemmDesc), c_vp],
     "asrx_gemm_kernel_name": [ctypes.POINTER(GemmDesc), ctypes.c_char_p, c_i32],
     "asrx_gemm_set_debug": [c_i32],
+    "asrx_set_tuning": [c_i32, c_i32],
     "asrx_gemm_grouped_xcd": [ctypes.POINTER(GemmDesc), c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp],
     "asrx_reduce_rows_grouped": [ctypes.POINTER(RowsumGroup), c_i32, c_vp],
     "asrx_attention_fwd": [ctypes.POINTER(AttnDesc), c_vp],

@@ -683,6 +683,15 @@ def adam_hyper(hyp, lr, beta1, beta2, step):
     upload(hyp, np.array([lr, 1.0 - beta1 ** step, 1.0 - beta2 ** step], dtype=np.float32))
 
 
+TUNE_KEYS = {"softmax_u": 1, "ln_rw": 2}
+
+
+def set_tuning(name, value):
+    """Process-wide kernel-variant override (asrx_set_tuning): "softmax_u" in (1, 2, 4), "ln_rw" in (1, 2, 4);
+    0 restores the environment / default choice.  Every variant computes the same values."""
+    call("asrx_set_tuning", TUNE_KEYS[name], int(value))
+
+
 def set_seed_offset(offset):
     """Per-step device-resident dropout seed offset (asrx_set_seed_offset), on the current stream."""
     call("asrx_set_seed_offset", int(offset) & _U64, stream())

@@ -72,11 +72,12 @@ struct AttnArgs {
   int dbg;   // phase timestamps of block 0 / wave 0 into g_attn_dbg (tools only; ASRX_ATTN_DBG=1)
 };
 
-__device__ unsigned long long g_attn_dbg[64 + 4 * 1024];   // [64..]: per-block real-time (fwd)
+__device__ unsigned long long g_attn_dbg[128 + 4 * 1024];   // [128..]: per-block real-time (fwd)
 #define FWD_TS(i) do { if (a.dbg && threadIdx.x == 0) sdbg[(i)] = __builtin_amdgcn_s_memtime(); } while (0)
 #define FWD_RT(i) do { if (a.dbg && threadIdx.x == 0) sdbg[(i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#define ATTN_TS(i) do { if (a.dbg && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && (i) < 64) \
-                          g_attn_dbg[(i)] = __builtin_amdgcn_s_memtime(); } while (0)
+// backward: wave 0 -> [i], wave 4 -> [64 + i] (block 0)
+#define ATTN_TS(i) do { if (a.dbg && blockIdx.x == 0 && blockIdx.y == 0 && (threadIdx.x & 255) == 0 && (i) < 64) \
+                          g_attn_dbg[(i) + (threadIdx.x >> 8) * 64] = __builtin_amdgcn_s_memtime(); } while (0)
 
 ASRX_DEV bool masked(const AttnArgs& a, int b, int q, int key) {
   if (key >= a.Lk) return true;
@@ -469,6 +470,11 @@ ASRX_DEV uint32_t ldu8_asm(const void* p) {
   return r;
 }
 template <typename T> ASRX_DEV void pin(T& x) { asm volatile("" : "+v"(x)); }
+ASRX_DEV void pin(uint4& x) {
+  s8_t t = __builtin_bit_cast(s8_t, x);
+  asm volatile("" : "+v"(t));
+  x = __builtin_bit_cast(uint4, t);
+}
 ASRX_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 ASRX_DEV f4_t mfma32(s8_t a, s8_t b, f4_t c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
@@ -732,10 +738,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
   if (a.dbg && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
     for (int i = 0; i < 12; ++i) g_attn_dbg[44 + i] = sdbg[i];
   if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0 && bh < 1024) {
-    g_attn_dbg[64 + 4 * bh] = sdbg[12];
-    g_attn_dbg[65 + 4 * bh] = sdbg[13];
-    g_attn_dbg[66 + 4 * bh] = __builtin_amdgcn_s_memrealtime();
-    g_attn_dbg[67 + 4 * bh] = __smid();
+    g_attn_dbg[128 + 4 * bh] = sdbg[12];
+    g_attn_dbg[129 + 4 * bh] = sdbg[13];
+    g_attn_dbg[130 + 4 * bh] = __builtin_amdgcn_s_memrealtime();
+    g_attn_dbg[131 + 4 * bh] = __smid();
   }
 }
 
@@ -977,28 +983,41 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
   // piece, dot the 8 elements and reduce over the row's 8 pieces (adjacent lanes) — no separate delta pass.
   const bf16_t* Ob = a.o + b * a.ob + h * 64;
   const bf16_t* Olb = a.o_lo ? a.o_lo + b * a.ob + h * 64 : nullptr;
-  uint4 preo[PRE], prel[PRE];
+  uint4 preo[PRE] = {}, prel[PRE] = {};
+  // The prefetch is inline-asm loads, waited for by one vmcnt(0) at the start of publish (the compiler does not
+  // count them): with compiler-tracked loads, its conservative merge at the loop head put a vmcnt(0) in front of
+  // the next fetch, which also waited for the dQ stores of the previous chunk (≈1k cycles per chunk).
   auto fetch = [&](int ch) {
     const int q0 = ch * 32;
     if (usebits) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t) dwn[t] = dmb[(int64_t)ch * a.Lk + keyc[t]];
+      for (int t = 0; t < 2; ++t) dwn[t] = ld32_asm(dmb + (int64_t)ch * a.Lk + keyc[t]);
     }
 #pragma unroll
     for (int i = 0; i < PRE; ++i) {
       const int c = tid + NTHR * i;
       const int which = c >> 8, row = (c >> 3) & 31, dc = (c & 7) * 8;
       const int q = min(q0 + row, a.Lq - 1);
-      pre[i] = *(const uint4*)((which ? Db + (int64_t)q * a.dor : Qb + (int64_t)q * a.qr) + dc);
+      pre[i] = __builtin_bit_cast(uint4, ld128_asm((which ? Db + (int64_t)q * a.dor : Qb + (int64_t)q * a.qr) + dc));
       if (which) {
-        preo[i] = *(const uint4*)(Ob + (int64_t)q * a.orr + dc);
-        if (Olb) prel[i] = *(const uint4*)(Olb + (int64_t)q * a.orr + dc);
+        preo[i] = __builtin_bit_cast(uint4, ld128_asm(Ob + (int64_t)q * a.orr + dc));
+        if (Olb) prel[i] = __builtin_bit_cast(uint4, ld128_asm(Olb + (int64_t)q * a.orr + dc));
       }
     }
-    if (tid < 32) praw = lseb[min(q0 + tid, a.Lq - 1)];
+    if (tid < 32) praw = __uint_as_float(ld32_asm(lseb + min(q0 + tid, a.Lq - 1)));
   };
   auto publish = [&](int buf, int ch) {
     const int q0 = ch * 32;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < PRE; ++i) {
+      pin(pre[i]);
+      pin(preo[i]);
+      pin(prel[i]);
+    }
+    pin(praw);
+    pin(dwn[0]);
+    pin(dwn[1]);
 #pragma unroll
     for (int i = 0; i < PRE; ++i) {
       const int c = tid + NTHR * i;
@@ -1168,6 +1187,7 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
     }
     ATTN_TS(3 + 4 * ch);
     if (ch + 1 < nch) publish(buf ^ 1, ch + 1);
+    ATTN_TS(5 + 4 * ch);
     __syncthreads();
     ATTN_TS(4 + 4 * ch);
   }
@@ -1379,7 +1399,7 @@ extern "C" int asrx_attention_bwd(const asrx_attn_desc* d, void* stream) {
 
 // tools only (not part of include/asrx.h): copy the phase timestamps of the last debug launch
 extern "C" int asrx_attn_debug_read(unsigned long long* host, int n) {
-  if (!host || n < 0 || n > 64 + 4 * 1024) return ASRX_ERR_ARG;
+  if (!host || n < 0 || n > 128 + 4 * 1024) return ASRX_ERR_ARG;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_attn_dbg), sizeof(unsigned long long) * n) == hipSuccess ? ASRX_OK
                                                                                                        : ASRX_ERR_LAUNCH;
 }

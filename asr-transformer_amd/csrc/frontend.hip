@@ -1132,6 +1132,17 @@ __global__ __launch_bounds__(256) void sum_chunks_bf16_kernel(const bf16_t* __re
   }
 }
 
+int g_tune_softmax_u = 0;
+int g_tune_ln_rw = 0;
+
+extern "C" int asrx_set_tuning(int32_t key, int32_t value) {
+  if (value != 0 && value != 1 && value != 2 && value != 4) return ASRX_ERR_ARG;
+  if (key == ASRX_TUNE_SOFTMAX_U) g_tune_softmax_u = value;
+  else if (key == ASRX_TUNE_LN_RW) g_tune_ln_rw = value;
+  else return ASRX_ERR_ARG;
+  return ASRX_OK;
+}
+
 extern "C" int asrx_sum_chunks_bf16(const void* in, int32_t world, int64_t chunk, void* out, void* stream) {
   if (world < 1 || chunk < 0) return ASRX_ERR_ARG;
   if (chunk == 0) return ASRX_OK;   // empty buckets may carry null pointers

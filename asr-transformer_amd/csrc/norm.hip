@@ -254,11 +254,12 @@ template <int CH, int NJ>
 bool ln_fwd_launch(int x_dtype, const void* x, int y_dtype, void* y, const float* gamma, const float* beta,
                    float* mean, float* rstd, int64_t rows, int d, float eps, hipStream_t st) {
   if (d != CH * NJ * 64) return false;
-  static const int rw = [] {   // rows per wave (ASRX_LN_RW = 1, 2 or 4; default 2: 9.4 -> 8.6 us at 15936 x 512)
+  static const int rw_env = [] {   // rows per wave (ASRX_LN_RW = 1, 2 or 4; default 2: 9.4 -> 8.6 us at 15936 x 512)
     const char* e = getenv("ASRX_LN_RW");
     const int v = e ? atoi(e) : 2;
     return (v == 1 || v == 4) ? v : 2;
   }();
+  const int rw = g_tune_ln_rw ? g_tune_ln_rw : rw_env;
   const unsigned blocks = (unsigned)((rows + 4 * rw - 1) / (4 * rw));
   if (rw == 4)
     hipLaunchKernelGGL((ln_fwd_kernel<CH, NJ, 4>), dim3(blocks), dim3(256), 0, st, x_dtype, x, y_dtype, y, gamma, beta,

@@ -250,12 +250,12 @@ bool dispatch_u(const SmArgs& a, bool bwd, void* ds, hipStream_t st) {
 }
 
 int softmax_u() {
-  static const int u = [] {
+  static const int env = [] {
     const char* e = getenv("ASRX_SOFTMAX_U");
     const int v = e ? atoi(e) : 1;
     return (v == 2 || v == 4) ? v : 1;
   }();
-  return u;
+  return g_tune_softmax_u ? g_tune_softmax_u : env;
 }
 
 template <int V>

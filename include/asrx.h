@@ -120,6 +120,14 @@ int asrx_gemm_kernel_name(const asrx_gemm_desc* d, char* buf, int32_t len);
  * operand loads (compute on stale LDS); 0 = normal.  Results are garbage while any flag is set. */
 int asrx_gemm_set_debug(int32_t flags);
 
+/* Process-wide kernel-variant switches (override the environment variables named; value 0 = back to the
+ * environment / default).  key ASRX_TUNE_SOFTMAX_U: rows per lane group of the short-row softmax kernels (1, 2, 4;
+ * ASRX_SOFTMAX_U); key ASRX_TUNE_LN_RW: rows per wave of the LayerNorm forward (1, 2, 4; ASRX_LN_RW).  Every
+ * variant computes the same values; the switch exists so tests and tools can run each one in one process. */
+#define ASRX_TUNE_SOFTMAX_U 1
+#define ASRX_TUNE_LN_RW 2
+int asrx_set_tuning(int32_t key, int32_t value);
+
 /* ---------------------------------------------------------------------------------------------------
  * Fused multi-head attention (bf16 in/out, fp32 softmax): per (batch b, head h)
  *   S = scale * Q K^T ; masked -> -inf ; P = nan_to_num(softmax(S)) ; O = dropout(P) V

@@ -243,9 +243,25 @@ def test_gemm_batched_heads():
 
 # ------------------------------------------------------------------------------------------------ LayerNorm
 
+@pytest.fixture
+def tuning():
+    """Set a kernel-variant switch (asrx_set_tuning) for one test and restore the default afterwards."""
+    used = []
+
+    def set_(name, value):
+        used.append(name)
+        K().set_tuning(name, value)
+    yield set_
+    for name in used:
+        K().set_tuning(name, 0)
+
+
 @pytest.mark.parametrize("d", [64, 128, 256, 512])
 @pytest.mark.parametrize("ydt", [torch.bfloat16, torch.float32])
-def test_layernorm(d, ydt):
+@pytest.mark.parametrize("rw", [0, 1, 4])
+def test_layernorm(d, ydt, rw, tuning):
+    """rw: rows per wave of the forward (0 = default 2; 1 and 4 are the ASRX_LN_RW variants)."""
+    tuning("ln_rw", rw)
     rows = 333
     g = torch.Generator().manual_seed(d)
     x = torch.randn(rows, d, generator=g) * 2 + 0.5
@@ -453,8 +469,11 @@ def test_attention_dense_mask_and_dropout_consistency(L, attn_variant, bits):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("Lk", [24, 64, 127, 249, 999])
-def test_softmax_masked(dtype, Lk):
+@pytest.mark.parametrize("u", [0, 2, 4])
+def test_softmax_masked(dtype, Lk, u, tuning):
+    """u: rows per lane group of the short-row kernels (0 = default 1; 2 and 4 are the ASRX_SOFTMAX_U variants)."""
     from asrx.kernels import MaskSpec
+    tuning("softmax_u", u)
     B, H, Lq = 2, 3, min(Lk, 70)
     g = torch.Generator().manual_seed(Lk)
     ld = (Lk + 7) // 8 * 8
@@ -482,6 +501,40 @@ def test_softmax_masked(dtype, Lk):
     P = p[..., :Lk].double().cpu()
     G = dpd[..., :Lk].double().cpu()
     ref_ds = P * (G - (P * G).sum(-1, keepdim=True)) * scale
+    assert relerr(ds[..., :Lk].float().cpu(), ref_ds) < tol * 2
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("Lk", [24, 249])
+@pytest.mark.parametrize("u", [0, 4])
+def test_softmax_dropout(dtype, Lk, u, tuning):
+    """Softmax with attention dropout p = 0.3 (layers.py:26): the forward's dropped copy pd = P * keep / (1 - p) and
+    the backward dS = P * (G' - rowsum(P * G')) * scale with G' = dPd * keep / (1 - p), keep from rng_ref.attn_keep."""
+    from asrx.kernels import MaskSpec
+    from rng_ref import attn_keep
+    tuning("softmax_u", u)
+    B, H, Lq, p_drop, seed = 2, 3, min(Lk, 40), 0.3, 0x5EED1234ABCD
+    g = torch.Generator().manual_seed(Lk + 1)
+    ld = (Lk + 7) // 8 * 8
+    s = torch.randn(B * H, Lq, ld, generator=g) * 3
+    sd = s.to(dev, dtype)
+    p = torch.empty_like(sd)
+    pd = torch.empty_like(sd)
+    scale = 0.125
+    K().softmax_fwd(sd, p, pd, B * H, H, Lq, Lk, ld, scale, MaskSpec(), dropout_p=p_drop, seed=seed)
+    keep = torch.from_numpy(attn_keep(seed, B * H, Lq, Lk, p_drop)).double()
+    assert abs(float(keep.mean()) - (1 - p_drop)) < 0.05
+    ref = torch.softmax(sd[..., :Lk].double().cpu() * scale, -1)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert relerr(p[..., :Lk].float().cpu(), ref) < tol
+    P = p[..., :Lk].double().cpu()
+    assert relerr(pd[..., :Lk].float().cpu(), P * keep / (1 - p_drop)) < tol
+    assert torch.equal(pd[..., :Lk].cpu() == 0, keep == 0)   # exactly the dropped elements are zero
+    dpd = torch.randn(B * H, Lq, ld, generator=g).to(dev, dtype)
+    ds = torch.empty_like(sd)
+    K().softmax_bwd(p, dpd, ds, B * H, Lq, Lk, ld, scale, dropout_p=p_drop, seed=seed)
+    Gk = dpd[..., :Lk].double().cpu() * keep / (1 - p_drop)
+    ref_ds = P * (Gk - (P * Gk).sum(-1, keepdim=True)) * scale
     assert relerr(ds[..., :Lk].float().cpu(), ref_ds) < tol * 2
 
 

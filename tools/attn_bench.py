@@ -55,7 +55,7 @@ def timeit(fn, reps):
     """ms per call: reps calls captured in a HIP graph and replayed (no host launch gaps)."""
     sys.path.insert(0, REPO)
     from bench import _graph_time_ms
-    return _graph_time_ms(fn, launches=reps)
+    return _graph_time_ms([fn], launches=reps)
 
 
 def main():
@@ -75,22 +75,21 @@ def main():
         args.only = ",".join(k for k in cases if k.startswith("s"))
     if args.dbg:
         import ctypes
+        os.environ["ASRX_ATTN_DBG"] = "1"   # read once, at the library's first attention call
         from asrx._lib import lib
         for key in args.only.split(","):
             name, fwd, bwd, ff, fb = case(*cases[key])
             fwd()
             bwd()
             torch.cuda.synchronize()
-            os.environ["ASRX_ATTN_DBG"] = "1"
             fwd()
             bwd()
             torch.cuda.synchronize()
-            os.environ.pop("ASRX_ATTN_DBG")
             nb = B * H
-            buf = (ctypes.c_ulonglong * (64 + 4 * nb))()
-            lib().asrx_attn_debug_read(buf, 64 + 4 * nb)
+            buf = (ctypes.c_ulonglong * (128 + 4 * nb))()
+            lib().asrx_attn_debug_read(buf, 128 + 4 * nb)
             ts = list(buf)
-            blk = [ts[64 + 4 * i:68 + 4 * i] for i in range(nb)]
+            blk = [ts[128 + 4 * i:132 + 4 * i] for i in range(nb)]
             t00 = min(x[0] for x in blk)
             pc = lambda v: [int(sorted(v)[int(q * (len(v) - 1))]) for q in (0, .1, .5, .9, 1)]   # noqa: E731
             print(name, "fwd per-block (10 ns ticks; pct 0/10/50/90/100): start", pc([x[0] - t00 for x in blk]),
@@ -106,13 +105,15 @@ def main():
             if f0:
                 print(name, "fwd: staging-issued", ts[45] - f0, " barrier", ts[46] - f0,
                       " tiles", [ts[47 + k] - f0 for k in range(8) if ts[47 + k] >= f0], " end", ts[55] - f0)
-            t0 = ts[0]
-            print(name, "prologue", ts[1] - t0, "cycles")
-            for ch in range(8):
-                a, b, c, d = ts[2 + 4 * ch:6 + 4 * ch]
-                if a == 0 or a < t0:
-                    break
-                print(f"  chunk {ch}: fetch-issued {a - t0:7d}  compute {b - a:6d}  publish+barrier {c - b:6d}  dQ {d - c:6d}")
+            for wv, base in ((0, 0), (4, 64)):
+                t0 = ts[base]
+                print(name, f"bwd wave {wv}: prologue", ts[base + 1] - t0, "cycles")
+                for ch in range(8):
+                    a, b, c, d = ts[base + 2 + 4 * ch:base + 6 + 4 * ch]
+                    if a == 0 or a < t0:
+                        break
+                    print(f"  chunk {ch}: fetch-issued {a - t0:7d}  compute {b - a:6d}  publish {d - b:6d}  "
+                          f"barrier {c - d:6d}")
         return
     for key in args.only.split(","):
         name, fwd, bwd, ff, fb = case(*cases[key])
