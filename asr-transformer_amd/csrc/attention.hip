@@ -1039,9 +1039,10 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
           for (int e = 0; e < 4; ++e)
             dot += bf2f(dd[e] & 0xffff) * bf2f(oo[e] & 0xffff) + bf2f(dd[e] >> 16) * bf2f(oo[e] >> 16);
         }
-        dot += __shfl_xor(dot, 1, 64);
-        dot += __shfl_xor(dot, 2, 64);
-        dot += __shfl_xor(dot, 4, 64);
+        // sum over the row's 8 adjacent lanes by DPP (quad swaps, then the half-row mirror): no LDS round trips
+        dot += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(dot), 0xB1, 0xF, 0xF, true));
+        dot += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(dot), 0x4E, 0xF, 0xF, true));
+        dot += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(dot), 0x141, 0xF, 0xF, true));
         if ((c & 7) == 0) sdel[buf * 32 + row] = qv ? dot : 0.f;
       }
     }

@@ -157,7 +157,9 @@ __global__ __launch_bounds__(256) void softmax_fwd_kernel(SmArgs a) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int k0 = (j * LPR + ll) * V;
-      const int nv = max(0, min(V, a.lk - k0));
+      // padding columns [lk, ld) hold exp2(-inf) = 0 and are stored with the row (whole 16-B stores: a partially
+      // written 32-B HBM sector costs a read-modify-write), except on the last row
+      const int nv = loadable(a, rr, k0, V);
       if (nv <= 0) continue;
       float o[V];
 #pragma unroll
@@ -220,7 +222,7 @@ __global__ __launch_bounds__(256) void softmax_bwd_kernel(SmArgs a, void* ds) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int k0 = (j * LPR + ll) * V;
-      const int nv = max(0, min(V, a.lk - k0));
+      const int nv = loadable(a, rr, k0, V);   // padding (pv = gv = 0 there) stored as zeros, as in the forward
       if (nv <= 0) continue;
       float o[V];
 #pragma unroll

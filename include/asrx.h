@@ -186,6 +186,8 @@ int asrx_attention_bwd(const asrx_attn_desc* d, void* stream);
  *   p = nan_to_num(softmax(scale * s  masked -> -inf)); if pd != NULL also pd = dropout(p)
  * Replaces layers.py:20 (scale), :22-23 masked_fill, :25 softmax+nan_to_num, :26 dropout.
  * bwd: ds = p * (dpd*keep/(1-p_drop) - sum_k p*dpd*keep/(1-p_drop)) * scale
+ * Outputs (p, pd, ds) get zeros in the padding columns [lk, ld) of every row but the last: whole 16-B stores, no
+ * partially written HBM sectors.  Inputs' padding is ignored.
  * ------------------------------------------------------------------------------------------------- */
 int asrx_softmax_fwd(int32_t dtype, const void* s, void* p, void* pd, int64_t nbh, int32_t heads, int32_t lq,
                      int32_t lk, int64_t ld, float scale, int32_t mask_mode, int32_t causal,

@@ -495,9 +495,11 @@ def test_softmax_masked(dtype, Lk, u, tuning):
     ref = torch.nan_to_num(torch.softmax(x, -1)).view(B * H, Lq, Lk)
     tol = 1e-5 if dtype == torch.float32 else 1e-2
     assert relerr(p[..., :Lk].float().cpu(), ref) < tol
+    assert (p.reshape(-1, ld)[:-1, Lk:] == 0).all()   # padding stored as zeros (all rows but the last)
     dpd = torch.randn(B * H, Lq, ld, generator=g).to(dev, dtype)
     ds = torch.empty_like(sd)
     K().softmax_bwd(p, dpd, ds, B * H, Lq, Lk, ld, scale)
+    assert (ds.reshape(-1, ld)[:-1, Lk:] == 0).all()
     P = p[..., :Lk].double().cpu()
     G = dpd[..., :Lk].double().cpu()
     ref_ds = P * (G - (P * G).sum(-1, keepdim=True)) * scale
