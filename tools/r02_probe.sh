@@ -33,3 +33,4 @@ for s in "$@"; do
     *) echo "unknown $s"; exit 2 ;;
   esac
 done
+
