@@ -360,7 +360,8 @@ def attn_variant(request):
                                            (2, 3, 33, 33, "decoder"), (1, 2, 300, 64, "none"),
                                            (2, 2, 256, 256, "decoder"), (1, 1, 5, 17, "none"),
                                            (1, 2, 999, 999, "none"), (1, 2, 300, 300, "decoder"),
-                                           (1, 2, 64, 257, "none"), (2, 2, 513, 1031, "none")])
+                                           (1, 2, 64, 257, "none"), (2, 2, 513, 1031, "none"),
+                                           (2, 2, 100, 200, "none")])
 def test_attention_fused(dh, B, H, Lq, Lk, kind, attn_variant):
     from asrx.kernels import MaskSpec
     g = torch.Generator().manual_seed(B * 100 + Lq + Lk + dh)
@@ -403,6 +404,43 @@ def test_attention_fused(dh, B, H, Lq, Lk, kind, attn_variant):
     assert relerr(dv_, vh.grad) < 2e-2
     assert relerr(dk_, kh.grad) < 2e-2
     assert relerr(dq_, qh.grad) < 2e-2
+
+
+@pytest.mark.parametrize("Lq,Lk", [(64, 249), (100, 200), (5, 17), (30, 256)])
+def test_attention_short_query_block_with_dropout(Lq, Lk):
+    """Short query blocks without a mask (MODE 0, Lq <= 128: the decoder's cross-attention shape) with dropout
+    p = 0.3 (keep bits from rng_ref): the output and the saved lse (checked through the backward's gradients) match
+    the float64 reference."""
+    from asrx.kernels import MaskSpec
+    from rng_ref import attn_keep
+    B, H, dh = 2, 2, 64
+    d = H * dh
+    g = torch.Generator().manual_seed(Lq * 1000 + Lk)
+    q, kv, valid = _mk(B, H, Lq, Lk, dh, "none", g)
+    qb, kvb = bf(q), bf(kv)
+    qd, kvd = qb.to(dev), kvb.to(dev)
+    st = ((d, Lq * d), (2 * d, Lk * 2 * d), (2 * d, Lk * 2 * d), (d, Lq * d))
+    p, seed = 0.3, 4321
+    o = torch.empty(B * Lq, d, device=dev, dtype=torch.bfloat16)
+    dm = K().dropmask_buffer(B, H, Lq, Lk, dh, p, dev)
+    lse = K().attention_fwd(qd, kvd, kvd[..., d:], o, B, H, Lq, Lk, dh, st, d ** -0.5, MaskSpec(), p, seed,
+                            dropmask=dm)
+    keep = torch.from_numpy(attn_keep(seed, B * H, Lq, Lk, p)).view(B, H, Lq, Lk).double() / (1 - p)
+    qh = qb.double().view(B, Lq, H, dh).transpose(1, 2).requires_grad_(True)
+    kh = kvb[..., :d].double().reshape(B, Lk, H, dh).transpose(1, 2).contiguous().requires_grad_(True)
+    vh = kvb[..., d:].double().reshape(B, Lk, H, dh).transpose(1, 2).contiguous().requires_grad_(True)
+    ref, _ = ref_attention(qh, kh, vh, d ** -0.5, _masked("none", B, Lq, Lk, valid), keep)
+    assert relerr(o.float().cpu().view(B, Lq, H, dh).transpose(1, 2), ref.detach()) < 1e-2
+    dO = bf(torch.randn(B, Lq, d, generator=g))
+    ref.backward(dO.double().view(B, Lq, H, dh).transpose(1, 2))
+    dq = torch.empty(B * Lq, d, device=dev, dtype=torch.bfloat16)
+    dkv = torch.empty(B * Lk, 2 * d, device=dev, dtype=torch.bfloat16)
+    gst = ((d, Lq * d), (d, Lq * d), (2 * d, Lk * 2 * d), (2 * d, Lk * 2 * d))
+    K().attention_bwd(qd, kvd, kvd[..., d:], o, lse, dO.to(dev), dq, dkv, dkv[:, d:], B, H, Lq, Lk, dh, st, gst,
+                      d ** -0.5, MaskSpec(), p, seed, dropmask=dm)
+    assert relerr(dq.float().cpu().view(B, Lq, H, dh).transpose(1, 2), qh.grad) < 2e-2
+    assert relerr(dkv[:, :d].float().cpu().view(B, Lk, H, dh).transpose(1, 2), kh.grad) < 2e-2
+    assert relerr(dkv[:, d:].float().cpu().view(B, Lk, H, dh).transpose(1, 2), vh.grad) < 2e-2
 
 
 @pytest.mark.parametrize("attn_variant", ["auto", "tiled"], indirect=True)
