@@ -998,10 +998,12 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
       const int c = tid + NTHR * i;
       const int which = c >> 8, row = (c >> 3) & 31, dc = (c & 7) * 8;
       const int q = min(q0 + row, a.Lq - 1);
-      pre[i] = __builtin_bit_cast(uint4, ld128_asm((which ? Db + (int64_t)q * a.dor : Qb + (int64_t)q * a.qr) + dc));
+      // 24-bit row offsets (resident_ok: strides < 2^23): full-rate v_mul_i32_i24, not 64-bit multiplies
+      pre[i] = __builtin_bit_cast(uint4, ld128_asm((which ? Db + __mul24(q, (int)a.dor) : Qb + __mul24(q, (int)a.qr)) + dc));
       if (which) {
-        preo[i] = __builtin_bit_cast(uint4, ld128_asm(Ob + (int64_t)q * a.orr + dc));
-        if (Olb) prel[i] = __builtin_bit_cast(uint4, ld128_asm(Olb + (int64_t)q * a.orr + dc));
+        const int oq = __mul24(q, (int)a.orr) + dc;
+        preo[i] = __builtin_bit_cast(uint4, ld128_asm(Ob + oq));
+        if (Olb) prel[i] = __builtin_bit_cast(uint4, ld128_asm(Olb + oq));
       }
     }
     if (tid < 32) praw = __uint_as_float(ld32_asm(lseb + min(q0 + tid, a.Lq - 1)));
@@ -1056,6 +1058,7 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
 
   // dQ^T[d][q] = sum_key K^T[d][key] dS^T[key][q] for chunk cc: its 8 (sub-tile, 16-column) tiles, TPW per wave,
   // every operand read before the MFMA chain (compile-time trip counts, no branches)
+  bf16_t* const dqh = a.dq + b * a.dqb + h * 64;
   auto dq_chunk = [&](int cc) {
     const int bq = cc & 1, q0 = cc * 32;
 #pragma unroll
@@ -1077,7 +1080,7 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
       uint2 x;                                           // (zero-dS) value would be wrong -> guarded below
       x.x = pack2bf(acc[0] * a.scale, acc[1] * a.scale);
       x.y = pack2bf(acc[2] * a.scale, acc[3] * a.scale);
-      if (q0 + 16 * qs + li < a.Lq) *(uint2*)(a.dq + b * a.dqb + (int64_t)q * a.dqr + h * 64 + 16 * u + 4 * g) = x;
+      if (q0 + 16 * qs + li < a.Lq) *(uint2*)(dqh + __mul24(q, (int)a.dqr) + 16 * u + 4 * g) = x;
     }
   };
 
@@ -1273,7 +1276,11 @@ int fill_args(const asrx_attn_desc* d, AttnArgs& a) {
 bool resident_ok(const asrx_attn_desc* d, const AttnArgs& a) {
   static const bool tiled = [] { const char* e = getenv("ASRX_ATTN_KERNEL"); return e && !strcmp(e, "tiled"); }();
   if (tiled) return false;
-  return d->dh == 64 && a.Lk <= R_MAXK && (a.orr % 4) == 0 && (a.ob % 4) == 0;
+  // row offsets inside the resident kernels are 24-bit products (q * row stride): strides and lengths < 2^23
+  constexpr int64_t L24 = 1 << 23;
+  const bool s24 = a.qr < L24 && a.kr < L24 && a.vr < L24 && a.orr < L24 && a.Lq < L24 && a.Lk < L24 &&
+                   (!a.dout || (a.dor < L24 && a.dqr < L24 && a.dkr < L24 && a.dvr < L24));
+  return d->dh == 64 && a.Lk <= R_MAXK && (a.orr % 4) == 0 && (a.ob % 4) == 0 && s24;
 }
 
 size_t bwd_smem(int nw, int dh) {
