@@ -986,13 +986,15 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
   uint4 preo[PRE] = {}, prel[PRE] = {};
   // The prefetch is inline-asm loads, waited for by one vmcnt(0) at the start of publish (the compiler does not
   // count them): with compiler-tracked loads, its conservative merge at the loop head put a vmcnt(0) in front of
-  // the next fetch, which also waited for the dQ stores of the previous chunk (≈1k cycles per chunk).
+  // the next fetch, which also waited for the dQ stores of the previous chunk (≈1k cycles per chunk).  Every asm
+  // load is UNCONDITIONAL (only its address is selected): a conditionally loaded value reaches its use through a
+  // phi, which the compiler may realise as a register copy issued before the wait — a copy of an in-flight load.
+  const bf16_t* const Olv = Olb ? Olb : Ob;
   auto fetch = [&](int ch) {
     const int q0 = ch * 32;
-    if (usebits) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t) dwn[t] = ld32_asm(dmb + (int64_t)ch * a.Lk + keyc[t]);
-    }
+    for (int t = 0; t < 2; ++t)
+      dwn[t] = ld32_asm(usebits ? dmb + (int64_t)ch * a.Lk + keyc[t] : (const uint32_t*)lseb);
 #pragma unroll
     for (int i = 0; i < PRE; ++i) {
       const int c = tid + NTHR * i;
@@ -1000,13 +1002,11 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
       const int q = min(q0 + row, a.Lq - 1);
       // 24-bit row offsets (resident_ok: strides < 2^23): full-rate v_mul_i32_i24, not 64-bit multiplies
       pre[i] = __builtin_bit_cast(uint4, ld128_asm((which ? Db + __mul24(q, (int)a.dor) : Qb + __mul24(q, (int)a.qr)) + dc));
-      if (which) {
-        const int oq = __mul24(q, (int)a.orr) + dc;
-        preo[i] = __builtin_bit_cast(uint4, ld128_asm(Ob + oq));
-        if (Olb) prel[i] = __builtin_bit_cast(uint4, ld128_asm(Olb + oq));
-      }
+      const int oq = __mul24(q, (int)a.orr) + dc;   // O / O_lo of the row (used by the dO pieces only)
+      preo[i] = __builtin_bit_cast(uint4, ld128_asm(Ob + oq));
+      prel[i] = __builtin_bit_cast(uint4, ld128_asm(Olv + oq));
     }
-    if (tid < 32) praw = __uint_as_float(ld32_asm(lseb + min(q0 + tid, a.Lq - 1)));
+    praw = __uint_as_float(ld32_asm(lseb + min(q0 + (tid & 31), a.Lq - 1)));
   };
   auto publish = [&](int buf, int ch) {
     const int q0 = ch * 32;
@@ -1118,7 +1118,7 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
                        ((uint32_t)(rng_half(h23, 0) >= a.thr) << 2) | ((uint32_t)(rng_half(h23, 1) >= a.thr) << 3);
         }
     }
-    if (ch + 1 < nch) fetch(ch + 1);
+    fetch(min(ch + 1, nch - 1));   // unconditional (see fetch); the last one re-reads chunk nch-1, unused
     ATTN_TS(2 + 4 * ch);
     const bf16_t* cq = sq + buf * 32 * R_CS;
     const bf16_t* cdo = sdo + buf * 32 * R_CS;
@@ -1195,6 +1195,7 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
     __syncthreads();
     ATTN_TS(4 + 4 * ch);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the unused last prefetch
   dq_chunk(nch - 1);
 
 #pragma unroll

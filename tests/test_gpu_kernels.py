@@ -406,8 +406,9 @@ def test_attention_fused(dh, B, H, Lq, Lk, kind, attn_variant):
     assert relerr(dq_, qh.grad) < 2e-2
 
 
-@pytest.mark.parametrize("Lq,Lk", [(64, 249), (100, 200), (5, 17), (30, 256)])
-def test_attention_short_query_block_with_dropout(Lq, Lk):
+@pytest.mark.parametrize("Lq,Lk", [(64, 249), (100, 200), (5, 17), (30, 256), (249, 249), (64, 64)])
+@pytest.mark.parametrize("with_lo", [False, True])
+def test_attention_short_query_block_with_dropout(Lq, Lk, with_lo):
     """Short query blocks without a mask (MODE 0, Lq <= 128: the decoder's cross-attention shape) with dropout
     p = 0.3 (keep bits from rng_ref): the output and the saved lse (checked through the backward's gradients) match
     the float64 reference."""
@@ -423,8 +424,9 @@ def test_attention_short_query_block_with_dropout(Lq, Lk):
     p, seed = 0.3, 4321
     o = torch.empty(B * Lq, d, device=dev, dtype=torch.bfloat16)
     dm = K().dropmask_buffer(B, H, Lq, Lk, dh, p, dev)
+    o_lo = torch.empty_like(o) if with_lo else None   # the training path's O rounding residual (exact delta)
     lse = K().attention_fwd(qd, kvd, kvd[..., d:], o, B, H, Lq, Lk, dh, st, d ** -0.5, MaskSpec(), p, seed,
-                            dropmask=dm)
+                            dropmask=dm, o_lo=o_lo)
     keep = torch.from_numpy(attn_keep(seed, B * H, Lq, Lk, p)).view(B, H, Lq, Lk).double() / (1 - p)
     qh = qb.double().view(B, Lq, H, dh).transpose(1, 2).requires_grad_(True)
     kh = kvb[..., :d].double().reshape(B, Lk, H, dh).transpose(1, 2).contiguous().requires_grad_(True)
@@ -437,7 +439,7 @@ def test_attention_short_query_block_with_dropout(Lq, Lk):
     dkv = torch.empty(B * Lk, 2 * d, device=dev, dtype=torch.bfloat16)
     gst = ((d, Lq * d), (d, Lq * d), (2 * d, Lk * 2 * d), (2 * d, Lk * 2 * d))
     K().attention_bwd(qd, kvd, kvd[..., d:], o, lse, dO.to(dev), dq, dkv, dkv[:, d:], B, H, Lq, Lk, dh, st, gst,
-                      d ** -0.5, MaskSpec(), p, seed, dropmask=dm)
+                      d ** -0.5, MaskSpec(), p, seed, dropmask=dm, o_lo=o_lo)
     assert relerr(dq.float().cpu().view(B, Lq, H, dh).transpose(1, 2), qh.grad) < 2e-2
     assert relerr(dkv[:, :d].float().cpu().view(B, Lk, H, dh).transpose(1, 2), kh.grad) < 2e-2
     assert relerr(dkv[:, d:].float().cpu().view(B, Lk, H, dh).transpose(1, 2), vh.grad) < 2e-2
