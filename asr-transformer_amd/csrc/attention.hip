@@ -459,6 +459,11 @@ ASRX_DEV s8_t ld128_asm(const void* p) {
   asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p));
   return r;
 }
+ASRX_DEV uint2 ld64_asm(const void* p) {
+  u2_t r;
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(r) : "v"(p));
+  return __builtin_bit_cast(uint2, r);
+}
 ASRX_DEV uint32_t ld32_asm(const void* p) {
   uint32_t r;
   asm volatile("global_load_dword %0, %1, off" : "=v"(r) : "v"(p));
@@ -470,6 +475,11 @@ ASRX_DEV uint32_t ldu8_asm(const void* p) {
   return r;
 }
 template <typename T> ASRX_DEV void pin(T& x) { asm volatile("" : "+v"(x)); }
+ASRX_DEV void pin(uint2& x) {
+  u2_t t = __builtin_bit_cast(u2_t, x);
+  asm volatile("" : "+v"(t));
+  x = __builtin_bit_cast(uint2, t);
+}
 ASRX_DEV void pin(uint4& x) {
   s8_t t = __builtin_bit_cast(s8_t, x);
   asm volatile("" : "+v"(t));
@@ -907,7 +917,7 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
   // NKT 32-key blocks (= waves); keys past Lk are zero rows with a -inf score bias
   constexpr int NK = NKT * 32, NTHR = NKT * 64;
   constexpr int RDT = 32 + 8;                                     // dS^T image [key][32 queries] row stride
-  constexpr int PRE = 512 / NTHR;                                 // 16-B prefetch pieces per thread
+  constexpr int PRE = 512 / NTHR;                                 // 8-B Q (and dO, O, O_lo) pieces per thread
   constexpr int TPW = 8 / NKT;                                    // dQ tiles per wave per chunk
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* sk = (bf16_t*)smem;                                // [NK][R_VS]
@@ -973,7 +983,7 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
   // chunk prefetch: 512 16-B pieces (Q rows then dO rows) + 32 lse + 32 delta (+ this lane's dropout words).
   // Loads go to raw registers from clamped (always valid) addresses; every test on them waits until the chunk
   // is published or used, so issuing the prefetch never stalls on its own latency.
-  uint4 pre[PRE];
+  uint2 pq[PRE], pdo[PRE];
   float praw = 0.f;
   const bool usebits = a.thr && a.dropmask;
   const uint32_t* dmb = usebits ? a.dropmask + (int64_t)bh * nch * a.Lk : nullptr;
@@ -983,12 +993,14 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
   // piece, dot the 8 elements and reduce over the row's 8 pieces (adjacent lanes) — no separate delta pass.
   const bf16_t* Ob = a.o + b * a.ob + h * 64;
   const bf16_t* Olb = a.o_lo ? a.o_lo + b * a.ob + h * 64 : nullptr;
-  uint4 preo[PRE] = {}, prel[PRE] = {};
+  uint2 po[PRE], pol[PRE];
   // The prefetch is inline-asm loads, waited for by one vmcnt(0) at the start of publish (the compiler does not
   // count them): with compiler-tracked loads, its conservative merge at the loop head put a vmcnt(0) in front of
   // the next fetch, which also waited for the dQ stores of the previous chunk (≈1k cycles per chunk).  Every asm
   // load is UNCONDITIONAL (only its address is selected): a conditionally loaded value reaches its use through a
   // phi, which the compiler may realise as a register copy issued before the wait — a copy of an in-flight load.
+  // Each thread stages PRE 8-B pieces of Q AND the same pieces of dO, O and O_lo (piece c: row c / 16, elements
+  // 4 (c % 16) ..): every wave does the same loads and its share of delta (the 16 lanes of a row reduce by DPP).
   const bf16_t* const Olv = Olb ? Olb : Ob;
   auto fetch = [&](int ch) {
     const int q0 = ch * 32;
@@ -998,13 +1010,14 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
 #pragma unroll
     for (int i = 0; i < PRE; ++i) {
       const int c = tid + NTHR * i;
-      const int which = c >> 8, row = (c >> 3) & 31, dc = (c & 7) * 8;
+      const int row = c >> 4, dc = (c & 15) * 4;
       const int q = min(q0 + row, a.Lq - 1);
       // 24-bit row offsets (resident_ok: strides < 2^23): full-rate v_mul_i32_i24, not 64-bit multiplies
-      pre[i] = __builtin_bit_cast(uint4, ld128_asm((which ? Db + __mul24(q, (int)a.dor) : Qb + __mul24(q, (int)a.qr)) + dc));
-      const int oq = __mul24(q, (int)a.orr) + dc;   // O / O_lo of the row (used by the dO pieces only)
-      preo[i] = __builtin_bit_cast(uint4, ld128_asm(Ob + oq));
-      prel[i] = __builtin_bit_cast(uint4, ld128_asm(Olv + oq));
+      pq[i] = ld64_asm(Qb + __mul24(q, (int)a.qr) + dc);
+      pdo[i] = ld64_asm(Db + __mul24(q, (int)a.dor) + dc);
+      const int oq = __mul24(q, (int)a.orr) + dc;
+      po[i] = ld64_asm(Ob + oq);
+      pol[i] = ld64_asm(Olv + oq);
     }
     praw = __uint_as_float(ld32_asm(lseb + min(q0 + (tid & 31), a.Lq - 1)));
   };
@@ -1013,9 +1026,10 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
     for (int i = 0; i < PRE; ++i) {
-      pin(pre[i]);
-      pin(preo[i]);
-      pin(prel[i]);
+      pin(pq[i]);
+      pin(pdo[i]);
+      pin(po[i]);
+      pin(pol[i]);
     }
     pin(praw);
     pin(dwn[0]);
@@ -1023,30 +1037,28 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
 #pragma unroll
     for (int i = 0; i < PRE; ++i) {
       const int c = tid + NTHR * i;
-      const int which = c >> 8, row = (c >> 3) & 31, dc = (c & 7) * 8;
+      const int row = c >> 4, dc = (c & 15) * 4;
       const bool qv = q0 + row < a.Lq;
-      *(uint4*)((which ? sdo : sq) + (buf * 32 + row) * R_CS + dc) = qv ? pre[i] : make_uint4(0, 0, 0, 0);
-      if (which) {   // wave-uniform: a wave's 64 pieces are all Q or all dO
-        const uint32_t* dd = (const uint32_t*)&pre[i];
-        const uint32_t* oo = (const uint32_t*)&preo[i];
-        const uint32_t* ol = (const uint32_t*)&prel[i];
-        float dot = 0.f;
-        if (Olb) {
+      *(uint2*)(sq + (buf * 32 + row) * R_CS + dc) = qv ? pq[i] : make_uint2(0, 0);
+      *(uint2*)(sdo + (buf * 32 + row) * R_CS + dc) = qv ? pdo[i] : make_uint2(0, 0);
+      const uint32_t dd[2] = {pdo[i].x, pdo[i].y}, oo[2] = {po[i].x, po[i].y}, ol[2] = {pol[i].x, pol[i].y};
+      float dot = 0.f;
+      if (Olb) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            dot += bf2f(dd[e] & 0xffff) * (bf2f(oo[e] & 0xffff) + bf2f(ol[e] & 0xffff)) +
-                   bf2f(dd[e] >> 16) * (bf2f(oo[e] >> 16) + bf2f(ol[e] >> 16));
-        } else {
+        for (int e = 0; e < 2; ++e)
+          dot += bf2f(dd[e] & 0xffff) * (bf2f(oo[e] & 0xffff) + bf2f(ol[e] & 0xffff)) +
+                 bf2f(dd[e] >> 16) * (bf2f(oo[e] >> 16) + bf2f(ol[e] >> 16));
+      } else {
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            dot += bf2f(dd[e] & 0xffff) * bf2f(oo[e] & 0xffff) + bf2f(dd[e] >> 16) * bf2f(oo[e] >> 16);
-        }
-        // sum over the row's 8 adjacent lanes by DPP (quad swaps, then the half-row mirror): no LDS round trips
-        dot += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(dot), 0xB1, 0xF, 0xF, true));
-        dot += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(dot), 0x4E, 0xF, 0xF, true));
-        dot += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(dot), 0x141, 0xF, 0xF, true));
-        if ((c & 7) == 0) sdel[buf * 32 + row] = qv ? dot : 0.f;
+        for (int e = 0; e < 2; ++e)
+          dot += bf2f(dd[e] & 0xffff) * bf2f(oo[e] & 0xffff) + bf2f(dd[e] >> 16) * bf2f(oo[e] >> 16);
       }
+      // sum over the row's 16 adjacent lanes by DPP (quad swaps, half-row and row mirrors): no LDS round trips
+      dot += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(dot), 0xB1, 0xF, 0xF, true));
+      dot += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(dot), 0x4E, 0xF, 0xF, true));
+      dot += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(dot), 0x141, 0xF, 0xF, true));
+      dot += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(dot), 0x140, 0xF, 0xF, true));
+      if ((c & 15) == 0) sdel[buf * 32 + row] = qv ? dot : 0.f;
     }
     if (tid < 32) {
       const int q = q0 + tid;
