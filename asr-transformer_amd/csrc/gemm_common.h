@@ -263,6 +263,20 @@ ASRX_DEV int epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int
       // bf16 C, 16-byte stores: fragments i and i+1 of a row pair up across lanes l and l ^ 16
       // (v_permlane16_swap), so lane group gq stores 8 consecutive columns of fragment i + (gq & 1) at column
       // offset 8 (gq >> 1): one store instruction covers 16 rows x 64 contiguous bytes (T21).
+      // gate bits read in place (no prefetch at the last K-step, p4): every word of the wave's tile is loaded
+      // before the first store — a load issued between the stores waits (in-order vmcnt) for all of them, which
+      // serialised one load latency per fragment row (FFN2 data gradient 57 -> see DESIGN §4)
+      constexpr bool GPL = !PRE && (EPI & E_GBITS) != 0 && (EPI & (E_RESID | E_ROWADD | E_GATE)) == 0;
+      uint32_t gwl[GPL ? TN / 2 : 1][GPL ? TM : 1];
+      if constexpr (GPL) {
+#pragma unroll
+        for (int i = 0; i < TN; i += 2)
+#pragma unroll
+          for (int j = 0; j < TM; ++j) {
+            const int m = m0 + wm + 16 * j + (l & 15), na = n0 + wn + 16 * i + 4 * gq;
+            gwl[i / 2][j] = (m < g.M && na < g.N) ? ((const uint32_t*)g.gate)[(int64_t)m * g.ld_gate + (na >> 5)] : 0u;
+          }
+      }
 #pragma unroll
       for (int i = 0; i < TN; i += 2) {
         const int na = n0 + wn + 16 * i + 4 * gq, nb = na + 16;
@@ -285,6 +299,9 @@ ASRX_DEV int epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int
             if constexpr (PRE) {
               if (na < g.N) va = epi_vals<EPI, true>(g, m, na, va, ba, ASRX_PGT(i, j), ASRX_PRR(i, j));
               if (nb < g.N) vb = epi_vals<EPI, true>(g, m, nb, vb, bb, ASRX_PGT(i + 1, j), ASRX_PRR(i + 1, j));
+            } else if constexpr (GPL) {   // (the gate is the only memory operand of these epilogues)
+              if (na < g.N) va = epi_vals<EPI, true>(g, m, na, va, ba, uint2{gwl[i / 2][j], 0u});
+              if (nb < g.N) vb = epi_vals<EPI, true>(g, m, nb, vb, bb, uint2{gwl[i / 2][j], 0u});
             } else {
               if (na < g.N) va = epi_vals<EPI>(g, m, na, va, ba);
               if (nb < g.N) vb = epi_vals<EPI>(g, m, nb, vb, bb);
