@@ -49,7 +49,7 @@ ASRX_DEV uint32_t rng_hash(uint64_t seed, uint32_t pidx) {
 // kernels that draw dropout decisions fold this device-resident offset into their seed once at entry
 // (seed_eff), so each replay draws fresh masks (asrx_set_seed_offset, called before every step).  Offset 0 =
 // the seed unchanged.  One copy per translation unit (no relocatable device code): asrx_set_seed_offset sets
-// every copy, each through its TU's setter kernel (ASRX_SEED_OFFSET_SETTER).
+// every copy with ONE launch, through the copies' device addresses (ASRX_SEED_OFFSET_SETTER exports each TU's).
 static __device__ uint64_t g_seed_offset;
 ASRX_DEV uint64_t seed_eff(uint64_t seed) {
   const uint64_t o = g_seed_offset;
@@ -60,16 +60,15 @@ ASRX_DEV uint64_t seed_eff(uint64_t seed) {
   return seed ^ z ^ (z >> 31);
 }
 #define ASRX_SEED_OFFSET_SETTER(tu)                                                                 \
-  __global__ void seed_offset_set_##tu##_kernel(uint64_t v) { g_seed_offset = v; }                  \
-  int asrx_seed_offset_##tu(uint64_t v, hipStream_t st) {                                           \
-    hipLaunchKernelGGL(seed_offset_set_##tu##_kernel, dim3(1), dim3(1), 0, st, v);                 \
-    return hipGetLastError() == hipSuccess ? 0 : -1;                                                \
+  uint64_t* asrx_seed_offset_addr_##tu() {                                                          \
+    void* p = nullptr;                                                                              \
+    return hipGetSymbolAddress(&p, HIP_SYMBOL(g_seed_offset)) == hipSuccess ? (uint64_t*)p : nullptr; \
   }
-int asrx_seed_offset_gemm(uint64_t v, hipStream_t st);
-int asrx_seed_offset_attention(uint64_t v, hipStream_t st);
-int asrx_seed_offset_norm(uint64_t v, hipStream_t st);
-int asrx_seed_offset_softmax(uint64_t v, hipStream_t st);
-int asrx_seed_offset_frontend(uint64_t v, hipStream_t st);
+uint64_t* asrx_seed_offset_addr_gemm();
+uint64_t* asrx_seed_offset_addr_attention();
+uint64_t* asrx_seed_offset_addr_norm();
+uint64_t* asrx_seed_offset_addr_softmax();
+uint64_t* asrx_seed_offset_addr_frontend();
 
 ASRX_DEV uint32_t rng_half(uint32_t h, uint32_t which) { return which ? (h >> 16) : (h & 0xffffu); }
 

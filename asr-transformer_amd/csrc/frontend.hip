@@ -1259,11 +1259,22 @@ extern "C" int asrx_upload(void* dst, const void* src, int64_t nbytes, void* str
   return ASRX_OK;
 }
 
+namespace {
+struct SeedAddrs { uint64_t* p[5]; };
+// one launch sets every translation unit's copy (threads 0..4: per-lane addresses, vector stores)
+__global__ void seed_offset_set_all_kernel(uint64_t v, SeedAddrs a) {
+  if (threadIdx.x < 5) *a.p[threadIdx.x] = v;
+}
+}  // namespace
+
 extern "C" int asrx_set_seed_offset(uint64_t offset, void* stream) {
-  hipStream_t st = (hipStream_t)stream;
-  if (asrx_seed_offset_gemm(offset, st) || asrx_seed_offset_attention(offset, st) ||
-      asrx_seed_offset_norm(offset, st) || asrx_seed_offset_softmax(offset, st) ||
-      asrx_seed_offset_frontend(offset, st))
-    return ASRX_ERR_LAUNCH;
+  static const SeedAddrs addrs = [] {
+    return SeedAddrs{{asrx_seed_offset_addr_gemm(), asrx_seed_offset_addr_attention(), asrx_seed_offset_addr_norm(),
+                      asrx_seed_offset_addr_softmax(), asrx_seed_offset_addr_frontend()}};
+  }();
+  for (uint64_t* q : addrs.p)
+    if (!q) return ASRX_ERR_LAUNCH;
+  hipLaunchKernelGGL(seed_offset_set_all_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, offset, addrs);
+  ASRX_CHECK_LAUNCH();
   return ASRX_OK;
 }
