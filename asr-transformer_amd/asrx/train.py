@@ -128,6 +128,47 @@ def train_epoch(model, data_loader, loss_function, optimizer, device):
     return {"Train Loss": total / max(1, len(data_loader))}, preds, targets
 
 
+def shift_inputs(text, mask):
+    """train.py:22-25 as written: the decoder input is a copy of text whose columns mask.sum(-1) - 1 (one column
+    per sample, applied to EVERY row: a batch-coupled index_put) take the last column, and the mask
+    the same; device ops, no host sync.  Returns (input_text, mask), both (B, L+1): the step drops the last column."""
+    idx = mask.sum(dim=-1).long() - 1
+    input_text = text.detach().clone()
+    input_text[:, idx] = input_text[:, -1]
+    mask = mask.clone()
+    mask[:, idx] = mask[:, -1]
+    return input_text, mask
+
+
+def train_epoch_native(trainer, data_loader, device=None):
+    """train_epoch (train.py:6-55) on the native step: the same shifted inputs, targets, per-step predictions
+    (`logits.argmax(-1)`, here the cross-entropy kernel's fused argmax) and mean loss, but losses are summed and
+    predictions kept on the device — ONE host synchronisation per epoch instead of two per step (`.item()`,
+    `.to('cpu')`; train.py:30,33).  trainer: an asrx.train.Trainer built with preds=True.
+    Returns ({"Train Loss": mean}, preds, targets) like train_epoch (preds / targets: CPU int64 (B, L))."""
+    if not trainer.want_preds:
+        raise ValueError("train_epoch_native needs Trainer(..., preds=True)")
+    dev = torch.device(device) if device is not None else trainer.store.flat.device
+    trainer.model.train()
+    total = torch.zeros((), dtype=torch.float32, device=dev)
+    preds, targets, n = [], [], 0
+    for batch in data_loader:
+        spectrum = batch["spectrum"].to(dev)
+        text = batch["text"].to(dev)
+        mask = batch["mask"].to(dev)
+        input_text, mask = shift_inputs(text, mask)
+        loss = trainer.step(spectrum, text, mask, input_text=input_text)
+        total += loss.reshape(())                      # before the next step overwrites a replayed graph's output
+        B, L = text.shape[0], text.shape[1] - 1
+        preds.append(trainer.last_preds.view(B, L).clone())
+        targets.append(text[:, :-1])
+        n += 1
+    torch.cuda.synchronize(dev)
+    preds = [p.cpu() for p in preds]
+    targets = [t.cpu() for t in targets]
+    return {"Train Loss": float(total) / max(1, n)}, preds, targets
+
+
 def eval_epoch(model, data_loader, eos_token_id, bos_token_id, loss_function, device):
     """train.py:58-108: greedy decode per batch (Transformer.evaluate), logits padded/truncated to the
     target length, CE loss averaged over batches."""
@@ -161,7 +202,7 @@ class Trainer:
     """Native data-parallel training step for an asrx.Transformer."""
 
     def __init__(self, model, lr=1e-4, betas=(0.9, 0.98), eps=1e-9, weight_decay=0.0, decoupled=True,
-                 ignore_index=-100, group=None, bucket_mb=64, allreduce_fn=None, graph=None, wire=None):
+                 ignore_index=-100, group=None, bucket_mb=64, allreduce_fn=None, graph=None, wire=None, preds=False):
         self.model = model
         self.store = get_store(model)
         self.m = torch.zeros_like(self.store.flat)
@@ -174,9 +215,14 @@ class Trainer:
         self.store.refresh_shadow(force=True)
         self._wonly = wgrad_only_params(model) if FRESH_GRADS else []
         self.graph = GRAPH if graph is None else bool(graph)
-        self._cap = None        # captured step: (segments, static inputs, loss)
+        self._cap = None        # captured step: (segments, static inputs, loss, preds buffer)
         self._hyp = torch.zeros(3, dtype=torch.float32, device=self.store.flat.device)
         self.ar_events = None   # list -> record the exposed all-reduce time of each step (_finish)
+        # preds=True: the cross-entropy kernel also writes each row's argmax over the V classes (train.py:29,
+        # `logits.argmax(-1)`, fused into the loss pass) into last_preds (int64 [B*L], device; in graph mode the
+        # captured buffer, overwritten by the next step)
+        self.want_preds = bool(preds)
+        self.last_preds = None
         if self._wonly:   # flat indices of everything else (zeroed each step by one index_fill)
             keep = torch.ones(self.store.grad.numel(), dtype=torch.bool)
             for p in self._wonly:
@@ -184,15 +230,19 @@ class Trainer:
                 keep[o:o + p.numel()] = False
             self._zero_idx = keep.nonzero().squeeze(1).to(self.store.grad.device)
 
-    def forward_backward(self, spectrum, text, mask, ready=None, capture=False):
-        """text: (B, L+1) with BOS ... ; inputs text[:, :-1], targets text[:, 1:] (train.py:24,32).
-        ready: gradient-range hook (default: the reducer's, when multi-GPU); capture: building a HIP graph."""
+    def forward_backward(self, spectrum, text, mask, ready=None, capture=False, input_text=None):
+        """text: (B, L+1) with BOS ... ; inputs text[:, :-1], targets text[:, 1:] (train.py:24,32).  input_text
+        (optional, (B, L+1)): the decoder input instead of text (train.py:22-25 feeds a shifted copy while the
+        targets stay text[:, 1:]).  ready: gradient-range hook (default: the reducer's, when multi-GPU); capture:
+        building a HIP graph."""
         model = self.model
         C = make_ctx(model, model.decoder.p)
-        logits, S = model_forward(C, model, spectrum, text[:, :-1], mask[:, :-1])
+        inp = text if input_text is None else input_text
+        logits, S = model_forward(C, model, spectrum, inp[:, :-1], mask[:, :-1])
         V = model.decoder._classifier.V
         tgt = text[:, 1:].reshape(-1).contiguous()
-        loss, dl, _ = K.cross_entropy(logits, V, tgt, ignore_index=self.ignore_index)
+        loss, dl, am = K.cross_entropy(logits, V, tgt, ignore_index=self.ignore_index, want_argmax=self.want_preds)
+        self.last_preds = am
         if self._wonly and C.cd == torch.bfloat16 and all(p.grad is not None for p in self.store.params):
             self.store.grad.index_fill_(0, self._zero_idx, 0.0)
             C.fresh = FreshGrads(self.store, self._wonly)
@@ -211,17 +261,20 @@ class Trainer:
                self.betas[1], self.eps, self.wd, max(1, self.step_count), grad_scale=1.0 / self.reducer.world,
                decoupled=self.decoupled, hyp=hyp)
 
-    def step(self, spectrum, text, mask):
+    def step(self, spectrum, text, mask, input_text=None):
         """One training step (forward, CE, backward, all-reduce, AdamW).  Returns the loss as a device scalar; in
-        graph mode it is the captured output tensor, overwritten by the next step."""
+        graph mode it is the captured output tensor, overwritten by the next step.  input_text: see
+        forward_backward."""
+        if input_text is None:
+            input_text = text
         if self.graph and self.model.precision == "bf16":
-            if self._cap is not None and not self._matches(spectrum, text, mask):
+            if self._cap is not None and not self._matches(spectrum, text, mask, input_text):
                 self._cap = None            # new input shapes: recapture
             if self._cap is None and self.step_count >= GRAPH_WARMUP:
-                self._capture(spectrum, text, mask)
+                self._capture(spectrum, text, mask, input_text)
             if self._cap is not None:
-                return self._replay(spectrum, text, mask)
-        loss = self.forward_backward(spectrum, text, mask)
+                return self._replay(spectrum, text, mask, input_text)
+        loss = self.forward_backward(spectrum, text, mask, input_text=input_text)
         self._finish()
         self.step_count += 1
         self._adam()
@@ -242,13 +295,13 @@ class Trainer:
             self.reducer.finish()
 
     # ---- HIP graph mode
-    def _matches(self, spectrum, text, mask):
+    def _matches(self, *xs):
         ins = self._cap[1]
-        return all(a.shape == b.shape and a.dtype == b.dtype for a, b in zip(ins, (spectrum, text, mask)))
+        return all(a.shape == b.shape and a.dtype == b.dtype for a, b in zip(ins, xs))
 
-    def _capture(self, spectrum, text, mask):
+    def _capture(self, spectrum, text, mask, input_text):
         dev = self.store.flat.device
-        ins = tuple(x.to(dev).clone() for x in (spectrum, text, mask))
+        ins = tuple(x.to(dev).clone() for x in (spectrum, text, mask, input_text))
         torch.cuda.synchronize(dev)
         pool = torch.cuda.graph_pool_handle()
         side = torch.cuda.Stream(device=dev)
@@ -257,7 +310,8 @@ class Trainer:
             seg = _Segments(pool)
             K.CAPTURE = seg
             try:
-                loss = self.forward_backward(*ins, ready=seg if self.reducer.active else None, capture=True)
+                loss = self.forward_backward(*ins[:3], ready=seg if self.reducer.active else None, capture=True,
+                                             input_text=ins[3])
                 if not self.reducer.active:
                     self._adam(self._hyp)
             finally:
@@ -265,11 +319,12 @@ class Trainer:
                 seg.close()
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
-        self._cap = (seg, ins, loss)
+        self._cap = (seg, ins, loss, self.last_preds)
 
-    def _replay(self, spectrum, text, mask):
-        seg, ins, loss = self._cap
-        for dst, src in zip(ins, (spectrum, text, mask)):
+    def _replay(self, spectrum, text, mask, input_text):
+        seg, ins, loss, preds = self._cap
+        self.last_preds = preds
+        for dst, src in zip(ins, (spectrum, text, mask, input_text)):
             if dst.data_ptr() != src.data_ptr():
                 dst.copy_(src, non_blocking=True)
         self.step_count += 1
