@@ -19,7 +19,7 @@ def timed(fn, reps):
     """GPU time per call: reps calls captured in a HIP graph and replayed (no host launch gaps)."""
     sys.path.insert(0, REPO)
     from bench import _graph_time_ms
-    return _graph_time_ms(fn, launches=reps) * 1e-3
+    return _graph_time_ms([fn], launches=reps) * 1e-3
 
 
 def main():
@@ -35,9 +35,12 @@ def main():
         beta = torch.randn(d, device="cuda", generator=g)
         y = torch.empty(rows, d, device="cuda", dtype=torch.bfloat16)
         mean, rstd = K.layernorm_fwd(x, gamma, beta, y)
-        t = timed(lambda: K.layernorm_fwd(x, gamma, beta, y), args.reps)
-        by = rows * d * (4 + 2) + rows * 8
-        print(f"ln_fwd {name} rows={rows}: {t*1e6:7.2f} us  {by/t/1e9:7.0f} GB/s", flush=True)
+        for rw in (1, 2, 4):   # rows per wave of the forward (asrx_set_tuning)
+            K.set_tuning("ln_rw", rw)
+            t = timed(lambda: K.layernorm_fwd(x, gamma, beta, y), args.reps)
+            by = rows * d * (4 + 2) + rows * 8
+            print(f"ln_fwd {name} rows={rows} rw={rw}: {t*1e6:7.2f} us  {by/t/1e9:7.0f} GB/s", flush=True)
+        K.set_tuning("ln_rw", 0)
         dy = torch.randn(rows, d, device="cuda", generator=g).bfloat16()
         dres = torch.randn(rows, d, device="cuda", generator=g)
         dxd = torch.empty(rows, d, device="cuda", dtype=torch.bfloat16)

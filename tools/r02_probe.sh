@@ -27,6 +27,7 @@ for s in "$@"; do
     attnb) step attnb 300 python tools/attn_bench.py ;;
     attndbg) step attndbg 300 python tools/attn_bench.py --dbg --only enc,cross ;;
     smx) step smx 300 python tools/softmax_probe.py ;;
+    ln) step ln 300 python tools/ln_bench.py --blocks 256,512,1024,2048 ;;
     counters) step counters 120 rocprofv3 -L ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 3 --no-cpu-baseline --no-probe --no-sub --no-other ;;
     pmcm) step pmcm 300 timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/pmcm -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-graph --no-cpu-baseline --no-probe --no-sub --no-other && python3 tools/pmc_mfma.py gpurun_out/pmcm/run_counter_collection.csv --out gpurun_out/c3_pmc_mfma.json ;;
