@@ -19,6 +19,8 @@
 
 #include "gemm_common.h"
 
+int blaslt_gemm_bf16(const asrx_gemm_desc* d, hipStream_t st);   // blaslt.hip: hipBLASLt for plain GEMMs
+
 namespace {
 using namespace asrxg;
 
@@ -1483,7 +1485,8 @@ void dispatch_bf16(const GemmArgs& g, bool at, bool bt, bool vec, int batch, hip
 // Kernel selection (shared by asrx_gemm and asrx_gemm_kernel_name so profiling can name the launch).
 struct GemmPlan {
   int use;     // 1 = p3 (256x128 LDS-DMA ring), 2 = p4 (256x256), 3 = register path 128, 4 = register path 64,
-               // 5 = ring 64x64, 6 = ring 128x64 (4-stage LDS-DMA, small grids), 9 = tall-K (conv2 dW)
+               // 5 = ring 64x64, 6 = ring 128x64 (4-stage LDS-DMA, small grids), 9 = tall-K (conv2 dW),
+               // 10 = hipBLASLt (plain GEMMs, blaslt.hip)
   bool vec;    // 16-byte aligned operands
   int epi;     // instantiated epilogue flags (E_GENERIC when the fast-path set has no match)
   int ntiles;  // output tiles of the chosen kernel
@@ -1498,6 +1501,12 @@ bool epi_instantiated(bool at, bool bt, int epi) {
   return false;
 }
 
+// ASRX_GEMM_BLASLT=0 keeps every auto-planned GEMM on the hand-written kernels (A/B switch; default on)
+bool blaslt_auto() {
+  static const bool on = [] { const char* e = getenv("ASRX_GEMM_BLASLT"); return !(e && e[0] == '0'); }();
+  return on;
+}
+
 GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
   GemmPlan pl;
   pl.vec = (d->lda % 8 == 0) && (d->ldb % 8 == 0) && ((uintptr_t)d->a % 16 == 0) && ((uintptr_t)d->b % 16 == 0) &&
@@ -1508,7 +1517,7 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
     tile = t128 >= 400 ? 128 : 64;
   }
   const int kvar = d->kernel == 1 ? 1 : d->kernel == 3 ? 3 : d->kernel == 4 ? 4 : d->kernel == 5 ? 5 :
-                   d->kernel == 6 ? 6 : 0;
+                   d->kernel == 6 ? 6 : d->kernel == 7 ? 7 : 0;
   const bool dma_ok = pl.vec && d->k % BK == 0 && (!d->a_trans || d->m % 8 == 0) && (!d->b_trans || d->n % 8 == 0) &&
                       d->m >= 8 && d->n >= 8;
   const int nt_p3 = ((d->m + P_BM - 1) / P_BM) * ((d->n + P_BN - 1) / P_BN);
@@ -1569,6 +1578,18 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
     pl.use = 1;   // p4 takes single, unsplit GEMMs with its instantiated epilogues; the rest stays on p3
     pl.ntiles = nt_p3;
   }
+  // plain data gradients C = A B (bf16 in / out, no epilogue) of the encoder's 512-wide outputs with a long
+  // reduction (Q/K/V and FFN1 data gradients, K = 1536 / 2048): hipBLASLt's kernel is faster there than p3
+  // (tools/blas_ref.py: 37.7 -> 30.3 and 51.4 -> 43.9 us); kernel code 7 forces the library for any plain GEMM.
+  // use 10 = hipBLASLt (blaslt.hip), falling back to p3 whenever the library declines the call.
+  const bool plain = dma_ok && epi == 0 && !d->a_trans && d->c_dtype == ASRX_BF16 && d->beta == 0.f &&
+                     batch == 1 && splitk == 1 && !d->rowsum_a && !d->mask_out && !d->sc_outer && !d->sc_inner;
+  if (plain && (kvar == 7 || (kvar == 0 && blaslt_auto() && d->b_trans && d->m >= 8192 && d->n == 512 &&
+                              d->k >= 1536))) {
+    pl.use = 10;
+    pl.epi = 0;
+    pl.ntiles = nt_p3;
+  }
   return pl;
 }
 
@@ -1591,7 +1612,9 @@ extern "C" int asrx_gemm_kernel_name(const asrx_gemm_desc* d, char* buf, int len
     return ASRX_OK;
   }
   const GemmPlan pl = plan_bf16(d, batch, splitk);
-  if (pl.use == 9)
+  if (pl.use == 10)
+    snprintf(buf, len, "hipblaslt");
+  else if (pl.use == 9)
     snprintf(buf, len, "gemm_bf16_tallk_kernel");
   else if (pl.use == 1 || pl.use == 2)
     snprintf(buf, len, "gemm_bf16_p%d_kernel<%s, %s, %d>", pl.use == 2 ? 4 : 3, tf[!!d->a_trans], tf[!!d->b_trans],
@@ -1676,6 +1699,13 @@ extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
         const int nt = ((d->m + P_BM - 1) / P_BM) * ((gc.N + bn - 1) / bn);
         if (pl.use == 2) dispatch_p3<false, false, true>(gc, epi, nt, 1, 1, st);
         else dispatch_p3<false, false>(gc, epi, nt, 1, 1, st);
+      }
+    } else if (pl.use == 10) {
+      const int rc = blaslt_gemm_bf16(d, st);
+      if (rc < 0) return rc;
+      if (rc == 1) {   // library declined (e.g. an unseen shape during graph capture): p3
+        if (d->b_trans) dispatch_p3<false, true>(g, 0, pl.ntiles, 1, 1, st);
+        else dispatch_p3<false, false>(g, 0, pl.ntiles, 1, 1, st);
       }
     } else if (pl.use == 9) {
       hipLaunchKernelGGL(gemm_bf16_tallk_kernel, dim3(splitk), dim3(512), 0, st, g, TallkConv{0, 0, 0, 0, 0, 0});

@@ -241,6 +241,24 @@ def test_gemm_batched_heads():
     assert relerr(S[:, :, :L].cpu(), ref) < 1e-5
 
 
+@pytest.mark.parametrize("M,N,Kd,bt", [(15936, 512, 2048, 1), (15936, 512, 1536, 1), (300, 200, 136, 1),
+                                        (257, 96, 64, 0), (64, 512, 2048, 1)])
+def test_gemm_hipblaslt_plain(M, N, Kd, bt):
+    """The hipBLASLt path of asrx_gemm (kernel code 7; chosen automatically for the encoder's plain 512-wide data
+    gradients): C = A . op(B) in bf16 against an fp64 reference, both B layouts."""
+    g = torch.Generator().manual_seed(M + N + Kd)
+    a = bf(torch.randn(M, Kd, generator=g))
+    b = bf(torch.randn(Kd, N, generator=g) if bt else torch.randn(N, Kd, generator=g))
+    c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    ref = a.double() @ (b.double() if bt else b.double().t())
+    K().gemm(a.to(dev), b.to(dev), c, M, N, Kd, lda=Kd, ldb=b.shape[1], ldc=N, b_trans=bool(bt), kernel="blaslt")
+    assert relerr(c.float().cpu(), ref) < 1e-2
+    if bt and N == 512 and Kd >= 1536 and M >= 8192:   # the auto plan takes the same path
+        c2 = torch.empty_like(c)
+        K().gemm(a.to(dev), b.to(dev), c2, M, N, Kd, lda=Kd, ldb=N, ldc=N, b_trans=True)
+        assert torch.equal(c, c2)
+
+
 # ------------------------------------------------------------------------------------------------ LayerNorm
 
 @pytest.fixture

@@ -163,7 +163,11 @@ def test_gemm_kernel_plan_names_without_gpu():
     # wide outputs (>= 320 256x256 tiles) take p4, the N = 512 outputs p3
     assert kernel_name(desc(15936, 1536, 512, bias=True)) == "gemm_bf16_p4_kernel<false, false, 1>"
     assert kernel_name(desc(15936, 2048, 512, bt=1)) == "gemm_bf16_p4_kernel<false, true, 0>"
-    assert kernel_name(desc(15936, 512, 2048, bt=1)) == "gemm_bf16_p3_kernel<false, true, 0>"
+    # the plain 512-wide data gradients with K >= 1536 go to hipBLASLt (ASRX_GEMM_BLASLT), shorter ones stay on p3
+    assert kernel_name(desc(15936, 512, 2048, bt=1)) == "hipblaslt"
+    assert kernel_name(desc(15936, 512, 1536, bt=1)) == "hipblaslt"
+    assert kernel_name(desc(15936, 512, 512, bt=1)) == "gemm_bf16_p3_kernel<false, true, 0>"
+    assert kernel_name(desc(4096, 512, 2048, bt=1)).startswith("gemm_bf16_ring_kernel")
     assert kernel_name(desc(15936, 512, 512, bias=True)) == "gemm_bf16_p3_kernel<false, false, 1>"
     wg = desc(2048, 512, 15936, at=1, bt=1, c_dtype=F32)
     wg.tile = 128                     # as kernels.wgrad_plan sets it
