@@ -244,31 +244,65 @@ def _grouped_p3_ok(items, beta):
 _XCD_PLANS = {}
 
 
-def xcd_plan(shapes, tile=256, nxcd=8):
+def xcd_plan(shapes, tile=256, nxcd=8, pack=None):
     """Lay grouped weight-gradient tiles out over the 8 XCDs (workgroup b runs on XCD b % 8): whole groups
     (longest reductions, then largest groups first) go to the least-loaded XCD, so the tiles of a group run on
     one XCD at the same time and share its L2, and every XCD gets about the same work.
+    pack (default ASRX_WGRAD_PACK): additionally pack the groups into rounds of 32 tiles — one workgroup per CU,
+    32 CUs per XCD — so that a group never straddles two rounds (the tiles of a straddling group run a whole
+    reduction apart and fetch their shared operand panels twice).
     shapes: (m, n, k) per group (C[m,n], reduction k).  Returns (group order, tiles per group, block -> tile map)."""
     import numpy as np
-    key = (tuple(shapes), tile, nxcd)
+    pack = WGRAD_PACK if pack is None else pack
+    key = (tuple(shapes), tile, nxcd, pack)
     if key in _XCD_PLANS:
         return _XCD_PLANS[key]
     tm, tn = tile if isinstance(tile, tuple) else (tile, tile)
     nts = [((m + tm - 1) // tm) * ((n + tn - 1) // tn) for (m, n, k) in shapes]
     order = sorted(range(len(shapes)), key=lambda i: (-shapes[i][2], -nts[i], i))
     load = [0] * nxcd
-    per_xcd = [[] for _ in range(nxcd)]
-    for i in order:
-        x = min(range(nxcd), key=lambda j: (load[j], j))
-        per_xcd[x].append(i)
-        load[x] += nts[i] * shapes[i][2]
-    group_order = [i for x in range(nxcd) for i in per_xcd[x]]
-    first = {}
-    t = 0
-    for i in group_order:
-        first[i] = t
-        t += nts[i]
-    slots = [[first[i] + j for i in per_xcd[x] for j in range(nts[i])] for x in range(nxcd)]
+    if not pack or nxcd == 1:
+        per_xcd = [[] for _ in range(nxcd)]
+        for i in order:
+            x = min(range(nxcd), key=lambda j: (load[j], j))
+            per_xcd[x].append(i)
+            load[x] += nts[i] * shapes[i][2]
+        group_order = [i for x in range(nxcd) for i in per_xcd[x]]
+        first = {}
+        t = 0
+        for i in group_order:
+            first[i] = t
+            t += nts[i]
+        slots = [[first[i] + j for i in per_xcd[x] for j in range(nts[i])] for x in range(nxcd)]
+    else:
+        cap = 32   # CUs per XCD
+        group_order = order
+        first = {}
+        t = 0
+        for i in group_order:
+            first[i] = t
+            t += nts[i]
+        # chunks of <= cap consecutive tiles (they share operand panel rows), first-fit decreasing into
+        # same-reduction bins of cap tiles
+        chunks = [(shapes[i][2], i, t0, min(nts[i], t0 + cap)) for i in order for t0 in range(0, nts[i], cap)]
+        chunks.sort(key=lambda c: (-c[0], -(c[3] - c[2]), c[1], c[2]))
+        bins = []   # [k, fill, chunks]
+        for c in chunks:
+            size = c[3] - c[2]
+            for b in bins:
+                if b[0] == c[0] and b[1] + size <= cap:
+                    b[1] += size
+                    b[2].append(c)
+                    break
+            else:
+                bins.append([c[0], size, [c]])
+        # longest reductions first, full rounds before partial ones (a partial round lets the next one start early)
+        bins.sort(key=lambda b: (-b[0], -b[1]))
+        slots = [[] for _ in range(nxcd)]
+        for b in bins:
+            x = min(range(nxcd), key=lambda j: (load[j], j))
+            slots[x].extend(first[i] + j for (_, i, t0, t1) in b[2] for j in range(t0, t1))
+            load[x] += b[1] * b[0]
     depth = max(len(sl) for sl in slots)
     block_tile = np.full(depth * nxcd, 0xFFFF, dtype=np.uint16)
     for x in range(nxcd):
@@ -336,6 +370,8 @@ def _grouped_xcd(items, common, kind="p3"):
 
 # lay each group's tiles on one XCD (ASRX_WGRAD_XCD=0: one table order over all XCDs, A/B)
 WGRAD_XCD = os.environ.get("ASRX_WGRAD_XCD", "1") != "0"
+# pack the groups into 32-tile rounds per XCD (xcd_plan; ASRX_WGRAD_PACK=1, A/B)
+WGRAD_PACK = os.environ.get("ASRX_WGRAD_PACK", "0") == "1"
 
 
 def linear_wgrad_grouped(items, *, beta=1.0, kind=None):

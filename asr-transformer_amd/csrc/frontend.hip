@@ -887,6 +887,37 @@ __global__ __launch_bounds__(256) void cast_kernel(int sd, const void* __restric
   }
 }
 
+ASRX_DEV void adam_f4(f4_t& pp, const f4_t gg, f4_t& mm, f4_t& vv, float lr, float b1, float b2, float eps,
+                      float wd, float bc1, float rbc2, float gs, int decoupled) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float gr = gg[k] * gs;
+    float pv = pp[k];
+    if (decoupled) pv *= (1.f - lr * wd);
+    else gr += wd * pv;
+    mm[k] = b1 * mm[k] + (1.f - b1) * gr;
+    vv[k] = b2 * vv[k] + (1.f - b2) * gr * gr;
+    const float denom = sqrtf(vv[k]) * rbc2 + eps;
+    pv -= (lr / bc1) * mm[k] / denom;
+    pp[k] = pv;
+  }
+}
+
+ASRX_DEV void adam_store(float* p, float* m, float* v, bf16_t* pb, int64_t i, const f4_t& pp, const f4_t& mm,
+                         const f4_t& vv) {
+  ((f4_t*)p)[i] = pp;
+  ((f4_t*)m)[i] = mm;
+  ((f4_t*)v)[i] = vv;
+  if (pb) {
+    uint2 u;
+    u.x = pack2bf(pp[0], pp[1]);
+    u.y = pack2bf(pp[2], pp[3]);
+    ((uint2*)pb)[i] = u;
+  }
+}
+
+// HBM-bound (30 B per parameter with the bf16 shadow): two 16-B vectors per operand per thread and iteration, all
+// eight loads issued before any arithmetic, so each wave keeps twice the bytes in flight of a one-vector loop.
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    bf16_t* __restrict__ pb, int64_t n, float lr, float b1, float b2,
@@ -897,30 +928,23 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
     bc1 = hyp[1];
     rbc2 = 1.f / sqrtf(hyp[2]);
   }
-  const int64_t n4 = n / 4;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-    f4_t pp = ((f4_t*)p)[i], gg = ((const f4_t*)g)[i], mm = ((f4_t*)m)[i], vv = ((f4_t*)v)[i];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      float gr = gg[k] * gs;
-      float pv = pp[k];
-      if (decoupled) pv *= (1.f - lr * wd);
-      else gr += wd * pv;
-      mm[k] = b1 * mm[k] + (1.f - b1) * gr;
-      vv[k] = b2 * vv[k] + (1.f - b2) * gr * gr;
-      const float denom = sqrtf(vv[k]) * rbc2 + eps;
-      pv -= (lr / bc1) * mm[k] / denom;
-      pp[k] = pv;
-    }
-    ((f4_t*)p)[i] = pp;
-    ((f4_t*)m)[i] = mm;
-    ((f4_t*)v)[i] = vv;
-    if (pb) {
-      uint2 u;
-      u.x = pack2bf(pp[0], pp[1]);
-      u.y = pack2bf(pp[2], pp[3]);
-      ((uint2*)pb)[i] = u;
-    }
+  const int64_t n4 = n / 4, stride = (int64_t)gridDim.x * 256;
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + stride < n4; i += 2 * stride) {
+    const int64_t j = i + stride;
+    f4_t p0 = ((f4_t*)p)[i], p1 = ((f4_t*)p)[j];
+    const f4_t g0 = __builtin_nontemporal_load((const f4_t*)g + i), g1 = __builtin_nontemporal_load((const f4_t*)g + j);
+    f4_t m0 = ((f4_t*)m)[i], m1 = ((f4_t*)m)[j];
+    f4_t v0 = ((f4_t*)v)[i], v1 = ((f4_t*)v)[j];
+    adam_f4(p0, g0, m0, v0, lr, b1, b2, eps, wd, bc1, rbc2, gs, decoupled);
+    adam_f4(p1, g1, m1, v1, lr, b1, b2, eps, wd, bc1, rbc2, gs, decoupled);
+    adam_store(p, m, v, pb, i, p0, m0, v0);
+    adam_store(p, m, v, pb, j, p1, m1, v1);
+  }
+  if (i < n4) {
+    f4_t pp = ((f4_t*)p)[i], mm = ((f4_t*)m)[i], vv = ((f4_t*)v)[i];
+    adam_f4(pp, ((const f4_t*)g)[i], mm, vv, lr, b1, b2, eps, wd, bc1, rbc2, gs, decoupled);
+    adam_store(p, m, v, pb, i, pp, mm, vv);
   }
   // tail
   if (blockIdx.x == 0) {

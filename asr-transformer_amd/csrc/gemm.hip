@@ -1486,10 +1486,11 @@ void dispatch_bf16(const GemmArgs& g, bool at, bool bt, bool vec, int batch, hip
 struct GemmPlan {
   int use;     // 1 = p3 (256x128 LDS-DMA ring), 2 = p4 (256x256), 3 = register path 128, 4 = register path 64,
                // 5 = ring 64x64, 6 = ring 128x64 (4-stage LDS-DMA, small grids), 9 = tall-K (conv2 dW),
-               // 10 = hipBLASLt (plain GEMMs, blaslt.hip)
+               // 10 = hipBLASLt (plain / bias / bias + fp32 residual GEMMs, blaslt.hip)
   bool vec;    // 16-byte aligned operands
   int epi;     // instantiated epilogue flags (E_GENERIC when the fast-path set has no match)
   int ntiles;  // output tiles of the chosen kernel
+  int fb_use = 0, fb_epi = 0, fb_ntiles = 0;   // use 10: the hand-written plan run when the library declines
 };
 
 bool epi_instantiated(bool at, bool bt, int epi) {
@@ -1505,6 +1506,26 @@ bool epi_instantiated(bool at, bool bt, int epi) {
 bool blaslt_auto() {
   static const bool on = [] { const char* e = getenv("ASRX_GEMM_BLASLT"); return !(e && e[0] == '0'); }();
   return on;
+}
+// ASRX_GEMM_BLASLT_RESID=0 keeps the bias + residual forward on p3 (A/B switch; default on)
+bool lt_resid_auto() {
+  static const bool on = [] { const char* e = getenv("ASRX_GEMM_BLASLT_RESID"); return !(e && e[0] == '0'); }();
+  return on;
+}
+
+// ASRX_GEMM_BLASLT_M: fewest rows for the automatic library path (A/B).  Default 8192, the encoder's GEMMs only:
+// with 4096 the decoder's instances also move to the library — each faster alone (tools/blas_ref.py), but the
+// graph-mode step went 13.50 -> 14.93 ms with 2.9 ms of host enqueue per step instead of 0.2 (measured, rejected)
+int lt_min_rows() {
+  static const int m = [] { const char* e = getenv("ASRX_GEMM_BLASLT_M"); return e ? atoi(e) : 8192; }();
+  return m;
+}
+
+bool lt_auto(const asrx_gemm_desc* d, int lt_epi) {
+  if (d->m < lt_min_rows() || d->n != 512 || d->k < 1536) return false;
+  if (lt_epi == 0) return d->b_trans;
+  if (lt_epi == (E_BIAS | E_RESID | E_F32)) return !d->b_trans && lt_resid_auto();
+  return false;
 }
 
 GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
@@ -1578,19 +1599,26 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
     pl.use = 1;   // p4 takes single, unsplit GEMMs with its instantiated epilogues; the rest stays on p3
     pl.ntiles = nt_p3;
   }
-  // plain data gradients C = A B (bf16 in / out, no epilogue) of the encoder's 512-wide outputs with a long
-  // reduction (Q/K/V and FFN1 data gradients, K = 1536 / 2048): hipBLASLt's kernel is faster there than p3
-  // (tools/blas_ref.py: 37.7 -> 30.3 and 51.4 -> 43.9 us); kernel code 7 forces the library for any plain GEMM.
-  // use 10 = hipBLASLt (blaslt.hip), falling back to p3 whenever the library declines the call.
-  const bool plain = dma_ok && epi == 0 && !d->a_trans && d->c_dtype == ASRX_BF16 && d->beta == 0.f &&
-                     batch == 1 && splitk == 1 && !d->rowsum_a && !d->mask_out && !d->sc_outer && !d->sc_inner;
-  if (plain && (kvar == 7 || (kvar == 0 && blaslt_auto() && d->b_trans && d->m >= 8192 && d->n == 512 &&
-                              d->k >= 1536))) {
+  // hipBLASLt (use 10 = blaslt.hip; falls back to the hand-written plan `fb_use` whenever the library declines) for
+  // the library-expressible GEMMs: no epilogue, or bias (+ fp32 residual, fp32 out) — forward single GEMMs with
+  // unit-stride rows.  Auto where the library kernel is faster (tools/blas_ref.py, interleaved in one process):
+  //  * plain data gradients C = A B (bf16 out) of the encoder's 512-wide outputs with a long reduction (Q/K/V and
+  //    FFN1 data gradients, K = 1536 / 2048): 37.7 -> 30.3 and 51.4 -> 43.9 us;
+  //  * the FFN2 forward C32 = A B^T + bias + resid (512-wide fp32 residual stream, K = 2048): 56.8 -> 43.1 us
+  //    alone, 52.3 -> 48.2 us in the step (rocprofv3 kernel trace).
+  // Kernel code 7 forces the library for any expressible GEMM.
+  const int lt_epi = epi & ~(E_ALPHA);
+  const bool lt_ok = dma_ok && !d->a_trans && batch == 1 && splitk == 1 && !d->rowsum_a && !d->mask_out &&
+                     !d->sc_outer && !d->sc_inner && d->beta == 0.f &&
+                     ((lt_epi == 0 && d->c_dtype == ASRX_BF16) || lt_epi == E_BIAS ||
+                      lt_epi == (E_BIAS | E_RESID | E_F32));
+  if (lt_ok && (kvar == 7 || (kvar == 0 && blaslt_auto() && lt_auto(d, lt_epi)))) {
+    pl.fb_use = pl.use;
+    pl.fb_epi = pl.epi;
+    pl.fb_ntiles = pl.ntiles;
     pl.use = 10;
-    pl.epi = 0;
-    pl.ntiles = nt_p3;
   }
-  return pl;
+    return pl;
 }
 
 }  // namespace
@@ -1625,6 +1653,73 @@ extern "C" int asrx_gemm_kernel_name(const asrx_gemm_desc* d, char* buf, int len
   else
     snprintf(buf, len, "gemm_bf16_kernel<%d, %d, %s, %s, %s>", pl.use == 3 ? 128 : 64, pl.use == 3 ? 128 : 64,
              tf[!!d->a_trans], tf[!!d->b_trans], tf[pl.vec]);
+  return ASRX_OK;
+}
+
+// Enqueue the bf16 plan `pl` (asrx_gemm after argument checks; also the fallback when hipBLASLt declines a call).
+int gemm_bf16_run(const asrx_gemm_desc* d, const GemmArgs& g, const GemmPlan& pl, int batch, int splitk,
+                  hipStream_t st) {
+  const int epi = pl.epi;
+  // the bit-mask output is written only by the paired bf16 store path of the fast epilogues
+  if (d->mask_out && (!(epi != E_GENERIC && (epi & E_MASKOUT)) || !d->relu || d->c_dtype != ASRX_BF16 || d->n % 32 != 0 ||
+                      d->ldc % 8 != 0 || (uintptr_t)d->c % 16 != 0 || (uintptr_t)d->mask_out % 4 != 0 ||
+                      d->ld_mask < d->n / 32))
+    return ASRX_ERR_UNSUPPORTED;
+  if ((pl.use == 1 || pl.use == 2) && (epi & E_BIAS) && epi != E_GENERIC && d->n > P_BIAS_BYTES / 4) {
+    // the p3 bias epilogue stages the whole bias vector in LDS (16 KiB): wider outputs run as column chunks
+    // (fast-path epilogues without dropout only: their element math does not depend on N)
+    if ((epi & E_DROP) || d->a_trans || d->b_trans || batch != 1 || splitk != 1) return ASRX_ERR_UNSUPPORTED;
+    for (int c0 = 0; c0 < d->n; c0 += P_BIAS_BYTES / 4) {
+      GemmArgs gc = g;
+      gc.N = std::min(P_BIAS_BYTES / 4, d->n - c0);
+      gc.b = (const bf16_t*)d->b + (int64_t)c0 * d->ldb;
+      gc.bias = d->bias + c0;
+      gc.c = (char*)d->c + (int64_t)c0 * (d->c_dtype == ASRX_F32 ? 4 : 2);
+      if (gc.rowadd) gc.rowadd = d->rowadd + c0;
+      if (gc.resid) gc.resid = (const float*)d->resid + c0;
+      if (gc.gate) gc.gate = d->gate_dtype == ASRX_BITS ? (const void*)((const uint32_t*)d->gate + c0 / 32)
+                                                        : (const void*)((const bf16_t*)d->gate + c0);
+      if (gc.mask_out) gc.mask_out = d->mask_out + c0 / 32;
+      const int bn = pl.use == 2 ? 256 : P_BN;
+      const int nt = ((d->m + P_BM - 1) / P_BM) * ((gc.N + bn - 1) / bn);
+      if (pl.use == 2) dispatch_p3<false, false, true>(gc, epi, nt, 1, 1, st);
+      else dispatch_p3<false, false>(gc, epi, nt, 1, 1, st);
+    }
+  } else if (pl.use == 10) {
+    const int rc = blaslt_gemm_bf16(d, st);
+    if (rc < 0) return rc;
+    if (rc == 1) {   // library declined (e.g. an unseen shape during graph capture): the hand-written plan
+      GemmPlan fb = pl;
+      fb.use = pl.fb_use;
+      fb.epi = pl.fb_epi;
+      fb.ntiles = pl.fb_ntiles;
+      return gemm_bf16_run(d, g, fb, batch, splitk, st);
+    }
+  } else if (pl.use == 9) {
+    hipLaunchKernelGGL(gemm_bf16_tallk_kernel, dim3(splitk), dim3(512), 0, st, g, TallkConv{0, 0, 0, 0, 0, 0});
+  } else if (pl.use == 2) {
+    if (!d->a_trans && !d->b_trans) dispatch_p3<false, false, true>(g, epi, pl.ntiles, splitk, batch, st);
+    else if (!d->a_trans && d->b_trans) dispatch_p3<false, true, true>(g, epi, pl.ntiles, splitk, batch, st);
+    else if (d->a_trans && !d->b_trans) dispatch_p3<true, false, true>(g, epi, pl.ntiles, splitk, batch, st);
+    else dispatch_p3<true, true, true>(g, epi, pl.ntiles, splitk, batch, st);
+  } else if (pl.use == 1) {
+    if (!d->a_trans && !d->b_trans) dispatch_p3<false, false>(g, epi, pl.ntiles, splitk, batch, st);
+    else if (!d->a_trans && d->b_trans) dispatch_p3<false, true>(g, epi, pl.ntiles, splitk, batch, st);
+    else if (d->a_trans && !d->b_trans) dispatch_p3<true, false>(g, epi, pl.ntiles, splitk, batch, st);
+    else dispatch_p3<true, true>(g, epi, pl.ntiles, splitk, batch, st);
+  } else if (pl.use >= 5) {
+    if (!d->b_trans) {
+      if (pl.use == 6) dispatch_ring<128, 64, false, false>(g, epi, splitk, batch, st);
+      else dispatch_ring<64, 64, false, false>(g, epi, splitk, batch, st);
+    } else {
+      if (pl.use == 6) dispatch_ring<128, 64, false, true>(g, epi, splitk, batch, st);
+      else dispatch_ring<64, 64, false, true>(g, epi, splitk, batch, st);
+    }
+  } else if (pl.use == 3) {
+    dispatch_bf16<128, 128>(g, d->a_trans, d->b_trans, pl.vec, batch, st);
+  } else {
+    dispatch_bf16<64, 64>(g, d->a_trans, d->b_trans, pl.vec, batch, st);
+  }
   return ASRX_OK;
 }
 
@@ -1674,64 +1769,8 @@ extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
     const GemmPlan pl = plan_bf16(d, batch, splitk);
     g.splitk = splitk;
     g.k_per_split = ((((int)d->k + BK - 1) / BK + splitk - 1) / splitk) * BK;
-    const int epi = pl.epi;
-    // the bit-mask output is written only by the paired bf16 store path of the fast epilogues
-    if (d->mask_out && (!(epi != E_GENERIC && (epi & E_MASKOUT)) || !d->relu || d->c_dtype != ASRX_BF16 || d->n % 32 != 0 ||
-                        d->ldc % 8 != 0 || (uintptr_t)d->c % 16 != 0 || (uintptr_t)d->mask_out % 4 != 0 ||
-                        d->ld_mask < d->n / 32))
-      return ASRX_ERR_UNSUPPORTED;
-    if ((pl.use == 1 || pl.use == 2) && (epi & E_BIAS) && epi != E_GENERIC && d->n > P_BIAS_BYTES / 4) {
-      // the p3 bias epilogue stages the whole bias vector in LDS (16 KiB): wider outputs run as column chunks
-      // (fast-path epilogues without dropout only: their element math does not depend on N)
-      if ((epi & E_DROP) || d->a_trans || d->b_trans || batch != 1 || splitk != 1) return ASRX_ERR_UNSUPPORTED;
-      for (int c0 = 0; c0 < d->n; c0 += P_BIAS_BYTES / 4) {
-        GemmArgs gc = g;
-        gc.N = std::min(P_BIAS_BYTES / 4, d->n - c0);
-        gc.b = (const bf16_t*)d->b + (int64_t)c0 * d->ldb;
-        gc.bias = d->bias + c0;
-        gc.c = (char*)d->c + (int64_t)c0 * (d->c_dtype == ASRX_F32 ? 4 : 2);
-        if (gc.rowadd) gc.rowadd = d->rowadd + c0;
-        if (gc.resid) gc.resid = (const float*)d->resid + c0;
-        if (gc.gate) gc.gate = d->gate_dtype == ASRX_BITS ? (const void*)((const uint32_t*)d->gate + c0 / 32)
-                                                          : (const void*)((const bf16_t*)d->gate + c0);
-        if (gc.mask_out) gc.mask_out = d->mask_out + c0 / 32;
-        const int bn = pl.use == 2 ? 256 : P_BN;
-        const int nt = ((d->m + P_BM - 1) / P_BM) * ((gc.N + bn - 1) / bn);
-        if (pl.use == 2) dispatch_p3<false, false, true>(gc, epi, nt, 1, 1, st);
-        else dispatch_p3<false, false>(gc, epi, nt, 1, 1, st);
-      }
-    } else if (pl.use == 10) {
-      const int rc = blaslt_gemm_bf16(d, st);
-      if (rc < 0) return rc;
-      if (rc == 1) {   // library declined (e.g. an unseen shape during graph capture): p3
-        if (d->b_trans) dispatch_p3<false, true>(g, 0, pl.ntiles, 1, 1, st);
-        else dispatch_p3<false, false>(g, 0, pl.ntiles, 1, 1, st);
-      }
-    } else if (pl.use == 9) {
-      hipLaunchKernelGGL(gemm_bf16_tallk_kernel, dim3(splitk), dim3(512), 0, st, g, TallkConv{0, 0, 0, 0, 0, 0});
-    } else if (pl.use == 2) {
-      if (!d->a_trans && !d->b_trans) dispatch_p3<false, false, true>(g, epi, pl.ntiles, splitk, batch, st);
-      else if (!d->a_trans && d->b_trans) dispatch_p3<false, true, true>(g, epi, pl.ntiles, splitk, batch, st);
-      else if (d->a_trans && !d->b_trans) dispatch_p3<true, false, true>(g, epi, pl.ntiles, splitk, batch, st);
-      else dispatch_p3<true, true, true>(g, epi, pl.ntiles, splitk, batch, st);
-    } else if (pl.use == 1) {
-      if (!d->a_trans && !d->b_trans) dispatch_p3<false, false>(g, epi, pl.ntiles, splitk, batch, st);
-      else if (!d->a_trans && d->b_trans) dispatch_p3<false, true>(g, epi, pl.ntiles, splitk, batch, st);
-      else if (d->a_trans && !d->b_trans) dispatch_p3<true, false>(g, epi, pl.ntiles, splitk, batch, st);
-      else dispatch_p3<true, true>(g, epi, pl.ntiles, splitk, batch, st);
-    } else if (pl.use >= 5) {
-      if (!d->b_trans) {
-        if (pl.use == 6) dispatch_ring<128, 64, false, false>(g, epi, splitk, batch, st);
-        else dispatch_ring<64, 64, false, false>(g, epi, splitk, batch, st);
-      } else {
-        if (pl.use == 6) dispatch_ring<128, 64, false, true>(g, epi, splitk, batch, st);
-        else dispatch_ring<64, 64, false, true>(g, epi, splitk, batch, st);
-      }
-    } else if (pl.use == 3) {
-      dispatch_bf16<128, 128>(g, d->a_trans, d->b_trans, pl.vec, batch, st);
-    } else {
-      dispatch_bf16<64, 64>(g, d->a_trans, d->b_trans, pl.vec, batch, st);
-    }
+    const int rc = gemm_bf16_run(d, g, pl, batch, splitk, st);
+    if (rc != ASRX_OK) return rc;
   } else {
     const int vec = (d->lda % 4 == 0) && (d->ldb % 4 == 0) && ((uintptr_t)d->a % 16 == 0) &&
                     ((uintptr_t)d->b % 16 == 0) && (d->sa_outer % 4 == 0) && (d->sa_inner % 4 == 0) &&

@@ -259,6 +259,27 @@ def test_gemm_hipblaslt_plain(M, N, Kd, bt):
         assert torch.equal(c, c2)
 
 
+@pytest.mark.parametrize("M,N,Kd,f32,resid", [(15936, 512, 2048, 1, 1), (4096, 512, 2048, 1, 1), (300, 200, 136, 1, 1),
+                                              (257, 96, 64, 1, 0), (257, 96, 64, 0, 0), (64, 512, 512, 1, 1)])
+def test_gemm_hipblaslt_bias_resid(M, N, Kd, f32, resid):
+    """The hipBLASLt path with the library's bias epilogue and the fp32 residual as its C matrix (beta = 1): the
+    FFN2 forward's out = x . w^T + bias + resid (E_BIAS | E_RESID | E_F32), forced (kernel code 7) and auto, against
+    an fp64 reference and against the hand-written p3 epilogue (same inputs, fp32 rounding-order differences only)."""
+    g = torch.Generator().manual_seed(M + 3 * N + Kd)
+    x, w = bf(torch.randn(M, Kd, generator=g)), bf(torch.randn(N, Kd, generator=g))
+    bias = torch.randn(N, generator=g)
+    r = torch.randn(M, N + 8, generator=g) if resid else None   # ld_resid = N + 8 != ldc
+    ref = x.double() @ w.double().t() + bias.double() + (r[:, :N].double() if resid else 0)
+    kw = dict(resid=r.to(dev), ld_resid=N + 8) if resid else {}
+    outs = {}
+    for kern in ("blaslt", "p3", None):
+        c = torch.empty(M, N, device=dev, dtype=torch.float32 if f32 else torch.bfloat16)
+        K().linear(x.to(dev), w.to(dev), c, bias=bias.to(dev), kernel=kern, **kw)
+        outs[kern] = c.float().cpu()
+        assert relerr(outs[kern], ref) < (1e-5 if f32 else 1e-2), kern
+    assert (outs["blaslt"] - outs["p3"]).abs().max() <= (1e-4 if f32 else 1e-2) * ref.abs().max()
+
+
 # ------------------------------------------------------------------------------------------------ LayerNorm
 
 @pytest.fixture

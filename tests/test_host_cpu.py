@@ -213,3 +213,53 @@ def test_release_spans_are_exact():
         assert inside == (id(p) in mine), p.shape
     assert covered >= sum(p.numel() for p in params)
     assert len(_spans(C, list(m.decoder.parameters()))) == 1
+
+
+def _c3_wgrad_shapes():
+    enc, dec, d, ff = 15936, 4096, 512, 2048
+    shapes = []
+    for _ in range(12):
+        shapes += [(3 * d, d, enc), (d, d, enc), (ff, d, enc), (d, ff, enc)]
+    for _ in range(12):
+        shapes += [(3 * d, d, dec), (d, d, dec), (d, d, dec), (d, d, dec), (ff, d, dec), (d, ff, dec)]
+    return shapes + [(12 * 2 * d, d, enc), (d, 19 * 64, enc), (256, d, dec)]
+
+
+@pytest.mark.parametrize("pack", [False, True])
+def test_xcd_plan_covers_every_tile_once(pack):
+    """The grouped weight-gradient workgroup -> tile map (kernels.xcd_plan) at the c3 step's shapes: every tile of
+    every group exactly once, tiles of a group contiguous in the tile numbering, and (pack) each group's tiles on
+    one XCD, in rounds of at most 32 per XCD that never split a group of <= 32 tiles."""
+    import numpy as np
+    from asrx import kernels
+    shapes = _c3_wgrad_shapes()
+    group_order, nts, block_tile, tmap = kernels.xcd_plan(shapes, tile=256, nxcd=8, pack=pack)
+    assert sorted(group_order) == list(range(len(shapes)))
+    total = sum(nts)
+    used = block_tile[block_tile != 0xFFFF].astype(np.int64)
+    assert sorted(used.tolist()) == list(range(total))
+    assert len(tmap) == total
+    starts = np.cumsum([0] + [nts[i] for i in group_order])
+    for slot, i in enumerate(group_order):
+        assert (tmap[starts[slot]:starts[slot + 1]] == slot).all()
+    for x in range(8):
+        col = block_tile[x::8]
+        col = col[col != 0xFFFF].astype(np.int64)
+        groups = tmap[col]
+        for slot in set(groups.tolist()):
+            pos = np.nonzero(groups == slot)[0]
+            assert pos[-1] - pos[0] + 1 == len(pos)          # a group's tiles are consecutive on its XCD
+        if pack:
+            for slot in set(groups.tolist()):
+                n = nts[group_order[slot]]
+                pos = np.nonzero(groups == slot)[0]
+                if n <= 32 and len(pos) == n:
+                    assert len(pos) <= 32
+    # each group on exactly one XCD (the packed plan may split a group of > 32 tiles over XCDs)
+    where = {}
+    for b, t in enumerate(block_tile.tolist()):
+        if t != 0xFFFF:
+            where.setdefault(int(tmap[t]), set()).add(b % 8)
+    for slot, xs in where.items():
+        if not pack or nts[group_order[slot]] <= 32:
+            assert len(xs) == 1

@@ -39,6 +39,10 @@ SHAPES = [
     ("dec ffn1 dg512", "dgrad", 4096, 2048, 512),
     ("dec qkv dg512", "dgrad", 4096, 1536, 512),
     ("dec out dg512", "dgrad", 4096, 512, 512),
+    # the FFN2 forward of the step: fp32 residual stream out = x . w^T + bias + resid
+    ("ffn2 fwd res", "fwdres", 15936, 512, 2048),
+    ("dec ffn2 fwd res", "fwdres", 4096, 512, 2048),
+    ("out fwd res", "fwdres", 15936, 512, 512),
 ]
 
 
@@ -106,9 +110,18 @@ def main():
             dy, w = rnd(M, N), rnd(N, Kd)
             y = torch.empty(M, Kd, device="cuda", dtype=torch.bfloat16)
             res["hipBLASLt"] = timeit(lambda: torch.mm(dy, w, out=y), args.reps, args.rounds)
-            for v in variants:
+            for v in variants + ["blaslt"]:
                 kk, fb = kb(v)
                 dbg_runs(res, v, lambda: K.linear_dgrad(dy, w, y, kernel=kk), fb)
+        elif kind == "fwdres":
+            x, w = rnd(M, Kd), rnd(N, Kd)
+            bias = torch.randn(N, device="cuda", generator=g)
+            r = torch.randn(M, N, device="cuda", generator=g)
+            y = torch.empty(M, N, device="cuda")
+            for v in variants + ["blaslt", "auto"]:
+                kk = None if v == "auto" else kb(v)[0]
+                res[v] = timeit(lambda: K.linear(x, w, y, bias=bias, resid=r, ld_resid=N, kernel=kk), args.reps,
+                                args.rounds)
         elif kind == "fwdepi":
             x, w = rnd(M, Kd), rnd(N, Kd)
             bias = torch.randn(N, device="cuda", generator=g)

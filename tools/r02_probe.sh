@@ -31,6 +31,13 @@ for s in "$@"; do
     counters) step counters 120 rocprofv3 -L ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 3 --no-cpu-baseline --no-probe --no-sub --no-other ;;
     pmcm) step pmcm 300 timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/pmcm -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-graph --no-cpu-baseline --no-probe --no-sub --no-other && python3 tools/pmc_mfma.py gpurun_out/pmcm/run_counter_collection.csv --out gpurun_out/c3_pmc_mfma.json ;;
+    newt) step newt 400 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 200 --timeout-method thread -m gpu -k "hipblaslt or adam" ;;
+    blasres) step blasres 300 python tools/blas_ref.py --variants p3 --nogrouped --only "ffn2 fwd res,dec ffn2 fwd res,out fwd res,dec ffn1 dg512,dec qkv dg512,enc qkv dg512,dec out dg512" ;;
+    abm) bash tools/ab_env.sh 2 ASRX_GEMM_BLASLT_M=8192 ASRX_GEMM_BLASLT_M=4096 || exit $? ;;
+    abpack) bash tools/ab_env.sh 2 ASRX_WGRAD_PACK=0 ASRX_WGRAD_PACK=1 || exit $? ;;
+    steptab) python3 tools/step_table.py gpurun_out/prof/run_kernel_trace.csv > gpurun_out/step_table.txt && head -45 gpurun_out/step_table.txt ;;
+    abres) bash tools/ab_env.sh 2 ASRX_GEMM_BLASLT_RESID=0 ASRX_GEMM_BLASLT_RESID=1 || exit $? ;;
+    gpu) step gputests 1000 python -u -m pytest tests -x -q --timeout 400 --timeout-method thread -m gpu ;;
     *) echo "unknown $s"; exit 2 ;;
   esac
 done
