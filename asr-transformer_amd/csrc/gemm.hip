@@ -1521,6 +1521,13 @@ int lt_min_rows() {
   return m;
 }
 
+// ASRX_P4_MIN_TILES: fewest 256x256 tiles for the automatic p4 plan (A/B of the wave quantisation: the c3 Q/K/V
+// projection has 378 such tiles = 1.48 rounds over 256 CUs, 756 p3 tiles = 2.95 rounds)
+int p4_min_tiles() {
+  static const int t = [] { const char* e = getenv("ASRX_P4_MIN_TILES"); return e ? atoi(e) : 400; }();
+  return t;
+}
+
 bool lt_auto(const asrx_gemm_desc* d, int lt_epi) {
   if (d->m < lt_min_rows() || d->n != 512 || d->k < 1536) return false;
   if (lt_epi == 0) return d->b_trans;
@@ -1559,7 +1566,7 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
       // FFN2 data gradient, the Q/K/V and cross K/V projections) take p4: half the operand ingest per FLOP
       // (tools/blas_ref.py: FFN1 forward 47 -> 39 us, FFN2 data gradient 52 -> 41 us); the N = 512 outputs (126
       // such tiles) stay on p3
-      if (nt_p4 * splitk * batch >= 320 && splitk == 1 && batch == 1) pl.use = 2;
+      if (nt_p4 * splitk * batch >= p4_min_tiles() && splitk == 1 && batch == 1) pl.use = 2;
       else if (nt_p3 * splitk * batch >= 192) pl.use = 1;
       // (64x64 tiles also win the long-K decoder GEMMs, K >= 1536: 4 x more workgroups to cover the latency)
       else pl.use = (nt_r128 * splitk * batch >= 192 && d->k < 1536) ? 6 : 5;

@@ -34,6 +34,8 @@ for s in "$@"; do
     newt) step newt 400 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 200 --timeout-method thread -m gpu -k "hipblaslt or adam" ;;
     blasres) step blasres 300 python tools/blas_ref.py --variants p3 --nogrouped --only "ffn2 fwd res,dec ffn2 fwd res,out fwd res,dec ffn1 dg512,dec qkv dg512,enc qkv dg512,dec out dg512" ;;
     abm) bash tools/ab_env.sh 2 ASRX_GEMM_BLASLT_M=8192 ASRX_GEMM_BLASLT_M=4096 || exit $? ;;
+    abp4) bash tools/ab_env.sh 2 ASRX_P4_MIN_TILES=320 ASRX_P4_MIN_TILES=400 || exit $? ;;
+    blasqkv) ASRX_P4_MIN_TILES=400 step blasqkv 300 python tools/blas_ref.py --variants p3,p4,auto --nogrouped --noblas --only "qkv fwd" ;;
     abpack) bash tools/ab_env.sh 2 ASRX_WGRAD_PACK=0 ASRX_WGRAD_PACK=1 || exit $? ;;
     steptab) python3 tools/step_table.py gpurun_out/prof/run_kernel_trace.csv > gpurun_out/step_table.txt && head -45 gpurun_out/step_table.txt ;;
     abres) bash tools/ab_env.sh 2 ASRX_GEMM_BLASLT_RESID=0 ASRX_GEMM_BLASLT_RESID=1 || exit $? ;;
