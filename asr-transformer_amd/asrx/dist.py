@@ -19,6 +19,9 @@ import torch
 import torch.distributed as dist
 
 WIRE = os.environ.get("ASRX_DP_WIRE", "fp32")
+# a one-rank process group still exchanges its gradients (RCCL calls, segmented graph replay, exposed-time events):
+# the single-GPU rehearsal of the multi-GPU step path (bench.py with ASRX_DP_REHEARSE=1)
+FORCE = os.environ.get("ASRX_DP_FORCE", "0") == "1"
 
 
 def _cast(src, dst):
@@ -73,7 +76,8 @@ class GradAllReduce:
 
     @property
     def active(self):
-        return self.allreduce_fn is not None or (dist.is_initialized() and dist.get_world_size(self.group) > 1)
+        return self.allreduce_fn is not None or (dist.is_initialized() and
+                                                 (FORCE or dist.get_world_size(self.group) > 1))
 
     def _issue(self, view):
         if self.allreduce_fn is not None:

@@ -342,14 +342,31 @@ def other_configs(names=("c2", "c5"), reps=5):
     return out
 
 
+def _free_port():
+    import socket
+    so = socket.socket()
+    so.bind(("127.0.0.1", 0))
+    port = so.getsockname()[1]
+    so.close()
+    return port
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
+    # ASRX_DP_REHEARSE=1 at one GPU: a one-rank RCCL group and the data-parallel step path (gradient exchange
+    # between captured backward segments, barriers, max-over-ranks timing), so it runs on a 1-GPU box too
+    rehearse = world == 1 and os.environ.get("ASRX_DP_REHEARSE", "0") == "1"
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    elif rehearse:
+        os.environ["ASRX_DP_FORCE"] = "1"
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                                device_id=torch.device("cuda", local))
+    dp = world > 1 or rehearse
     import asrx
     from asrx import kernels as K
     from asrx.train import GRAPH_WARMUP, Trainer
@@ -362,7 +379,7 @@ def main():
     torch.manual_seed(0)
     model = asrx.Transformer(cfg.vocab_size, cfg.input_dim, cfg.d_model, cfg.dec_len, cfg.enc_len, cfg.n_enc,
                              cfg.n_dec, cfg.n_heads, cfg.ff_dim, dropout=cfg.dropout, precision="bf16").cuda().train()
-    if world > 1:   # identical initial weights on every rank
+    if dp:   # identical initial weights on every rank
         for p in model.parameters():
             dist.broadcast(p.data, 0)
     trainer = Trainer(model, lr=1e-4, graph=not args.no_graph)
@@ -391,26 +408,26 @@ def main():
     if probe is not None:
         probe.events = {}
         probe.flops = {}
-    if world > 1:
+    if dp:
         dist.barrier()
     torch.cuda.synchronize()
-    if world > 1:
+    if dp:
         trainer.ar_events = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = trainer.step(s, t, m)
     t_enq = time.perf_counter() - t0      # host time to enqueue the K steps (the GPU runs behind it)
     torch.cuda.synchronize()
-    if world > 1:
+    if dp:
         dist.barrier()
     dt = time.perf_counter() - t0
     K.PROBE = None
-    if world > 1:
+    if dp:
         x = torch.tensor([dt], device="cuda", dtype=torch.float64)
         dist.all_reduce(x, op=dist.ReduceOp.MAX)
         dt = float(x)
     exposed = None
-    if world > 1 and trainer.ar_events:
+    if dp and trainer.ar_events:
         mine = sum(a.elapsed_time(b) for a, b in trainer.ar_events) / len(trainer.ar_events)
         x = torch.tensor([mine], device="cuda", dtype=torch.float64)
         allv = [torch.zeros_like(x) for _ in range(world)]
@@ -442,7 +459,8 @@ def main():
            "frames_per_sec_per_gpu": round(value / world, 1),
            "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 3),
            "graph": trainer._cap is not None, "setup_steps": setup,
-           "allreduce_exposed_ms_per_rank": exposed, "grad_wire": trainer.reducer.wire if world > 1 else None,
+           "allreduce_exposed_ms_per_rank": exposed, "grad_wire": trainer.reducer.wire if dp else None,
+           "dp_rehearsal": rehearse,
            "loss": round(float(loss), 4),
            "roofline": roof}
     if rank == 0 and not args.no_sub:
@@ -454,7 +472,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(cfg, T, L, args.cpu_batch, args.cpu_steps)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dp:
         dist.destroy_process_group()
 
 

@@ -93,3 +93,56 @@ def test_gloo_two_ranks_overlapped_allreduce_exact():
     for rank, n_ready, exact, err in res:
         assert n_ready >= 2, n_ready          # decoder + upper encoder half (+ _norm_out) released early
         assert exact, err
+
+
+def _rehearsal_worker(port, wire, q):
+    """One-rank RCCL group with the gradient exchange forced on (asrx.dist.FORCE): the multi-GPU step path of a
+    graph-mode Trainer — backward captured in segments, RCCL all-reduce (or the bf16 wire's all-to-all + chunk sum
+    + all-gather) between the segment replays — against the plain single-GPU Trainer from the same weights."""
+    import copy
+    import torch.distributed as dist
+    os.environ["ASRX_DP_FORCE"] = "1"
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    torch.cuda.set_device(0)
+    import asrx
+    from asrx import dist as D
+    from asrx.train import GRAPH_WARMUP, Trainer
+    from oracle.ref_model import CONFIGS, synthetic_batch
+    spec = CONFIGS["c1"]
+    cfg = spec["cfg"]
+    torch.manual_seed(0)
+    m0 = asrx.Transformer(cfg.vocab_size, cfg.input_dim, cfg.d_model, cfg.dec_len, cfg.enc_len, cfg.n_enc,
+                          cfg.n_dec, cfg.n_heads, cfg.ff_dim, dropout=0.0, precision="bf16")
+    m1 = copy.deepcopy(m0)
+    s, t, mk = synthetic_batch(cfg, spec["batch"], spec["frames"], spec["text_len"] + 1, seed=7)
+    s, t, mk = s.cuda(), t.cuda(), mk.cuda()
+    out = {}
+    for name, m, force in (("dp", m0, True), ("ref", m1, False)):
+        D.FORCE = force
+        tr = Trainer(m.cuda().train(), lr=1e-3, graph=True, wire=wire, bucket_mb=1)
+        losses = [float(tr.step(s, t, mk)) for _ in range(GRAPH_WARMUP + 3)]
+        torch.cuda.synchronize()
+        out[name] = (tr.store.flat.detach().clone().cpu(), losses, tr.reducer.active, tr._cap is not None)
+    (p_dp, l_dp, act_dp, g_dp), (p_ref, l_ref, act_ref, g_ref) = out["dp"], out["ref"]
+    err = float((p_dp - p_ref).abs().max() / p_ref.abs().max())
+    q.put((act_dp, act_ref, g_dp, g_ref, bool(torch.equal(p_dp, p_ref)), err, l_dp, l_ref))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("wire", ["fp32", "bf16"])
+def test_rccl_one_rank_rehearsal_matches_single_gpu(wire):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rehearsal_worker, args=(_free_port(), wire, q))
+    p.start()
+    act_dp, act_ref, g_dp, g_ref, exact, err, l_dp, l_ref = q.get(timeout=600)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    assert act_dp and not act_ref and g_dp and g_ref
+    if wire == "fp32":   # a one-rank fp32 all-reduce is the identity: bit-identical training
+        assert exact, (err, l_dp, l_ref)
+    else:                # one bf16 rounding of every gradient per step
+        assert err < 2e-2, (err, l_dp, l_ref)
