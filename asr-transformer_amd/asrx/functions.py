@@ -153,9 +153,19 @@ def _release(C, ready, params):
     C.defer_wgrad()
 
 
-# encoder layers per gradient release of the multi-GPU backward (ASRX_DP_RELEASE_LAYERS; 0 = half the stack).  Every
-# release ends a grouped weight-gradient launch, so finer releases trade all-reduce overlap for fuller launches.
+# encoder layers per gradient release of the multi-GPU backward (ASRX_DP_RELEASE_LAYERS; 0 = by tile rounds, below).
+# Every release ends a grouped weight-gradient launch, so finer releases trade all-reduce overlap for fuller launches.
 RELEASE_LAYERS = int(os.environ.get("ASRX_DP_RELEASE_LAYERS", "0"))
+
+
+def _queued_tiles(C, start=0):
+    """256x256 output tiles of the weight gradients queued since queue position `start` (one tile per workgroup in
+    the grouped launch, one workgroup per CU)."""
+    return sum(-(-dy.shape[1] // 256) * -(-x.shape[1] // 256) for (dy, x, _, _) in (C.wq or [])[start:])
+
+
+def _num_cus(dev):
+    return torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 256
 
 
 def release_groups(n, every=None):
@@ -178,15 +188,26 @@ def encoder_bwd(C, enc, S, dy, gate_feats, ready=None, release_every=None):
     dx_c = torch.empty(x.shape, dtype=C.cd, device=x.device)
     dx = Bk.ln_bwd(C, x, dy, enc._norm_out, S["mean"], S["rstd"], drop_out=dx_c)
     n = len(S["layers"])
-    groups = {lo: hi for lo, hi in release_groups(n, release_every)}
+    # by tile rounds (the default): a group closes when one more layer's weight-gradient tiles would overflow one
+    # workgroup per CU — each grouped launch then runs as one full round (c3: 5 layers x 48 tiles = 240 of 256 CUs;
+    # fixed halves of 6 layers = 288 tiles take two rounds each, the second nearly empty); the bottom group goes with
+    # _lin_in and the front-end to the reducer's finish()
+    by_rounds = ready is not None and C.wq is not None and release_every is None and RELEASE_LAYERS == 0
+    groups = {} if by_rounds else {lo: hi for lo, hi in release_groups(n, release_every)}
+    hi, q0, cus = n, len(C.wq or []), _num_cus(x.device)
     for i, layer_S in reversed(list(enumerate(S["layers"]))):
         nxt = torch.empty(x.shape, dtype=C.cd, device=x.device)
         dx = Bk.enc_layer_bwd(C, layer_S, dx, dx_c, nxt)
         dx_c = nxt
         C.flush_wgrad_side()
+        if by_rounds and i > 0 and C.wq is not None:
+            tiles = _queued_tiles(C, q0)
+            if tiles + tiles // (hi - i) > cus:
+                groups[i] = hi
         if i in groups:
             extra = list(enc._norm_out.parameters()) if groups[i] == n else []
             _release(C, ready, [p for l in enc._layers[i:groups[i]] for p in l.parameters()] + extra)
+            hi, q0 = i, len(C.wq or [])
     feats = S["feats"]
     dfeats = torch.empty(feats.shape, dtype=C.cd, device=x.device)
     w = enc._lin_in.weight

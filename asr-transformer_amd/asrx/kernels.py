@@ -370,8 +370,11 @@ def _grouped_xcd(items, common, kind="p3"):
 
 # lay each group's tiles on one XCD (ASRX_WGRAD_XCD=0: one table order over all XCDs, A/B)
 WGRAD_XCD = os.environ.get("ASRX_WGRAD_XCD", "1") != "0"
-# pack the groups into 32-tile rounds per XCD (xcd_plan; ASRX_WGRAD_PACK=1, A/B)
-WGRAD_PACK = os.environ.get("ASRX_WGRAD_PACK", "0") == "1"
+# pack the groups into 32-tile rounds per XCD (xcd_plan; ASRX_WGRAD_PACK=0: whole groups per XCD).  Neutral for
+# the single-GPU step's one grouped launch (13.37-13.40 ms either way), but a multi-GPU backward's decoder release
+# launch is the cross K/V group (96 long tiles) plus short decoder tiles: whole groups put all 96 on one XCD's 32 CUs
+# (three rounds, modelled makespan 747 K-steps) where packed 32-tile chunks spread them (313)
+WGRAD_PACK = os.environ.get("ASRX_WGRAD_PACK", "1") == "1"
 
 
 def linear_wgrad_grouped(items, *, beta=1.0, kind=None):

@@ -45,7 +45,10 @@ class _Segments:
 
     def _begin(self, timed):
         g = torch.cuda.CUDAGraph()
-        g.capture_begin(pool=self.pool)
+        # thread_local: another thread's query of a non-captured stream (torch's RCCL watchdog polls the events of
+        # finished all-reduces) must not invalidate this capture — "global" mode turned such a poll into a failed
+        # capture and an aborted process in the one-rank RCCL rehearsal
+        g.capture_begin(pool=self.pool, capture_error_mode="thread_local")
         self.graphs.append(g)
         self.timed.append(timed)
 

@@ -22,6 +22,8 @@ def _free_port():
 
 def _worker(rank, world, port, q):
     import torch.distributed as dist
+    os.environ["ASRX_DP_RELEASE_LAYERS"] = "1"   # fixed one-layer groups (the default, by tile rounds, keeps c1's
+    #                                              small encoder whole): the mid-encoder release path
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -114,7 +116,9 @@ def _rehearsal_worker(port, wire, q):
     torch.manual_seed(0)
     m0 = asrx.Transformer(cfg.vocab_size, cfg.input_dim, cfg.d_model, cfg.dec_len, cfg.enc_len, cfg.n_enc,
                           cfg.n_dec, cfg.n_heads, cfg.ff_dim, dropout=0.0, precision="bf16")
-    m1 = copy.deepcopy(m0)
+    m1 = asrx.Transformer(cfg.vocab_size, cfg.input_dim, cfg.d_model, cfg.dec_len, cfg.enc_len, cfg.n_enc,
+                          cfg.n_dec, cfg.n_heads, cfg.ff_dim, dropout=0.0, precision="bf16")
+    m1.load_state_dict(copy.deepcopy(m0.state_dict()))
     s, t, mk = synthetic_batch(cfg, spec["batch"], spec["frames"], spec["text_len"] + 1, seed=7)
     s, t, mk = s.cuda(), t.cuda(), mk.cuda()
     out = {}

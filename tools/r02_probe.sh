@@ -38,6 +38,10 @@ for s in "$@"; do
     blasqkv) ASRX_P4_MIN_TILES=400 step blasqkv 300 python tools/blas_ref.py --variants p3,p4,auto --nogrouped --noblas --only "qkv fwd" ;;
     abpack) bash tools/ab_env.sh 2 ASRX_WGRAD_PACK=0 ASRX_WGRAD_PACK=1 || exit $? ;;
     steptab) python3 tools/step_table.py gpurun_out/prof/run_kernel_trace.csv > gpurun_out/step_table.txt && head -45 gpurun_out/step_table.txt ;;
+    distt) step distt 600 python -u -m pytest tests/test_gpu_dist.py -x -v --timeout 500 --timeout-method thread -m gpu ;;
+    rehearse) ASRX_DP_REHEARSE=1 step rehearse 400 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-sub --no-other && ASRX_DP_REHEARSE=1 ASRX_DP_WIRE=bf16 step rehearse_bf16 400 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-sub --no-other ;;
+    abrel) for v in 6 0 6 0; do ASRX_DP_REHEARSE=1 ASRX_DP_RELEASE_LAYERS=$v step rel$v 400 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-sub --no-other; grep -o '"ms_per_step": [0-9.]*\|"launches_per_step": [0-9]*\|"avg_launch_us": [0-9.]*\|"allreduce_exposed_ms_per_rank": [^]]*' gpurun_out/rel$v.log | tr '\n' ' '; echo; done ;;
+    abpackdp) for v in 0 1; do ASRX_DP_REHEARSE=1 ASRX_WGRAD_PACK=$v step packdp$v 400 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-sub --no-other; grep -o '"ms_per_step": [0-9.]*\|"launches_per_step": [0-9]*\|"avg_launch_us": [0-9.]*\|"host_enqueue_ms_per_step": [0-9.]*' gpurun_out/packdp$v.log | tr '\n' ' '; echo; done ;;
     abres) bash tools/ab_env.sh 2 ASRX_GEMM_BLASLT_RESID=0 ASRX_GEMM_BLASLT_RESID=1 || exit $? ;;
     gpu) step gputests 1000 python -u -m pytest tests -x -q --timeout 400 --timeout-method thread -m gpu ;;
     *) echo "unknown $s"; exit 2 ;;
