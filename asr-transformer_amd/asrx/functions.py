@@ -180,10 +180,10 @@ def release_groups(n, every=None):
     return out
 
 
-def encoder_bwd(C, enc, S, dy, gate_feats, ready=None, release_every=None):
+def encoder_bwd(C, enc, S, dy, gate_feats, ready=None, release_every=None, carry=None):
     """dy: grad of the encoder output (fp32 or compute dtype). Returns dfeats (compute dtype).  With `ready`, the
     layers are released to the gradient all-reduce in groups (release_groups; the first with _norm_out) as soon as
-    their gradients are final."""
+    their gradients are final.  carry: parameters (the decoder's) released with the first group (else at finish)."""
     x = S["x"]
     dx_c = torch.empty(x.shape, dtype=C.cd, device=x.device)
     dx = Bk.ln_bwd(C, x, dy, enc._norm_out, S["mean"], S["rstd"], drop_out=dx_c)
@@ -206,7 +206,8 @@ def encoder_bwd(C, enc, S, dy, gate_feats, ready=None, release_every=None):
                 groups[i] = hi
         if i in groups:
             extra = list(enc._norm_out.parameters()) if groups[i] == n else []
-            _release(C, ready, [p for l in enc._layers[i:groups[i]] for p in l.parameters()] + extra)
+            _release(C, ready, [p for l in enc._layers[i:groups[i]] for p in l.parameters()] + extra + (carry or []))
+            carry = None
             hi, q0 = i, len(C.wq or [])
     feats = S["feats"]
     dfeats = torch.empty(feats.shape, dtype=C.cd, device=x.device)
@@ -312,10 +313,17 @@ def model_backward(C, model, S, dlogits_c, ready=None):
     _prepare_grads(C)
     own = C.defer_wgrad()
     denc = decoder_bwd(C, model.decoder, S["d"], dlogits_c)
+    # by tile rounds (the default release schedule): the decoder's weight gradients (the 96 long cross K/V tiles and
+    # 672 short ones) are not a launch of their own but join the first encoder group's — one ~2-round launch instead
+    # of a 313-K-step one plus a 249-K-step one (modelled with kernels.xcd_plan) and one segment boundary fewer;
+    # their all-reduce then starts five encoder layers later, still overlapping the rest of the backward
+    carry = ready is not None and own and RELEASE_LAYERS == 0
     if own:
         C.flush_wgrad_side()
-        _release(C, ready, list(model.decoder.parameters()))
-    dfeats = encoder_bwd(C, model.encoder, S["e"], denc, gate_feats=True, ready=ready if own else None)
+        if not carry:
+            _release(C, ready, list(model.decoder.parameters()))
+    dfeats = encoder_bwd(C, model.encoder, S["e"], denc, gate_feats=True, ready=ready if own else None,
+                         carry=list(model.decoder.parameters()) if carry else None)
     Bk.frontend_bwd(C, S["f"], dfeats, model.input_layer[0], model.input_layer[2])
     if own:
         C.flush_wgrad()

@@ -97,7 +97,7 @@ def test_gloo_two_ranks_overlapped_allreduce_exact():
         assert exact, err
 
 
-def _rehearsal_worker(port, wire, q):
+def _rehearsal_worker(port, wire, cname, q):
     """One-rank RCCL group with the gradient exchange forced on (asrx.dist.FORCE): the multi-GPU step path of a
     graph-mode Trainer — backward captured in segments, RCCL all-reduce (or the bf16 wire's all-to-all + chunk sum
     + all-gather) between the segment replays — against the plain single-GPU Trainer from the same weights."""
@@ -111,15 +111,16 @@ def _rehearsal_worker(port, wire, q):
     from asrx import dist as D
     from asrx.train import GRAPH_WARMUP, Trainer
     from oracle.ref_model import CONFIGS, synthetic_batch
-    spec = CONFIGS["c1"]
+    spec = CONFIGS[cname]
     cfg = spec["cfg"]
+    batch = spec["batch"] if cname == "c1" else 2    # c3 dims (its release groups close: 5 + 5 layers) at B = 2
     torch.manual_seed(0)
     m0 = asrx.Transformer(cfg.vocab_size, cfg.input_dim, cfg.d_model, cfg.dec_len, cfg.enc_len, cfg.n_enc,
                           cfg.n_dec, cfg.n_heads, cfg.ff_dim, dropout=0.0, precision="bf16")
     m1 = asrx.Transformer(cfg.vocab_size, cfg.input_dim, cfg.d_model, cfg.dec_len, cfg.enc_len, cfg.n_enc,
                           cfg.n_dec, cfg.n_heads, cfg.ff_dim, dropout=0.0, precision="bf16")
     m1.load_state_dict(copy.deepcopy(m0.state_dict()))
-    s, t, mk = synthetic_batch(cfg, spec["batch"], spec["frames"], spec["text_len"] + 1, seed=7)
+    s, t, mk = synthetic_batch(cfg, batch, spec["frames"], spec["text_len"] + 1, seed=7)
     s, t, mk = s.cuda(), t.cuda(), mk.cuda()
     out = {}
     for name, m, force in (("dp", m0, True), ("ref", m1, False)):
@@ -134,13 +135,13 @@ def _rehearsal_worker(port, wire, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("wire", ["fp32", "bf16"])
-def test_rccl_one_rank_rehearsal_matches_single_gpu(wire):
+@pytest.mark.parametrize("wire,cname", [("fp32", "c1"), ("bf16", "c1"), ("fp32", "c3")])
+def test_rccl_one_rank_rehearsal_matches_single_gpu(wire, cname):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_rehearsal_worker, args=(_free_port(), wire, q))
+    p = ctx.Process(target=_rehearsal_worker, args=(_free_port(), wire, cname, q))
     p.start()
     act_dp, act_ref, g_dp, g_ref, exact, err, l_dp, l_ref = q.get(timeout=600)
     p.join(timeout=120)
