@@ -903,16 +903,18 @@ ASRX_DEV void adam_f4(f4_t& pp, const f4_t gg, f4_t& mm, f4_t& vv, float lr, flo
   }
 }
 
+// every operand is streamed once per step (2.7 GB at c3, far beyond the caches): non-temporal stores
 ASRX_DEV void adam_store(float* p, float* m, float* v, bf16_t* pb, int64_t i, const f4_t& pp, const f4_t& mm,
                          const f4_t& vv) {
-  ((f4_t*)p)[i] = pp;
-  ((f4_t*)m)[i] = mm;
-  ((f4_t*)v)[i] = vv;
+  __builtin_nontemporal_store(pp, (f4_t*)p + i);
+  __builtin_nontemporal_store(mm, (f4_t*)m + i);
+  __builtin_nontemporal_store(vv, (f4_t*)v + i);
   if (pb) {
-    uint2 u;
+    typedef uint32_t u2_t __attribute__((ext_vector_type(2)));
+    u2_t u;
     u.x = pack2bf(pp[0], pp[1]);
     u.y = pack2bf(pp[2], pp[3]);
-    ((uint2*)pb)[i] = u;
+    __builtin_nontemporal_store(u, (u2_t*)pb + i);
   }
 }
 
@@ -932,10 +934,10 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
   int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   for (; i + stride < n4; i += 2 * stride) {
     const int64_t j = i + stride;
-    f4_t p0 = ((f4_t*)p)[i], p1 = ((f4_t*)p)[j];
+    f4_t p0 = __builtin_nontemporal_load((const f4_t*)p + i), p1 = __builtin_nontemporal_load((const f4_t*)p + j);
     const f4_t g0 = __builtin_nontemporal_load((const f4_t*)g + i), g1 = __builtin_nontemporal_load((const f4_t*)g + j);
-    f4_t m0 = ((f4_t*)m)[i], m1 = ((f4_t*)m)[j];
-    f4_t v0 = ((f4_t*)v)[i], v1 = ((f4_t*)v)[j];
+    f4_t m0 = __builtin_nontemporal_load((const f4_t*)m + i), m1 = __builtin_nontemporal_load((const f4_t*)m + j);
+    f4_t v0 = __builtin_nontemporal_load((const f4_t*)v + i), v1 = __builtin_nontemporal_load((const f4_t*)v + j);
     adam_f4(p0, g0, m0, v0, lr, b1, b2, eps, wd, bc1, rbc2, gs, decoupled);
     adam_f4(p1, g1, m1, v1, lr, b1, b2, eps, wd, bc1, rbc2, gs, decoupled);
     adam_store(p, m, v, pb, i, p0, m0, v0);
