@@ -80,11 +80,14 @@ def test_graph_dropout_masks_change_per_replay():
     K.set_seed_offset(0)
 
 
-def test_graph_segments_with_release_path():
+def test_graph_segments_with_release_path(monkeypatch):
     """Multi-GPU structure on one GPU: with a reducer the backward is captured in segments ending where gradient
     ranges become final; the injected all-reduce (doubling each range) runs between segment replays.  Graph
-    replays must give the same gradients as eager steps with the same reducer (dropout 0, lr 0)."""
+    replays must give the same gradients as eager steps with the same reducer (dropout 0, lr 0).  Fixed one-layer
+    release groups: the default (groups sized to a round of weight-gradient tiles) keeps c2's small encoder whole."""
+    from asrx import functions
     from asrx.train import Trainer
+    monkeypatch.setattr(functions, "RELEASE_LAYERS", 1)
     m, cfg = build("c2", 0.0)
     spec = CONFIGS["c2"]
     (b,) = batches(cfg, spec, 1, batch=8)

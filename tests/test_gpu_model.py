@@ -282,11 +282,16 @@ def test_trainer_fresh_grads_match_zeroed(cfgname):
     assert torch.equal(g_fresh, tr.store.grad)
 
 
-def test_trainer_release_path_fresh_grads():
+@pytest.mark.parametrize("every", [1, 0])
+def test_trainer_release_path_fresh_grads(every, monkeypatch):
     """Multi-GPU backward structure on one GPU: an injected all-reduce (doubling every range it is handed)
     receives decoder / upper-encoder ranges mid-backward and the rest at finish(); with unzeroed weight
-    gradients (FreshGrads) every range must already hold its final gradient when handed over."""
+    gradients (FreshGrads) every range must already hold its final gradient when handed over.  every: fixed
+    one-layer release groups, or 0 = the default by tile rounds (at c2's size: everything at finish, so the
+    decoder's carried gradients are handed over there)."""
+    from asrx import functions
     from asrx.train import Trainer
+    monkeypatch.setattr(functions, "RELEASE_LAYERS", every)
     m, cfg = build("c2", "bf16", dropout=0.0)
     m.train()
     spec = CONFIGS["c2"]
@@ -311,7 +316,8 @@ def test_trainer_release_path_fresh_grads():
     tr.forward_backward(s, t, k)              # fresh mode, ranges released mid-backward
     tr.reducer.finish()
     torch.cuda.synchronize()
-    assert len(seen) > 1
+    assert len(seen) > 1 or every == 0
+    assert sum(seen) == tr.store.grad.numel()
     assert torch.equal(tr.store.grad, 2.0 * g_ref)
 
 
