@@ -27,6 +27,35 @@ FRESH_GRADS = os.environ.get("ASRX_FRESH_GRADS", "1") == "1"
 # capture the training step as HIP graph(s) after the eager warm-up steps (ASRX_GRAPH=0: eager steps, A/B)
 GRAPH = os.environ.get("ASRX_GRAPH", "1") == "1"
 GRAPH_WARMUP = 2
+# multi-GPU: AdamW of the ranges all-reduced mid-backward runs on a side stream as soon as their all-reduces are
+# done, beside the rest of the backward (the last grouped weight-gradient launch fills ~40% of the CUs), instead of
+# after the final all-reduce (ASRX_DP_EARLY_ADAM=0: one AdamW launch after finish())
+EARLY_ADAM = os.environ.get("ASRX_DP_EARLY_ADAM", "1") == "1"
+
+
+def _aligned_spans(spans, n, q=4):
+    """Union of [a, b) spans shrunk to multiples of q elements (16-B aligned fp32 / 8-B aligned bf16 views)."""
+    out = []
+    for a, b in sorted(spans):
+        a, b = -(-a // q) * q, min(n, b) // q * q
+        if b <= a:
+            continue
+        if out and a <= out[-1][1]:
+            out[-1][1] = max(out[-1][1], b)
+        else:
+            out.append([a, b])
+    return [tuple(x) for x in out]
+
+
+def _complement(spans, n):
+    out, pos = [], 0
+    for a, b in spans:
+        if a > pos:
+            out.append((pos, a))
+        pos = b
+    if pos < n:
+        out.append((pos, n))
+    return out
 
 
 class _Segments:
@@ -221,6 +250,7 @@ class Trainer:
         self._cap = None        # captured step: (segments, static inputs, loss, preds buffer)
         self._hyp = torch.zeros(3, dtype=torch.float32, device=self.store.flat.device)
         self.ar_events = None   # list -> record the exposed all-reduce time of each step (_finish)
+        self._adam_side = None  # multi-GPU early AdamW stream (_reduce_and_adam)
         # preds=True: the cross-entropy kernel also writes each row's argmax over the V classes (train.py:29,
         # `logits.argmax(-1)`, fused into the loss pass) into last_preds (int64 [B*L], device; in graph mode the
         # captured buffer, overwritten by the next step)
@@ -259,10 +289,41 @@ class Trainer:
             C.fresh = None
         return loss
 
-    def _adam(self, hyp=None):
-        K.adam(self.store.flat, self.store.grad, self.m, self.v, self.store.shadow, self.lr, self.betas[0],
+    def _adam(self, hyp=None, span=None):
+        a, b = span if span is not None else (0, self.store.flat.numel())
+        sh = self.store.shadow[a:b] if self.store.shadow is not None else None
+        K.adam(self.store.flat[a:b], self.store.grad[a:b], self.m[a:b], self.v[a:b], sh, self.lr, self.betas[0],
                self.betas[1], self.eps, self.wd, max(1, self.step_count), grad_scale=1.0 / self.reducer.world,
                decoupled=self.decoupled, hyp=hyp)
+
+    def _reduce_and_adam(self, hyp=None):
+        """finish() the gradient exchange and run AdamW.  Multi-GPU over RCCL (fp32 wire): the ranges released
+        mid-backward get their AdamW on a side stream that waits only for their all-reduces — each of which RCCL
+        ordered after the backward's release point, so every read of those weights and gradients in this step is
+        behind it — and the compute stream takes the rest after finish(), then joins the side stream."""
+        red = self.reducer
+        n = self.store.flat.numel()
+        early = []
+        if EARLY_ADAM and red.active and red.allreduce_fn is None and red.wire == "fp32" and red._issued:
+            early = _aligned_spans(red._issued, n)
+        if not early:
+            self._finish()
+            self._adam(hyp)
+            return
+        dev = self.store.flat.device
+        if self._adam_side is None:
+            self._adam_side = torch.cuda.Stream(device=dev)
+        side, main = self._adam_side, torch.cuda.current_stream(dev)
+        works = list(red._works)
+        with torch.cuda.stream(side):
+            for w in works:
+                w.wait()
+            for sp in early:
+                self._adam(hyp, sp)
+        self._finish()
+        for sp in _complement(early, n):
+            self._adam(hyp, sp)
+        main.wait_stream(side)
 
     def step(self, spectrum, text, mask, input_text=None):
         """One training step (forward, CE, backward, all-reduce, AdamW).  Returns the loss as a device scalar; in
@@ -278,9 +339,8 @@ class Trainer:
             if self._cap is not None:
                 return self._replay(spectrum, text, mask, input_text)
         loss = self.forward_backward(spectrum, text, mask, input_text=input_text)
-        self._finish()
         self.step_count += 1
-        self._adam()
+        self._reduce_and_adam()
         self.store.mark_shadow_fresh()
         return loss
 
@@ -335,7 +395,6 @@ class Trainer:
         K.adam_hyper(self._hyp, self.lr, self.betas[0], self.betas[1], self.step_count)
         seg.replay(self.reducer)
         if self.reducer.active:
-            self._finish()
-            self._adam(self._hyp)
+            self._reduce_and_adam(self._hyp)
         self.store.mark_shadow_fresh()
         return loss

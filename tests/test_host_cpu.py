@@ -270,3 +270,27 @@ def test_xcd_plan_covers_every_tile_once(pack):
     for slot, xs in where.items():
         if not pack or nts[group_order[slot]] <= 32:
             assert len(xs) == 1
+
+
+def test_early_adam_spans_cover_the_buffer_once():
+    """Trainer._reduce_and_adam's split of the flat buffer: the released ranges shrunk to 16-B aligned spans plus
+    their complement cover every element exactly once, and every span starts 4-element aligned."""
+    from asrx.train import _aligned_spans, _complement
+    import random
+    rng = random.Random(0)
+    for _ in range(200):
+        n = rng.randrange(1, 5000)
+        spans = []
+        for _ in range(rng.randrange(0, 6)):
+            a = rng.randrange(0, n)
+            spans.append((a, rng.randrange(a, n + 1)))
+        early = _aligned_spans(spans, n)
+        late = _complement(early, n)
+        cover = [0] * n
+        for a, b in early + late:
+            assert a % 4 == 0
+            for i in range(a, b):
+                cover[i] += 1
+        assert cover == [1] * n
+        released = set(i for a, b in spans for i in range(a, b))
+        assert all(i in released for a, b in early for i in range(a, b))
