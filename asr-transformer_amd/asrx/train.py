@@ -27,10 +27,11 @@ FRESH_GRADS = os.environ.get("ASRX_FRESH_GRADS", "1") == "1"
 # capture the training step as HIP graph(s) after the eager warm-up steps (ASRX_GRAPH=0: eager steps, A/B)
 GRAPH = os.environ.get("ASRX_GRAPH", "1") == "1"
 GRAPH_WARMUP = 2
-# multi-GPU: AdamW of the ranges all-reduced mid-backward runs on a side stream as soon as their all-reduces are
-# done, beside the rest of the backward (the last grouped weight-gradient launch fills ~40% of the CUs), instead of
-# after the final all-reduce (ASRX_DP_EARLY_ADAM=0: one AdamW launch after finish())
-EARLY_ADAM = os.environ.get("ASRX_DP_EARLY_ADAM", "1") == "1"
+# multi-GPU, ASRX_DP_EARLY_ADAM=1: AdamW of the ranges all-reduced mid-backward runs on a side stream as soon as
+# their all-reduces are done, beside the rest of the backward, instead of after the final all-reduce.  Off: in the
+# one-rank RCCL rehearsal it was slower (14.35 / 14.26 vs 14.12 / 14.13 ms, ABAB) — the side AdamW starts right at
+# the release point and takes HBM bandwidth from the HBM-bound encoder backward it runs beside
+EARLY_ADAM = os.environ.get("ASRX_DP_EARLY_ADAM", "0") == "1"
 
 
 def _aligned_spans(spans, n, q=4):
