@@ -97,13 +97,14 @@ def test_gloo_two_ranks_overlapped_allreduce_exact():
         assert exact, err
 
 
-def _rehearsal_worker(port, wire, cname, q):
+def _rehearsal_worker(port, wire, cname, early, q):
     """One-rank RCCL group with the gradient exchange forced on (asrx.dist.FORCE): the multi-GPU step path of a
     graph-mode Trainer — backward captured in segments, RCCL all-reduce (or the bf16 wire's all-to-all + chunk sum
     + all-gather) between the segment replays — against the plain single-GPU Trainer from the same weights."""
     import copy
     import torch.distributed as dist
     os.environ["ASRX_DP_FORCE"] = "1"
+    os.environ["ASRX_DP_EARLY_ADAM"] = str(early)   # optional: AdamW of released ranges on a side stream
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
                             device_id=torch.device("cuda", 0))
     torch.cuda.set_device(0)
@@ -135,13 +136,14 @@ def _rehearsal_worker(port, wire, cname, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("wire,cname", [("fp32", "c1"), ("bf16", "c1"), ("fp32", "c3")])
-def test_rccl_one_rank_rehearsal_matches_single_gpu(wire, cname):
+@pytest.mark.parametrize("wire,cname,early", [("fp32", "c1", 0), ("bf16", "c1", 0), ("fp32", "c3", 0),
+                                              ("fp32", "c3", 1)])
+def test_rccl_one_rank_rehearsal_matches_single_gpu(wire, cname, early):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_rehearsal_worker, args=(_free_port(), wire, cname, q))
+    p = ctx.Process(target=_rehearsal_worker, args=(_free_port(), wire, cname, early, q))
     p.start()
     act_dp, act_ref, g_dp, g_ref, exact, err, l_dp, l_ref = q.get(timeout=600)
     p.join(timeout=120)
