@@ -46,6 +46,7 @@ for s in "$@"; do
     pmcsub) step pmcsf 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcsf -o run --output-format csv -- python3 tools/sub_pmc.py && step pmcsw 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmcsw -o run --output-format csv -- python3 tools/sub_pmc.py && step pmcsj 120 python3 tools/pmc_traffic.py gpurun_out/pmcsf/run_counter_collection.csv gpurun_out/pmcsw/run_counter_collection.csv sub gpurun_out/sub_pmc_traffic.json && cat gpurun_out/sub_pmc_traffic.json | head -60 ;;
     m4096) for kv in "ASRX_GEMM_BLASLT_M=4096 ASRX_GEMM_BLASLT_RESID=0" "ASRX_GEMM_BLASLT_M=4096" "ASRX_GEMM_BLASLT_M=8192"; do env $kv timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-sub --no-other > gpurun_out/m4096.log 2>&1 || exit $?; echo "$kv $(grep -o '"ms_per_step": [0-9.]*\|"host_enqueue_ms_per_step": [0-9.]*' gpurun_out/m4096.log | tr '\n' ' ')"; done; ASRX_GEMM_BLASLT_M=4096 step profm 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profm -o run --output-format csv -- python3 bench.py --steps 5 --warmup 3 --no-cpu-baseline --no-probe --no-sub --no-other && python3 tools/step_table.py gpurun_out/profm/run_kernel_trace.csv > gpurun_out/steptab_m.txt && head -12 gpurun_out/steptab_m.txt ;;
     abearly) for v in 0 1 0 1; do ASRX_DP_REHEARSE=1 ASRX_DP_EARLY_ADAM=$v step early$v 400 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-sub --no-other; echo "early=$v $(grep -o '"ms_per_step": [0-9.]*\|"allreduce_exposed_ms_per_rank": [^]]*' gpurun_out/early$v.log | tr '\n' ' ')"; done ;;
+    smt) step smt 400 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 200 --timeout-method thread -m gpu -k "softmax" ;;
     abres) bash tools/ab_env.sh 2 ASRX_GEMM_BLASLT_RESID=0 ASRX_GEMM_BLASLT_RESID=1 || exit $? ;;
     gpu) step gputests 1000 python -u -m pytest tests -x -q --timeout 400 --timeout-method thread -m gpu ;;
     *) echo "unknown $s"; exit 2 ;;
