@@ -188,21 +188,24 @@ def encoder_bwd(C, enc, S, dy, gate_feats, ready=None, release_every=None, carry
     dx_c = torch.empty(x.shape, dtype=C.cd, device=x.device)
     dx = Bk.ln_bwd(C, x, dy, enc._norm_out, S["mean"], S["rstd"], drop_out=dx_c)
     n = len(S["layers"])
-    # by tile rounds (the default): a group closes when one more layer's weight-gradient tiles would overflow one
-    # workgroup per CU — each grouped launch then runs as one full round (c3: 5 layers x 48 tiles = 240 of 256 CUs;
-    # fixed halves of 6 layers = 288 tiles take two rounds each, the second nearly empty); the bottom group goes with
-    # _lin_in and the front-end to the reducer's finish()
+    # by tile rounds (the default): ONE release, at the highest layer i whose lower layers 0..i-1 plus _lin_in fit
+    # one round of weight-gradient tiles (one workgroup per CU).  The released launch carries the decoder's weight
+    # gradients and layers n-1..i (c3: 7 layers; modelled makespan 626 K-steps), the finish() launch the rest (250
+    # tiles, 249 K-steps): 875 in all, the single-GPU launch's makespan.  (Releases every 5 layers — one round each —
+    # overlapped more of the all-reduce but made 505 + 249 + 249 K-steps.)
     by_rounds = ready is not None and C.wq is not None and release_every is None and RELEASE_LAYERS == 0
     groups = {} if by_rounds else {lo: hi for lo, hi in release_groups(n, release_every)}
     hi, q0, cus = n, len(C.wq or []), _num_cus(x.device)
+    lw = enc._lin_in.weight
+    tail = -(-lw.shape[0] // 256) * -(-lw.shape[1] // 256)
     for i, layer_S in reversed(list(enumerate(S["layers"]))):
         nxt = torch.empty(x.shape, dtype=C.cd, device=x.device)
         dx = Bk.enc_layer_bwd(C, layer_S, dx, dx_c, nxt)
         dx_c = nxt
         C.flush_wgrad_side()
-        if by_rounds and i > 0 and C.wq is not None:
-            tiles = _queued_tiles(C, q0)
-            if tiles + tiles // (hi - i) > cus:
+        if by_rounds and i > 0 and C.wq is not None and hi == n:
+            per = _queued_tiles(C, q0) // (n - i)
+            if i * per + tail <= cus:
                 groups[i] = hi
         if i in groups:
             extra = list(enc._norm_out.parameters()) if groups[i] == n else []
