@@ -94,8 +94,8 @@ class GradAllReduce:
         W = dist.get_world_size(self.group)
         n = view.numel()
         c = -(-n // W)
-        send = torch.zeros(W * c, dtype=torch.bfloat16, device=view.device)
-        _cast(view, send[:n])
+        send = torch.empty(W * c, dtype=torch.bfloat16, device=view.device)   # the padding past n is summed
+        _cast(view, send[:n])                                                   # but never copied back
         recv = torch.empty_like(send)
         dist.all_to_all_single(recv, send, group=self.group, async_op=True).wait()
         mine = torch.empty(c, dtype=torch.bfloat16, device=view.device)
