@@ -55,10 +55,27 @@ def get_store(m):
     return st
 
 
-def draw_seed():
-    """Dropout seed base of one call, drawn from torch's default CPU generator: runs are reproducible under
-    torch.manual_seed, as the reference's nn.Dropout is (its masks come from torch's RNG)."""
-    return int(torch.randint(0, 1 << 62, (1,), dtype=torch.int64))
+_SEED_FALLBACK = {}   # device index -> (initial seed, counter) when the CUDA generator cannot be read (capture)
+
+
+def draw_seed(device):
+    """Dropout seed base of one training call, taken where the reference's nn.Dropout takes its masks on the GPU:
+    torch's CUDA generator of `device` — its seed and Philox offset, the offset advanced by 4 as a dropout kernel
+    of torch would.  Runs are reproducible under torch.manual_seed / torch.cuda.manual_seed, and neither torch's
+    CPU generator (DataLoader shuffling, other CPU RNG users) nor eval / no-dropout calls consume anything."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    gen = torch.cuda.default_generators[idx]
+    seed = gen.initial_seed()
+    if torch.cuda.is_current_stream_capturing():
+        base, n = _SEED_FALLBACK.get(idx, (seed, 0))
+        if base != seed:
+            n = 0
+        _SEED_FALLBACK[idx] = (seed, n + 1)
+        off = (1 << 40) + n
+    else:
+        off = gen.get_offset()
+        gen.set_offset(off + 4)
+    return int((seed * 0x9E3779B97F4A7C15 + off * 0xBF58476D1CE4E5B9) & ((1 << 62) - 1))
 
 
 def make_ctx(m, p_drop):
@@ -69,7 +86,7 @@ def make_ctx(m, p_drop):
     if cd == torch.bfloat16:
         st.refresh_shadow()
     train = m.training
-    seeds = Bk.Seeds(draw_seed())
+    seeds = Bk.Seeds(draw_seed(st.device) if train and p_drop > 0 else 0)
     return Bk.Ctx(st, cd, train, p_drop, seeds, getattr(root, "attention", "fused"))
 
 

@@ -6,8 +6,14 @@ smaller configurations (c2: d_model 256, B=32) that host time exceeds the GPU ti
 with the new inputs copied into the captured buffers — the forward's launches then cost one graph launch.  The
 returned logits are the captured output tensor, overwritten by the next call (copy it to keep it).  Same numerics
 as the eager forward: the same kernels run on the same buffers' contents.
+
+Weights: the bf16 operand shadow of the flat parameter store is refreshed eagerly before every replay (version
+checked, so a no-op unless a parameter changed: optimizer.step(), load_state_dict), and a graph captured against
+a flat store that has since been rebuilt (parameters re-bound) is dropped and captured again.
 """
 import torch
+
+from .functions import get_store
 
 
 class GraphedForward:
@@ -25,10 +31,15 @@ class GraphedForward:
         if self.model.training:
             raise RuntimeError("asrx.infer.GraphedForward replays inference forwards: call model.eval() first")
         key = self._key(spectrum, text, mask)
+        st = get_store(self.model)              # (rebuilt if the parameters were re-bound)
         ent = self._graphs.get(key)
+        if ent is not None and ent[3] is not st:
+            ent = None                          # captured against buffers that no longer hold the weights
         if ent is None:
             ent = self._graphs[key] = self._capture(spectrum, text, mask)
-        graph, ins, out = ent
+        graph, ins, out, _ = ent
+        if self.model.precision == "bf16":
+            st.refresh_shadow()                 # weights changed since the capture: re-cast outside the graph
         for dst, src in zip(ins, (spectrum, text, mask)):
             if dst.data_ptr() != src.data_ptr():
                 dst.copy_(src, non_blocking=True)
@@ -45,4 +56,4 @@ class GraphedForward:
             with torch.cuda.graph(graph):
                 out = self.model(*ins)
         torch.cuda.synchronize(dev)
-        return graph, ins, out
+        return graph, ins, out, get_store(self.model)

@@ -248,7 +248,9 @@ class Trainer:
         self.store.refresh_shadow(force=True)
         self._wonly = wgrad_only_params(model) if FRESH_GRADS else []
         self.graph = GRAPH if graph is None else bool(graph)
-        self._cap = None        # captured step: (segments, static inputs, loss, preds buffer)
+        self._cap = None        # captured step of the current input shape: (segments, static inputs, loss, preds)
+        self._caps = {}         # every captured step, keyed by input shapes (a smaller last batch keeps its own graph)
+        self._eager_keys = set()   # input shapes that have run one eager step (captured only after one)
         self._hyp = torch.zeros(3, dtype=torch.float32, device=self.store.flat.device)
         self.ar_events = None   # list -> record the exposed all-reduce time of each step (_finish)
         self._adam_side = None  # multi-GPU early AdamW stream (_reduce_and_adam)
@@ -333,12 +335,15 @@ class Trainer:
         if input_text is None:
             input_text = text
         if self.graph and self.model.precision == "bf16":
-            if self._cap is not None and not self._matches(spectrum, text, mask, input_text):
-                self._cap = None            # new input shapes: recapture
-            if self._cap is None and self.step_count >= GRAPH_WARMUP:
+            key = self._key(spectrum, text, mask, input_text)
+            self._cap = self._caps.get(key)
+            # a new input shape runs one eager step first (kernel objects, allocator), then is captured and kept
+            if self._cap is None and self.step_count >= GRAPH_WARMUP and key in self._eager_keys:
                 self._capture(spectrum, text, mask, input_text)
+                self._caps[key] = self._cap
             if self._cap is not None:
                 return self._replay(spectrum, text, mask, input_text)
+            self._eager_keys.add(key)
         loss = self.forward_backward(spectrum, text, mask, input_text=input_text)
         self.step_count += 1
         self._reduce_and_adam()
@@ -359,9 +364,9 @@ class Trainer:
             self.reducer.finish()
 
     # ---- HIP graph mode
-    def _matches(self, *xs):
-        ins = self._cap[1]
-        return all(a.shape == b.shape and a.dtype == b.dtype for a, b in zip(ins, xs))
+    @staticmethod
+    def _key(*xs):
+        return tuple((tuple(x.shape), x.dtype) for x in xs)
 
     def _capture(self, spectrum, text, mask, input_text):
         dev = self.store.flat.device

@@ -1293,7 +1293,12 @@ bool resident_ok(const asrx_attn_desc* d, const AttnArgs& a) {
   constexpr int64_t L24 = 1 << 23;
   const bool s24 = a.qr < L24 && a.kr < L24 && a.vr < L24 && a.orr < L24 && a.Lq < L24 && a.Lk < L24 &&
                    (!a.dout || (a.dor < L24 && a.dqr < L24 && a.dkr < L24 && a.dvr < L24));
-  return d->dh == 64 && a.Lk <= R_MAXK && (a.orr % 4) == 0 && (a.ob % 4) == 0 && s24;
+  // ... and the products themselves are 32-bit int offsets: every row index times its stride < 2^31
+  constexpr int64_t L31 = (int64_t)1 << 31;
+  const int64_t qs = std::max({(int64_t)a.qr, (int64_t)a.orr, a.dout ? (int64_t)a.dor : 0, a.dout ? (int64_t)a.dqr : 0});
+  const int64_t ks = std::max({(int64_t)a.kr, (int64_t)a.vr, a.dout ? (int64_t)a.dkr : 0, a.dout ? (int64_t)a.dvr : 0});
+  const bool s31 = (int64_t)a.Lq * qs < L31 && (int64_t)a.Lk * ks < L31;
+  return d->dh == 64 && a.Lk <= R_MAXK && (a.orr % 4) == 0 && (a.ob % 4) == 0 && s24 && s31;
 }
 
 size_t bwd_smem(int nw, int dh) {

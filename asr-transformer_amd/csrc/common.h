@@ -69,6 +69,7 @@ uint64_t* asrx_seed_offset_addr_attention();
 uint64_t* asrx_seed_offset_addr_norm();
 uint64_t* asrx_seed_offset_addr_softmax();
 uint64_t* asrx_seed_offset_addr_frontend();
+uint64_t* asrx_seed_offset_addr_gemm_ws();
 
 ASRX_DEV uint32_t rng_half(uint32_t h, uint32_t which) { return which ? (h >> 16) : (h & 0xffffu); }
 

@@ -1286,17 +1286,18 @@ extern "C" int asrx_upload(void* dst, const void* src, int64_t nbytes, void* str
 }
 
 namespace {
-struct SeedAddrs { uint64_t* p[5]; };
-// one launch sets every translation unit's copy (threads 0..4: per-lane addresses, vector stores)
+struct SeedAddrs { uint64_t* p[6]; };
+// one launch sets every translation unit's copy (threads 0..5: per-lane addresses, vector stores)
 __global__ void seed_offset_set_all_kernel(uint64_t v, SeedAddrs a) {
-  if (threadIdx.x < 5) *a.p[threadIdx.x] = v;
+  if (threadIdx.x < 6) *a.p[threadIdx.x] = v;
 }
 }  // namespace
 
 extern "C" int asrx_set_seed_offset(uint64_t offset, void* stream) {
   static const SeedAddrs addrs = [] {
     return SeedAddrs{{asrx_seed_offset_addr_gemm(), asrx_seed_offset_addr_attention(), asrx_seed_offset_addr_norm(),
-                      asrx_seed_offset_addr_softmax(), asrx_seed_offset_addr_frontend()}};
+                      asrx_seed_offset_addr_softmax(), asrx_seed_offset_addr_frontend(),
+                      asrx_seed_offset_addr_gemm_ws()}};
   }();
   for (uint64_t* q : addrs.p)
     if (!q) return ASRX_ERR_LAUNCH;

@@ -19,7 +19,6 @@
 
 #include "gemm_common.h"
 
-int blaslt_gemm_bf16(const asrx_gemm_desc* d, hipStream_t st);   // blaslt.hip: hipBLASLt for plain GEMMs
 
 namespace {
 using namespace asrxg;
@@ -312,26 +311,6 @@ struct PStage {
   }
 };
 
-template <int R, bool KSTRIDED>
-ASRX_DEV s8_t p_frag(const unsigned char* img, int i0, int ks) {
-  const int l = threadIdx.x & 63, g = l >> 4;
-  if constexpr (!KSTRIDED) {
-    const int r = i0 + (l & 15);
-    const int c = (ks * 4 + g) ^ ((r >> 1) & 7);
-    return *(const s8_t*)(img + r * 128 + c * 16);
-  } else {
-    const bf16_t* t = (const bf16_t*)img;
-    const int i = l & 15, q = i >> 2, p = i & 3;
-    const int k1 = ks * 32 + 8 * g + q;
-    const int k2 = k1 + 4;
-    const bf16_t* a1 = t + k1 * R + (((i0 >> 4) ^ ks_swz<128>(k1)) << 4) + 4 * p;
-    const bf16_t* a2 = t + k2 * R + (((i0 >> 4) ^ ks_swz<128>(k2)) << 4) + 4 * p;
-    s4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4_t*)a1);
-    s4_t v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4_t*)a2);
-    return s8_t{v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
-  }
-}
-
 // (An XCD-owned ROW order — row-block tm served by the workgroups with b % 8 == tm % 8 — was measured 10-50%
 // slower on every c3 shape; the XCD-contiguous TILE ranges of gemm_bf16_p3_kernel's `xcd` mode are 1-7% faster.)
 
@@ -601,30 +580,6 @@ struct P4Stage {
 #endif
   }
 };
-
-// p4 fragment read: as p_frag, but the k-strided image's 32-byte-chunk XOR is taken as a per-lane byte offset S
-// (ks_swz<128> of the lane's k-rows: the same for both k-row halves and both k-slices), so a fragment's address
-// is base + ((j * 32) ^ S) computed next to its read.  S is re-laundered at every phase (p4_body), which keeps
-// the compiler from hoisting 8 x 4 such addresses out of the K loop (they spilled the k-strided instantiations).
-ASRX_DEV uint32_t p4_swz_bytes() {
-  const int l = threadIdx.x & 63;
-  return (uint32_t)(ks_swz<128>(8 * (l >> 4) + ((l & 15) >> 2)) * 32);
-}
-template <int R, bool KSTRIDED>
-ASRX_DEV s8_t p4_frag(const unsigned char* img, int i0, int ks, uint32_t S) {
-  if constexpr (!KSTRIDED) {
-    return p_frag<R, false>(img, i0, ks);
-  } else {
-    const int l = threadIdx.x & 63, g = l >> 4, i = l & 15, q = i >> 2, p = i & 3;
-    const int k1 = ks * 32 + 8 * g + q;
-    // (i0 >> 4) * 32 ^ S == (i0 & ~255) * 2 + (((i0 & 255) * 2) ^ S): the row block's window, then the XOR
-    const unsigned char* a1 = img + k1 * R * 2 + 8 * p + (i0 & ~127) * 2 + (((uint32_t)(i0 & 127) * 2) ^ S);
-    const unsigned char* a2 = a1 + 4 * R * 2;
-    s4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4_t*)a1);
-    s4_t v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4_t*)a2);
-    return s8_t{v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
-  }
-}
 
 template <bool AT, bool BT, int EPI, int BN>
 ASRX_DEV void p4_body(const GemmArgs& g, const TileSeq tl, int split, int z, unsigned char* lds) {
@@ -1486,11 +1441,10 @@ void dispatch_bf16(const GemmArgs& g, bool at, bool bt, bool vec, int batch, hip
 struct GemmPlan {
   int use;     // 1 = p3 (256x128 LDS-DMA ring), 2 = p4 (256x256), 3 = register path 128, 4 = register path 64,
                // 5 = ring 64x64, 6 = ring 128x64 (4-stage LDS-DMA, small grids), 9 = tall-K (conv2 dW),
-               // 10 = hipBLASLt (plain / bias / bias + fp32 residual GEMMs, blaslt.hip)
+               // 11 = ws (warp-specialised 256x128, one-round N = 512 outputs)
   bool vec;    // 16-byte aligned operands
   int epi;     // instantiated epilogue flags (E_GENERIC when the fast-path set has no match)
   int ntiles;  // output tiles of the chosen kernel
-  int fb_use = 0, fb_epi = 0, fb_ntiles = 0;   // use 10: the hand-written plan run when the library declines
 };
 
 bool epi_instantiated(bool at, bool bt, int epi) {
@@ -1502,23 +1456,15 @@ bool epi_instantiated(bool at, bool bt, int epi) {
   return false;
 }
 
-// ASRX_GEMM_BLASLT=0 keeps every auto-planned GEMM on the hand-written kernels (A/B switch; default on)
-bool blaslt_auto() {
-  static const bool on = [] { const char* e = getenv("ASRX_GEMM_BLASLT"); return !(e && e[0] == '0'); }();
+// ASRX_WS=0 keeps the N = 512 encoder GEMMs on p3 (A/B switch; default on)
+bool ws_auto() {
+  static const bool on = [] { const char* e = getenv("ASRX_WS"); return !(e && e[0] == '0'); }();
   return on;
 }
-// ASRX_GEMM_BLASLT_RESID=0 keeps the bias + residual forward on p3 (A/B switch; default on)
-bool lt_resid_auto() {
-  static const bool on = [] { const char* e = getenv("ASRX_GEMM_BLASLT_RESID"); return !(e && e[0] == '0'); }();
-  return on;
-}
-
-// ASRX_GEMM_BLASLT_M: fewest rows for the automatic library path (A/B).  Default 8192, the encoder's GEMMs only:
-// with 4096 the decoder's instances also move to the library — each faster alone (tools/blas_ref.py), but the
-// graph-mode step went 13.50 -> 14.93 ms with 2.9 ms of host enqueue per step instead of 0.2 (measured, rejected)
-int lt_min_rows() {
-  static const int m = [] { const char* e = getenv("ASRX_GEMM_BLASLT_M"); return e ? atoi(e) : 8192; }();
-  return m;
+// ASRX_WS_MIN_K: shortest reduction planned on ws (A/B; every K from 512 up measured faster than p3 at c3)
+int ws_min_k() {
+  static const int k = [] { const char* e = getenv("ASRX_WS_MIN_K"); return e ? atoi(e) : 64; }();
+  return k;
 }
 
 // ASRX_P4_MIN_TILES: fewest 256x256 tiles for the automatic p4 plan (A/B of the wave quantisation: the c3 Q/K/V
@@ -1526,13 +1472,6 @@ int lt_min_rows() {
 int p4_min_tiles() {
   static const int t = [] { const char* e = getenv("ASRX_P4_MIN_TILES"); return e ? atoi(e) : 400; }();
   return t;
-}
-
-bool lt_auto(const asrx_gemm_desc* d, int lt_epi) {
-  if (d->m < lt_min_rows() || d->n != 512 || d->k < 1536) return false;
-  if (lt_epi == 0) return d->b_trans;
-  if (lt_epi == (E_BIAS | E_RESID | E_F32)) return !d->b_trans && lt_resid_auto();
-  return false;
 }
 
 GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
@@ -1545,7 +1484,7 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
     tile = t128 >= 400 ? 128 : 64;
   }
   const int kvar = d->kernel == 1 ? 1 : d->kernel == 3 ? 3 : d->kernel == 4 ? 4 : d->kernel == 5 ? 5 :
-                   d->kernel == 6 ? 6 : d->kernel == 7 ? 7 : 0;
+                   d->kernel == 6 ? 6 : d->kernel == 8 ? 8 : 0;
   const bool dma_ok = pl.vec && d->k % BK == 0 && (!d->a_trans || d->m % 8 == 0) && (!d->b_trans || d->n % 8 == 0) &&
                       d->m >= 8 && d->n >= 8;
   const int nt_p3 = ((d->m + P_BM - 1) / P_BM) * ((d->n + P_BN - 1) / P_BN);
@@ -1606,24 +1545,18 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
     pl.use = 1;   // p4 takes single, unsplit GEMMs with its instantiated epilogues; the rest stays on p3
     pl.ntiles = nt_p3;
   }
-  // hipBLASLt (use 10 = blaslt.hip; falls back to the hand-written plan `fb_use` whenever the library declines) for
-  // the library-expressible GEMMs: no epilogue, or bias (+ fp32 residual, fp32 out) — forward single GEMMs with
-  // unit-stride rows.  Auto where the library kernel is faster (tools/blas_ref.py, interleaved in one process):
-  //  * plain data gradients C = A B (bf16 out) of the encoder's 512-wide outputs with a long reduction (Q/K/V and
-  //    FFN1 data gradients, K = 1536 / 2048): 37.7 -> 30.3 and 51.4 -> 43.9 us;
-  //  * the FFN2 forward C32 = A B^T + bias + resid (512-wide fp32 residual stream, K = 2048): 56.8 -> 43.1 us
-  //    alone, 52.3 -> 48.2 us in the step (rocprofv3 kernel trace).
-  // Kernel code 7 forces the library for any expressible GEMM.
-  const int lt_epi = epi & ~(E_ALPHA);
-  const bool lt_ok = dma_ok && !d->a_trans && batch == 1 && splitk == 1 && !d->rowsum_a && !d->mask_out &&
-                     !d->sc_outer && !d->sc_inner && d->beta == 0.f &&
-                     ((lt_epi == 0 && d->c_dtype == ASRX_BF16) || lt_epi == E_BIAS ||
-                      lt_epi == (E_BIAS | E_RESID | E_F32));
-  if (lt_ok && (kvar == 7 || (kvar == 0 && blaslt_auto() && lt_auto(d, lt_epi)))) {
-    pl.fb_use = pl.use;
-    pl.fb_epi = pl.epi;
-    pl.fb_ntiles = pl.ntiles;
-    pl.use = 10;
+  // ws (use 11): the warp-specialised 256x128 tiles for the N = 512 outputs that make one round of tiles on the
+  // chip (c3, every encoder GEMM with a 512-wide output: _lin_in + PE, the out-projection with dropout + residual,
+  // the FFN2 forward with bias + fp32 residual, the Q/K/V, FFN1 and out-projection data gradients; tools/blas_ref.py:
+  // 13.8-36.2 us against p3's 16.6-51.1 and hipBLASLt's 18.7-35.4 on the plain ones); kernel code 8 forces it for
+  // any GEMM it can take.
+  const bool ws_ok = dma_ok && !d->a_trans && batch == 1 && splitk == 1 && d->n % WS_BN == 0 && d->k >= BK &&
+                     !d->rowsum_a && !d->mask_out && !d->sc_outer && !d->sc_inner && epi != E_GENERIC &&
+                     ws_instantiated(d->b_trans, epi);
+  if (ws_ok && (kvar == 8 || (kvar == 0 && ws_auto() && d->n == 512 && d->m >= 8192 && d->k >= ws_min_k()))) {
+    pl.use = 11;
+    pl.epi = epi;
+    pl.ntiles = ((d->m + WS_BM - 1) / WS_BM) * (d->n / WS_BN);
   }
     return pl;
 }
@@ -1647,8 +1580,8 @@ extern "C" int asrx_gemm_kernel_name(const asrx_gemm_desc* d, char* buf, int len
     return ASRX_OK;
   }
   const GemmPlan pl = plan_bf16(d, batch, splitk);
-  if (pl.use == 10)
-    snprintf(buf, len, "hipblaslt");
+  if (pl.use == 11)
+    snprintf(buf, len, "gemm_bf16_ws_kernel<%s, %d>", tf[!!d->b_trans], pl.epi);
   else if (pl.use == 9)
     snprintf(buf, len, "gemm_bf16_tallk_kernel");
   else if (pl.use == 1 || pl.use == 2)
@@ -1663,7 +1596,7 @@ extern "C" int asrx_gemm_kernel_name(const asrx_gemm_desc* d, char* buf, int len
   return ASRX_OK;
 }
 
-// Enqueue the bf16 plan `pl` (asrx_gemm after argument checks; also the fallback when hipBLASLt declines a call).
+// Enqueue the bf16 plan `pl` (asrx_gemm after argument checks).
 int gemm_bf16_run(const asrx_gemm_desc* d, const GemmArgs& g, const GemmPlan& pl, int batch, int splitk,
                   hipStream_t st) {
   const int epi = pl.epi;
@@ -1692,16 +1625,8 @@ int gemm_bf16_run(const asrx_gemm_desc* d, const GemmArgs& g, const GemmPlan& pl
       if (pl.use == 2) dispatch_p3<false, false, true>(gc, epi, nt, 1, 1, st);
       else dispatch_p3<false, false>(gc, epi, nt, 1, 1, st);
     }
-  } else if (pl.use == 10) {
-    const int rc = blaslt_gemm_bf16(d, st);
-    if (rc < 0) return rc;
-    if (rc == 1) {   // library declined (e.g. an unseen shape during graph capture): the hand-written plan
-      GemmPlan fb = pl;
-      fb.use = pl.fb_use;
-      fb.epi = pl.fb_epi;
-      fb.ntiles = pl.fb_ntiles;
-      return gemm_bf16_run(d, g, fb, batch, splitk, st);
-    }
+  } else if (pl.use == 11) {
+    launch_ws(g, d->b_trans, epi, pl.ntiles, st);
   } else if (pl.use == 9) {
     hipLaunchKernelGGL(gemm_bf16_tallk_kernel, dim3(splitk), dim3(512), 0, st, g, TallkConv{0, 0, 0, 0, 0, 0});
   } else if (pl.use == 2) {

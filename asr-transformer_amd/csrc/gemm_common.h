@@ -467,4 +467,54 @@ ASRX_DEV void keep_live(f4_t (&acc)[TN][TM]) {
     for (int j = 0; j < TM; ++j) asm volatile("" ::"v"(acc[i][j]));
 }
 
+// ---- LDS fragment reads of the LDS-DMA ring images (p3 / p4 / ws kernels)
+template <int R, bool KSTRIDED>
+ASRX_DEV s8_t p_frag(const unsigned char* img, int i0, int ks) {
+  const int l = threadIdx.x & 63, g = l >> 4;
+  if constexpr (!KSTRIDED) {
+    const int r = i0 + (l & 15);
+    const int c = (ks * 4 + g) ^ ((r >> 1) & 7);
+    return *(const s8_t*)(img + r * 128 + c * 16);
+  } else {
+    const bf16_t* t = (const bf16_t*)img;
+    const int i = l & 15, q = i >> 2, p = i & 3;
+    const int k1 = ks * 32 + 8 * g + q;
+    const int k2 = k1 + 4;
+    const bf16_t* a1 = t + k1 * R + (((i0 >> 4) ^ ks_swz<128>(k1)) << 4) + 4 * p;
+    const bf16_t* a2 = t + k2 * R + (((i0 >> 4) ^ ks_swz<128>(k2)) << 4) + 4 * p;
+    s4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4_t*)a1);
+    s4_t v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4_t*)a2);
+    return s8_t{v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
+  }
+}
+
+// p4 fragment read: as p_frag, but the k-strided image's 32-byte-chunk XOR is taken as a per-lane byte offset S
+// (ks_swz<128> of the lane's k-rows: the same for both k-row halves and both k-slices), so a fragment's address
+// is base + ((j * 32) ^ S) computed next to its read.  S is re-laundered at every phase (p4_body), which keeps
+// the compiler from hoisting 8 x 4 such addresses out of the K loop (they spilled the k-strided instantiations).
+ASRX_DEV uint32_t p4_swz_bytes() {
+  const int l = threadIdx.x & 63;
+  return (uint32_t)(ks_swz<128>(8 * (l >> 4) + ((l & 15) >> 2)) * 32);
+}
+template <int R, bool KSTRIDED>
+ASRX_DEV s8_t p4_frag(const unsigned char* img, int i0, int ks, uint32_t S) {
+  if constexpr (!KSTRIDED) {
+    return p_frag<R, false>(img, i0, ks);
+  } else {
+    const int l = threadIdx.x & 63, g = l >> 4, i = l & 15, q = i >> 2, p = i & 3;
+    const int k1 = ks * 32 + 8 * g + q;
+    // (i0 >> 4) * 32 ^ S == (i0 & ~255) * 2 + (((i0 & 255) * 2) ^ S): the row block's window, then the XOR
+    const unsigned char* a1 = img + k1 * R * 2 + 8 * p + (i0 & ~127) * 2 + (((uint32_t)(i0 & 127) * 2) ^ S);
+    const unsigned char* a2 = a1 + 4 * R * 2;
+    s4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4_t*)a1);
+    s4_t v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4_t*)a2);
+    return s8_t{v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
+  }
+}
+
+// ws kernel (gemm_ws.hip): instantiated epilogues and the launch
+constexpr int WS_BM = 256, WS_BN = 128;
+bool ws_instantiated(bool bt, int epi);
+void launch_ws(const GemmArgs& g, bool bt, int epi, int ntiles, hipStream_t st);
+
 }  // namespace asrxg

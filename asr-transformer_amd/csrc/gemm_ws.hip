@@ -1,0 +1,296 @@
+// Warp-specialised bf16 GEMM ("ws") for the one-round N = 512 GEMMs of the encoder (gfx950, MFMA 16x16x32).
+// Replaces the reference's nn.Linear forward of FeedForward.unsqueeze (layers.py:51, + the residual add of
+// model.py:24) and the data gradients of the Q/K/V and FFN1 projections (layers.py:10-12,48 backward, train.py:34).
+#include "gemm_common.h"
+
+namespace asrxg {
+namespace {
+
+// ------------------------------------------------------------------------------------------------
+// "ws" kernel: warp-specialised 256x128x64 tiles for the one-round N = 512 GEMMs of the encoder (c3: 15 936 rows,
+// 63 x 4 = 252 tiles = one per CU): the FFN2 forward x.W^T + bias + fp32 residual (K = 2048) and the plain data
+// gradients dY.W of the Q/K/V and FFN1 projections (K = 1536 / 2048, W k-strided).
+//   512 threads: waves 0-3 COMPUTE (one per SIMD, 128x64 each: the p4 wave tile, 128 fp32 accumulators), waves
+//   4-7 LOAD (one per SIMD: every LDS-DMA piece of the 3-stage ring, 48 KiB stages, 12 pieces per loader lane and
+//   stage, two stages in flight during the compute).  The compute waves issue no vector-memory instruction in the
+//   main loop: their K-step is the p4 software pipeline (one barrier per K-step, between its two 32-deep k-slices;
+//   every fragment read overlaps the MFMAs of the other k-slice) without the DMA issue that p4 interleaves.
+//   Epilogue through LDS: the compute waves write the fp32 tile into the dead ring (256 x 132 floats), then all 8
+//   waves apply bias / residual / dropout and store whole rows (16-B stores, each wave two rows of 512 B fp32 or
+//   four rows of 256 B bf16); the loader waves load their residual values before that barrier.
+// One tile per workgroup, tile = XCD-contiguous range (the 4 column tiles of a row panel share an XCD's L2).
+// ------------------------------------------------------------------------------------------------
+constexpr int WS_NST = 3;
+constexpr int WS_PA = WS_BM * BK * 2, WS_PB = WS_BN * BK * 2, WS_STAGE = WS_PA + WS_PB;
+constexpr int WS_LDS = WS_NST * WS_STAGE;                     // 144 KiB
+constexpr int WS_SP = WS_BN + 4;                              // epilogue staging row stride (floats)
+constexpr int WS_NIA = WS_PA / (4 * 1024), WS_NIB = WS_PB / (4 * 1024);
+constexpr int WS_INST = WS_NIA + WS_NIB;                      // LDS-DMA instructions per loader lane per stage
+static_assert(WS_BM * WS_SP * 4 <= WS_LDS, "epilogue staging fits the ring");
+
+// Loader-wave staging of one operand: piece j of loader wave lw fills image bytes [(4 j + lw) KiB, +1 KiB); one
+// per-lane byte offset per tile, piece j at + j * jstep (4 KiB of image = 32 rows, or 16 k-rows when k-strided;
+// both swizzles are invariant under that step).
+template <int R, bool KSTRIDED>
+struct WsStage {
+  static constexpr int NI = R * BK * 2 / (4 * 1024);
+  uint32_t vlane, jstep;
+  ASRX_DEV void set_tile(int lw, int r0, int64_t ld) {
+    const int l = threadIdx.x & 63;
+    const int o = lw * 1024 + l * 16;
+    if constexpr (!KSTRIDED) {
+      const int r = o >> 7, c = ((o >> 4) & 7) ^ ((r >> 1) & 7);
+      vlane = (uint32_t)(((int64_t)(r0 + r) * ld + c * 8) * 2);
+      jstep = (uint32_t)(32 * ld * 2);
+    } else {
+      static_assert(R == 128, "k-strided ws operand: 128 columns (ks_swz<128>)");
+      constexpr int RB = R * 2;
+      const int kr = o / RB, c16 = (o % RB) >> 4;
+      const int c32 = (c16 >> 1) ^ ks_swz<128>(kr);
+      vlane = (uint32_t)(((int64_t)kr * ld + r0 + c32 * 16 + (c16 & 1) * 8) * 2);
+      jstep = (uint32_t)(4096 / RB * ld * 2);
+    }
+    jstep = __builtin_amdgcn_readfirstlane(jstep);
+  }
+  ASRX_DEV v4i_t srd(const bf16_t* base, int64_t ld, int64_t total_bytes, int k0) const {
+    const int64_t koff = KSTRIDED ? (int64_t)k0 * ld * 2 : (int64_t)k0 * 2;
+    return make_srd((const char*)base + koff, total_bytes - koff);
+  }
+  ASRX_DEV void issue(unsigned char* img, v4i_t d, int lw) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      uint32_t v = vlane;
+      asm volatile("" : "+v"(v));
+      dma16_asm(img + (j * 4 + lw) * 1024, d, v + j * jstep);
+    }
+#endif
+  }
+};
+
+template <bool BT, int EPI>
+__global__ __launch_bounds__(512) void gemm_bf16_ws_kernel(GemmArgs g, int ntiles) {
+  g.seed = seed_eff(g.seed);
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[WS_LDS];
+  constexpr int TM = 8, TN = 4;
+  const int per8 = (ntiles + 7) / 8;
+  const int t = (int)(blockIdx.x % 8) * per8 + (int)(blockIdx.x / 8);
+  if (t >= ntiles) return;
+  const int ntn = g.N / WS_BN;
+  const int m0 = (t / ntn) * WS_BM, n0 = (t % ntn) * WS_BN;
+  const bf16_t* A = (const bf16_t*)g.a;
+  const bf16_t* B = (const bf16_t*)g.b;
+  const int64_t a_bytes = ((int64_t)(g.M - 1) * g.lda + g.K) * 2;
+  const int64_t b_bytes = BT ? ((int64_t)(g.K - 1) * g.ldb + g.N) * 2 : ((int64_t)(g.N - 1) * g.ldb + g.K) * 2;
+  const int nk = g.K / BK;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int l = threadIdx.x & 63;
+  const bool loader = wave >= 4;
+  const int lw = wave & 3;
+  const int wm = (lw >> 1) * 128, wn = (lw & 1) * 64;
+  const bool noload = (g.dbg & 8) != 0;
+
+  float* stg = (float*)lds;
+  // RES: a memory operand added by the epilogue, loaded into registers ahead of the store pass: the fp32 residual
+  // (E_RESID) or the row-periodic table (E_ROWADD: the positional encoding of _lin_in)
+  constexpr bool F32 = (EPI & E_F32) != 0, RES = (EPI & (E_RESID | E_ROWADD)) != 0;
+  static_assert(F32 || !RES, "ws: the residual / row-add epilogues write the fp32 stream");
+  static_assert((EPI & (E_GATE | E_GBITS | E_MASKOUT)) == 0, "ws: no gate / mask epilogues");
+  const int tid = threadIdx.x;
+  // epilogue ownership: fp32 C: lane (tid & 31) owns columns 4 (tid & 31) .. +3 of rows (tid >> 5) + 16 i; bf16 C:
+  // lane (tid & 15) owns columns 8 (tid & 15) .. +7 of rows (tid >> 4) + 32 i
+  constexpr int NR = F32 ? 16 : 8;
+  const int cq = F32 ? (tid & 31) * 4 : (tid & 15) * 8;
+  const int rb = F32 ? tid >> 5 : tid >> 4;
+  constexpr int RS = F32 ? 16 : 32;
+  f4_t rr[RES ? NR : 1];
+  auto load_resid = [&]() {
+    if constexpr (RES) {
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        const int m = m0 + rb + RS * i;
+        rr[i] = f4_t{0.f, 0.f, 0.f, 0.f};
+        if (m < g.M) {
+          if constexpr ((EPI & E_RESID) != 0)
+            rr[i] = *(const f4_t*)((const float*)g.resid + (int64_t)m * g.ld_resid + n0 + cq);
+          else
+            rr[i] = *(const f4_t*)(g.rowadd + (int64_t)(m % g.rowadd_mod) * g.ld_rowadd + n0 + cq);
+        }
+      }
+    }
+  };
+
+  // The two roles run separate loops with the same barrier count (1 + nk): a shared loop with role branches made
+  // the compiler merge the accumulators through phi copies (and spill them).
+  if (loader) {
+    // ---------------- loader waves: 3-stage ring, stage s + 3 issued once step s has released its buffer
+    WsStage<WS_BM, false> sa;
+    WsStage<WS_BN, BT> sb;
+    sa.set_tile(lw, m0, g.lda);
+    sb.set_tile(lw, n0, g.ldb);
+    int ni = 0;   // stages issued
+    auto issue = [&](int buf) {
+      if (!noload) {
+        unsigned char* img = lds + buf * WS_STAGE;
+        sa.issue(img, sa.srd(A, g.lda, a_bytes, ni * BK), lw);
+        sb.issue(img + WS_PA, sb.srd(B, g.ldb, b_bytes, ni * BK), lw);
+      }
+      ++ni;
+    };
+    issue(0);
+    if (nk > 1) issue(1);
+    if (nk > 2) issue(2);
+    if (noload) wait_vmcnt<0>();
+    else wait_stages<WS_INST, 2>(min(nk, 3) - 1);
+    __builtin_amdgcn_s_barrier();
+    int cb = 0;
+    for (int s = 0; s < nk; ++s) {
+      // stage s + 1 landed (visible after the barrier); the stages issued after it stay in flight
+      if (s + 1 < nk) {
+        if (noload) wait_vmcnt<0>();
+        else wait_stages<WS_INST, 1>(ni - (s + 2));
+      }
+      __builtin_amdgcn_s_barrier();
+      if (ni < nk) issue(cb);   // stage s + 3 into the buffer step s released
+      cb = cb == WS_NST - 1 ? 0 : cb + 1;
+    }
+    load_resid();   // (before the epilogue barrier: its latency overlaps the compute waves' last k-slice)
+  } else {
+    // ---------------- compute waves: the p4 pipeline on a 128x64 wave tile
+    f4_t acc[TN][TM];
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+    s8_t fa0[TM], fb0[TN], fa1[TM], fb1[TN];
+    uint32_t S = p4_swz_bytes();
+#define WS_ROLL_ORDER()                                                                       \
+  do {                                                                                        \
+    __builtin_amdgcn_sched_group_barrier(0x100, TN * (BT ? 2 : 1), 0);                        \
+    _Pragma("unroll") for (int j_ = 0; j_ < TM; ++j_) {                                       \
+      __builtin_amdgcn_sched_group_barrier(0x008, TN, 0);                                     \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                      \
+    }                                                                                         \
+  } while (0)
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int j = 0; j < TM; ++j) fa0[j] = p4_frag<WS_BM, false>(lds, wm + 16 * j, 0, S);
+#pragma unroll
+    for (int i = 0; i < TN; ++i) fb0[i] = p4_frag<WS_BN, BT>(lds + WS_PA, wn + 16 * i, 0, S);
+    uint32_t cbo = 0;   // byte offset of step s's ring buffer
+    for (int s = 0; s < nk; ++s) {
+      asm volatile("" : "+s"(cbo));
+      const uint32_t nbo = cbo == (WS_NST - 1) * WS_STAGE ? 0u : cbo + WS_STAGE;
+      const unsigned char* la = lds + cbo;
+      // ---- phase A: k-slice 0 MFMAs of step s | k-slice 1 fragment reads of step s
+      asm volatile("" : "+v"(S));
+#pragma unroll
+      for (int i = 0; i < TN; ++i) fb1[i] = p4_frag<WS_BN, BT>(la + WS_PA, wn + 16 * i, 1, S);
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+#pragma unroll
+        for (int i = 0; i < TN; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[i], fa0[j], acc[i][j], 0, 0, 0);
+        fa1[j] = p4_frag<WS_BM, false>(la, wm + 16 * j, 1, S);
+      }
+      WS_ROLL_ORDER();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // ---- mid-step barrier: stage s + 1 visible, buffer s dead (every k-slice-1 read of step s returned)
+      __builtin_amdgcn_s_barrier();
+      // ---- phase B: k-slice 1 MFMAs of step s | k-slice 0 fragment reads of step s + 1
+      const unsigned char* ln = lds + nbo;
+      asm volatile("" : "+v"(S));
+      const bool more = s + 1 < nk;
+      if (more) {
+#pragma unroll
+        for (int i = 0; i < TN; ++i) fb0[i] = p4_frag<WS_BN, BT>(ln + WS_PA, wn + 16 * i, 0, S);
+      }
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+#pragma unroll
+        for (int i = 0; i < TN; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[i], fa1[j], acc[i][j], 0, 0, 0);
+        if (more) fa0[j] = p4_frag<WS_BM, false>(ln, wm + 16 * j, 0, S);
+      }
+      WS_ROLL_ORDER();
+      cbo = nbo;
+    }
+#undef WS_ROLL_ORDER
+    // every ring buffer is dead after the last mid-step barrier: the fp32 tile goes to the staging image
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j)
+        *(f4_t*)(stg + (wm + 16 * j + (l & 15)) * WS_SP + wn + 16 * i + 4 * (l >> 4)) = acc[i][j];
+  }
+  __syncthreads();
+  if (!loader) load_resid();
+  if (g.dbg & 1) return;
+  if constexpr (F32) {
+    f4_t b4 = f4_t{0.f, 0.f, 0.f, 0.f};
+    if constexpr ((EPI & E_BIAS) != 0) b4 = *(const f4_t*)(g.bias + n0 + cq);
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int r = rb + RS * i, m = m0 + r;
+      f4_t v = *(const f4_t*)(stg + r * WS_SP + cq);
+      f4_t pr = f4_t{0.f, 0.f, 0.f, 0.f};
+      if constexpr (RES) pr = rr[i];
+      v = epi_vals<EPI, true>(g, m, n0 + cq, v, b4, uint2{0u, 0u}, pr);
+      if (m < g.M) {
+        float* c = (float*)g.c + (int64_t)m * g.ldc + n0 + cq;
+        if constexpr ((EPI & E_BETA) != 0) v += *(const f4_t*)c;
+        *(f4_t*)c = v;
+      }
+    }
+  } else {
+    f4_t ba = f4_t{0.f, 0.f, 0.f, 0.f}, bb = ba;
+    if constexpr ((EPI & E_BIAS) != 0) {
+      ba = *(const f4_t*)(g.bias + n0 + cq);
+      bb = *(const f4_t*)(g.bias + n0 + cq + 4);
+    }
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int r = rb + RS * i, m = m0 + r;
+      f4_t va = *(const f4_t*)(stg + r * WS_SP + cq);
+      f4_t vb = *(const f4_t*)(stg + r * WS_SP + cq + 4);
+      if (m < g.M) {
+        va = epi_vals<EPI>(g, m, n0 + cq, va, ba);
+        vb = epi_vals<EPI>(g, m, n0 + cq + 4, vb, bb);
+        v4u_t u = {pack2bf(va[0], va[1]), pack2bf(va[2], va[3]), pack2bf(vb[0], vb[1]), pack2bf(vb[2], vb[3])};
+        *(v4u_t*)((bf16_t*)g.c + (int64_t)m * g.ldc + n0 + cq) = u;
+      }
+    }
+  }
+}
+
+// ws instantiations (the N = 512 encoder GEMMs of the training step): x.W^T (+ bias (+ dropout) + fp32 residual)
+// and dY.W (k-strided W)
+#define ASRX_EPIWS_NT(X) X(0) X(E_BIAS) X(E_F32) X(E_BIAS | E_F32) X(E_BIAS | E_RESID | E_F32) \
+  X(E_BIAS | E_DROP | E_RESID | E_F32) X(E_BIAS | E_ROWADD | E_F32)
+#define ASRX_EPIWS_NN(X) X(0) X(E_F32)
+
+}  // namespace
+
+bool ws_instantiated(bool bt, int epi) {
+#define ASRX_HAS(E) if (epi == (E)) return true;
+  if (!bt) { ASRX_EPIWS_NT(ASRX_HAS) }
+  else { ASRX_EPIWS_NN(ASRX_HAS) }
+#undef ASRX_HAS
+  return false;
+}
+
+void launch_ws(const GemmArgs& g, bool bt, int epi, int ntiles, hipStream_t st) {
+  const dim3 grid(8 * ((ntiles + 7) / 8)), blk(512);
+#define ASRX_CASE(E) case (E): hipLaunchKernelGGL((gemm_bf16_ws_kernel<BT_, (E)>), grid, blk, 0, st, g, ntiles); return;
+  if (!bt) {
+    constexpr bool BT_ = false;
+    switch (epi) { ASRX_EPIWS_NT(ASRX_CASE) default: break; }
+  } else {
+    constexpr bool BT_ = true;
+    switch (epi) { ASRX_EPIWS_NN(ASRX_CASE) default: break; }
+  }
+#undef ASRX_CASE
+}
+
+
+}  // namespace asrxg
+
+ASRX_SEED_OFFSET_SETTER(gemm_ws)

@@ -79,8 +79,9 @@ typedef struct asrx_gemm_desc {
    * ASRX_ERR_UNSUPPORTED. */
   uint32_t* mask_out; int64_t ld_mask;
   /* kernel family (tests / A-B; 0 = auto): 1 = 256x128 LDS-DMA ring (p3), 3 = register-staged tiles, 4 = 64x64
-   * LDS-DMA ring, 5 = 128x64 LDS-DMA ring, 6 = 256x256 LDS-DMA ring (p4) — honoured where the family's
-   * preconditions hold, else auto. */
+   * LDS-DMA ring, 5 = 128x64 LDS-DMA ring, 6 = 256x256 LDS-DMA ring (p4), 8 = warp-specialised 256x128 tiles
+   * (ws: 4 MFMA waves + 4 LDS-DMA loader waves; A k-contiguous, N % 128 == 0) — honoured where the family's
+   * preconditions hold, else auto.  Every family is a hand-written kernel of this library. */
   int32_t kernel;
 } asrx_gemm_desc;
 

@@ -5,6 +5,8 @@ backend-independent and is exercised here with gloo."""
 import os
 import socket
 
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 import pytest
 import torch
 import torch.distributed as dist
@@ -230,3 +232,26 @@ def test_release_groups_cover_each_parameter_once():
                 r.ready(a, b)
         r.finish()
         assert counts.eq(1).all(), every
+
+
+def test_bench_gpus_flag_launches_ranks_on_cpu():
+    """`python bench.py --gpus 2` with no launcher environment starts the two ranks itself (child
+    torch.distributed.run, gloo self-test mode: no GPU) and relays rank 0's single JSON line with n_gpus = 2;
+    a rank whose WORLD_SIZE disagrees with --gpus exits non-zero."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "1"
+    bench = os.path.join(REPO, "bench.py")
+    r = subprocess.run([sys.executable, bench, "--gpus", "2", "--steps", "3", "--warmup", "0", "--cpu-dist-selftest"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["steps"] == 3
+    env_bad = dict(env, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, bench, "--gpus", "2", "--cpu-dist-selftest"], env=env_bad,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0

@@ -109,3 +109,46 @@ def test_graph_segments_with_release_path(monkeypatch):
         assert len(seen) > 1
         grads.append(tr.store.grad.clone())
     assert torch.equal(grads[0], grads[1])
+
+
+def test_graph_steps_keyed_by_shape():
+    """Alternating input shapes (a smaller last batch every other step): each shape runs one eager step, is then
+    captured once and replayed — both graphs are kept — and the 8 steps equal the eager Trainer's bit for bit."""
+    from asrx.train import Trainer
+    spec = CONFIGS["c1"]
+    params = []
+    for graph in (False, True):
+        m, cfg = build("c1", 0.0)
+        big, small = batches(cfg, spec, 1)[0], batches(cfg, spec, 1, batch=2)[0]
+        tr = Trainer(m, lr=1e-3, graph=graph)
+        for i in range(8):
+            tr.step(*(big if i % 2 == 0 else small))
+        if graph:
+            assert len(tr._caps) == 2
+        params.append(tr.store.flat.clone())
+    assert torch.equal(params[0], params[1])
+
+
+def test_graphed_forward_sees_weight_updates():
+    """asrx.infer.GraphedForward after the weights change (in-place update, as optimizer.step() does): the replay
+    re-casts the bf16 operand copy and equals a fresh eager forward; re-binding the parameters (load_state_dict
+    into new tensors is the same) makes it capture again."""
+    from asrx.infer import GraphedForward
+    m, cfg = build("c1", 0.0)
+    m.eval()
+    s, t, k = batches(cfg, CONFIGS["c1"], 1)[0]
+    fwd = GraphedForward(m)
+    with torch.no_grad():
+        out0 = fwd(s, t[:, :-1], k[:, :-1]).clone()
+        for p in m.parameters():
+            p.mul_(1.05)
+        out1 = fwd(s, t[:, :-1], k[:, :-1]).clone()
+        ref1 = m(s, t[:, :-1], k[:, :-1])
+    assert not torch.equal(out0, out1)
+    assert torch.equal(out1, ref1)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.data = p.data * 0.5          # new storage: the flat store is rebuilt, the old graph dropped
+        out2 = fwd(s, t[:, :-1], k[:, :-1]).clone()
+        ref2 = m(s, t[:, :-1], k[:, :-1])
+    assert torch.equal(out2, ref2)

@@ -241,17 +241,39 @@ def test_gemm_batched_heads():
     assert relerr(S[:, :, :L].cpu(), ref) < 1e-5
 
 
-@pytest.mark.parametrize("M,N,Kd,bt", [(15936, 512, 2048, 1), (15936, 512, 1536, 1), (300, 200, 136, 1),
-                                        (257, 96, 64, 0), (64, 512, 2048, 1)])
-def test_gemm_hipblaslt_plain(M, N, Kd, bt):
-    """The hipBLASLt path of asrx_gemm (kernel code 7; chosen automatically for the encoder's plain 512-wide data
-    gradients): C = A . op(B) in bf16 against an fp64 reference, both B layouts."""
+def plan_name(M, N, Kd, bt=False, bias=False, c_f32=False, resid=False, dropout=False, kernel=0):
+    """asrx_gemm_kernel_name of a (M, N, K) GEMM with fake 16-B aligned pointers: the kernel the plan picks."""
+    from asrx._lib import BF16, F32, GemmDesc
+    from asrx.kernels import KERNEL_CODES, kernel_name
+    d = GemmDesc()
+    d.m, d.n, d.k, d.in_dtype = M, N, Kd, BF16
+    d.a, d.lda = 1 << 20, Kd
+    d.b, d.ldb, d.b_trans = 2 << 20, (N if bt else Kd), int(bt)
+    d.c, d.ldc, d.c_dtype = 3 << 20, N, (F32 if c_f32 else BF16)
+    d.alpha, d.batch, d.batch_inner, d.splitk = 1.0, 1, 1, 1
+    d.kernel = KERNEL_CODES.get(kernel, kernel)
+    if bias:
+        d.bias = 4 << 20
+    if resid:
+        d.resid, d.ld_resid, d.resid_dtype = 5 << 20, N + 8, F32
+    if dropout:
+        d.dropout_p = 0.1
+    return kernel_name(d)
+
+
+@pytest.mark.parametrize("M,N,Kd,bt", [(15936, 512, 2048, 1), (15936, 512, 1536, 1), (300, 256, 192, 1),
+                                        (257, 128, 64, 0), (64, 512, 2048, 1), (1000, 384, 640, 0)])
+def test_gemm_ws_plain(M, N, Kd, bt):
+    """The warp-specialised 256x128 kernel (kernel code 8; chosen automatically for the encoder's plain 512-wide data
+    gradients, K >= 1536): C = A . op(B) in bf16 against an fp64 reference, both B layouts, ragged M (rows past M
+    read as zero, stores masked), and identical to the auto plan at the bench shapes."""
     g = torch.Generator().manual_seed(M + N + Kd)
     a = bf(torch.randn(M, Kd, generator=g))
     b = bf(torch.randn(Kd, N, generator=g) if bt else torch.randn(N, Kd, generator=g))
     c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     ref = a.double() @ (b.double() if bt else b.double().t())
-    K().gemm(a.to(dev), b.to(dev), c, M, N, Kd, lda=Kd, ldb=b.shape[1], ldc=N, b_trans=bool(bt), kernel="blaslt")
+    assert plan_name(M, N, Kd, bt=bt, kernel="ws").startswith("gemm_bf16_ws_kernel")
+    K().gemm(a.to(dev), b.to(dev), c, M, N, Kd, lda=Kd, ldb=b.shape[1], ldc=N, b_trans=bool(bt), kernel="ws")
     assert relerr(c.float().cpu(), ref) < 1e-2
     if bt and N == 512 and Kd >= 1536 and M >= 8192:   # the auto plan takes the same path
         c2 = torch.empty_like(c)
@@ -259,25 +281,56 @@ def test_gemm_hipblaslt_plain(M, N, Kd, bt):
         assert torch.equal(c, c2)
 
 
-@pytest.mark.parametrize("M,N,Kd,f32,resid", [(15936, 512, 2048, 1, 1), (4096, 512, 2048, 1, 1), (300, 200, 136, 1, 1),
-                                              (257, 96, 64, 1, 0), (257, 96, 64, 0, 0), (64, 512, 512, 1, 1)])
-def test_gemm_hipblaslt_bias_resid(M, N, Kd, f32, resid):
-    """The hipBLASLt path with the library's bias epilogue and the fp32 residual as its C matrix (beta = 1): the
-    FFN2 forward's out = x . w^T + bias + resid (E_BIAS | E_RESID | E_F32), forced (kernel code 7) and auto, against
-    an fp64 reference and against the hand-written p3 epilogue (same inputs, fp32 rounding-order differences only)."""
+@pytest.mark.parametrize("M,N,Kd,f32,resid,drop", [(15936, 512, 2048, 1, 1, 0), (4096, 512, 2048, 1, 1, 0),
+                                                   (300, 256, 128, 1, 1, 0), (257, 128, 64, 1, 0, 0),
+                                                   (257, 128, 64, 0, 0, 0), (15936, 512, 512, 1, 1, 1),
+                                                   (700, 384, 256, 1, 1, 1)])
+def test_gemm_ws_bias_resid(M, N, Kd, f32, resid, drop):
+    """The ws kernel's LDS-staged epilogue: out = x . w^T + bias (+ dropout) (+ fp32 residual, ld_resid != ldc) —
+    the FFN2 forward (E_BIAS | E_RESID | E_F32) and the out-projection (+ E_DROP) — forced (kernel code 8) against
+    an fp64 reference, and element-for-element against the p3 epilogue on the same inputs (same keep bits; fp32
+    accumulation-order differences only)."""
     g = torch.Generator().manual_seed(M + 3 * N + Kd)
     x, w = bf(torch.randn(M, Kd, generator=g)), bf(torch.randn(N, Kd, generator=g))
     bias = torch.randn(N, generator=g)
     r = torch.randn(M, N + 8, generator=g) if resid else None   # ld_resid = N + 8 != ldc
-    ref = x.double() @ w.double().t() + bias.double() + (r[:, :N].double() if resid else 0)
+    ref = x.double() @ w.double().t() + bias.double()
     kw = dict(resid=r.to(dev), ld_resid=N + 8) if resid else {}
+    if drop:
+        kw.update(dropout_p=0.1, seed=77)
     outs = {}
-    for kern in ("blaslt", "p3", None):
+    for kern in ("ws", "p3"):
         c = torch.empty(M, N, device=dev, dtype=torch.float32 if f32 else torch.bfloat16)
         K().linear(x.to(dev), w.to(dev), c, bias=bias.to(dev), kernel=kern, **kw)
         outs[kern] = c.float().cpu()
-        assert relerr(outs[kern], ref) < (1e-5 if f32 else 1e-2), kern
-    assert (outs["blaslt"] - outs["p3"]).abs().max() <= (1e-4 if f32 else 1e-2) * ref.abs().max()
+    kn = plan_name(M, N, Kd, bias=True, c_f32=bool(f32), resid=bool(resid), dropout=bool(drop), kernel="ws")
+    assert kn.startswith("gemm_bf16_ws_kernel"), kn
+    if drop:   # same keep bits in both kernels; the reference is p3's kept pattern
+        keep = (outs["p3"] - (r[:, :N] if resid else 0)) != 0
+        ref = torch.where(keep, ref / 0.9, torch.zeros_like(ref))
+    if resid:
+        ref = ref + r[:, :N].double()
+    for kern, o in outs.items():
+        assert relerr(o, ref) < (1e-5 if f32 else 1e-2), kern
+    assert (outs["ws"] - outs["p3"]).abs().max() <= (1e-4 if f32 else 1e-2) * ref.abs().max()
+
+
+def test_gemm_ws_rowadd():
+    """The ws kernel's row-periodic add (E_ROWADD, the _lin_in GEMM's positional-encoding epilogue: row m takes
+    table row m % T'), fp32 out, against fp64 and against p3."""
+    M, N, Kd, T2 = 15936, 512, 1216, 249
+    g = torch.Generator().manual_seed(11)
+    x, w = bf(torch.randn(M, Kd, generator=g)), bf(torch.randn(N, Kd, generator=g))
+    bias, pe = torch.randn(N, generator=g), torch.randn(T2, N, generator=g)
+    ref = x.double() @ w.double().t() + bias.double() + pe.double().repeat(M // T2 + 1, 1)[:M]
+    outs = {}
+    for kern in ("ws", "p3"):
+        c = torch.empty(M, N, device=dev)
+        K().gemm(x.to(dev), w.to(dev), c, M, N, Kd, lda=Kd, ldb=Kd, ldc=N, bias=bias.to(dev), rowadd=pe.to(dev),
+                 rowadd_mod=T2, ld_rowadd=N, kernel=kern)
+        outs[kern] = c.cpu()
+        assert relerr(outs[kern], ref) < 1e-5, kern
+    assert (outs["ws"] - outs["p3"]).abs().max() <= 1e-4 * ref.abs().max()
 
 
 # ------------------------------------------------------------------------------------------------ LayerNorm

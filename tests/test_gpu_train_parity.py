@@ -177,3 +177,66 @@ def test_trainer_c3_full_batch_properties():
     losses = [float(tr.step(s, t, k)) for _ in range(5)]
     assert all(np.isfinite(losses)), losses
     assert losses[-1] < losses[0], losses
+
+
+def _plan_log(fn):
+    """Run fn() with a KernelProbe that logs every GEMM launch (kernel instantiation, m, n, k, batch, splitk)."""
+    from asrx import kernels as K
+    probe = K.KernelProbe(target="", log=[])
+    probe.active = True
+    K.PROBE = probe
+    try:
+        out = fn()
+        torch.cuda.synchronize()
+    finally:
+        K.PROBE = None
+    return out, probe.log
+
+
+def _assert_bench_plan(log, rows):
+    """The GEMM kernels of a c3 step at B = 64 (bench.py's workload): the wide encoder projections on p4 (FFN1
+    forward, the gated FFN2 data gradient, the all-layer cross K/V), the Q/K/V projection on p3, every 512-wide
+    encoder output on the warp-specialised ws kernel, the weight gradients in one grouped p4g launch."""
+    by_shape = {}
+    for name, m, n, k, *_ in log:
+        by_shape.setdefault((m, n, k), set()).add(name.split("<")[0])
+    fam = {nm for names in by_shape.values() for nm in names}
+    assert by_shape[(rows, 2048, 512)] == {"gemm_bf16_p4_kernel"}, by_shape[(rows, 2048, 512)]   # FFN1 fwd + FFN2 dX
+    assert by_shape[(rows, 1536, 512)] == {"gemm_bf16_p3_kernel"}, by_shape[(rows, 1536, 512)]   # Q/K/V fwd
+    for kk in (512, 1216, 1536, 2048):                                                          # N = 512 outputs
+        assert by_shape[(rows, 512, kk)] == {"gemm_bf16_ws_kernel"}, (kk, by_shape[(rows, 512, kk)])
+    assert "gemm_bf16_p4g_kernel" in fam, fam
+
+
+def test_trainer_grads_vs_oracle_bench_batch():
+    """The bench's GEMM plan pinned at model level: c3 at B = 64, T = 1000 (15 936 encoder rows, the exact kernel
+    plan bench.py times — asserted from the launch log), dropout 0: every parameter gradient and the loss of the
+    steady-state bf16 Trainer step vs the oracle's fp32 autograd (GRAD_TOL / MAX_TOL, or within BF16_FACTOR of the
+    reference's own bf16-autocast path), and the teacher-forced bf16 forward vs the oracle's fp32 forward."""
+    m, cfg = build("c3")
+    spec = CONFIGS["c3"]
+    B = spec["batch"]
+    s, t, k = synthetic_batch(cfg, B, spec["frames"], spec["text_len"] + 1, seed=2025)
+    (loss, _), log = _plan_log(lambda: trainer_grads(m, s.to(dev), t.to(dev), k.to(dev)))
+    rows = B * 249
+    _assert_bench_plan(log, rows)
+    gsd = ref_key_grads(m, cfg)
+    m.eval()
+    with torch.no_grad():
+        logits, flog = _plan_log(lambda: m(s.to(dev), t[:, :-1].to(dev), k[:, :-1].to(dev)).cpu())
+    assert {nm.split("<")[0] for nm, mm, n, kk, *_ in flog if (mm, n) == (rows, 512)} == {"gemm_bf16_ws_kernel"}
+    torch.set_num_threads(max(1, min(32, len(os.sched_getaffinity(0)))))
+    P = {kk: v.clone().requires_grad_(True) for kk, v in det_params(cfg, 0).items()}
+    ref_loss, ref = train_step_grads(P, s, t, k, cfg, training=False)
+    assert abs(loss - float(ref_loss)) < 1e-2 * abs(float(ref_loss))
+    P16 = {kk: v.clone().requires_grad_(True) for kk, v in det_params(cfg, 0).items()}
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        _, ref16 = train_step_grads(P16, s, t, k, cfg, training=False)
+    names = [kk for kk, v in ref.items() if v is not None]
+    check_grads(gsd, ref, names, "c3 B=64", ref_bf16=ref16)
+    del P, P16, ref, ref16
+    from oracle.ref_model import forward as oracle_forward
+    with torch.no_grad():
+        ref_logits = oracle_forward(det_params(cfg, 0), s, t[:, :-1], k[:, :-1], cfg, False)
+    assert relerr(logits, ref_logits) < 1.5e-2
+    assert float((logits.argmax(-1) == ref_logits.argmax(-1)).double().mean()) >= 0.98

@@ -36,6 +36,8 @@ SHAPES = [
     ("ffn2 dgrad gated", "dgradg", 15936, 512, 2048),
     # the step's plain data gradients (out 512 wide; dgrad kind: y[M, Kd] = dy[M, N] . w[N, Kd])
     ("enc qkv dg512", "dgrad", 15936, 1536, 512),
+    ("enc ffn1 dg512", "dgrad", 15936, 2048, 512),
+    ("enc out dg512", "dgrad", 15936, 512, 512),
     ("dec ffn1 dg512", "dgrad", 4096, 2048, 512),
     ("dec qkv dg512", "dgrad", 4096, 1536, 512),
     ("dec out dg512", "dgrad", 4096, 512, 512),
@@ -43,6 +45,7 @@ SHAPES = [
     ("ffn2 fwd res", "fwdres", 15936, 512, 2048),
     ("dec ffn2 fwd res", "fwdres", 4096, 512, 2048),
     ("out fwd res", "fwdres", 15936, 512, 512),
+    ("lin_in fwd pe", "fwdres", 15936, 512, 1216),
 ]
 
 
@@ -110,7 +113,7 @@ def main():
             dy, w = rnd(M, N), rnd(N, Kd)
             y = torch.empty(M, Kd, device="cuda", dtype=torch.bfloat16)
             res["hipBLASLt"] = timeit(lambda: torch.mm(dy, w, out=y), args.reps, args.rounds)
-            for v in variants + ["blaslt"]:
+            for v in variants + ["ws"]:
                 kk, fb = kb(v)
                 dbg_runs(res, v, lambda: K.linear_dgrad(dy, w, y, kernel=kk), fb)
         elif kind == "fwdres":
@@ -118,7 +121,7 @@ def main():
             bias = torch.randn(N, device="cuda", generator=g)
             r = torch.randn(M, N, device="cuda", generator=g)
             y = torch.empty(M, N, device="cuda")
-            for v in variants + ["blaslt", "auto"]:
+            for v in variants + ["ws", "auto"]:
                 kk = None if v == "auto" else kb(v)[0]
                 res[v] = timeit(lambda: K.linear(x, w, y, bias=bias, resid=r, ld_resid=N, kernel=kk), args.reps,
                                 args.rounds)
