@@ -175,10 +175,20 @@ def _release(C, ready, params):
 RELEASE_LAYERS = int(os.environ.get("ASRX_DP_RELEASE_LAYERS", "0"))
 
 
+def _wgrad_tile():
+    """(rows, cols) of one weight-gradient tile of the grouped launch's kernel (kernels.WGRAD_KIND)."""
+    return K._TILE_CODE.get(K.WGRAD_KIND, ((256, 256), 0))[0]
+
+
+def _tiles(m, n):
+    tm, tn = _wgrad_tile()
+    return -(-m // tm) * -(-n // tn)
+
+
 def _queued_tiles(C, start=0):
-    """256x256 output tiles of the weight gradients queued since queue position `start` (one tile per workgroup in
-    the grouped launch, one workgroup per CU)."""
-    return sum(-(-dy.shape[1] // 256) * -(-x.shape[1] // 256) for (dy, x, _, _) in (C.wq or [])[start:])
+    """Output tiles of the weight gradients queued since queue position `start` (one tile per workgroup in the
+    grouped launch, one workgroup per CU)."""
+    return sum(_tiles(dy.shape[1], x.shape[1]) for (dy, x, _, _) in (C.wq or [])[start:])
 
 
 def _num_cus(dev):
@@ -214,7 +224,7 @@ def encoder_bwd(C, enc, S, dy, gate_feats, ready=None, release_every=None, carry
     groups = {} if by_rounds else {lo: hi for lo, hi in release_groups(n, release_every)}
     hi, q0, cus = n, len(C.wq or []), _num_cus(x.device)
     lw = enc._lin_in.weight
-    tail = -(-lw.shape[0] // 256) * -(-lw.shape[1] // 256)
+    tail = _tiles(lw.shape[0], lw.shape[1])
     for i, layer_S in reversed(list(enumerate(S["layers"]))):
         nxt = torch.empty(x.shape, dtype=C.cd, device=x.device)
         dx = Bk.enc_layer_bwd(C, layer_S, dx, dx_c, nxt)

@@ -218,6 +218,7 @@ GROUPED_TABLE_KERNEL = "gemm_bf16_grouped_dev_kernel<true, true>"
 # (beta != 1, beta == 1) instantiations (96 = E_BETA | E_F32: accumulate into the fp32 grads)
 GROUPED_P3_KERNELS = ("gemm_bf16_p3g_kernel<64>", "gemm_bf16_p3g_kernel<96>")
 GROUPED_P4_KERNELS = ("gemm_bf16_p4g_kernel<64>", "gemm_bf16_p4g_kernel<96>")
+GROUPED_WS_KERNELS = ("gemm_bf16_wsg_kernel<64>", "gemm_bf16_wsg_kernel<96>")
 
 
 def wgrad_groupable(dy, x, wgrad):
@@ -228,15 +229,17 @@ def wgrad_groupable(dy, x, wgrad):
             and x.data_ptr() % 16 == 0 and dy.shape[0] <= 65536)
 
 
-# Weight-gradient kernel: "p4" = 256x256 tiles on the software-pipelined LDS-DMA ring (gemm.hip p4_body; c3 step
-# 14.11 -> 13.80 ms against "p3", the 256x128 ring), "reg" = the register-staged 128x128 tiles (also the fallback
-# for tables the ring cannot take).  ASRX_WGRAD_KIND overrides.
-WGRAD_KIND = os.environ.get("ASRX_WGRAD_KIND", "p4")
+# Weight-gradient kernel: "ws" = the warp-specialised 256x128 tiles (gemm_ws.hip: 4 MFMA waves + 4 LDS-DMA loader
+# waves, 3-stage ring, bias-gradient row sums on the loader waves; c3 step 13.55-13.61 -> 13.06-13.13 ms against
+# "p4", same box, alternating), "p4" = 256x256 tiles on the software-pipelined LDS-DMA ring (gemm.hip p4_body),
+# "p3" = the 256x128 ring, "reg" = the register-staged 128x128 tiles (also the fallback for tables the rings
+# cannot take).  ASRX_WGRAD_KIND overrides.
+WGRAD_KIND = os.environ.get("ASRX_WGRAD_KIND", "ws")
 
 
 def _grouped_p3_ok(items, beta):
     """Can the LDS-DMA ring kernel take these weight gradients (fp32 C rows 16-byte aligned, beta 0 or 1)?"""
-    return WGRAD_KIND in ("p3", "p4") and beta in (0.0, 1.0) and all(
+    return WGRAD_KIND in ("p3", "p4", "ws") and beta in (0.0, 1.0) and all(
         x.shape[1] % 4 == 0 and wgrad.stride(0) % 4 == 0 and wgrad.data_ptr() % 16 == 0
         for (_, x, wgrad, _) in items)
 
@@ -313,7 +316,7 @@ def xcd_plan(shapes, tile=256, nxcd=8, pack=None):
     return plan
 
 
-_TILE_CODE = {"p3": ((256, 128), 3), "p4": ((256, 256), 4), "reg": ((128, 128), 128)}
+_TILE_CODE = {"p3": ((256, 128), 3), "p4": ((256, 256), 4), "ws": ((256, 128), 5), "reg": ((128, 128), 128)}
 
 
 def upload(dst, host_bytes):
@@ -388,7 +391,7 @@ def linear_wgrad_grouped(items, *, beta=1.0, kind=None):
     common.alpha, common.beta = 1.0, beta
     p3 = _grouped_p3_ok(items, beta)
     kind = kind or WGRAD_KIND
-    kname = ({"p4": GROUPED_P4_KERNELS}.get(kind, GROUPED_P3_KERNELS)[beta == 1.0] if p3
+    kname = ({"p4": GROUPED_P4_KERNELS, "ws": GROUPED_WS_KERNELS}.get(kind, GROUPED_P3_KERNELS)[beta == 1.0] if p3
              else GROUPED_TABLE_KERNEL)
     probe = PROBE
     if probe is not None and probe.active and probe.log is not None:

@@ -3,8 +3,8 @@
 // model.py:24) and the data gradients of the Q/K/V and FFN1 projections (layers.py:10-12,48 backward, train.py:34).
 #include "gemm_common.h"
 
-namespace asrxg {
 namespace {
+using namespace asrxg;
 
 // ------------------------------------------------------------------------------------------------
 // "ws" kernel: warp-specialised 256x128x64 tiles for the one-round N = 512 GEMMs of the encoder (c3: 15 936 rows,
@@ -28,29 +28,42 @@ constexpr int WS_NIA = WS_PA / (4 * 1024), WS_NIB = WS_PB / (4 * 1024);
 constexpr int WS_INST = WS_NIA + WS_NIB;                      // LDS-DMA instructions per loader lane per stage
 static_assert(WS_BM * WS_SP * 4 <= WS_LDS, "epilogue staging fits the ring");
 
-// Loader-wave staging of one operand: piece j of loader wave lw fills image bytes [(4 j + lw) KiB, +1 KiB); one
-// per-lane byte offset per tile, piece j at + j * jstep (4 KiB of image = 32 rows, or 16 k-rows when k-strided;
-// both swizzles are invariant under that step).
+// Sum of an A fragment's 8 bf16 values (one column of the k-strided image, 8 consecutive k) into acc: 4
+// v_dot2c_f32_bf16 against (1, 1).
+ASRX_DEV float frag_sum(s8_t f, float acc) {
+  typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
+  const bf2_t one = {(__bf16)1.0f, (__bf16)1.0f};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const uint32_t u = (uint32_t)(uint16_t)f[2 * e] | ((uint32_t)(uint16_t)f[2 * e + 1] << 16);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, u), one, acc, false);
+  }
+  return acc;
+}
+
+// Loader-wave staging of one operand: piece j of loader wave lw fills image bytes [(4 j + lw) KiB, +1 KiB) of the
+// p4 image layouts (k-contiguous: rows of 128 B, 16-B chunks XOR (row >> 1) & 7; k-strided: k-rows of R columns,
+// 32-B chunks XOR ks_swz<128>(k-row)); one per-lane byte offset per piece and tile (loader waves have registers to
+// spare: the k-strided 256-column swizzle is not invariant under the 8-k-row step between a lane's pieces).
 template <int R, bool KSTRIDED>
 struct WsStage {
   static constexpr int NI = R * BK * 2 / (4 * 1024);
-  uint32_t vlane, jstep;
+  uint32_t voff[NI];
   ASRX_DEV void set_tile(int lw, int r0, int64_t ld) {
     const int l = threadIdx.x & 63;
-    const int o = lw * 1024 + l * 16;
-    if constexpr (!KSTRIDED) {
-      const int r = o >> 7, c = ((o >> 4) & 7) ^ ((r >> 1) & 7);
-      vlane = (uint32_t)(((int64_t)(r0 + r) * ld + c * 8) * 2);
-      jstep = (uint32_t)(32 * ld * 2);
-    } else {
-      static_assert(R == 128, "k-strided ws operand: 128 columns (ks_swz<128>)");
-      constexpr int RB = R * 2;
-      const int kr = o / RB, c16 = (o % RB) >> 4;
-      const int c32 = (c16 >> 1) ^ ks_swz<128>(kr);
-      vlane = (uint32_t)(((int64_t)kr * ld + r0 + c32 * 16 + (c16 & 1) * 8) * 2);
-      jstep = (uint32_t)(4096 / RB * ld * 2);
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int o = (4 * j + lw) * 1024 + l * 16;
+      if constexpr (!KSTRIDED) {
+        const int r = o >> 7, c = ((o >> 4) & 7) ^ ((r >> 1) & 7);
+        voff[j] = (uint32_t)(((int64_t)(r0 + r) * ld + c * 8) * 2);
+      } else {
+        constexpr int RB = R * 2;
+        const int kr = o / RB, c16 = (o % RB) >> 4;
+        const int c32 = (c16 >> 1) ^ ks_swz<128>(kr);
+        voff[j] = (uint32_t)(((int64_t)kr * ld + r0 + c32 * 16 + (c16 & 1) * 8) * 2);
+      }
     }
-    jstep = __builtin_amdgcn_readfirstlane(jstep);
   }
   ASRX_DEV v4i_t srd(const bf16_t* base, int64_t ld, int64_t total_bytes, int k0) const {
     const int64_t koff = KSTRIDED ? (int64_t)k0 * ld * 2 : (int64_t)k0 * 2;
@@ -59,30 +72,98 @@ struct WsStage {
   ASRX_DEV void issue(unsigned char* img, v4i_t d, int lw) const {
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      uint32_t v = vlane;
-      asm volatile("" : "+v"(v));
-      dma16_asm(img + (j * 4 + lw) * 1024, d, v + j * jstep);
-    }
+    for (int j = 0; j < NI; ++j) dma16_asm(img + (j * 4 + lw) * 1024, d, voff[j]);
 #endif
   }
 };
 
-template <bool BT, int EPI>
-__global__ __launch_bounds__(512) void gemm_bf16_ws_kernel(GemmArgs g, int ntiles) {
-  g.seed = seed_eff(g.seed);
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[WS_LDS];
+// The compute waves' part of a ws tile: the p4 pipeline on a 128x64 wave tile, then the fp32 accumulators into the
+// staging image.  (No row sums here: the bias gradient's column sums are the loader waves' — a per-wave branch in
+// this MFMA stream split it into small blocks, 1.68 vs 1.29 ms for the 12 encoder layers' weight gradients, and a
+// branch-free sum needs registers these waves do not have.)
+template <bool AT, bool BT>
+ASRX_DEV void ws_compute(const GemmArgs& g, int m0, int nk, int wm, int wn, unsigned char* lds) {
   constexpr int TM = 8, TN = 4;
-  const int per8 = (ntiles + 7) / 8;
-  const int t = (int)(blockIdx.x % 8) * per8 + (int)(blockIdx.x / 8);
-  if (t >= ntiles) return;
-  const int ntn = g.N / WS_BN;
-  const int m0 = (t / ntn) * WS_BM, n0 = (t % ntn) * WS_BN;
+  const int l = threadIdx.x & 63;
+  float* stg = (float*)lds;
+  // ---------------- compute waves: the p4 pipeline on a 128x64 wave tile
+  f4_t acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+  s8_t fa0[TM], fb0[TN], fa1[TM], fb1[TN];
+  uint32_t S = p4_swz_bytes();
+#define WS_ROLL_ORDER()                                                                       \
+do {                                                                                        \
+  __builtin_amdgcn_sched_group_barrier(0x100, TN * (BT ? 2 : 1), 0);                        \
+  _Pragma("unroll") for (int j_ = 0; j_ < TM; ++j_) {                                       \
+    __builtin_amdgcn_sched_group_barrier(0x008, TN, 0);                                     \
+    __builtin_amdgcn_sched_group_barrier(0x100, AT ? 2 : 1, 0);                             \
+  }                                                                                         \
+} while (0)
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int j = 0; j < TM; ++j) fa0[j] = p4_frag<WS_BM, AT>(lds, wm + 16 * j, 0, S);
+#pragma unroll
+  for (int i = 0; i < TN; ++i) fb0[i] = p4_frag<WS_BN, BT>(lds + WS_PA, wn + 16 * i, 0, S);
+  uint32_t cbo = 0;   // byte offset of step s's ring buffer
+  for (int s = 0; s < nk; ++s) {
+    asm volatile("" : "+s"(cbo));
+    const uint32_t nbo = cbo == (WS_NST - 1) * WS_STAGE ? 0u : cbo + WS_STAGE;
+    const unsigned char* la = lds + cbo;
+    // ---- phase A: k-slice 0 MFMAs of step s | k-slice 1 fragment reads of step s
+    asm volatile("" : "+v"(S));
+#pragma unroll
+    for (int i = 0; i < TN; ++i) fb1[i] = p4_frag<WS_BN, BT>(la + WS_PA, wn + 16 * i, 1, S);
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+#pragma unroll
+      for (int i = 0; i < TN; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[i], fa0[j], acc[i][j], 0, 0, 0);
+      fa1[j] = p4_frag<WS_BM, AT>(la, wm + 16 * j, 1, S);
+    }
+    WS_ROLL_ORDER();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // ---- mid-step barrier: stage s + 1 visible, buffer s dead (every k-slice-1 read of step s returned)
+    __builtin_amdgcn_s_barrier();
+    // ---- phase B: k-slice 1 MFMAs of step s | k-slice 0 fragment reads of step s + 1
+    const unsigned char* ln = lds + nbo;
+    asm volatile("" : "+v"(S));
+    const bool more = s + 1 < nk;
+    if (more) {
+#pragma unroll
+      for (int i = 0; i < TN; ++i) fb0[i] = p4_frag<WS_BN, BT>(ln + WS_PA, wn + 16 * i, 0, S);
+    }
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+#pragma unroll
+      for (int i = 0; i < TN; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[i], fa1[j], acc[i][j], 0, 0, 0);
+      if (more) fa0[j] = p4_frag<WS_BM, AT>(ln, wm + 16 * j, 0, S);
+    }
+    WS_ROLL_ORDER();
+    cbo = nbo;
+  }
+#undef WS_ROLL_ORDER
+  // every ring buffer is dead after the last mid-step barrier: the fp32 tile goes to the staging image
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j)
+      *(f4_t*)(stg + (wm + 16 * j + (l & 15)) * WS_SP + wn + 16 * i + 4 * (l >> 4)) = acc[i][j];
+}
+
+// One 256x128 output tile [m0, +256) x [n0, +128) of C = op(A) op(B)^T.  AT: A stored k-strided ([K][M], the
+// weight gradient's dY); BT: B stored k-strided ([K][N]).  Ragged K only with both operands k-strided (rows past K
+// read as zero through the descriptor range); ragged M / N tiles: rows / column groups past them are not stored.
+// g.rowsum (AT only): += the row sums of op(A) (the fused bias gradient), by the compute waves of column block 0.
+template <bool AT, bool BT, int EPI>
+ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned char* lds) {
+  constexpr int TM = 8, TN = 4;
   const bf16_t* A = (const bf16_t*)g.a;
   const bf16_t* B = (const bf16_t*)g.b;
-  const int64_t a_bytes = ((int64_t)(g.M - 1) * g.lda + g.K) * 2;
+  const int64_t a_bytes = AT ? ((int64_t)(g.K - 1) * g.lda + g.M) * 2 : ((int64_t)(g.M - 1) * g.lda + g.K) * 2;
   const int64_t b_bytes = BT ? ((int64_t)(g.K - 1) * g.ldb + g.N) * 2 : ((int64_t)(g.N - 1) * g.ldb + g.K) * 2;
-  const int nk = g.K / BK;
+  const int nk = (g.K + BK - 1) / BK;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int l = threadIdx.x & 63;
   const bool loader = wave >= 4;
@@ -124,7 +205,9 @@ __global__ __launch_bounds__(512) void gemm_bf16_ws_kernel(GemmArgs g, int ntile
   // the compiler merge the accumulators through phi copies (and spill them).
   if (loader) {
     // ---------------- loader waves: 3-stage ring, stage s + 3 issued once step s has released its buffer
-    WsStage<WS_BM, false> sa;
+    float lrs[4] = {0.f, 0.f, 0.f, 0.f};
+    const uint32_t S = p4_swz_bytes();
+    WsStage<WS_BM, AT> sa;
     WsStage<WS_BN, BT> sb;
     sa.set_tile(lw, m0, g.lda);
     sb.set_tile(lw, n0, g.ldb);
@@ -145,6 +228,19 @@ __global__ __launch_bounds__(512) void gemm_bf16_ws_kernel(GemmArgs g, int ntile
     __builtin_amdgcn_s_barrier();
     int cb = 0;
     for (int s = 0; s < nk; ++s) {
+      // the bias gradient (AT: row sums of op(A) = column sums of the k-strided A image): loader wave lw sums
+      // columns [64 lw, +64) of stage s (visible since the last barrier, overwritten after the next) through the
+      // compute waves' transposing fragment reads — lane l gets 8 consecutive k of column 16 c + (l & 15) — and 4
+      // v_dot2c_f32_bf16 against (1, 1) per fragment: 16 reads + 32 VALU per K-step, each lane's column its own
+      if constexpr (AT) {
+        if (rs_tile) {
+          const unsigned char* img = lds + cb * WS_STAGE;
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) lrs[c] = frag_sum(p4_frag<WS_BM, true>(img, 64 * lw + 16 * c, ks, S), lrs[c]);
+        }
+      }
       // stage s + 1 landed (visible after the barrier); the stages issued after it stay in flight
       if (s + 1 < nk) {
         if (noload) wait_vmcnt<0>();
@@ -155,71 +251,20 @@ __global__ __launch_bounds__(512) void gemm_bf16_ws_kernel(GemmArgs g, int ntile
       cb = cb == WS_NST - 1 ? 0 : cb + 1;
     }
     load_resid();   // (before the epilogue barrier: its latency overlaps the compute waves' last k-slice)
-  } else {
-    // ---------------- compute waves: the p4 pipeline on a 128x64 wave tile
-    f4_t acc[TN][TM];
+    if constexpr (AT) {   // fold the 4 k-groups (lanes l, l ^ 16, l ^ 32, l ^ 48); lanes 0-15 own the columns
+      if (rs_tile) {
 #pragma unroll
-    for (int i = 0; i < TN; ++i)
-#pragma unroll
-      for (int j = 0; j < TM; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
-    s8_t fa0[TM], fb0[TN], fa1[TM], fb1[TN];
-    uint32_t S = p4_swz_bytes();
-#define WS_ROLL_ORDER()                                                                       \
-  do {                                                                                        \
-    __builtin_amdgcn_sched_group_barrier(0x100, TN * (BT ? 2 : 1), 0);                        \
-    _Pragma("unroll") for (int j_ = 0; j_ < TM; ++j_) {                                       \
-      __builtin_amdgcn_sched_group_barrier(0x008, TN, 0);                                     \
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                      \
-    }                                                                                         \
-  } while (0)
-    __builtin_amdgcn_s_barrier();
-#pragma unroll
-    for (int j = 0; j < TM; ++j) fa0[j] = p4_frag<WS_BM, false>(lds, wm + 16 * j, 0, S);
-#pragma unroll
-    for (int i = 0; i < TN; ++i) fb0[i] = p4_frag<WS_BN, BT>(lds + WS_PA, wn + 16 * i, 0, S);
-    uint32_t cbo = 0;   // byte offset of step s's ring buffer
-    for (int s = 0; s < nk; ++s) {
-      asm volatile("" : "+s"(cbo));
-      const uint32_t nbo = cbo == (WS_NST - 1) * WS_STAGE ? 0u : cbo + WS_STAGE;
-      const unsigned char* la = lds + cbo;
-      // ---- phase A: k-slice 0 MFMAs of step s | k-slice 1 fragment reads of step s
-      asm volatile("" : "+v"(S));
-#pragma unroll
-      for (int i = 0; i < TN; ++i) fb1[i] = p4_frag<WS_BN, BT>(la + WS_PA, wn + 16 * i, 1, S);
-#pragma unroll
-      for (int j = 0; j < TM; ++j) {
-#pragma unroll
-        for (int i = 0; i < TN; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[i], fa0[j], acc[i][j], 0, 0, 0);
-        fa1[j] = p4_frag<WS_BM, false>(la, wm + 16 * j, 1, S);
+        for (int c = 0; c < 4; ++c) {
+          float v = lrs[c];
+          v += __shfl_xor(v, 16, 64);
+          v += __shfl_xor(v, 32, 64);
+          const int m = m0 + 64 * lw + 16 * c + l;
+          if (l < 16 && m < g.M) g.rowsum[m] += v;
+        }
       }
-      WS_ROLL_ORDER();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      // ---- mid-step barrier: stage s + 1 visible, buffer s dead (every k-slice-1 read of step s returned)
-      __builtin_amdgcn_s_barrier();
-      // ---- phase B: k-slice 1 MFMAs of step s | k-slice 0 fragment reads of step s + 1
-      const unsigned char* ln = lds + nbo;
-      asm volatile("" : "+v"(S));
-      const bool more = s + 1 < nk;
-      if (more) {
-#pragma unroll
-        for (int i = 0; i < TN; ++i) fb0[i] = p4_frag<WS_BN, BT>(ln + WS_PA, wn + 16 * i, 0, S);
-      }
-#pragma unroll
-      for (int j = 0; j < TM; ++j) {
-#pragma unroll
-        for (int i = 0; i < TN; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[i], fa1[j], acc[i][j], 0, 0, 0);
-        if (more) fa0[j] = p4_frag<WS_BM, false>(ln, wm + 16 * j, 0, S);
-      }
-      WS_ROLL_ORDER();
-      cbo = nbo;
     }
-#undef WS_ROLL_ORDER
-    // every ring buffer is dead after the last mid-step barrier: the fp32 tile goes to the staging image
-#pragma unroll
-    for (int i = 0; i < TN; ++i)
-#pragma unroll
-      for (int j = 0; j < TM; ++j)
-        *(f4_t*)(stg + (wm + 16 * j + (l & 15)) * WS_SP + wn + 16 * i + 4 * (l >> 4)) = acc[i][j];
+  } else {
+    ws_compute<AT, BT>(g, m0, nk, wm, wn, lds);
   }
   __syncthreads();
   if (!loader) load_resid();
@@ -227,6 +272,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_ws_kernel(GemmArgs g, int ntile
   if constexpr (F32) {
     f4_t b4 = f4_t{0.f, 0.f, 0.f, 0.f};
     if constexpr ((EPI & E_BIAS) != 0) b4 = *(const f4_t*)(g.bias + n0 + cq);
+    const bool ncol = n0 + cq < g.N;   // (N % 4 == 0: a column group is wholly in or out)
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
       const int r = rb + RS * i, m = m0 + r;
@@ -234,7 +280,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_ws_kernel(GemmArgs g, int ntile
       f4_t pr = f4_t{0.f, 0.f, 0.f, 0.f};
       if constexpr (RES) pr = rr[i];
       v = epi_vals<EPI, true>(g, m, n0 + cq, v, b4, uint2{0u, 0u}, pr);
-      if (m < g.M) {
+      if (m < g.M && ncol) {
         float* c = (float*)g.c + (int64_t)m * g.ldc + n0 + cq;
         if constexpr ((EPI & E_BETA) != 0) v += *(const f4_t*)c;
         *(f4_t*)c = v;
@@ -251,7 +297,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_ws_kernel(GemmArgs g, int ntile
       const int r = rb + RS * i, m = m0 + r;
       f4_t va = *(const f4_t*)(stg + r * WS_SP + cq);
       f4_t vb = *(const f4_t*)(stg + r * WS_SP + cq + 4);
-      if (m < g.M) {
+      if (m < g.M && n0 + cq < g.N) {   // (bf16 C: N % 8 == 0)
         va = epi_vals<EPI>(g, m, n0 + cq, va, ba);
         vb = epi_vals<EPI>(g, m, n0 + cq + 4, vb, bb);
         v4u_t u = {pack2bf(va[0], va[1]), pack2bf(va[2], va[3]), pack2bf(vb[0], vb[1]), pack2bf(vb[2], vb[3])};
@@ -259,6 +305,43 @@ __global__ __launch_bounds__(512) void gemm_bf16_ws_kernel(GemmArgs g, int ntile
       }
     }
   }
+}
+
+template <bool BT, int EPI>
+__global__ __launch_bounds__(512) void gemm_bf16_ws_kernel(GemmArgs g, int ntiles) {
+  g.seed = seed_eff(g.seed);
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[WS_LDS];
+  const int per8 = (ntiles + 7) / 8;
+  const int t = (int)(blockIdx.x % 8) * per8 + (int)(blockIdx.x / 8);
+  if (t >= ntiles) return;
+  const int ntn = g.N / WS_BN;
+  ws_tile<false, BT, EPI>(g, (t / ntn) * WS_BM, (t % ntn) * WS_BN, false, lds);
+}
+
+// Grouped weight gradients dW (+)= dY^T X of every layer in ONE launch on ws tiles: one 256x128 tile per workgroup,
+// block -> tile through block_tile (the host's XCD-aware layout, kernels.xcd_plan) and tile -> group through
+// tile_group; the bias gradient (row sums of dY^T) fused.  Layout-identical table entries to the p3 / p4 grouped
+// kernels (asrx_gemm_group_dev).
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_bf16_wsg_kernel(const GroupEnt* __restrict__ ents,
+                                                            const uint16_t* __restrict__ tile_group,
+                                                            const uint16_t* __restrict__ block_tile, int ntiles,
+                                                            int dbg) {
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[WS_LDS];
+  const int tid = block_tile ? (int)block_tile[blockIdx.x] : (int)blockIdx.x;
+  if (tid >= ntiles) return;
+  const int gi = __builtin_amdgcn_readfirstlane((int)tile_group[tid]);
+  const GroupEnt e = ents[gi];
+  GemmArgs g = {};
+  g.M = e.m; g.N = e.n; g.K = e.k;
+  g.a = e.a; g.lda = e.lda; g.b = e.b; g.ldb = e.ldb; g.c = e.c; g.ldc = e.ldc; g.c_dtype = ASRX_F32;
+  g.batch_inner = 1; g.alpha = 1.f; g.beta = (EPI & E_BETA) ? 1.f : 0.f; g.rowadd_mod = 1;
+  g.splitk = 1; g.k_per_split = e.k; g.cvec = 1;
+  g.rowsum = e.rowsum;
+  g.dbg = dbg & 9;
+  const int t = tid - e.tile_start;
+  const int ntn = (e.n + WS_BN - 1) / WS_BN;
+  ws_tile<true, true, EPI>(g, (t / ntn) * WS_BM, (t % ntn) * WS_BN, e.rowsum != nullptr && (t % ntn) == 0, lds);
 }
 
 // ws instantiations (the N = 512 encoder GEMMs of the training step): x.W^T (+ bias (+ dropout) + fp32 residual)
@@ -269,12 +352,27 @@ __global__ __launch_bounds__(512) void gemm_bf16_ws_kernel(GemmArgs g, int ntile
 
 }  // namespace
 
+namespace asrxg {
+
 bool ws_instantiated(bool bt, int epi) {
 #define ASRX_HAS(E) if (epi == (E)) return true;
   if (!bt) { ASRX_EPIWS_NT(ASRX_HAS) }
   else { ASRX_EPIWS_NN(ASRX_HAS) }
 #undef ASRX_HAS
   return false;
+}
+
+int launch_ws_grouped(const GroupEnt* ents, const uint16_t* tile_group, const uint16_t* block_tile, int ntiles,
+                      int blocks, float beta, int dbg, hipStream_t st) {
+  if (beta == 1.f)
+    hipLaunchKernelGGL((gemm_bf16_wsg_kernel<E_BETA | E_F32>), dim3(blocks), dim3(512), 0, st, ents, tile_group,
+                       block_tile, ntiles, dbg);
+  else if (beta == 0.f)
+    hipLaunchKernelGGL((gemm_bf16_wsg_kernel<E_F32>), dim3(blocks), dim3(512), 0, st, ents, tile_group, block_tile,
+                       ntiles, dbg);
+  else
+    return -1;
+  return 0;
 }
 
 void launch_ws(const GemmArgs& g, bool bt, int epi, int ntiles, hipStream_t st) {

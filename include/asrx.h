@@ -104,7 +104,8 @@ typedef struct asrx_gemm_group_dev {
  * one XCD at the same time lets them share that XCD's L2 (the operand panels of dW = dY^T X are re-read by
  * every tile of the group).  common->tile selects the tile: 3 = the p3 LDS-DMA ring, 256x128 tiles (m x n;
  * fp32 C with 16-byte aligned rows, every group's n % 4 == 0, alpha 1, beta 0 or 1), 4 = the p4 ring, 256x256
- * tiles (same conditions), 128 = register-staged
+ * tiles (same conditions), 5 = the warp-specialised ws kernel, 256x128 tiles (4 MFMA waves + 4 LDS-DMA loader
+ * waves, 3-stage ring; same conditions), 128 = register-staged
  * 128x128 tiles (any alignment-checked table; common->relu carries its "every C row 16-byte aligned" flag).
  * Replaces the weight/bias-gradient mm + sum of autograd for every nn.Linear (layers.py:10-12,36,48,51). */
 int asrx_gemm_grouped_xcd(const asrx_gemm_desc* common, const asrx_gemm_group_dev* groups,

@@ -169,7 +169,7 @@ def test_gemm_fused_rowsum(tile, splitk, kernel_variant):
 
 
 @pytest.mark.parametrize("wkind,xcd", [("reg", False), ("reg", True), ("p3", False), ("p3", True), ("p4", False),
-                                       ("p4", True)])
+                                       ("p4", True), ("ws", False), ("ws", True)])
 @pytest.mark.parametrize("ngroups", [1, 7, 60])
 def test_gemm_grouped_wgrad(ngroups, wkind, xcd, monkeypatch):
     """Grouped weight gradients (asrx_gemm_grouped_xcd): ragged shapes, K not a multiple of 64, fused bias-grad
