@@ -95,6 +95,8 @@ SIGNATURES = {
     "asrx_reduce_rows_grouped": [ctypes.POINTER(RowsumGroup), c_i32, c_vp],
     "asrx_attention_fwd": [ctypes.POINTER(AttnDesc), c_vp],
     "asrx_attn_dropgen": [ctypes.POINTER(AttnDesc), c_vp],
+    "asrx_layernorm_fwd_attn_dropgen": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32,
+                                        ctypes.POINTER(AttnDesc), c_vp],
     "asrx_attention_bwd": [ctypes.POINTER(AttnDesc), c_vp],
     "asrx_attn_delta": [ctypes.POINTER(AttnDesc), c_vp],
     "asrx_softmax_fwd": [c_i32, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i64, c_f32, c_i32, c_i32, c_vp, c_vp,

@@ -170,6 +170,9 @@ GATE_BITS = os.environ.get("ASRX_GATE_BITS", "1") == "1"
 # generating the keep bits on a side stream (overlapping the LN + Q/K/V GEMM) measured SLOWER than generating
 # them in line (18.2 vs 17.75 ms/step: the VALU-heavy generator steals the GEMM's CUs): off by default
 _SIDE_DROPGEN = os.environ.get("ASRX_DROPGEN_SIDE", "0") == "1"
+# the attention keep bits generated inside the preceding LayerNorm's launch (ASRX_LN_DROPGEN=0: by the attention
+# forward's own launch)
+LN_DROPGEN = os.environ.get("ASRX_LN_DROPGEN", "1") == "1"
 
 
 def _side_stream(device):
@@ -241,10 +244,10 @@ def attn_fwd(C, q, k, v, o, B, H, Lq, Lk, dh, strides, scale, spec, prep=None):
     seed = prep["seed"]
     S = {"seed": seed, "spec": spec, "dims": (B, H, Lq, Lk, dh), "strides": strides, "scale": scale}
     if C.cd == torch.bfloat16 and C.attn_impl == "fused" and dh in (32, 64):
-        dm, ready = prep["dropmask"], prep["event"] is not None
-        if ready:
+        dm, ready = prep["dropmask"], prep["event"] is not None or prep.get("ready", False)
+        if prep["event"] is not None:
             torch.cuda.current_stream(q.device).wait_event(prep["event"])
-        else:
+        elif not ready:
             dm = K.dropmask_buffer(B, H, Lq, Lk, dh, C.p, q.device)
         S["dropmask"] = dm
         # training: the O rounding residual keeps the backward's delta exact (see include/asrx.h o_lo)
@@ -304,7 +307,15 @@ def self_attn_fwd(C, x, ln, mha, B, T, H, spec):
     M, d = x.shape
     dh = d // H
     prep = attn_prepare(C, B, H, T, T, dh, x.device)
-    h, mean, rstd = ln_fwd(C, x, ln)
+    dm = (K.dropmask_buffer(B, H, T, T, dh, C.p, x.device)
+          if LN_DROPGEN and prep["dropmask"] is None and C.cd == torch.bfloat16 and C.attn_impl == "fused"
+          and d == 512 and x.dtype == torch.float32 else None)
+    if dm is not None:   # the LayerNorm and the attention's keep bits in one launch (asrx_layernorm_fwd_attn_dropgen)
+        h = _empty(x.shape, C.cd, x)
+        mean, rstd = K.layernorm_fwd_dropgen(x, ln.weight.data, ln.bias.data, h, B, H, T, T, dh, C.p, prep["seed"], dm)
+        prep["dropmask"], prep["ready"] = dm, True
+    else:
+        h, mean, rstd = ln_fwd(C, x, ln)
     qkv = _empty((M, 3 * d), C.cd, x)
     K.linear(h, C.W(mha.wqkv), qkv, bias=mha.bqkv.data)
     o = _empty((M, d), C.cd, x)

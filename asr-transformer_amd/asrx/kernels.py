@@ -441,7 +441,7 @@ def reduce_rows_grouped(items):
         call("asrx_reduce_rows_grouped", arr, len(chunk), stream())
 
 
-LN_BWD_BLOCKS = int(os.environ.get("ASRX_LN_BWD_BLOCKS", "1024"))
+LN_BWD_BLOCKS = int(os.environ.get("ASRX_LN_BWD_BLOCKS", "512"))   # (tools/ln_bench.py: 26.1-26.6 us cold vs 26.7 at 1024)
 
 
 def layernorm_bwd(x, dy, gamma, mean, rstd, dgb, *, dres=None, dx_drop=None, dropout_p=0.0, seed=0, defer=None):
@@ -529,6 +529,23 @@ def attention_dropgen(B, H, Lq, Lk, dh, dropout_p, seed, dropmask):
     d.dropout_p, d.seed = dropout_p, seed & _U64
     d.dropmask = dropmask.data_ptr()
     call("asrx_attn_dropgen", ctypes.byref(d), stream())
+
+
+def layernorm_fwd_dropgen(x, gamma, beta, y, B, H, Lq, Lk, dh, dropout_p, seed, dropmask, eps=1e-5):
+    """layernorm_fwd (x fp32 [rows, 512] -> y bf16) and attention_dropgen in ONE launch (asrx_layernorm_fwd_attn_dropgen):
+    the keep-bit hashing runs beside the HBM-bound LayerNorm.  Returns (mean, rstd)."""
+    _cuda(x, gamma, beta, y, dropmask)
+    rows, d = x.shape
+    mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+    rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
+    a = AttnDesc()
+    a.batch, a.heads, a.lq, a.lk, a.dh = B, H, Lq, Lk, dh
+    a.q = a.k = a.v = dropmask.data_ptr()      # not read; fill_args only checks them
+    a.dropout_p, a.seed = dropout_p, seed & _U64
+    a.dropmask = dropmask.data_ptr()
+    call("asrx_layernorm_fwd_attn_dropgen", x.data_ptr(), y.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+         mean.data_ptr(), rstd.data_ptr(), rows, d, eps, ctypes.byref(a), stream())
+    return mean, rstd
 
 
 def attention_fwd(q, k, v, o, B, H, Lq, Lk, dh, strides, scale, spec, dropout_p=0.0, seed=0, dropmask=None,
@@ -725,12 +742,13 @@ def adam_hyper(hyp, lr, beta1, beta2, step):
     upload(hyp, np.array([lr, 1.0 - beta1 ** step, 1.0 - beta2 ** step], dtype=np.float32))
 
 
-TUNE_KEYS = {"softmax_u": 1, "ln_rw": 2}
+TUNE_KEYS = {"softmax_u": 1, "ln_rw": 2, "ln_pf": 3, "ln_bpc": 4}
 
 
 def set_tuning(name, value):
-    """Process-wide kernel-variant override (asrx_set_tuning): "softmax_u" in (1, 2, 4), "ln_rw" in (1, 2, 4);
-    0 restores the environment / default choice.  Every variant computes the same values."""
+    """Process-wide kernel-variant override (asrx_set_tuning): "softmax_u" in (1, 2, 4), "ln_rw" in (1, 2, 4),
+    "ln_pf" in (1, 2, 4; 8 = the general LayerNorm kernels), "ln_bpc" in 1..16; 0 restores the environment /
+    default choice.  Every variant computes the same values."""
     call("asrx_set_tuning", TUNE_KEYS[name], int(value))
 
 

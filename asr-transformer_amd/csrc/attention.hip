@@ -20,6 +20,7 @@
 
 #include "common.h"
 #include "gemm_common.h"
+#include "ln512.h"
 
 namespace {
 
@@ -507,19 +508,14 @@ ASRX_DEV float xsum4(float v) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-// MODE: 0 = no mask, 1 = causal / key-valid / query-valid vectors (folded into per-key biases and lse),
-// 2 = dense byte mask (generic per-element test).
-// Forward grid (ceil(Lq/256), B*H), 8 waves x 32 queries (two 16-query sub-tiles per wave).
 // Dropout keep bits for the resident kernels, generated once per attention call (the counter-based RNG of
 // common.h, pairs along queries), in two layouts so that each kernel reads whole words in its own lane order:
 //   key-major   kmaj[(bh * nqc + qc) * Lk + key], bit i = keep(query 32 qc + i, key)      (backward)
 //   query-major qmaj[(bh * Lq + q) * nkw + kw],   bit j = keep(q, key 32 kw + j)            (forward)
 // grid (nqc, B*H), 256 threads: thread = key (32 queries -> 16 pair hashes), LDS transpose for qmaj.
-__global__ __launch_bounds__(256) void attn_dropgen_kernel(AttnArgs a, uint32_t* kmaj, uint32_t* qmaj) {
-  a.seed = seed_eff(a.seed);
-  __shared__ uint32_t sw[R_MAXK];
-  const int qc = blockIdx.x, bh = blockIdx.y, tid = threadIdx.x;
-  const int nqc = gridDim.x, nkw = (a.Lk + 31) >> 5, q0 = qc * 32;
+ASRX_DEV void dropgen_block(const AttnArgs& a, int qc, int bh, int nqc, uint32_t* kmaj, uint32_t* qmaj, uint32_t* sw) {
+  const int tid = threadIdx.x;
+  const int nkw = (a.Lk + 31) >> 5, q0 = qc * 32;
   const int key = tid;
   uint32_t word = 0;
   if (key < a.Lk) {
@@ -541,6 +537,32 @@ __global__ __launch_bounds__(256) void attn_dropgen_kernel(AttnArgs a, uint32_t*
     for (int j = 0; j < 32; ++j) qw |= ((sw[32 * kw + j] >> ql) & 1u) << j;
     qmaj[((int64_t)bh * a.Lq + q0 + ql) * nkw + kw] = qw;
   }
+}
+
+__global__ __launch_bounds__(256) void attn_dropgen_kernel(AttnArgs a, uint32_t* kmaj, uint32_t* qmaj) {
+  a.seed = seed_eff(a.seed);
+  __shared__ uint32_t sw[R_MAXK];
+  dropgen_block(a, blockIdx.x, blockIdx.y, gridDim.x, kmaj, qmaj, sw);
+}
+
+// Horizontal fusion of the attention's LayerNorm (d = 512) and its keep bits: blocks [0, nln) run the LayerNorm
+// rows (ln512.h, HBM-bound), blocks [nln, nln + nqc * B * H) the keep-bit generator (VALU-bound), in one launch —
+// the two block types share the CUs, so the hashing runs in the LayerNorm's memory waits instead of a launch of
+// its own (8.5 us x 36 per c3 step).
+struct LnJob {
+  const float* x; bf16_t* y; const float* gamma; const float* beta; float* mean; float* rstd; int64_t rows; float eps;
+};
+__global__ __launch_bounds__(256) void ln_dropgen_kernel(AttnArgs a, uint32_t* kmaj, uint32_t* qmaj, LnJob ln,
+                                                        int nln) {
+  __shared__ uint32_t sw[R_MAXK];
+  if ((int)blockIdx.x < nln) {
+    asrxln::ln_fwd512_rows<1>(ln.x, ln.y, ln.gamma, ln.beta, ln.mean, ln.rstd, ln.rows, ln.eps,
+                              (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), (int64_t)nln * 4);
+    return;
+  }
+  a.seed = seed_eff(a.seed);
+  const int nqc = (a.Lq + 31) / 32, j = (int)blockIdx.x - nln;
+  dropgen_block(a, j % nqc, j / nqc, nqc, kmaj, qmaj, sw);
 }
 
 // MODE: 0 = no mask, 1 = causal / key-valid / query-valid vectors (folded into per-key biases and lse),
@@ -1320,6 +1342,28 @@ extern "C" int asrx_attn_dropgen(const asrx_attn_desc* d, void* stream) {
   uint32_t* kmaj = a.dropmask;
   uint32_t* qmaj = a.dropmask + (int64_t)a.B * a.H * nqc * a.Lk;
   hipLaunchKernelGGL(attn_dropgen_kernel, dim3(nqc, a.B * a.H), dim3(256), 0, (hipStream_t)stream, a, kmaj, qmaj);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
+extern "C" int asrx_layernorm_fwd_attn_dropgen(const float* x, void* y, const float* gamma, const float* beta,
+                                               float* mean, float* rstd, int64_t rows, int32_t d_model, float eps,
+                                               const asrx_attn_desc* d, void* stream) {
+  if (!x || !y || !gamma || !beta || !mean || !rstd || rows <= 0 || d_model != 512) return ASRX_ERR_ARG;
+  if (((uintptr_t)x | (uintptr_t)y) % 16) return ASRX_ERR_ARG;
+  AttnArgs a;
+  int rc = fill_args(d, a);
+  if (rc) return rc;
+  if (!a.dropmask || a.Lk > R_MAXK) return ASRX_ERR_ARG;
+  const int nqc = (a.Lq + 31) / 32;
+  uint32_t* kmaj = a.dropmask;
+  uint32_t* qmaj = a.dropmask + (int64_t)a.B * a.H * nqc * a.Lk;
+  const int nln = (int)std::max<int64_t>(1, std::min<int64_t>((rows + 3) / 4, 1024));
+  const int64_t ndg = a.thr ? (int64_t)nqc * a.B * a.H : 0;
+  if (nln + ndg > 0x7fffffff) return ASRX_ERR_ARG;
+  const LnJob ln{x, (bf16_t*)y, gamma, beta, mean, rstd, rows, eps};
+  hipLaunchKernelGGL(ln_dropgen_kernel, dim3((unsigned)(nln + ndg)), dim3(256), 0, (hipStream_t)stream, a, kmaj, qmaj,
+                     ln, nln);
   ASRX_CHECK_LAUNCH();
   return ASRX_OK;
 }

@@ -125,3 +125,5 @@ static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 // Kernel-variant overrides set by asrx_set_tuning (host globals, defined in frontend.hip; 0 = environment / default)
 extern int g_tune_softmax_u;
 extern int g_tune_ln_rw;
+extern int g_tune_ln_pf;
+extern int g_tune_ln_bpc;

@@ -1160,8 +1160,20 @@ __global__ __launch_bounds__(256) void sum_chunks_bf16_kernel(const bf16_t* __re
 
 int g_tune_softmax_u = 0;
 int g_tune_ln_rw = 0;
+int g_tune_ln_pf = 0;
+int g_tune_ln_bpc = 0;
 
 extern "C" int asrx_set_tuning(int32_t key, int32_t value) {
+  if (key == ASRX_TUNE_LN_PF) {   // 0 = environment / default; 8 = the general kernels
+    if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8) return ASRX_ERR_ARG;
+    g_tune_ln_pf = value;
+    return ASRX_OK;
+  }
+  if (key == ASRX_TUNE_LN_BPC) {
+    if (value < 0 || value > 16) return ASRX_ERR_ARG;
+    g_tune_ln_bpc = value;
+    return ASRX_OK;
+  }
   if (value != 0 && value != 1 && value != 2 && value != 4) return ASRX_ERR_ARG;
   if (key == ASRX_TUNE_SOFTMAX_U) g_tune_softmax_u = value;
   else if (key == ASRX_TUNE_LN_RW) g_tune_ln_rw = value;

@@ -1,11 +1,14 @@
 // LayerNorm forward/backward and deterministic row reductions (HBM-bound kernels).
 // Replaces nn.LayerNorm (model.py:14,16,33,59,61,63,101) = aten::native_layer_norm(+_backward).
 // One wave per row, CH contiguous elements per lane per step (16-B fp32 / 8-B bf16 accesses), NJ steps.
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.h"
+#include "ln512.h"
 
 namespace {
+using namespace asrxln;
 
 template <int CH>
 ASRX_DEV void load_ch(const void* p, int dtype, int64_t off, float* v) {
@@ -175,6 +178,101 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int x_dtype, const void* x,
     part[(int64_t)blockIdx.x * 2 * D + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
 }
 
+template <int PF>
+__global__ __launch_bounds__(256) void ln_fwd512_kernel(const float* __restrict__ x, bf16_t* __restrict__ y,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, float* __restrict__ mean,
+                                                        float* __restrict__ rstd, int64_t rows, float eps) {
+  asrxln::ln_fwd512_rows<PF>(x, y, gamma, beta, mean, rstd, rows, eps, (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6),
+                             (int64_t)gridDim.x * 4);
+}
+
+// Backward, d = 512: as ln_bwd_kernel (dgamma | dbeta partials per block into part[block][2 D]), lanes own 8
+// columns, PF rows of x / dy / dres / stats in flight per wave.  dy bf16 (the compute dtype).
+template <int PF>
+__global__ __launch_bounds__(256) void ln_bwd512_kernel(const float* __restrict__ x, const bf16_t* __restrict__ dy,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ mean,
+                                                        const float* __restrict__ rstd,
+                                                        const float* __restrict__ dres, float* __restrict__ dx_out,
+                                                        bf16_t* __restrict__ dx_drop, uint32_t thr, float dscale,
+                                                        uint64_t seed, float* __restrict__ part, int64_t rows) {
+  seed = seed_eff(seed);
+  constexpr int D = 512;
+  __shared__ float red[4][2 * D];
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const int64_t gw = (int64_t)blockIdx.x * 4 + w;
+  float pg[8], pb[8], ga[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { pg[i] = 0.f; pb[i] = 0.f; }
+  float xv[PF][8], dv[PF][8], rv[PF][8], mu[PF], rsv[PF];
+  auto load = [&](int p, int64_t r) {
+    ld8f(x + r * D + 8 * l, xv[p]);
+    ld8b(dy + r * D + 8 * l, dv[p]);
+    if (dres) ld8f(dres + r * D + 8 * l, rv[p]);
+    mu[p] = mean[r];
+    rsv[p] = rstd[r];
+  };
+#pragma unroll
+  for (int p = 0; p < PF; ++p)
+    if (gw + p * nw < rows) load(p, gw + p * nw);
+  ld8f(gamma + 8 * l, ga);
+  for (int64_t r0 = gw; r0 < rows; r0 += PF * nw) {
+#pragma unroll
+    for (int p = 0; p < PF; ++p) {
+      const int64_t row = r0 + p * nw;
+      if (row >= rows) break;   // wave-uniform
+      float xh[8], g[8], sg = 0.f, sgx = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        xh[i] = (xv[p][i] - mu[p]) * rsv[p];
+        g[i] = dv[p][i] * ga[i];
+        sg += g[i];
+        sgx += g[i] * xh[i];
+        pg[i] += dv[p][i] * xh[i];
+        pb[i] += dv[p][i];
+      }
+      sg = wave_sum(sg) * (1.f / D);
+      sgx = wave_sum(sgx) * (1.f / D);
+      float o[8];
+      const float rs = rsv[p];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = rs * (g[i] - sg - xh[i] * sgx) + (dres ? rv[p][i] : 0.f);
+      const int64_t nxt = row + PF * nw;
+      if (nxt < rows) load(p, nxt);
+      const int64_t off = row * D + 8 * l;
+      st8f(dx_out + off, o);
+      if (dx_drop) {
+        float od[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) od[i] = (thr == 0u || rng_keep(seed, (uint32_t)(off + i), thr)) ? o[i] * dscale : 0.f;
+        st8b(dx_drop + off, od);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    red[w][8 * l + i] = pg[i];
+    red[w][D + 8 * l + i] = pb[i];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 2 * D; c += 256)
+    part[(int64_t)blockIdx.x * 2 * D + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+}
+
+// LN variant selection (asrx_set_tuning ASRX_TUNE_LN_PF / ASRX_LN_PF: rows in flight per wave of the d = 512
+// kernels, 8 (ASRX_LN_PF=0) = the general CH x NJ kernels; ASRX_TUNE_LN_BPC / ASRX_LN_BPC: blocks of 4 waves per
+// CU of the forward)
+int ln_pf() {
+  static const int env = [] { const char* e = getenv("ASRX_LN_PF"); return e ? atoi(e) : 1; }();
+  return g_tune_ln_pf == 8 ? 0 : g_tune_ln_pf > 0 ? g_tune_ln_pf : env;
+}
+int ln_bpc() {
+  static const int env = [] { const char* e = getenv("ASRX_LN_BPC"); return e ? atoi(e) : 4; }();
+  return g_tune_ln_bpc > 0 ? g_tune_ln_bpc : env;
+}
+
 // Column sums: stage 1 (per block partial over a row range), stage 2 (sum of partials in block order).
 __global__ __launch_bounds__(256) void colsum_stage1(int dtype, const void* in, int64_t rows, int cols, int64_t ld,
                                                      float* part, int64_t rows_per_block) {
@@ -295,6 +393,18 @@ extern "C" int asrx_layernorm_fwd(int32_t x_dtype, const void* x, int32_t y_dtyp
   if (!x || !y || !gamma || !beta || !mean || !rstd || rows < 0) return ASRX_ERR_ARG;
   if (rows == 0) return ASRX_OK;
   hipStream_t st = (hipStream_t)stream;
+  const int pf = ln_pf();
+  if (d == 512 && x_dtype == ASRX_F32 && y_dtype == ASRX_BF16 && pf > 0 && ((uintptr_t)x | (uintptr_t)y) % 16 == 0) {
+    const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((rows + 3) / 4, 256 * ln_bpc()));
+#define ASRX_LNF(PF) hipLaunchKernelGGL((ln_fwd512_kernel<PF>), dim3(blocks), dim3(256), 0, st, (const float*)x, \
+                                        (bf16_t*)y, gamma, beta, mean, rstd, rows, eps)
+    if (pf == 1) ASRX_LNF(1);
+    else if (pf == 4) ASRX_LNF(4);
+    else ASRX_LNF(2);
+#undef ASRX_LNF
+    ASRX_CHECK_LAUNCH();
+    return ASRX_OK;
+  }
   bool ok = ln_fwd_launch<1, 1>(x_dtype, x, y_dtype, y, gamma, beta, mean, rstd, rows, d, eps, st) ||
             ln_fwd_launch<2, 1>(x_dtype, x, y_dtype, y, gamma, beta, mean, rstd, rows, d, eps, st) ||
             ln_fwd_launch<4, 1>(x_dtype, x, y_dtype, y, gamma, beta, mean, rstd, rows, d, eps, st) ||
@@ -313,6 +423,21 @@ extern "C" int asrx_layernorm_bwd(int32_t x_dtype, const void* x, int32_t dy_dty
                                   float* part, int32_t nblocks, int64_t rows, int32_t d, void* stream) {
   if (!x || !dy || !gamma || !mean || !rstd || !dx_out || !part || nblocks <= 0 || rows < 0) return ASRX_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
+  const int pf = ln_pf();
+  if (d == 512 && x_dtype == ASRX_F32 && dy_dtype == ASRX_BF16 && pf > 0 && (!dx_drop || drop_dtype == ASRX_BF16) &&
+      ((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx_out | (uintptr_t)dres | (uintptr_t)dx_drop) % 16 == 0) {
+    const uint32_t thr = drop_threshold(dropout_p);
+    const float sc = (dropout_p > 0.f && dropout_p < 1.f) ? 1.f / (1.f - dropout_p) : 1.f;
+#define ASRX_LNB(PF) hipLaunchKernelGGL((ln_bwd512_kernel<PF>), dim3(nblocks), dim3(256), 0, st, (const float*)x, \
+                                        (const bf16_t*)dy, gamma, mean, rstd, dres, dx_out, (bf16_t*)dx_drop, thr, \
+                                        sc, seed, part, rows)
+    if (pf == 1) ASRX_LNB(1);
+    else if (pf == 4) ASRX_LNB(4);
+    else ASRX_LNB(2);
+#undef ASRX_LNB
+    ASRX_CHECK_LAUNCH();
+    return ASRX_OK;
+  }
   bool ok = ln_bwd_launch<1, 1>(x_dtype, x, dy_dtype, dy, gamma, mean, rstd, dres, dx_out, dx_drop, drop_dtype, dropout_p, seed, part, nblocks, rows, d, st) ||
             ln_bwd_launch<2, 1>(x_dtype, x, dy_dtype, dy, gamma, mean, rstd, dres, dx_out, dx_drop, drop_dtype, dropout_p, seed, part, nblocks, rows, d, st) ||
             ln_bwd_launch<4, 1>(x_dtype, x, dy_dtype, dy, gamma, mean, rstd, dres, dx_out, dx_drop, drop_dtype, dropout_p, seed, part, nblocks, rows, d, st) ||

@@ -128,6 +128,8 @@ int asrx_gemm_set_debug(int32_t flags);
  * variant computes the same values; the switch exists so tests and tools can run each one in one process. */
 #define ASRX_TUNE_SOFTMAX_U 1
 #define ASRX_TUNE_LN_RW 2
+#define ASRX_TUNE_LN_PF 3    /* rows in flight per wave of the d = 512 LayerNorm kernels (1, 2, 4; 8 = the general kernels) */
+#define ASRX_TUNE_LN_BPC 4   /* blocks per CU of the d = 512 LayerNorm forward (1..16; 0 = ASRX_LN_BPC) */
 int asrx_set_tuning(int32_t key, int32_t value);
 
 /* ---------------------------------------------------------------------------------------------------
@@ -180,6 +182,12 @@ int asrx_attention_fwd(const asrx_attn_desc* d, void* stream);
 /* Fill d->dropmask with the dropout keep bits of (seed, dropout_p, shapes) — both layouts (see dropmask).  Only
  * the shape/dropout fields of d are read; independent of the Q/K/V data, so it can run ahead on another stream. */
 int asrx_attn_dropgen(const asrx_attn_desc* d, void* stream);
+/* asrx_layernorm_fwd (x fp32 [rows][512], y bf16) and asrx_attn_dropgen(d) in ONE launch (their block types share
+ * the CUs: the VALU-bound hashing runs in the HBM-bound LayerNorm's memory waits).  Replaces the pre-attention
+ * nn.LayerNorm (model.py:20,66) and the keep-bit draw of the attention dropout (layers.py:26). */
+int asrx_layernorm_fwd_attn_dropgen(const float* x, void* y, const float* gamma, const float* beta, float* mean,
+                                    float* rstd, int64_t rows, int32_t d_model, float eps, const asrx_attn_desc* d,
+                                    void* stream);
 int asrx_attention_bwd(const asrx_attn_desc* d, void* stream);
 
 /* ---------------------------------------------------------------------------------------------------

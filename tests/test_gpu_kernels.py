@@ -333,6 +333,28 @@ def test_gemm_ws_rowadd():
     assert (outs["ws"] - outs["p3"]).abs().max() <= 1e-4 * ref.abs().max()
 
 
+@pytest.mark.parametrize("B,H,L,rows_extra", [(64, 8, 249, 0), (64, 8, 64, 0), (3, 2, 37, 0)])
+def test_layernorm_fused_with_keep_bits(B, H, L, rows_extra):
+    """asrx_layernorm_fwd_attn_dropgen: the LayerNorm part equals asrx_layernorm_fwd bit for bit and the keep bits
+    (both layouts) equal asrx_attn_dropgen's, for the encoder (249 keys), decoder (64) and a ragged shape."""
+    d = 512
+    rows = B * L
+    g = torch.Generator(device=dev).manual_seed(rows)
+    x = torch.randn(rows, d, device=dev, generator=g) * 2 + 0.3
+    gam = torch.rand(d, device=dev, generator=g) + 0.5
+    bet = torch.randn(d, device=dev, generator=g)
+    y1 = torch.empty(rows, d, device=dev, dtype=torch.bfloat16)
+    y2 = torch.empty_like(y1)
+    m1, r1 = K().layernorm_fwd(x, gam, bet, y1)
+    dm1 = K().dropmask_buffer(B, H, L, L, 64, 0.1, dev)
+    dm2 = K().dropmask_buffer(B, H, L, L, 64, 0.1, dev)
+    K().attention_dropgen(B, H, L, L, 64, 0.1, 1234567, dm1)
+    m2, r2 = K().layernorm_fwd_dropgen(x, gam, bet, y2, B, H, L, L, 64, 0.1, 1234567, dm2)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2) and torch.equal(m1, m2) and torch.equal(r1, r2)
+    assert torch.equal(dm1, dm2)
+
+
 # ------------------------------------------------------------------------------------------------ LayerNorm
 
 @pytest.fixture
@@ -350,11 +372,15 @@ def tuning():
 
 @pytest.mark.parametrize("d", [64, 128, 256, 512])
 @pytest.mark.parametrize("ydt", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("rw", [0, 1, 4])
-def test_layernorm(d, ydt, rw, tuning):
-    """rw: rows per wave of the forward (0 = default 2; 1 and 4 are the ASRX_LN_RW variants)."""
+@pytest.mark.parametrize("rw,pf", [(0, 0), (1, 8), (4, 8), (2, 8), (0, 1), (0, 4)])
+@pytest.mark.parametrize("rows", [333, 15936])
+def test_layernorm(d, ydt, rw, pf, rows, tuning):
+    """rw: rows per wave of the general forward (0 = default 2; 1 and 4 are the ASRX_LN_RW variants); pf: rows in
+    flight per wave of the d = 512 streaming kernels (0 = default 2; 8 = the general kernels)."""
     tuning("ln_rw", rw)
-    rows = 333
+    tuning("ln_pf", pf)
+    if rows > 1000 and (d != 512 or rw != 0):
+        pytest.skip("the bench-size row count only for the d = 512 streaming variants")
     g = torch.Generator().manual_seed(d)
     x = torch.randn(rows, d, generator=g) * 2 + 0.5
     gam = 1 + 0.1 * torch.randn(d, generator=g)
