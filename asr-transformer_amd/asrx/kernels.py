@@ -109,7 +109,7 @@ def kernel_name(d):
 PROBE = None
 
 # asrx_gemm_desc.kernel: forced kernel family (0 = auto).  ASRX_GEMM_KERNEL picks a process-wide default (A/B).
-KERNEL_CODES = {"auto": 0, "p3": 1, "reg": 3, "ring": 4, "ring128": 5, "p4": 6, "ws": 8}
+KERNEL_CODES = {"auto": 0, "p3": 1, "reg": 3, "ring": 4, "ring128": 5, "p4": 6, "ws": 8, "wsp": 9}
 GEMM_KERNEL = KERNEL_CODES.get(os.environ.get("ASRX_GEMM_KERNEL", "auto"), 0)
 
 

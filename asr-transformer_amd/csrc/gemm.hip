@@ -1441,7 +1441,7 @@ void dispatch_bf16(const GemmArgs& g, bool at, bool bt, bool vec, int batch, hip
 struct GemmPlan {
   int use;     // 1 = p3 (256x128 LDS-DMA ring), 2 = p4 (256x256), 3 = register path 128, 4 = register path 64,
                // 5 = ring 64x64, 6 = ring 128x64 (4-stage LDS-DMA, small grids), 9 = tall-K (conv2 dW),
-               // 11 = ws (warp-specialised 256x128, one-round N = 512 outputs)
+               // 11 = ws (warp-specialised 256x128, one-round N = 512 outputs), 12 = wsp (ws roles, persistent tiles)
   bool vec;    // 16-byte aligned operands
   int epi;     // instantiated epilogue flags (E_GENERIC when the fast-path set has no match)
   int ntiles;  // output tiles of the chosen kernel
@@ -1460,6 +1460,23 @@ bool epi_instantiated(bool at, bool bt, int epi) {
 bool ws_auto() {
   static const bool on = [] { const char* e = getenv("ASRX_WS"); return !(e && e[0] == '0'); }();
   return on;
+}
+// ASRX_WSP=0 keeps the wide projections off the persistent ws kernel (A/B switch; default on)
+// ASRX_WSP: 1 = plan the persistent ws kernel for the wide GEMMs below, 2 = the bias / plain forwards only, 3 = the
+// gated data gradients only, 0 (default) = off.  Each is faster alone (tools/blas_ref.py) and under rocprofv3
+// (12.37 vs 12.47 ms), but the graph-mode bench step measured 12.86-13.05 (1), 12.70-12.74 (2) and 12.98-13.01 (3)
+// against 12.67-12.71 ms (0), alternating on one box: off.
+int wsp_auto_mode() {
+  static const int m = [] { const char* e = getenv("ASRX_WSP"); return e ? atoi(e) : 0; }();
+  return m;
+}
+bool wsp_auto(int epi) {
+  const int m = wsp_auto_mode();
+  return m == 1 || (m == 2 && !(epi & E_GBITS)) || (m == 3 && (epi & E_GBITS));
+}
+int wsp_min_rows() {
+  static const int m = [] { const char* e = getenv("ASRX_WSP_M"); return e ? atoi(e) : 4096; }();
+  return m;
 }
 // ASRX_WS_MIN_K: shortest reduction planned on ws (A/B; every K from 512 up measured faster than p3 at c3)
 int ws_min_k() {
@@ -1484,7 +1501,7 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
     tile = t128 >= 400 ? 128 : 64;
   }
   const int kvar = d->kernel == 1 ? 1 : d->kernel == 3 ? 3 : d->kernel == 4 ? 4 : d->kernel == 5 ? 5 :
-                   d->kernel == 6 ? 6 : d->kernel == 8 ? 8 : 0;
+                   d->kernel == 6 ? 6 : d->kernel == 8 ? 8 : d->kernel == 9 ? 9 : 0;
   const bool dma_ok = pl.vec && d->k % BK == 0 && (!d->a_trans || d->m % 8 == 0) && (!d->b_trans || d->n % 8 == 0) &&
                       d->m >= 8 && d->n >= 8;
   const int nt_p3 = ((d->m + P_BM - 1) / P_BM) * ((d->n + P_BN - 1) / P_BN);
@@ -1558,6 +1575,20 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
     pl.epi = epi;
     pl.ntiles = ((d->m + WS_BM - 1) / WS_BM) * (d->n / WS_BN);
   }
+  // wsp (use 12): the same roles over a persistent tile walk (multi-round grids: the wide projections); kernel
+  // code 9 forces it.  Candidates (tools/blas_ref.py): the Q/K/V projections with bias and the FFN2 data gradients
+  // gated by the FFN1 mask bits, N 1024 .. 4096, >= 4096 rows (encoder Q/K/V 39.3 -> 35.8 us, gated dX 53.8 ->
+  // 48.7-52.6; decoder 15.7 -> 13.4, 19.6 -> 17.0); the FFN1 forward's ReLU / dropout / mask epilogue stays on
+  // p4 / p3 (50.3 vs 59.1 us) and the 12 288-wide cross K/V on p4 (246 vs 313).  Auto only with ASRX_WSP (above).
+  const bool wsp_ok = dma_ok && !d->a_trans && batch == 1 && splitk == 1 && d->n % WS_BN == 0 && d->k >= BK &&
+                      !d->rowsum_a && !d->sc_outer && !d->sc_inner && epi != E_GENERIC &&
+                      wsp_instantiated(d->b_trans, epi);
+  if (wsp_ok && (kvar == 9 || (kvar == 0 && wsp_auto(epi) && d->n >= 1024 && d->n <= 4096 && d->m >= wsp_min_rows() &&
+                                !(epi & E_RELU)))) {
+    pl.use = 12;
+    pl.epi = epi;
+    pl.ntiles = ((d->m + WS_BM - 1) / WS_BM) * (d->n / WS_BN);
+  }
     return pl;
 }
 
@@ -1582,6 +1613,8 @@ extern "C" int asrx_gemm_kernel_name(const asrx_gemm_desc* d, char* buf, int len
   const GemmPlan pl = plan_bf16(d, batch, splitk);
   if (pl.use == 11)
     snprintf(buf, len, "gemm_bf16_ws_kernel<%s, %d>", tf[!!d->b_trans], pl.epi);
+  else if (pl.use == 12)
+    snprintf(buf, len, "gemm_bf16_wsp_kernel<%s, %d>", tf[!!d->b_trans], pl.epi);
   else if (pl.use == 9)
     snprintf(buf, len, "gemm_bf16_tallk_kernel");
   else if (pl.use == 1 || pl.use == 2)
@@ -1627,6 +1660,8 @@ int gemm_bf16_run(const asrx_gemm_desc* d, const GemmArgs& g, const GemmPlan& pl
     }
   } else if (pl.use == 11) {
     launch_ws(g, d->b_trans, epi, pl.ntiles, st);
+  } else if (pl.use == 12) {
+    launch_wsp(g, d->b_trans, epi, pl.ntiles, st);
   } else if (pl.use == 9) {
     hipLaunchKernelGGL(gemm_bf16_tallk_kernel, dim3(splitk), dim3(512), 0, st, g, TallkConv{0, 0, 0, 0, 0, 0});
   } else if (pl.use == 2) {

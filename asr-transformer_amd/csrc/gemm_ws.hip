@@ -344,6 +344,159 @@ __global__ __launch_bounds__(512) void gemm_bf16_wsg_kernel(const GroupEnt* __re
   ws_tile<true, true, EPI>(g, (t / ntn) * WS_BM, (t % ntn) * WS_BN, e.rowsum != nullptr && (t % ntn) == 0, lds);
 }
 
+// ------------------------------------------------------------------------------------------------
+// "wsp": the ws roles over a PERSISTENT tile sequence (multi-round grids: the wide projections, N = 1536 ... 12288).
+// One workgroup per CU walks its tiles (XCD-contiguous ranges, TileSeq::persistent); the loader waves run the
+// 3-stage ring straight across tile boundaries, so the next tile's first stages land while the compute waves run
+// the finished tile's epilogue — from registers (gemm_common.h epilogue_tile: 16-B bf16 stores via permlane16
+// swaps, the fused bias / ReLU / dropout / 1-bit mask / gate epilogues), bias read from global (the compute waves
+// issue no LDS-DMA, so their own loads need no ledger against the ring).
+// ------------------------------------------------------------------------------------------------
+template <bool BT, int EPI>
+__global__ __launch_bounds__(512) void gemm_bf16_wsp_kernel(GemmArgs g, int ntiles) {
+  g.seed = seed_eff(g.seed);
+  // + the current tile's 128 bias values past the ring (each compute wave writes and reads its own 64 columns)
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[WS_LDS + WS_BN * 4];
+  constexpr int TM = 8, TN = 4;
+  const TileSeq tl = TileSeq::persistent(ntiles, 1, blockIdx.x, gridDim.x);
+  if (tl.count == 0) return;
+  const int ntn = (g.N + WS_BN - 1) / WS_BN;
+  const int nk = g.K / BK;
+  const int total = tl.count * nk;
+  const bf16_t* A = (const bf16_t*)g.a;
+  const bf16_t* B = (const bf16_t*)g.b;
+  const int64_t a_bytes = ((int64_t)(g.M - 1) * g.lda + g.K) * 2;
+  const int64_t b_bytes = BT ? ((int64_t)(g.K - 1) * g.ldb + g.N) * 2 : ((int64_t)(g.N - 1) * g.ldb + g.K) * 2;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int l = threadIdx.x & 63;
+  const int lw = wave & 3;
+  const int wm = (lw >> 1) * 128, wn = (lw & 1) * 64;
+  const bool noload = (g.dbg & 8) != 0;
+  if (wave >= 4) {
+    // ---------------- loader waves
+    WsStage<WS_BM, false> sa;
+    WsStage<WS_BN, BT> sb;
+    int ni = 0, iv = 0, ik = 0;   // stages issued; tile / k-step of the next one
+    auto issue = [&](int buf) {
+      if (ik == 0) {
+        const int t = tl(iv);
+        sa.set_tile(lw, (t / ntn) * WS_BM, g.lda);
+        sb.set_tile(lw, (t % ntn) * WS_BN, g.ldb);
+      }
+      if (!noload) {
+        unsigned char* img = lds + buf * WS_STAGE;
+        sa.issue(img, sa.srd(A, g.lda, a_bytes, ik * BK), lw);
+        sb.issue(img + WS_PA, sb.srd(B, g.ldb, b_bytes, ik * BK), lw);
+      }
+      ++ni;
+      if (++ik == nk) { ik = 0; ++iv; }
+    };
+    issue(0);
+    if (total > 1) issue(1);
+    if (total > 2) issue(2);
+    if (noload) wait_vmcnt<0>();
+    else wait_stages<WS_INST, 2>(min(total, 3) - 1);
+    __builtin_amdgcn_s_barrier();
+    int cb = 0;
+    for (int s = 0; s < total; ++s) {
+      if (s + 1 < total) {
+        if (noload) wait_vmcnt<0>();
+        else wait_stages<WS_INST, 1>(ni - (s + 2));
+      }
+      __builtin_amdgcn_s_barrier();
+      if (ni < total) issue(cb);
+      cb = cb == WS_NST - 1 ? 0 : cb + 1;
+    }
+    return;
+  }
+  // ---------------- compute waves
+  f4_t acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+  s8_t fa0[TM], fb0[TN], fa1[TM], fb1[TN];
+  uint32_t S = p4_swz_bytes();
+#define WSP_ROLL_ORDER()                                                                      \
+  do {                                                                                        \
+    __builtin_amdgcn_sched_group_barrier(0x100, TN * (BT ? 2 : 1), 0);                        \
+    _Pragma("unroll") for (int j_ = 0; j_ < TM; ++j_) {                                       \
+      __builtin_amdgcn_sched_group_barrier(0x008, TN, 0);                                     \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                      \
+    }                                                                                         \
+  } while (0)
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int j = 0; j < TM; ++j) fa0[j] = p4_frag<WS_BM, false>(lds, wm + 16 * j, 0, S);
+#pragma unroll
+  for (int i = 0; i < TN; ++i) fb0[i] = p4_frag<WS_BN, BT>(lds + WS_PA, wn + 16 * i, 0, S);
+  uint32_t cbo = 0;
+  int vc = 0, kk = 0;   // tile / k-step of step s
+  for (int s = 0; s < total; ++s) {
+    asm volatile("" : "+s"(cbo));
+    const uint32_t nbo = cbo == (WS_NST - 1) * WS_STAGE ? 0u : cbo + WS_STAGE;
+    const unsigned char* la = lds + cbo;
+    asm volatile("" : "+v"(S));
+#pragma unroll
+    for (int i = 0; i < TN; ++i) fb1[i] = p4_frag<WS_BN, BT>(la + WS_PA, wn + 16 * i, 1, S);
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+#pragma unroll
+      for (int i = 0; i < TN; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[i], fa0[j], acc[i][j], 0, 0, 0);
+      fa1[j] = p4_frag<WS_BM, false>(la, wm + 16 * j, 1, S);
+    }
+    WSP_ROLL_ORDER();
+    // bias of a tile's last K-step: loaded here (its latency hides behind the k-slice), written to LDS after the
+    // barrier (every wave is then past the previous tile's epilogue), read by this tile's epilogue
+    f4_t bias4 = f4_t{0.f, 0.f, 0.f, 0.f};
+    constexpr bool LB = (EPI & E_BIAS) != 0;
+    if constexpr (LB) {
+      if (kk == nk - 1 && l < 16) {
+        const int n = (tl(vc) % ntn) * WS_BN + wn + 4 * l;
+        if (n < g.N) bias4 = *(const f4_t*)(g.bias + n);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if constexpr (LB) {
+      if (kk == nk - 1 && l < 16) *(f4_t*)(lds + WS_LDS + (wn + 4 * l) * 4) = bias4;
+    }
+    const unsigned char* ln = lds + nbo;
+    asm volatile("" : "+v"(S));
+    const bool more = s + 1 < total;
+    if (more) {
+#pragma unroll
+      for (int i = 0; i < TN; ++i) fb0[i] = p4_frag<WS_BN, BT>(ln + WS_PA, wn + 16 * i, 0, S);
+    }
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+#pragma unroll
+      for (int i = 0; i < TN; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[i], fa1[j], acc[i][j], 0, 0, 0);
+      if (more) fa0[j] = p4_frag<WS_BM, false>(ln, wm + 16 * j, 0, S);
+    }
+    WSP_ROLL_ORDER();
+    if (kk == nk - 1) {
+      const int t = tl(vc);
+      const int m0 = (t / ntn) * WS_BM, n0 = (t % ntn) * WS_BN;
+      if (g.dbg & 1) keep_live(acc);
+      else epilogue_tile<EPI, TN, TM, LB>(g, 0, m0, n0, wm, wn, acc, (lds_cfloat_t*)(lds + WS_LDS));
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+    }
+    if (++kk == nk) { kk = 0; ++vc; }
+    cbo = nbo;
+  }
+#undef WSP_ROLL_ORDER
+}
+
+// wsp instantiations: the wide projections of the training step (Q/K/V and cross K/V forwards with bias, the FFN1
+// forward's ReLU / dropout / 1-bit mask epilogue, the FFN2 data gradient gated by those bits) and plain GEMMs
+#define ASRX_EPIWSP_NT(X) X(0) X(E_BIAS) X(E_BIAS | E_RELU) X(E_BIAS | E_RELU | E_DROP) X(E_BIAS | E_RELU | E_MASKOUT) \
+  X(E_BIAS | E_RELU | E_DROP | E_MASKOUT)
+#define ASRX_EPIWSP_NN(X) X(0) X(E_GBITS) X(E_GBITS | E_ALPHA)
+
 // ws instantiations (the N = 512 encoder GEMMs of the training step): x.W^T (+ bias (+ dropout) + fp32 residual)
 // and dY.W (k-strided W)
 #define ASRX_EPIWS_NT(X) X(0) X(E_BIAS) X(E_F32) X(E_BIAS | E_F32) X(E_BIAS | E_RESID | E_F32) \
@@ -373,6 +526,28 @@ int launch_ws_grouped(const GroupEnt* ents, const uint16_t* tile_group, const ui
   else
     return -1;
   return 0;
+}
+
+bool wsp_instantiated(bool bt, int epi) {
+#define ASRX_HAS(E) if (epi == (E)) return true;
+  if (!bt) { ASRX_EPIWSP_NT(ASRX_HAS) }
+  else { ASRX_EPIWSP_NN(ASRX_HAS) }
+#undef ASRX_HAS
+  return false;
+}
+
+void launch_wsp(const GemmArgs& g, bool bt, int epi, int ntiles, hipStream_t st) {
+  const int G = ntiles >= 256 ? 256 : 8 * ((ntiles + 7) / 8);
+  const dim3 grid(G), blk(512);
+#define ASRX_CASE(E) case (E): hipLaunchKernelGGL((gemm_bf16_wsp_kernel<BT_, (E)>), grid, blk, 0, st, g, ntiles); return;
+  if (!bt) {
+    constexpr bool BT_ = false;
+    switch (epi) { ASRX_EPIWSP_NT(ASRX_CASE) default: break; }
+  } else {
+    constexpr bool BT_ = true;
+    switch (epi) { ASRX_EPIWSP_NN(ASRX_CASE) default: break; }
+  }
+#undef ASRX_CASE
 }
 
 void launch_ws(const GemmArgs& g, bool bt, int epi, int ntiles, hipStream_t st) {

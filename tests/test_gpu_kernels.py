@@ -315,6 +315,36 @@ def test_gemm_ws_bias_resid(M, N, Kd, f32, resid, drop):
     assert (outs["ws"] - outs["p3"]).abs().max() <= (1e-4 if f32 else 1e-2) * ref.abs().max()
 
 
+@pytest.mark.parametrize("M,N,Kd", [(15936, 1536, 512), (15936, 2048, 512), (4096, 2048, 512), (1000, 384, 192)])
+def test_gemm_wsp_epilogues(M, N, Kd):
+    """The persistent warp-specialised kernel (kernel code 9, wsp) on the wide projections: bias (Q/K/V), bias + ReLU
+    + dropout + 1-bit mask out (FFN1 forward) and the data gradient gated by those bits with alpha (FFN2 dX) —
+    element for element equal to the p4 kernel (same MFMA accumulation order, same epilogue code) and the plain
+    product against fp64."""
+    g = torch.Generator(device=dev).manual_seed(M + N)
+    x = bf(torch.randn(M, Kd, device=dev, generator=g))
+    w = bf(torch.randn(N, Kd, device=dev, generator=g))
+    bias = torch.randn(N, device=dev, generator=g)
+    assert plan_name(M, N, Kd, bias=True, kernel="wsp").startswith("gemm_bf16_wsp_kernel")
+    outs = {}
+    for kern in ("wsp", "p4"):
+        y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        K().linear(x, w, y, bias=bias, kernel=kern)
+        yr = torch.empty_like(y)
+        bits = torch.zeros(M, N // 32, device=dev, dtype=torch.int32)
+        K().linear(x, w, yr, bias=bias, relu=True, dropout_p=0.1, seed=9, mask_out=bits, ld_mask=N // 32, kernel=kern)
+        dy = bf(torch.randn(M, Kd, device=dev, generator=torch.Generator(device=dev).manual_seed(5)))
+        wt = bf(torch.randn(Kd, N, device=dev, generator=torch.Generator(device=dev).manual_seed(6)))
+        dx = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        K().linear_dgrad(dy, wt, dx, alpha=1 / 0.9, gate=bits, ld_gate=N // 32, gate_bits=True, kernel=kern)
+        outs[kern] = (y, yr, bits, dx)
+    torch.cuda.synchronize()
+    for a, b in zip(outs["wsp"], outs["p4"]):
+        assert torch.equal(a, b)
+    ref = x.double() @ w.double().t() + bias.double()
+    assert relerr(outs["wsp"][0].float(), ref) < 1e-2
+
+
 def test_gemm_ws_rowadd():
     """The ws kernel's row-periodic add (E_ROWADD, the _lin_in GEMM's positional-encoding epilogue: row m takes
     table row m % T'), fp32 out, against fp64 and against p3."""

@@ -160,10 +160,17 @@ def test_gemm_kernel_plan_names_without_gpu():
             d.bias = 4 << 20
         return d
 
-    # wide outputs (>= 400 256x256 tiles) take p4; the Q/K/V projection (378) and the N = 512 outputs p3
+    # wide outputs (>= 400 256x256 tiles) take p4; the Q/K/V projection (378) p3 (the persistent ws kernel, wsp,
+    # only when forced or with ASRX_WSP)
     assert kernel_name(desc(15936, 1536, 512, bias=True)) == "gemm_bf16_p3_kernel<false, false, 1>"
-    assert kernel_name(desc(15936, 2048, 512, bias=True)) == "gemm_bf16_p4_kernel<false, false, 1>"
+    forced = desc(15936, 1536, 512, bias=True)
+    forced.kernel = 9
+    assert kernel_name(forced) == "gemm_bf16_wsp_kernel<false, 1>"
     assert kernel_name(desc(15936, 2048, 512, bt=1)) == "gemm_bf16_p4_kernel<false, true, 0>"
+    ffn1 = desc(15936, 2048, 512, bias=True)
+    ffn1.relu = 1
+    assert kernel_name(ffn1) == "gemm_bf16_p4_kernel<false, false, 3>"
+    assert kernel_name(desc(15936, 12288, 512, bias=True)) == "gemm_bf16_p4_kernel<false, false, 1>"
     # the plain 512-wide data gradients with K >= 1536 take the warp-specialised ws kernel, shorter ones stay on p3
     assert kernel_name(desc(15936, 512, 2048, bt=1)) == "gemm_bf16_ws_kernel<true, 0>"
     assert kernel_name(desc(15936, 512, 1536, bt=1)) == "gemm_bf16_ws_kernel<true, 0>"
@@ -185,7 +192,7 @@ def test_gemm_kernel_plan_names_without_gpu():
         d7.kernel = code
         assert kernel_name(d7) == "gemm_bf16_ws_kernel<true, 0>"
     forced = desc(15936, 1536, 512)
-    forced.kernel = 3                 # asrx_gemm_desc.kernel: register-staged family
+    forced.kernel = 3  # noqa                 # asrx_gemm_desc.kernel: register-staged family
     assert kernel_name(forced).startswith("gemm_bf16_kernel<128, 128, false, false, true>")
 
 

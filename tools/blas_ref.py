@@ -34,6 +34,9 @@ SHAPES = [
     # gradient gated by those bits (alpha = 1/0.9)
     ("ffn1 fwd epi", "fwdepi", 15936, 2048, 512),
     ("ffn2 dgrad gated", "dgradg", 15936, 512, 2048),
+    ("dec ffn1 fwd epi", "fwdepi", 4096, 2048, 512),
+    ("dec ffn2 dgrad gated", "dgradg", 4096, 512, 2048),
+    ("dec qkv fwd", "fwd", 4096, 1536, 512),
     # the step's plain data gradients (out 512 wide; dgrad kind: y[M, Kd] = dy[M, N] . w[N, Kd])
     ("enc qkv dg512", "dgrad", 15936, 1536, 512),
     ("enc ffn1 dg512", "dgrad", 15936, 2048, 512),
