@@ -569,7 +569,9 @@ __global__ __launch_bounds__(256) void ln_dropgen_kernel(AttnArgs a, uint32_t* k
 // 2 = dense byte mask (generic per-element test).
 // Forward grid (ceil(Lq/256), B*H), 8 waves x 32 queries (two 16-query sub-tiles per wave).  Dropout factors
 // come from the query-major keep bits (a 4-bit nibble per (sub-tile, 16-key half) -> one LDS table read).
-template <int MODE>
+// W8: the keep words of a query are 8 (225 <= Lk <= 256, the c3 encoder): loaded as two 16-B vectors per query
+// (a template parameter, not a branch: every prefetch load below is unconditional, see the backward's note)
+template <int MODE, bool W8 = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void attn_fwd_res_kernel(AttnArgs a, const uint32_t* qmaj) {
   a.seed = seed_eff(a.seed);
   __shared__ __attribute__((aligned(1024))) bf16_t sk[R_MAXK * 64];
@@ -608,6 +610,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
   }
   s8_t qf[2][2];
   uint32_t dw[2][8];   // query-major keep words of this lane's two queries (one per 32-key tile)
+  s8_t dwv[2][2];      // W8: the same words as two raw 16-B loads per query
 #pragma unroll
   for (int qs = 0; qs < 2; ++qs) {
     const int qc = min(qw0 + 16 * qs + li, a.Lq - 1);
@@ -619,8 +622,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
   for (int qs = 0; qs < 2; ++qs) {
     const int qc = min(qw0 + 16 * qs + li, a.Lq - 1);
     const uint32_t* dp = qmaj ? qmaj + ((int64_t)bh * a.Lq + qc) * nkw : (const uint32_t*)a.q;
+    if constexpr (W8) {   // (the caller launches W8 only with qmaj set, nkw == 8); unpacked after the wait below
 #pragma unroll
-    for (int kt = 0; kt < 8; ++kt) dw[qs][kt] = ld32_asm(dp + (qmaj ? min(kt, nkw - 1) : 0));
+      for (int hlf = 0; hlf < 2; ++hlf) dwv[qs][hlf] = ld128_asm(dp + 4 * hlf);
+    } else {
+#pragma unroll
+      for (int kt = 0; kt < 8; ++kt) dw[qs][kt] = ld32_asm(dp + (qmaj ? min(kt, nkw - 1) : 0));
+    }
   }
   {
     const asrxg::v4i_t ksrd = asrxg::make_srd(Kb, ((int64_t)(a.Lk - 1) * a.kr + 64) * 2);
@@ -640,8 +648,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
   for (int qs = 0; qs < 2; ++qs) {
     pin(qf[qs][0]);
     pin(qf[qs][1]);
+    if constexpr (W8) {   // (a use of an asm-loaded register before the wait above would read it in flight)
 #pragma unroll
-    for (int kt = 0; kt < 8; ++kt) pin(dw[qs][kt]);
+      for (int hlf = 0; hlf < 2; ++hlf) {
+        pin(dwv[qs][hlf]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          dw[qs][4 * hlf + e] = (uint32_t)(uint16_t)dwv[qs][hlf][2 * e] |
+                                ((uint32_t)(uint16_t)dwv[qs][hlf][2 * e + 1] << 16);
+      }
+    } else {
+#pragma unroll
+      for (int kt = 0; kt < 8; ++kt) pin(dw[qs][kt]);
+    }
     if (!qmaj) {
 #pragma unroll
       for (int kt = 0; kt < 8; ++kt) dw[qs][kt] = 0xffffffffu;
@@ -1387,7 +1406,10 @@ extern "C" int asrx_attention_fwd(const asrx_attn_desc* d, void* stream) {
     }
     // 8 waves always: idle query waves still help stage K/V, then leave
     dim3 grid((a.Lq + 255) / 256, a.B * a.H);
-    if (a.mode == 0) hipLaunchKernelGGL(attn_fwd_res_kernel<0>, grid, dim3(512), 0, st, a, qmaj);
+    static const bool w8ok = [] { const char* e = getenv("ASRX_ATTN_W8"); return !(e && e[0] == '0'); }();
+    const bool w8 = w8ok && qmaj && ((a.Lk + 31) >> 5) == 8 && ((uintptr_t)qmaj % 16) == 0;
+    if (a.mode == 0 && w8) hipLaunchKernelGGL((attn_fwd_res_kernel<0, true>), grid, dim3(512), 0, st, a, qmaj);
+    else if (a.mode == 0) hipLaunchKernelGGL(attn_fwd_res_kernel<0>, grid, dim3(512), 0, st, a, qmaj);
     else if (a.mode == 1) hipLaunchKernelGGL(attn_fwd_res_kernel<1>, grid, dim3(512), 0, st, a, qmaj);
     else hipLaunchKernelGGL(attn_fwd_res_kernel<2>, grid, dim3(512), 0, st, a, qmaj);
     ASRX_CHECK_LAUNCH();
