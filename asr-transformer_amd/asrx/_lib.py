@@ -118,6 +118,7 @@ SIGNATURES = {
     "asrx_embed_bwd": [c_vp, c_i64, c_i32, c_vp, c_i32, c_i32, c_i32, c_f32, c_u64, c_vp, c_vp],
     "asrx_cross_entropy": [c_vp, c_i64, c_i32, c_i64, c_vp, c_i64, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp],
     "asrx_cast": [c_i32, c_vp, c_i32, c_vp, c_i64, c_vp],
+    "asrx_ewise": [c_i32, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp, c_i64, c_f32, c_u64, c_vp],
     "asrx_sum_chunks_bf16": [c_vp, c_i32, c_i64, c_vp, c_vp],
     "asrx_greedy_argmax": [c_vp, c_i64, c_i32, c_i64, c_vp, c_i64, c_vp, c_vp],
     "asrx_spectrogram": [c_vp, c_i64, c_i64, c_i64, c_vp, c_i32, c_i32, c_i32, c_i32, ctypes.c_float, c_vp, c_i64,

@@ -210,8 +210,8 @@ def ln_bwd(C, x, dy, ln, mean, rstd, dres=None, drop_out=None, drop_seed=0, drop
                          seed=drop_seed, defer=C.lnq if split is None else None)
     if split is not None:
         d = split[0].numel()
-        split[0].add_(buf[:d].view_as(split[0]))
-        split[1].add_(buf[d:].view_as(split[1]))
+        K.ewise(K.EW_ADD, split[0], split[0], b=buf[:d])
+        K.ewise(K.EW_ADD, split[1], split[1], b=buf[d:])
     return dx
 
 

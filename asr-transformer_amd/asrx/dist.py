@@ -14,6 +14,7 @@ The reference has no multi-device code; the step semantics it 
 per batch — DP averages per-shard mean losses, which equals the global mean for equal token counts per shard.
 """
 import os
+from contextlib import nullcontext as _nullctx
 
 import torch
 import torch.distributed as dist
@@ -87,26 +88,40 @@ class GradAllReduce:
         else:
             self._works.append(dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
 
+    def _side(self, device):
+        """The bf16 wire's own stream (device tensors only): its cast, all-to-all wait, chunk sum and all-gather
+        issue there, so the compute stream does not wait for the all-to-all between backward segments."""
+        if device.type != "cuda":
+            return None
+        if getattr(self, "_side_stream", None) is None:
+            self._side_stream = torch.cuda.Stream(device=device)
+        return self._side_stream
+
     def _issue_bf16(self, view):
         """Reduce-scatter by all-to-all on bf16 chunks, fp32 sum of the W copies, all-gather of the bf16 sums.
-        The all-to-all must finish before the sum: its wait is a stream dependency (no host sync), on the stream
-        the caller issues from (the Trainer's compute stream, between captured backward segments)."""
+        On a side stream that first waits for the compute stream (the released gradients are final there): the
+        all-to-all's wait and the sum are dependencies of that stream only, and finish() joins the compute stream
+        to the all-gather before the cast back."""
         W = dist.get_world_size(self.group)
         n = view.numel()
         c = -(-n // W)
-        send = torch.empty(W * c, dtype=torch.bfloat16, device=view.device)   # the padding past n is summed
-        _cast(view, send[:n])                                                   # but never copied back
-        recv = torch.empty_like(send)
-        dist.all_to_all_single(recv, send, group=self.group, async_op=True).wait()
-        mine = torch.empty(c, dtype=torch.bfloat16, device=view.device)
-        if self.chunk_sum is not None:
-            self.chunk_sum(recv, W, c, mine)
-        else:
-            from . import kernels as K
-            K.sum_chunks_bf16(recv, W, c, mine)
-        full = torch.empty(W * c, dtype=torch.bfloat16, device=view.device)
-        work = dist.all_gather_into_tensor(full, mine, group=self.group, async_op=True)
-        self._post.append((view, full, work))
+        side = self._side(view.device)
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream(view.device))
+        with torch.cuda.stream(side) if side is not None else _nullctx():
+            send = torch.empty(W * c, dtype=torch.bfloat16, device=view.device)   # the padding past n is summed
+            _cast(view, send[:n])                                                   # but never copied back
+            recv = torch.empty_like(send)
+            dist.all_to_all_single(recv, send, group=self.group, async_op=True).wait()
+            mine = torch.empty(c, dtype=torch.bfloat16, device=view.device)
+            if self.chunk_sum is not None:
+                self.chunk_sum(recv, W, c, mine)
+            else:
+                from . import kernels as K
+                K.sum_chunks_bf16(recv, W, c, mine)
+            full = torch.empty(W * c, dtype=torch.bfloat16, device=view.device)
+            work = dist.all_gather_into_tensor(full, mine, group=self.group, async_op=True)
+        self._post.append((view, full, work, (send, recv, mine)))
 
     def ready(self, start, end):
         """Gradients in flat[start:end] are final: start their all-reduce now (in buckets)."""
@@ -133,7 +148,7 @@ class GradAllReduce:
                 self._issue(v)
         for w in self._works:
             w.wait()
-        for view, full, work in self._post:
+        for view, full, work, _bufs in self._post:   # (the side stream's buffers live until here)
             work.wait()
             _cast(full[:view.numel()], view)
         self._works = []

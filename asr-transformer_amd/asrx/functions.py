@@ -407,7 +407,7 @@ class _FrontEndFn(torch.autograd.Function):
         buf = g.permute(0, 3, 2, 1).to(C.cd).contiguous()
         B, F, T, F1, T1, F2, T2 = S["dims"]
         dy2 = buf.view(B * T2, F2 * 64)
-        dy2 = torch.where(S["feats"] > 0, dy2, torch.zeros((), dtype=dy2.dtype, device=dy2.device))
+        K.ewise(K.EW_RELU_GRAD, dy2, dy2, b=S["feats"])   # the conv2 ReLU gate (model.py:170), in place
         Bk.frontend_bwd(C, S, dy2, ctx.fe[0], ctx.fe[2])
         return (None,) * (3 + len(_params(ctx.fe)))
 
@@ -662,13 +662,12 @@ class _MHAFn(torch.autograd.Function):
         B, Lq, Lk, d = S["dims"]
         dev = S["xc"].device
         # dropout bwd of the output (same RNG stream as the forward epilogue)
-        g2 = g.reshape(B * Lq, d).float().contiguous()
+        g2 = g.reshape(B * Lq, d).contiguous()
         dy_c = torch.empty(B * Lq, d, dtype=C.cd, device=dev)
-        if C.p > 0:
-            keep = K.dropout_mask(B * Lq * d, C.p, S["sd"], dev).view(B * Lq, d)
-            dy_c.copy_(g2 * keep / (1.0 - C.p))
+        if C.p > 0:   # the forward epilogue's element mask (same seed), scaled, cast to the compute dtype
+            K.ewise(K.EW_DROPOUT, g2, dy_c, p=C.p, seed=S["sd"])
         else:
-            dy_c.copy_(g2)
+            K.cast(g2, dy_c)
         do = torch.empty(B * Lq, d, dtype=C.cd, device=dev)
         K.linear_dgrad(dy_c, C.W(m._out_linear.weight), do)
         K.linear_wgrad(dy_c, S["o"], C.G(m._out_linear.weight), bias_grad=C.G(m._out_linear.bias))
@@ -690,10 +689,19 @@ class _MHAFn(torch.autograd.Function):
         K.linear_dgrad(dkv, Wkv, dk_in)
         K.linear_wgrad(dkv, S["kc"], gWkv, bias_grad=gbkv)
         if S["self_attn"]:
-            dx.add_(dk_in)
-            return (None, None, dx.view(B, Lq, d).to(S["xdtype"]), None, None) + (None,) * len(_params(m))
-        return (None, None, dx.view(B, Lq, d).to(S["xdtype"]), dk_in.view(B, Lk, d).to(S["kdtype"]), None) + \
-            (None,) * len(_params(m))
+            K.ewise(K.EW_ADD, dx, dx, b=dk_in)
+            return (None, None, _as_dtype(dx.view(B, Lq, d), S["xdtype"]), None, None) + (None,) * len(_params(m))
+        return (None, None, _as_dtype(dx.view(B, Lq, d), S["xdtype"]), _as_dtype(dk_in.view(B, Lk, d), S["kdtype"]),
+                None) + (None,) * len(_params(m))
+
+
+def _as_dtype(t, dtype):
+    """t in `dtype` (the caller's input dtype): the native cast kernel when it differs."""
+    if t.dtype == dtype:
+        return t
+    out = torch.empty(t.shape, dtype=dtype, device=t.device)
+    K.cast(t.contiguous(), out)
+    return out
 
 
 def mha(m, x, enc_x=None, attention_mask=None):

@@ -109,7 +109,7 @@ def kernel_name(d):
 PROBE = None
 
 # asrx_gemm_desc.kernel: forced kernel family (0 = auto).  ASRX_GEMM_KERNEL picks a process-wide default (A/B).
-KERNEL_CODES = {"auto": 0, "p3": 1, "reg": 3, "ring": 4, "ring128": 5, "p4": 6, "ws": 8, "wsp": 9}
+KERNEL_CODES = {"auto": 0, "p3": 1, "reg": 3, "ring": 4, "ring128": 5, "p4": 6, "ws": 8, "wsp": 9, "ws64": 10}
 GEMM_KERNEL = KERNEL_CODES.get(os.environ.get("ASRX_GEMM_KERNEL", "auto"), 0)
 
 
@@ -513,11 +513,19 @@ def _attn_desc(q, k, v, o, B, H, Lq, Lk, dh, strides, scale, spec, dropout_p, se
     return d
 
 
+def qmaj_stride(Lk):
+    """Row stride (32-bit words) of the query-major keep bits: ceil(Lk / 32) up to 256 keys, rounded up to a
+    multiple of 4 past that (the streamed forward moves 4 words per query and 128-key chunk)."""
+    nkw = (Lk + 31) // 32
+    return nkw if Lk <= 256 else (nkw + 3) // 4 * 4
+
+
 def dropmask_buffer(B, H, Lq, Lk, dh, dropout_p, device):
-    """Keep-bit buffer the resident-K/V attention forward fills for its backward (None when unused)."""
-    if dropout_p <= 0.0 or dh != 64 or Lk > 256:
+    """Keep-bit buffer the fused attention forward fills for its backward (None when unused): key-major words
+    [B*H][ceil(Lq/32)][Lk], then query-major words [B*H][Lq][qmaj_stride(Lk)]."""
+    if dropout_p <= 0.0 or dh != 64:
         return None
-    return torch.empty(B * H * (((Lq + 31) // 32) * Lk + Lq * ((Lk + 31) // 32)), device=device, dtype=torch.int32)
+    return torch.empty(B * H * (((Lq + 31) // 32) * Lk + Lq * qmaj_stride(Lk)), device=device, dtype=torch.int32)
 
 
 def attention_dropgen(B, H, Lq, Lk, dh, dropout_p, seed, dropmask):
@@ -604,6 +612,20 @@ def cast(src, dst):
     _cuda(src, dst)
     assert src.numel() == dst.numel()
     call("asrx_cast", code(src), src.data_ptr(), code(dst), dst.data_ptr(), src.numel(), stream())
+
+
+EW_RELU_GRAD, EW_DROPOUT, EW_ADD = 0, 1, 2
+
+
+def ewise(op, a, out, b=None, p=0.0, seed=0):
+    """out = op(a, b) elementwise over contiguous tensors of equal size (asrx_ewise; fp32 / bf16, may alias):
+    EW_RELU_GRAD (b > 0 ? a : 0), EW_DROPOUT (keep(seed, i) ? a / (1 - p) : 0), EW_ADD (a + b)."""
+    _cuda(a, b, out)
+    n = a.numel()
+    assert out.numel() == n and (b is None or b.numel() == n)
+    assert a.is_contiguous() and out.is_contiguous() and (b is None or b.is_contiguous())
+    call("asrx_ewise", op, code(a), a.data_ptr(), code(b) if b is not None else 0, _p(b), code(out), out.data_ptr(),
+         n, float(p), seed & _U64, stream())
 
 
 def greedy_argmax(logits, V, tok_col, cur=None):

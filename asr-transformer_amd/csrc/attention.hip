@@ -508,15 +508,23 @@ ASRX_DEV float xsum4(float v) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-// Dropout keep bits for the resident kernels, generated once per attention call (the counter-based RNG of
-// common.h, pairs along queries), in two layouts so that each kernel reads whole words in its own lane order:
-//   key-major   kmaj[(bh * nqc + qc) * Lk + key], bit i = keep(query 32 qc + i, key)      (backward)
-//   query-major qmaj[(bh * Lq + q) * nkw + kw],   bit j = keep(q, key 32 kw + j)            (forward)
-// grid (nqc, B*H), 256 threads: thread = key (32 queries -> 16 pair hashes), LDS transpose for qmaj.
-ASRX_DEV void dropgen_block(const AttnArgs& a, int qc, int bh, int nqc, uint32_t* kmaj, uint32_t* qmaj, uint32_t* sw) {
+// Dropout keep bits, generated once per attention call (the counter-based RNG of common.h, pairs along queries), in
+// two layouts so that each kernel reads whole words in its own lane order:
+//   key-major   kmaj[(bh * nqc + qc) * Lk + key],       bit i = keep(query 32 qc + i, key)      (backward)
+//   query-major qmaj[(bh * Lq + q) * qmaj_stride + kw],  bit j = keep(q, key 32 kw + j)           (forward)
+// qmaj_stride = ceil(Lk / 32) for Lk <= 256 (the resident kernels), rounded up to a multiple of 4 past that (the
+// streamed forward moves a 128-key chunk's 4 words per query by one LDS-DMA dword each).
+// grid (nqc, B*H, ceil(Lk / 256)), 256 threads: thread = key (32 queries -> 16 pair hashes), LDS transpose for qmaj.
+__host__ __device__ inline int qmaj_stride(int lk) {
+  const int nkw = (lk + 31) >> 5;
+  return lk <= R_MAXK ? nkw : (nkw + 3) & ~3;
+}
+
+ASRX_DEV void dropgen_block(const AttnArgs& a, int qc, int bh, int kblk, int nqc, uint32_t* kmaj, uint32_t* qmaj,
+                            uint32_t* sw) {
   const int tid = threadIdx.x;
-  const int nkw = (a.Lk + 31) >> 5, q0 = qc * 32;
-  const int key = tid;
+  const int q0 = qc * 32;
+  const int key = kblk * R_MAXK + tid;
   uint32_t word = 0;
   if (key < a.Lk) {
     const uint32_t lqh = (uint32_t)((a.Lq + 1) >> 1);
@@ -528,27 +536,28 @@ ASRX_DEV void dropgen_block(const AttnArgs& a, int qc, int bh, int nqc, uint32_t
     }
     kmaj[((int64_t)bh * nqc + qc) * a.Lk + key] = word;
   }
-  if (key < R_MAXK) sw[key] = key < a.Lk ? word : 0u;
+  sw[tid] = key < a.Lk ? word : 0u;
   __syncthreads();
-  const int ql = tid & 31, kw = tid >> 5;
-  if (kw < nkw && q0 + ql < a.Lq) {
+  const int ql = tid & 31, kw = kblk * (R_MAXK / 32) + (tid >> 5);
+  const int qst = qmaj_stride(a.Lk);
+  if (kw < qst && q0 + ql < a.Lq) {   // (words past ceil(Lk / 32): the padding, zero)
     uint32_t qw = 0;
 #pragma unroll 8
-    for (int j = 0; j < 32; ++j) qw |= ((sw[32 * kw + j] >> ql) & 1u) << j;
-    qmaj[((int64_t)bh * a.Lq + q0 + ql) * nkw + kw] = qw;
+    for (int j = 0; j < 32; ++j) qw |= ((sw[32 * (tid >> 5) + j] >> ql) & 1u) << j;
+    qmaj[((int64_t)bh * a.Lq + q0 + ql) * qst + kw] = qw;
   }
 }
 
 __global__ __launch_bounds__(256) void attn_dropgen_kernel(AttnArgs a, uint32_t* kmaj, uint32_t* qmaj) {
   a.seed = seed_eff(a.seed);
   __shared__ uint32_t sw[R_MAXK];
-  dropgen_block(a, blockIdx.x, blockIdx.y, gridDim.x, kmaj, qmaj, sw);
+  dropgen_block(a, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, kmaj, qmaj, sw);
 }
 
 // Horizontal fusion of the attention's LayerNorm (d = 512) and its keep bits: blocks [0, nln) run the LayerNorm
-// rows (ln512.h, HBM-bound), blocks [nln, nln + nqc * B * H) the keep-bit generator (VALU-bound), in one launch —
-// the two block types share the CUs, so the hashing runs in the LayerNorm's memory waits instead of a launch of
-// its own (8.5 us x 36 per c3 step).
+// rows (ln512.h, HBM-bound), blocks [nln, nln + nqc * B * H * nkb) the keep-bit generator (VALU-bound), in one
+// launch — the two block types share the CUs, so the hashing runs in the LayerNorm's memory waits instead of a
+// launch of its own (8.5 us x 36 per c3 step).
 struct LnJob {
   const float* x; bf16_t* y; const float* gamma; const float* beta; float* mean; float* rstd; int64_t rows; float eps;
 };
@@ -561,8 +570,8 @@ __global__ __launch_bounds__(256) void ln_dropgen_kernel(AttnArgs a, uint32_t* k
     return;
   }
   a.seed = seed_eff(a.seed);
-  const int nqc = (a.Lq + 31) / 32, j = (int)blockIdx.x - nln;
-  dropgen_block(a, j % nqc, j / nqc, nqc, kmaj, qmaj, sw);
+  const int nqc = (a.Lq + 31) / 32, nkb = (a.Lk + R_MAXK - 1) / R_MAXK, j = (int)blockIdx.x - nln;
+  dropgen_block(a, (j / nkb) % nqc, j / (nkb * nqc), j % nkb, nqc, kmaj, qmaj, sw);
 }
 
 // MODE: 0 = no mask, 1 = causal / key-valid / query-valid vectors (folded into per-key biases and lse),
@@ -796,21 +805,55 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
   }
 }
 
-// Long key ranges without mask or dropout (Lk > 256, eval / inference: the c5 encoder self-attention at T' = 999 and
-// the decoder's cross-attention over it; training keeps attn_fwd_kernel): the resident kernel's 8 waves x 32
-// queries and key-tile body, with K/V streamed through LDS in 128-key chunks, double-buffered — chunk c + 2 is
-// issued by LDS-DMA as soon as every wave has finished chunk c, and waited for (counted vmcnt + barrier) just
-// before chunk c + 1 is used.  Keys past Lk read as zero rows (descriptor range) and get a -inf score.
+// One 4-byte-per-lane LDS-DMA (buffer_load_dword ... lds: lane l's dword lands at M0 + 4 l), as inline asm like
+// asrxg::dma16_asm (counted by the kernel's own vmcnt waits).
+ASRX_DEV void dma4_asm(const void* lds_dst, asrxg::v4i_t srd, uint32_t voff) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)lds_dst);
+  asrxg::v4i_t d;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) d[i] = __builtin_amdgcn_readfirstlane(srd[i]);
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, 0 offen lds" ::"s"(m0), "v"(voff), "s"(d)
+               : "memory", "m0");
+}
+
+// Long key ranges (Lk > 256, dh = 64: the c5 encoder self-attention at T' = 999 and the decoder's cross-attention
+// over it), training and inference: the resident kernel's 8 waves x 32 queries and key-tile body, with K/V streamed
+// through LDS in 128-key chunks, double-buffered — chunk c + 2 is issued by LDS-DMA as soon as every wave has
+// finished chunk c, and waited for (counted vmcnt + barrier) just before chunk c + 1 is used.  Keys past Lk read as
+// zero rows (descriptor range) and get a -inf score.  The same LDS-DMA pass moves each chunk's
+//   DROP: query-major keep words (4 per query and chunk, qmaj_stride layout) into skw — dropout is a bitwise AND
+//         of the packed bf16 probabilities with a nibble mask table, 1/(1-p) folded into the final 1 / rowsum;
+//   MODE 1: key-validity bytes into skv (causal: tiles wholly above the wave's last query are skipped, the
+//         diagonal tiles compare); query validity (+inf lse, zero output) is loaded once.
+// (Dense byte masks, MODE 2, over > 256 keys stay on the tiled kernels: a per-element mask load inside this
+// unrolled tile body was miscompiled — its -inf select dropped, then garbage once written branch-free.)
+// The running max is over raw scores (scale > 0): one fma per score applies the scale and the max together.
 constexpr int S_CK = 128;
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void attn_fwd_stream_kernel(AttnArgs a) {
+template <int MODE, bool DROP>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
+void attn_fwd_stream_kernel(AttnArgs a, const uint32_t* qmaj) {
+  static_assert(MODE == 0 || MODE == 1, "streamed forward: no mask or the structured mask");
   __shared__ __attribute__((aligned(1024))) bf16_t sk[2 * S_CK * 64];
   __shared__ __attribute__((aligned(1024))) bf16_t sv[2 * S_CK * 64];
+  __shared__ __attribute__((aligned(16))) uint32_t skw[DROP ? 2 * 8 * 32 * 4 : 4];   // [buf][wave][query][4 words]
+  __shared__ __attribute__((aligned(16))) uint8_t skv[MODE == 1 ? 2 * 256 : 16];       // [buf][key of the chunk]
+  __shared__ __attribute__((aligned(16))) uint2 smask[16];   // keep nibble -> AND masks of two bf16 pairs
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, li = l & 15;
   const int nch = (a.Lk + S_CK - 1) / S_CK;
   const bf16_t* Kb = a.k + b * a.kb + h * 64;
   const bf16_t* Vb = a.v + b * a.vb + h * 64;
   const int qw0 = (blockIdx.x * 8 + w) * 32;
+  // ---- prologue loads: [MODE 1: query validity bytes], Q fragments, then chunks 0 and 1
+  uint32_t qval[2] = {1u, 1u};
+  if (MODE == 1) {
+#pragma unroll
+    for (int qs = 0; qs < 2; ++qs) {
+      const int qc = min(qw0 + 16 * qs + li, a.Lq - 1);
+      qval[qs] = ldu8_asm(a.qvalid ? a.qvalid + b * a.validb + qc : (const uint8_t*)a.q);
+    }
+  }
   s8_t qf[2][2];
 #pragma unroll
   for (int qs = 0; qs < 2; ++qs) {
@@ -822,19 +865,37 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
   const asrxg::v4i_t ksrd = asrxg::make_srd(Kb, ((int64_t)(a.Lk - 1) * a.kr + 64) * 2);
   const asrxg::v4i_t vsrd = asrxg::make_srd(Vb, ((int64_t)(a.Lk - 1) * a.vr + 64) * 2);
   const int rl = l >> 3, sl = l & 7;
+  const int qst = qmaj_stride(a.Lk);
+  asrxg::v4i_t wsrd = ksrd, msrd = ksrd;
+  uint32_t wvo[2] = {0u, 0u};
+  if constexpr (DROP) {   // dword i * 64 + l of the wave's image = word (l & 3) of query (i * 64 + l) / 4
+    wsrd = asrxg::make_srd(qmaj + (int64_t)bh * a.Lq * qst, (int64_t)a.Lq * qst * 4);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      wvo[i] = (uint32_t)((min(qw0 + ((i * 64 + l) >> 2), a.Lq - 1) * qst + (l & 3)) * 4);
+  }
+  const bool kvm = MODE == 1 && a.kvalid;
+  if (kvm) msrd = asrxg::make_srd(a.kvalid + b * a.validb, a.Lk);
+  constexpr int NC = 4 + (DROP ? 2 : 0) + (MODE == 1 ? 1 : 0);   // vector-memory ops per chunk and wave
   // chunk c -> buffer c & 1: two 64-key pieces, wave w moves key rows 64 i + 8 w .. + 7 of K and of V
-#define STREAM_ISSUE(c)                                                                                    \
-  do {                                                                                                     \
-    _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                                        \
-      const int lr = ((c) & 1) * S_CK + 64 * i + 8 * w, r = (c) * S_CK + 64 * i + 8 * w + rl;            \
-      asrxg::dma16_asm(sk + lr * 64, ksrd, (uint32_t)(r * a.kr + 8 * kslot(r, sl)) * 2u);                 \
-      asrxg::dma16_asm(sv + lr * 64, vsrd, (uint32_t)(r * a.vr + 8 * vslot(r, sl)) * 2u);                 \
-    }                                                                                                      \
-  } while (0)
-  STREAM_ISSUE(0);
+  auto issue = [&](int c) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int lr = (c & 1) * S_CK + 64 * i + 8 * w, r = c * S_CK + 64 * i + 8 * w + rl;
+      asrxg::dma16_asm(sk + lr * 64, ksrd, (uint32_t)(r * a.kr + 8 * kslot(r, sl)) * 2u);
+      asrxg::dma16_asm(sv + lr * 64, vsrd, (uint32_t)(r * a.vr + 8 * vslot(r, sl)) * 2u);
+    }
+    if constexpr (DROP) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) dma4_asm(skw + (c & 1) * 1024 + w * 128 + i * 64, wsrd, wvo[i] + 16u * c);
+    }
+    if constexpr (MODE == 1)   // every wave moves the same 256 bytes (keys of chunks c and c + 1, range-clipped)
+      dma4_asm(skv + (c & 1) * 256, msrd, (uint32_t)(4 * l + c * S_CK));
+  };
+  issue(0);
   if (nch > 1) {
-    STREAM_ISSUE(1);
-    asrxg::wait_vmcnt<4>();   // Q and chunk 0 (chunk 1 may still be in flight)
+    issue(1);
+    asrxg::wait_vmcnt<NC>();   // Q (+ query validity) and chunk 0 (chunk 1 may still be in flight)
   } else {
     asrxg::wait_vmcnt<0>();
   }
@@ -843,8 +904,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
     pin(qf[qs][0]);
     pin(qf[qs][1]);
   }
+  bool qdead[2] = {false, false};
+  if (MODE == 1) {
+    pin(qval[0]);
+    pin(qval[1]);
+#pragma unroll
+    for (int qs = 0; qs < 2; ++qs) qdead[qs] = a.qvalid && (qval[qs] & 0xff) == 0;
+  }
+  if (threadIdx.x < 16) {
+    const uint32_t n = threadIdx.x;
+    smask[n] = make_uint2(((n & 1) ? 0xffffu : 0u) | ((n & 2) ? 0xffff0000u : 0u),
+                          ((n & 4) ? 0xffffu : 0u) | ((n & 8) ? 0xffff0000u : 0u));
+  }
   lds_barrier();
   const bool act = qw0 < a.Lq;
+  const int qlast = min(a.Lq, qw0 + 32) - 1;   // the wave's last query (causal: later key tiles are all masked)
+  const float sc2 = a.scale2;
 
   f4_t o[4][2];
 #pragma unroll
@@ -854,10 +929,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
     const bf16_t* skc = sk + (c & 1) * S_CK * 64;
     const bf16_t* svc = sv + (c & 1) * S_CK * 64;
     if (act) {
+      uint4 dwc[2] = {make_uint4(~0u, ~0u, ~0u, ~0u), make_uint4(~0u, ~0u, ~0u, ~0u)};
+      if constexpr (DROP) {
+#pragma unroll
+        for (int qs = 0; qs < 2; ++qs) dwc[qs] = *(const uint4*)(skw + (c & 1) * 1024 + w * 128 + (16 * qs + li) * 4);
+      }
 #pragma unroll
       for (int kt = 0; kt < S_CK / 32; ++kt) {
         const int key0 = c * S_CK + kt * 32;
-        if (key0 >= a.Lk) break;   // workgroup-uniform
+        if (key0 >= a.Lk) break;                             // workgroup-uniform
+        if (MODE == 1 && a.causal && key0 > qlast) break;    // wave-uniform: no key of the tile is visible
         f4_t s[2][2];
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
@@ -867,40 +948,59 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
           for (int qs = 0; qs < 2; ++qs) s[t][qs] = mfma32(k1, qf[qs][1], mfma32(k0, qf[qs][0], f4_t{0.f, 0.f, 0.f, 0.f}));
         }
         const bool tail = key0 + 32 > a.Lk;
-        s4_t pf[2][2];
+        const bool diag = MODE == 1 && a.causal && key0 + 31 > qw0;   // the tile reaches above some query
+        uint32_t kvw[2] = {~0u, ~0u};
+        if (kvm) {
 #pragma unroll
-        for (int qs = 0; qs < 2; ++qs) {
-          float mt = -INFINITY;
+          for (int t = 0; t < 2; ++t) kvw[t] = *(const uint32_t*)(skv + (c & 1) * 256 + kt * 32 + 16 * t + 4 * g);
+        }
+        if (tail || diag || kvm) {
 #pragma unroll
           for (int t = 0; t < 2; ++t)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              float x = s[t][qs][r] * a.scale2;
-              if (tail && key0 + 16 * t + 4 * g + r >= a.Lk) x = -INFINITY;
-              s[t][qs][r] = x;
-              mt = fmaxf(mt, x);
+              const int key = key0 + 16 * t + 4 * g + r;
+              const bool bad = key >= a.Lk || (kvm && ((kvw[t] >> (8 * r)) & 0xff) == 0);
+#pragma unroll
+              for (int qs = 0; qs < 2; ++qs)
+                s[t][qs][r] = (bad || (diag && key > qw0 + 16 * qs + li)) ? -INFINITY : s[t][qs][r];
             }
+        }
+        s4_t pf[2][2];
+#pragma unroll
+        for (int qs = 0; qs < 2; ++qs) {
+          float mt = fmaxf(fmaxf(fmaxf(s[0][qs][0], s[0][qs][1]), fmaxf(s[0][qs][2], s[0][qs][3])),
+                           fmaxf(fmaxf(s[1][qs][0], s[1][qs][1]), fmaxf(s[1][qs][2], s[1][qs][3])));
           mt = xmax4(mt);
           const float m_new = fmaxf(m_run[qs], mt);
           const float m_use = m_new == -INFINITY ? 0.f : m_new;
           if (__ballot(m_new != m_run[qs])) {   // rescale only when some row's max grew (exact, wave-uniform)
-            const float alpha = exp2_raw(m_run[qs] - m_use);
+            const float alpha = exp2_raw((m_run[qs] - m_use) * sc2);
             l_run[qs] *= alpha;
 #pragma unroll
             for (int u = 0; u < 4; ++u) o[u][qs] *= alpha;
             m_run[qs] = m_new;
           }
+          const float nm = -m_use * sc2;
+          const uint32_t dword = (&dwc[qs].x)[kt];
           float rs = 0.f;
 #pragma unroll
           for (int t = 0; t < 2; ++t) {
-            f4_t pv;
+            f4_t e;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const float e = exp2_raw(s[t][qs][r] - m_use);
-              rs += e;
-              pv[r] = e;
+              e[r] = exp2_raw(fmaf(s[t][qs][r], sc2, nm));
+              rs += e[r];
             }
-            pf[t][qs] = to_bf4(pv);
+            s4_t pk = to_bf4(e);
+            if constexpr (DROP) {
+              const uint2 mk = smask[(dword >> (16 * t + 4 * g)) & 15u];
+              u2_t pu = __builtin_bit_cast(u2_t, pk);
+              pu[0] &= mk.x;
+              pu[1] &= mk.y;
+              pk = __builtin_bit_cast(s4_t, pu);
+            }
+            pf[t][qs] = pk;
           }
           l_run[qs] += xsum4(rs);
         }
@@ -917,35 +1017,35 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
     if (c + 1 < nch) {
       lds_barrier();                 // every wave is done with buffer c & 1
       if (c + 2 < nch) {
-        STREAM_ISSUE(c + 2);
-        asrxg::wait_vmcnt<4>();      // chunk c + 1 landed (chunk c + 2 may still be in flight)
+        issue(c + 2);
+        asrxg::wait_vmcnt<NC>();     // chunk c + 1 landed (chunk c + 2 may still be in flight)
       } else {
         asrxg::wait_vmcnt<0>();
       }
       lds_barrier();                 // ... and visible to every wave
     }
   }
-#undef STREAM_ISSUE
   if (!act) return;
+  const float dsc = DROP ? a.dscale : 1.f;
 #pragma unroll
   for (int qs = 0; qs < 2; ++qs) {
     const int q = qw0 + 16 * qs + li;
     if (q >= a.Lq) continue;
-    const bool live = l_run[qs] > 0.f;
-    const float inv = live ? 1.f / l_run[qs] : 0.f;
+    const bool live = !qdead[qs] && l_run[qs] > 0.f;
+    const float inv = live ? dsc / l_run[qs] : 0.f;
     const int64_t oo = b * a.ob + (int64_t)q * a.orr + h * 64 + 4 * g;
 #pragma unroll
     for (int u = 0; u < 4; ++u)
       store_o4(a.o + oo + 16 * u, a.o_lo ? a.o_lo + oo + 16 * u : nullptr, o[u][qs][0] * inv, o[u][qs][1] * inv,
                o[u][qs][2] * inv, o[u][qs][3] * inv);
-    if (g == 0 && a.lse) {
-      const float mu = m_run[qs] == -INFINITY ? 0.f : m_run[qs];
-      a.lse[(int64_t)bh * a.Lq + q] = live ? mu + log2f(l_run[qs]) : INFINITY;
-    }
+    if (g == 0 && a.lse) a.lse[(int64_t)bh * a.Lq + q] = live ? m_run[qs] * sc2 + log2f(l_run[qs]) : INFINITY;
   }
 }
 
-// Backward: grid (B*H), nw = max(2, ceil(Lk/32)) waves; wave w owns keys [32w, 32w+32) (dK, dV in registers)
+// Backward: grid (B*H, key blocks), NKT waves; wave w owns keys kb0 + [32w, 32w+32) (dK, dV in registers), with
+// kb0 = 256 * blockIdx.y — one block per head for Lk <= 256; for longer key ranges (the streamed forward's training
+// path) each block sweeps every query for its 256 keys and adds its share of dQ into an fp32 accumulator by atomics
+// (dq_finish scales and casts).
 // and the workgroup sweeps the queries in chunks of 32: S and dP are recomputed with the query on the accumulator
 // row; Pd / dS feed dV^T / dK^T as B operands directly; dS (bf16) is published in LDS and, after the chunk's only
 // barrier, the waves split the chunk's dQ = dS K tiles (full key range -> final values, no atomics).  Q / dO of
@@ -971,7 +1071,9 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
 
   const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, g = l >> 4, li = l & 15;
-  const int kw0 = 32 * w;
+  // key block (grid.y > 1 only for Lk > NK: the streamed training path) — kb0 + the wave's local 32-key slice
+  const int kb0 = (int)blockIdx.y * NK, nkb = (int)gridDim.y;
+  const int kwl = 32 * w, kw0 = kb0 + kwl;
 
   const bf16_t* Kb = a.k + b * a.kb + h * 64;
   const bf16_t* Vb = a.v + b * a.vb + h * 64;
@@ -980,12 +1082,12 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
 #pragma unroll
     for (int i = 0; i < NK * 8 / NTHR; ++i) {
       const int c = tid + i * NTHR, row = c >> 3, dc = (c & 7) * 8;
-      kv[i] = *(const uint4*)(Kb + (int64_t)min(row, a.Lk - 1) * a.kr + dc);
+      kv[i] = *(const uint4*)(Kb + (int64_t)min(kb0 + row, a.Lk - 1) * a.kr + dc);
     }
 #pragma unroll
     for (int i = 0; i < NK * 8 / NTHR; ++i) {
       const int c = tid + i * NTHR, row = c >> 3, dc = (c & 7) * 8;
-      *(uint4*)(sk + row * R_VS + dc) = row < a.Lk ? kv[i] : make_uint4(0, 0, 0, 0);
+      *(uint4*)(sk + row * R_VS + dc) = kb0 + row < a.Lk ? kv[i] : make_uint4(0, 0, 0, 0);
     }
   }
   s8_t kf[2][2], vf[2][2];
@@ -1130,10 +1232,19 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
 #pragma unroll
       for (int kc = 0; kc < NKT; ++kc) acc = mfma32(ka[kc], da[kc], acc);
       const int q = min(q0 + 16 * qs + li, a.Lq - 1);   // rows past Lq: duplicate store of the last row's
-      uint2 x;                                           // (zero-dS) value would be wrong -> guarded below
-      x.x = pack2bf(acc[0] * a.scale, acc[1] * a.scale);
-      x.y = pack2bf(acc[2] * a.scale, acc[3] * a.scale);
-      if (q0 + 16 * qs + li < a.Lq) *(uint2*)(dqh + __mul24(q, (int)a.dqr) + 16 * u + 4 * g) = x;
+      if (nkb > 1) {                                     // (zero-dS) value would be wrong -> guarded below
+        // several key blocks: this block's share of dQ into the fp32 accumulator (dq_finish scales and casts)
+        if (q0 + 16 * qs + li < a.Lq) {
+          float* dst = a.dq_acc + (((int64_t)b * a.Lq + q) * a.H + h) * 64 + 16 * u + 4 * g;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) unsafeAtomicAdd(dst + e, acc[e]);
+        }
+      } else {
+        uint2 x;
+        x.x = pack2bf(acc[0] * a.scale, acc[1] * a.scale);
+        x.y = pack2bf(acc[2] * a.scale, acc[3] * a.scale);
+        if (q0 + 16 * qs + li < a.Lq) *(uint2*)(dqh + __mul24(q, (int)a.dqr) + 16 * u + 4 * g) = x;
+      }
     }
   };
 
@@ -1181,7 +1292,7 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
       for (int qs = 0; qs < 2; ++qs)
 #pragma unroll
         for (int t = 0; t < 2; ++t)
-          *(uint2*)(sds + (buf * NK + kw0 + 16 * t + li) * RDT + 16 * qs + 4 * g) = make_uint2(0, 0);
+          *(uint2*)(sds + (buf * NK + kwl + 16 * t + li) * RDT + 16 * qs + 4 * g) = make_uint2(0, 0);
       if (ch > 0) dq_chunk(ch - 1);
     } else {
       f4_t s[2][2], dp[2][2];   // [qs][t]
@@ -1226,7 +1337,7 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
           pdb[qs][t] = to_bf4(pd);
           dsb[qs][t] = to_bf4(dsv);
           // dS^T image: this lane's 4 consecutive queries of one key -> one 8-byte write
-          *(s4_t*)(sds + (buf * NK + key) * RDT + 16 * qs + 4 * g) = dsb[qs][t];
+          *(s4_t*)(sds + (buf * NK + kwl + 16 * t + li) * RDT + 16 * qs + 4 * g) = dsb[qs][t];
         }
       }
       // dV^T += dO^T Pd ; dK^T += Q^T dS   (k-slots: queries 4g+j of sub-tile 0, then of sub-tile 1)
@@ -1326,10 +1437,15 @@ int fill_args(const asrx_attn_desc* d, AttnArgs& a) {
   return ASRX_OK;
 }
 
-// Lk <= 256 and dh = 64 -> resident-K/V kernels (ASRX_ATTN_KERNEL=tiled forces the general tiled kernels)
+// ASRX_ATTN_KERNEL=tiled forces the general tiled kernels (read per call: the tests switch it between cases)
+bool force_tiled() {
+  const char* e = getenv("ASRX_ATTN_KERNEL");
+  return e && !strcmp(e, "tiled");
+}
+
+// Lk <= 256 and dh = 64 -> resident-K/V kernels
 bool resident_ok(const asrx_attn_desc* d, const AttnArgs& a) {
-  static const bool tiled = [] { const char* e = getenv("ASRX_ATTN_KERNEL"); return e && !strcmp(e, "tiled"); }();
-  if (tiled) return false;
+  if (force_tiled()) return false;
   // row offsets inside the resident kernels are 24-bit products (q * row stride): strides and lengths < 2^23
   constexpr int64_t L24 = 1 << 23;
   const bool s24 = a.qr < L24 && a.kr < L24 && a.vr < L24 && a.orr < L24 && a.Lq < L24 && a.Lk < L24 &&
@@ -1340,6 +1456,22 @@ bool resident_ok(const asrx_attn_desc* d, const AttnArgs& a) {
   const int64_t ks = std::max({(int64_t)a.kr, (int64_t)a.vr, a.dout ? (int64_t)a.dkr : 0, a.dout ? (int64_t)a.dvr : 0});
   const bool s31 = (int64_t)a.Lq * qs < L31 && (int64_t)a.Lk * ks < L31;
   return d->dh == 64 && a.Lk <= R_MAXK && (a.orr % 4) == 0 && (a.ob % 4) == 0 && s24 && s31;
+}
+
+// Lk > 256, dh = 64, no mask or the structured mask -> the streamed forward / key-block backward
+// (ASRX_ATTN_KERNEL=tiled: the general tiled kernels): 16-B aligned K/V rows for the LDS-DMA, 32-bit byte offsets of every K/V row of the padded last chunk,
+// and the backward's 24-bit query-row products
+bool stream_ok(const asrx_attn_desc* d, const AttnArgs& a) {
+  if (force_tiled()) return false;
+  if (d->dh != 64 || a.Lk <= R_MAXK || a.mode == 2) return false;
+  constexpr int64_t L24 = 1 << 23, L31 = (int64_t)1 << 31;
+  const bool s24 = a.qr < L24 && a.orr < L24 && a.Lq < L24 && (!a.dout || (a.dor < L24 && a.dqr < L24));
+  const int64_t qs = std::max({(int64_t)a.qr, (int64_t)a.orr, a.dout ? (int64_t)a.dor : 0, a.dout ? (int64_t)a.dqr : 0});
+  const int64_t ks = std::max({(int64_t)a.kr, (int64_t)a.vr, a.dout ? (int64_t)a.dkr : 0, a.dout ? (int64_t)a.dvr : 0});
+  const bool s31 = (int64_t)a.Lq * qs < L31 && ((int64_t)a.Lk + R_MAXK) * ks * 2 < L31 &&
+                   (int64_t)a.Lq * qmaj_stride(a.Lk) * 4 < L31;
+  return a.orr % 4 == 0 && a.ob % 4 == 0 && a.kr % 8 == 0 && a.vr % 8 == 0 && ((uintptr_t)a.k % 16) == 0 &&
+         ((uintptr_t)a.v % 16) == 0 && s24 && s31;
 }
 
 size_t bwd_smem(int nw, int dh) {
@@ -1355,12 +1487,13 @@ extern "C" int asrx_attn_dropgen(const asrx_attn_desc* d, void* stream) {
   AttnArgs a;
   int rc = fill_args(d, a);
   if (rc) return rc;
-  if (!a.dropmask || a.Lk > R_MAXK) return ASRX_ERR_ARG;
+  if (!a.dropmask) return ASRX_ERR_ARG;
   if (!a.thr) return ASRX_OK;
-  const int nqc = (a.Lq + 31) / 32;
+  const int nqc = (a.Lq + 31) / 32, nkb = (a.Lk + R_MAXK - 1) / R_MAXK;
   uint32_t* kmaj = a.dropmask;
   uint32_t* qmaj = a.dropmask + (int64_t)a.B * a.H * nqc * a.Lk;
-  hipLaunchKernelGGL(attn_dropgen_kernel, dim3(nqc, a.B * a.H), dim3(256), 0, (hipStream_t)stream, a, kmaj, qmaj);
+  hipLaunchKernelGGL(attn_dropgen_kernel, dim3(nqc, a.B * a.H, nkb), dim3(256), 0, (hipStream_t)stream, a, kmaj,
+                     qmaj);
   ASRX_CHECK_LAUNCH();
   return ASRX_OK;
 }
@@ -1373,12 +1506,12 @@ extern "C" int asrx_layernorm_fwd_attn_dropgen(const float* x, void* y, const fl
   AttnArgs a;
   int rc = fill_args(d, a);
   if (rc) return rc;
-  if (!a.dropmask || a.Lk > R_MAXK) return ASRX_ERR_ARG;
-  const int nqc = (a.Lq + 31) / 32;
+  if (!a.dropmask) return ASRX_ERR_ARG;
+  const int nqc = (a.Lq + 31) / 32, nkb = (a.Lk + R_MAXK - 1) / R_MAXK;
   uint32_t* kmaj = a.dropmask;
   uint32_t* qmaj = a.dropmask + (int64_t)a.B * a.H * nqc * a.Lk;
   const int nln = (int)std::max<int64_t>(1, std::min<int64_t>((rows + 3) / 4, 1024));
-  const int64_t ndg = a.thr ? (int64_t)nqc * a.B * a.H : 0;
+  const int64_t ndg = a.thr ? (int64_t)nqc * a.B * a.H * nkb : 0;
   if (nln + ndg > 0x7fffffff) return ASRX_ERR_ARG;
   const LnJob ln{x, (bf16_t*)y, gamma, beta, mean, rstd, rows, eps};
   hipLaunchKernelGGL(ln_dropgen_kernel, dim3((unsigned)(nln + ndg)), dim3(256), 0, (hipStream_t)stream, a, kmaj, qmaj,
@@ -1415,11 +1548,21 @@ extern "C" int asrx_attention_fwd(const asrx_attn_desc* d, void* stream) {
     ASRX_CHECK_LAUNCH();
     return ASRX_OK;
   }
-  static const bool tiled = [] { const char* e = getenv("ASRX_ATTN_KERNEL"); return e && !strcmp(e, "tiled"); }();
-  if (!tiled && d->dh == 64 && a.mode == 0 && !a.thr && a.Lk > R_MAXK && a.orr % 4 == 0 && a.ob % 4 == 0 &&
-      a.kr % 8 == 0 && a.vr % 8 == 0 && ((uintptr_t)a.k % 16) == 0 && ((uintptr_t)a.v % 16) == 0 &&
-      (int64_t)a.Lk * std::max(a.kr, a.vr) * 2 < 0x7fffffffLL) {
-    hipLaunchKernelGGL(attn_fwd_stream_kernel, dim3((a.Lq + 255) / 256, a.B * a.H), dim3(512), 0, st, a);
+  if (stream_ok(d, a) && (!a.thr || a.dropmask)) {   // Lk > 256: K/V streamed through LDS, training or inference
+    const uint32_t* qmaj = nullptr;
+    if (a.thr) {
+      if (!d->dropmask_ready) {
+        const int rc2 = asrx_attn_dropgen(d, stream);
+        if (rc2) return rc2;
+      }
+      qmaj = a.dropmask + (int64_t)a.B * a.H * ((a.Lq + 31) / 32) * a.Lk;
+    }
+    const dim3 grid((a.Lq + 255) / 256, a.B * a.H);
+#define ASRX_STREAM(M) do { if (qmaj) hipLaunchKernelGGL((attn_fwd_stream_kernel<M, true>), grid, dim3(512), 0, st, a, qmaj); \
+                            else hipLaunchKernelGGL((attn_fwd_stream_kernel<M, false>), grid, dim3(512), 0, st, a, qmaj); } while (0)
+    if (a.mode == 0) ASRX_STREAM(0);
+    else ASRX_STREAM(1);
+#undef ASRX_STREAM
     ASRX_CHECK_LAUNCH();
     return ASRX_OK;
   }
@@ -1453,16 +1596,28 @@ extern "C" int asrx_attention_bwd(const asrx_attn_desc* d, void* stream) {
   const int64_t ostr[] = {a.orr, a.ob, a.dor, a.dob, a.dkr, a.dkb, a.dvr, a.dvb};
   for (int64_t s : ostr) if (s % 8) return ASRX_ERR_UNSUPPORTED;
   hipStream_t st = (hipStream_t)stream;
-  if (resident_ok(d, a) && a.dqr % 4 == 0 && a.dqb % 4 == 0 && (uintptr_t)a.dq % 8 == 0) {   // forms delta itself
+  const bool longk = stream_ok(d, a) && (!a.thr || a.dropmask);
+  if ((resident_ok(d, a) || longk) && a.dqr % 4 == 0 && a.dqb % 4 == 0 && (uintptr_t)a.dq % 8 == 0) {   // forms delta itself
     const int nkt = bwd_res_nkt(a.Lk);
     const size_t sm = bwd_res_smem(a.Lk);
-    const dim3 grid(a.B * a.H), blk(64 * nkt);
+    const int nkb = (a.Lk + R_MAXK - 1) / R_MAXK;
+    if (nkb > 1) {   // key blocks add their dQ shares into dq_acc
+      if (!a.dq_acc) return ASRX_ERR_ARG;
+      hipMemsetAsync(a.dq_acc, 0, sizeof(float) * (size_t)a.B * a.Lq * a.H * d->dh, st);
+    }
+    const dim3 grid(a.B * a.H, nkb), blk(64 * nkt);
 #define ASRX_BWD_RES(M, N) hipLaunchKernelGGL((attn_bwd_res_kernel<M, N>), grid, blk, sm, st, a)
     if (a.mode == 0) { if (nkt == 2) ASRX_BWD_RES(0, 2); else if (nkt == 4) ASRX_BWD_RES(0, 4); else ASRX_BWD_RES(0, 8); }
     else if (a.mode == 1) { if (nkt == 2) ASRX_BWD_RES(1, 2); else if (nkt == 4) ASRX_BWD_RES(1, 4); else ASRX_BWD_RES(1, 8); }
     else { if (nkt == 2) ASRX_BWD_RES(2, 2); else if (nkt == 4) ASRX_BWD_RES(2, 4); else ASRX_BWD_RES(2, 8); }
 #undef ASRX_BWD_RES
     ASRX_CHECK_LAUNCH();
+    if (nkb > 1) {
+      const int64_t total = (int64_t)a.B * a.Lq * a.H * d->dh;
+      const unsigned blocks = (unsigned)std::min<int64_t>((total + 255) / 256, 8192);
+      hipLaunchKernelGGL(dq_finish_kernel, dim3(blocks), dim3(256), 0, st, a, d->dh);
+      ASRX_CHECK_LAUNCH();
+    }
     return ASRX_OK;
   }
   rc = asrx_attn_delta(d, stream);

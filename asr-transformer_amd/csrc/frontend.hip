@@ -963,6 +963,23 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
   }
 }
 
+ASRX_DEV float ld_any(int dt, const void* p, int64_t i) {
+  return dt == ASRX_F32 ? ((const float*)p)[i] : bf2f(((const bf16_t*)p)[i]);
+}
+__global__ __launch_bounds__(256) void ewise_kernel(int op, int da, const void* a, int db, const void* b, int dout,
+                                                    void* out, int64_t n, uint32_t thr, float dscale, uint64_t seed) {
+  if (op == ASRX_EW_DROPOUT) seed = seed_eff(seed);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float x = ld_any(da, a, i);
+    float r;
+    if (op == ASRX_EW_RELU_GRAD) r = ld_any(db, b, i) > 0.f ? x : 0.f;
+    else if (op == ASRX_EW_DROPOUT) r = (thr == 0u || rng_keep(seed, (uint32_t)i, thr)) ? x * dscale : 0.f;
+    else r = x + ld_any(db, b, i);
+    if (dout == ASRX_F32) ((float*)out)[i] = r;
+    else ((bf16_t*)out)[i] = f2bf(r);
+  }
+}
+
 __global__ __launch_bounds__(256) void dropout_mask_kernel(uint8_t* keep, int64_t n, uint32_t thr, uint64_t seed) {
   seed = seed_eff(seed);
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
@@ -1196,6 +1213,22 @@ extern "C" int asrx_cast(int32_t src_dtype, const void* src, int32_t dst_dtype, 
   if (n == 0) return ASRX_OK;
   hipLaunchKernelGGL(cast_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, src_dtype, src, dst_dtype, dst,
                      n);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
+extern "C" int asrx_ewise(int32_t op, int32_t dtype_a, const void* a, int32_t dtype_b, const void* b,
+                          int32_t dtype_out, void* out, int64_t n, float p, uint64_t seed, void* stream) {
+  if (op < ASRX_EW_RELU_GRAD || op > ASRX_EW_ADD || n < 0) return ASRX_ERR_ARG;
+  const auto okdt = [](int32_t t) { return t == ASRX_F32 || t == ASRX_BF16; };
+  if (!okdt(dtype_a) || !okdt(dtype_out) || (op != ASRX_EW_DROPOUT && !okdt(dtype_b))) return ASRX_ERR_ARG;
+  if (n == 0) return ASRX_OK;
+  if (!a || !out || (op != ASRX_EW_DROPOUT && !b) || (op == ASRX_EW_DROPOUT && !(p >= 0.f && p < 1.f)))
+    return ASRX_ERR_ARG;
+  const uint32_t thr = op == ASRX_EW_DROPOUT ? drop_threshold(p) : 0u;
+  const float dscale = op == ASRX_EW_DROPOUT && p > 0.f ? 1.f / (1.f - p) : 1.f;
+  hipLaunchKernelGGL(ewise_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (int)op, (int)dtype_a, a,
+                     (int)dtype_b, b, (int)dtype_out, out, n, thr, dscale, seed);
   ASRX_CHECK_LAUNCH();
   return ASRX_OK;
 }

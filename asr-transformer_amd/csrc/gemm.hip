@@ -1478,6 +1478,12 @@ int wsp_min_rows() {
   static const int m = [] { const char* e = getenv("ASRX_WSP_M"); return e ? atoi(e) : 4096; }();
   return m;
 }
+// ASRX_WS64=0 keeps the decoder's 4096-row N = 512 GEMMs on the ring kernels (A/B switch; default on): ws with
+// 64 x 128 tiles (64 x 4 = 256 tiles = one per CU) for 2048 <= M < 8192
+bool ws64_auto() {
+  static const bool on = [] { const char* e = getenv("ASRX_WS64"); return !(e && e[0] == '0'); }();
+  return on;
+}
 // ASRX_WS_MIN_K: shortest reduction planned on ws (A/B; every K from 512 up measured faster than p3 at c3)
 int ws_min_k() {
   static const int k = [] { const char* e = getenv("ASRX_WS_MIN_K"); return e ? atoi(e) : 64; }();
@@ -1501,7 +1507,7 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
     tile = t128 >= 400 ? 128 : 64;
   }
   const int kvar = d->kernel == 1 ? 1 : d->kernel == 3 ? 3 : d->kernel == 4 ? 4 : d->kernel == 5 ? 5 :
-                   d->kernel == 6 ? 6 : d->kernel == 8 ? 8 : d->kernel == 9 ? 9 : 0;
+                   d->kernel == 6 ? 6 : d->kernel == 8 ? 8 : d->kernel == 9 ? 9 : d->kernel == 10 ? 10 : 0;
   const bool dma_ok = pl.vec && d->k % BK == 0 && (!d->a_trans || d->m % 8 == 0) && (!d->b_trans || d->n % 8 == 0) &&
                       d->m >= 8 && d->n >= 8;
   const int nt_p3 = ((d->m + P_BM - 1) / P_BM) * ((d->n + P_BN - 1) / P_BN);
@@ -1574,6 +1580,13 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
     pl.use = 11;
     pl.epi = epi;
     pl.ntiles = ((d->m + WS_BM - 1) / WS_BM) * (d->n / WS_BN);
+  } else if (ws_ok && (kvar == 10 || (kvar == 0 && ws64_auto() && d->n == 512 && d->m >= 2048 && d->m < 8192 &&
+                                      d->k >= ws_min_k()))) {
+    // ws on 64 x 128 tiles (use 13): the decoder's 4096-row GEMMs with a 512-wide output, where 256 x 128 tiles
+    // would make 64 workgroups; kernel code 10 forces it
+    pl.use = 13;
+    pl.epi = epi;
+    pl.ntiles = ((d->m + 63) / 64) * (d->n / WS_BN);
   }
   // wsp (use 12): the same roles over a persistent tile walk (multi-round grids: the wide projections); kernel
   // code 9 forces it.  Candidates (tools/blas_ref.py): the Q/K/V projections with bias and the FFN2 data gradients
@@ -1611,8 +1624,8 @@ extern "C" int asrx_gemm_kernel_name(const asrx_gemm_desc* d, char* buf, int len
     return ASRX_OK;
   }
   const GemmPlan pl = plan_bf16(d, batch, splitk);
-  if (pl.use == 11)
-    snprintf(buf, len, "gemm_bf16_ws_kernel<%s, %d>", tf[!!d->b_trans], pl.epi);
+  if (pl.use == 11 || pl.use == 13)
+    snprintf(buf, len, "gemm_bf16_ws_kernel<%s, %d, %d>", tf[!!d->b_trans], pl.epi, pl.use == 13 ? 64 : 256);
   else if (pl.use == 12)
     snprintf(buf, len, "gemm_bf16_wsp_kernel<%s, %d>", tf[!!d->b_trans], pl.epi);
   else if (pl.use == 9)
@@ -1658,8 +1671,8 @@ int gemm_bf16_run(const asrx_gemm_desc* d, const GemmArgs& g, const GemmPlan& pl
       if (pl.use == 2) dispatch_p3<false, false, true>(gc, epi, nt, 1, 1, st);
       else dispatch_p3<false, false>(gc, epi, nt, 1, 1, st);
     }
-  } else if (pl.use == 11) {
-    launch_ws(g, d->b_trans, epi, pl.ntiles, st);
+  } else if (pl.use == 11 || pl.use == 13) {
+    launch_ws(g, d->b_trans, epi, pl.ntiles, pl.use == 13 ? 64 : 256, st);
   } else if (pl.use == 12) {
     launch_wsp(g, d->b_trans, epi, pl.ntiles, st);
   } else if (pl.use == 9) {

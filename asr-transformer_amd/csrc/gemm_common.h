@@ -515,7 +515,7 @@ ASRX_DEV s8_t p4_frag(const unsigned char* img, int i0, int ks, uint32_t S) {
 // ws kernel (gemm_ws.hip): instantiated epilogues and the launch
 constexpr int WS_BM = 256, WS_BN = 128;
 bool ws_instantiated(bool bt, int epi);
-void launch_ws(const GemmArgs& g, bool bt, int epi, int ntiles, hipStream_t st);
+void launch_ws(const GemmArgs& g, bool bt, int epi, int ntiles, int bm, hipStream_t st);
 bool wsp_instantiated(bool bt, int epi);
 void launch_wsp(const GemmArgs& g, bool bt, int epi, int ntiles, hipStream_t st);
 int launch_ws_grouped(const GroupEnt* ents, const uint16_t* tile_group, const uint16_t* block_tile, int ntiles,

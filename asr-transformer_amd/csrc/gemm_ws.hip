@@ -20,13 +20,25 @@ using namespace asrxg;
 //   four rows of 256 B bf16); the loader waves load their residual values before that barrier.
 // One tile per workgroup, tile = XCD-contiguous range (the 4 column tiles of a row panel share an XCD's L2).
 // ------------------------------------------------------------------------------------------------
-constexpr int WS_NST = 3;
-constexpr int WS_PA = WS_BM * BK * 2, WS_PB = WS_BN * BK * 2, WS_STAGE = WS_PA + WS_PB;
-constexpr int WS_LDS = WS_NST * WS_STAGE;                     // 144 KiB
-constexpr int WS_SP = WS_BN + 4;                              // epilogue staging row stride (floats)
-constexpr int WS_NIA = WS_PA / (4 * 1024), WS_NIB = WS_PB / (4 * 1024);
-constexpr int WS_INST = WS_NIA + WS_NIB;                      // LDS-DMA instructions per loader lane per stage
-static_assert(WS_BM * WS_SP * 4 <= WS_LDS, "epilogue staging fits the ring");
+// Tile configurations: BM = 256 (the one-round c3 encoder GEMMs, the grouped weight gradients) and BM = 64 (the
+// decoder's 4096-row GEMMs with a 512-wide output: 64 x 4 = 256 tiles = one per CU, where 256 x 128 tiles would
+// fill a quarter of the chip).  The 4 compute waves are 2 x 2 wave tiles of (16 TM) x 64; the ring has NST stages.
+template <int BM_>
+struct WsCfg {
+  static constexpr int BM = BM_, BN = WS_BN;
+  static constexpr int TM = BM / 32, TN = 4;                   // wave tile (16 TM) x 64
+  static constexpr int NST = BM == 256 ? 3 : 6;
+  static constexpr int PA = BM * BK * 2, PB = BN * BK * 2, STAGE = PA + PB;
+  static constexpr int LDS = NST * STAGE;                      // 144 KiB either way
+  static constexpr int SP = BN + 4;                            // epilogue staging row stride (floats)
+  static constexpr int NIA = PA / (4 * 1024), NIB = PB / (4 * 1024);
+  static constexpr int INST = NIA + NIB;                       // LDS-DMA instructions per loader lane per stage
+  static_assert(BM * SP * 4 <= LDS, "epilogue staging fits the ring");
+};
+constexpr int WS_NST = WsCfg<256>::NST;
+constexpr int WS_PA = WsCfg<256>::PA, WS_PB = WsCfg<256>::PB, WS_STAGE = WsCfg<256>::STAGE;
+constexpr int WS_LDS = WsCfg<256>::LDS;
+constexpr int WS_INST = WsCfg<256>::INST;
 
 // Sum of an A fragment's 8 bf16 values (one column of the k-strided image, 8 consecutive k) into acc: 4
 // v_dot2c_f32_bf16 against (1, 1).
@@ -81,9 +93,10 @@ struct WsStage {
 // staging image.  (No row sums here: the bias gradient's column sums are the loader waves' — a per-wave branch in
 // this MFMA stream split it into small blocks, 1.68 vs 1.29 ms for the 12 encoder layers' weight gradients, and a
 // branch-free sum needs registers these waves do not have.)
-template <bool AT, bool BT>
+template <bool AT, bool BT, int BM = 256>
 ASRX_DEV void ws_compute(const GemmArgs& g, int m0, int nk, int wm, int wn, unsigned char* lds) {
-  constexpr int TM = 8, TN = 4;
+  using C = WsCfg<BM>;
+  constexpr int TM = C::TM, TN = C::TN;
   const int l = threadIdx.x & 63;
   float* stg = (float*)lds;
   // ---------------- compute waves: the p4 pipeline on a 128x64 wave tile
@@ -104,23 +117,23 @@ do {                                                                            
 } while (0)
   __builtin_amdgcn_s_barrier();
 #pragma unroll
-  for (int j = 0; j < TM; ++j) fa0[j] = p4_frag<WS_BM, AT>(lds, wm + 16 * j, 0, S);
+  for (int j = 0; j < TM; ++j) fa0[j] = p4_frag<BM, AT>(lds, wm + 16 * j, 0, S);
 #pragma unroll
-  for (int i = 0; i < TN; ++i) fb0[i] = p4_frag<WS_BN, BT>(lds + WS_PA, wn + 16 * i, 0, S);
+  for (int i = 0; i < TN; ++i) fb0[i] = p4_frag<C::BN, BT>(lds + C::PA, wn + 16 * i, 0, S);
   uint32_t cbo = 0;   // byte offset of step s's ring buffer
   for (int s = 0; s < nk; ++s) {
     asm volatile("" : "+s"(cbo));
-    const uint32_t nbo = cbo == (WS_NST - 1) * WS_STAGE ? 0u : cbo + WS_STAGE;
+    const uint32_t nbo = cbo == (C::NST - 1) * C::STAGE ? 0u : cbo + C::STAGE;
     const unsigned char* la = lds + cbo;
     // ---- phase A: k-slice 0 MFMAs of step s | k-slice 1 fragment reads of step s
     asm volatile("" : "+v"(S));
 #pragma unroll
-    for (int i = 0; i < TN; ++i) fb1[i] = p4_frag<WS_BN, BT>(la + WS_PA, wn + 16 * i, 1, S);
+    for (int i = 0; i < TN; ++i) fb1[i] = p4_frag<C::BN, BT>(la + C::PA, wn + 16 * i, 1, S);
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
 #pragma unroll
       for (int i = 0; i < TN; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[i], fa0[j], acc[i][j], 0, 0, 0);
-      fa1[j] = p4_frag<WS_BM, AT>(la, wm + 16 * j, 1, S);
+      fa1[j] = p4_frag<BM, AT>(la, wm + 16 * j, 1, S);
     }
     WS_ROLL_ORDER();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -132,13 +145,13 @@ do {                                                                            
     const bool more = s + 1 < nk;
     if (more) {
 #pragma unroll
-      for (int i = 0; i < TN; ++i) fb0[i] = p4_frag<WS_BN, BT>(ln + WS_PA, wn + 16 * i, 0, S);
+      for (int i = 0; i < TN; ++i) fb0[i] = p4_frag<C::BN, BT>(ln + C::PA, wn + 16 * i, 0, S);
     }
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
 #pragma unroll
       for (int i = 0; i < TN; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[i], fa1[j], acc[i][j], 0, 0, 0);
-      if (more) fa0[j] = p4_frag<WS_BM, AT>(ln, wm + 16 * j, 0, S);
+      if (more) fa0[j] = p4_frag<BM, AT>(ln, wm + 16 * j, 0, S);
     }
     WS_ROLL_ORDER();
     cbo = nbo;
@@ -149,16 +162,16 @@ do {                                                                            
   for (int i = 0; i < TN; ++i)
 #pragma unroll
     for (int j = 0; j < TM; ++j)
-      *(f4_t*)(stg + (wm + 16 * j + (l & 15)) * WS_SP + wn + 16 * i + 4 * (l >> 4)) = acc[i][j];
+      *(f4_t*)(stg + (wm + 16 * j + (l & 15)) * C::SP + wn + 16 * i + 4 * (l >> 4)) = acc[i][j];
 }
 
 // One 256x128 output tile [m0, +256) x [n0, +128) of C = op(A) op(B)^T.  AT: A stored k-strided ([K][M], the
 // weight gradient's dY); BT: B stored k-strided ([K][N]).  Ragged K only with both operands k-strided (rows past K
 // read as zero through the descriptor range); ragged M / N tiles: rows / column groups past them are not stored.
 // g.rowsum (AT only): += the row sums of op(A) (the fused bias gradient), by the compute waves of column block 0.
-template <bool AT, bool BT, int EPI>
+template <bool AT, bool BT, int EPI, int BM = 256>
 ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned char* lds) {
-  constexpr int TM = 8, TN = 4;
+  using C = WsCfg<BM>;
   const bf16_t* A = (const bf16_t*)g.a;
   const bf16_t* B = (const bf16_t*)g.b;
   const int64_t a_bytes = AT ? ((int64_t)(g.K - 1) * g.lda + g.M) * 2 : ((int64_t)(g.M - 1) * g.lda + g.K) * 2;
@@ -168,7 +181,7 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
   const int l = threadIdx.x & 63;
   const bool loader = wave >= 4;
   const int lw = wave & 3;
-  const int wm = (lw >> 1) * 128, wn = (lw & 1) * 64;
+  const int wm = (lw >> 1) * (16 * C::TM), wn = (lw & 1) * 64;
   const bool noload = (g.dbg & 8) != 0;
 
   float* stg = (float*)lds;
@@ -180,7 +193,7 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
   const int tid = threadIdx.x;
   // epilogue ownership: fp32 C: lane (tid & 31) owns columns 4 (tid & 31) .. +3 of rows (tid >> 5) + 16 i; bf16 C:
   // lane (tid & 15) owns columns 8 (tid & 15) .. +7 of rows (tid >> 4) + 32 i
-  constexpr int NR = F32 ? 16 : 8;
+  constexpr int NR = F32 ? BM / 16 : BM / 32;
   const int cq = F32 ? (tid & 31) * 4 : (tid & 15) * 8;
   const int rb = F32 ? tid >> 5 : tid >> 4;
   constexpr int RS = F32 ? 16 : 32;
@@ -207,24 +220,24 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
     // ---------------- loader waves: 3-stage ring, stage s + 3 issued once step s has released its buffer
     float lrs[4] = {0.f, 0.f, 0.f, 0.f};
     const uint32_t S = p4_swz_bytes();
-    WsStage<WS_BM, AT> sa;
-    WsStage<WS_BN, BT> sb;
+    WsStage<BM, AT> sa;
+    WsStage<C::BN, BT> sb;
     sa.set_tile(lw, m0, g.lda);
     sb.set_tile(lw, n0, g.ldb);
     int ni = 0;   // stages issued
     auto issue = [&](int buf) {
       if (!noload) {
-        unsigned char* img = lds + buf * WS_STAGE;
+        unsigned char* img = lds + buf * C::STAGE;
         sa.issue(img, sa.srd(A, g.lda, a_bytes, ni * BK), lw);
-        sb.issue(img + WS_PA, sb.srd(B, g.ldb, b_bytes, ni * BK), lw);
+        sb.issue(img + C::PA, sb.srd(B, g.ldb, b_bytes, ni * BK), lw);
       }
       ++ni;
     };
-    issue(0);
-    if (nk > 1) issue(1);
-    if (nk > 2) issue(2);
+#pragma unroll
+    for (int i = 0; i < C::NST; ++i)
+      if (i < nk) issue(i);
     if (noload) wait_vmcnt<0>();
-    else wait_stages<WS_INST, 2>(min(nk, 3) - 1);
+    else wait_stages<C::INST, C::NST - 1>(min(nk, C::NST) - 1);
     __builtin_amdgcn_s_barrier();
     int cb = 0;
     for (int s = 0; s < nk; ++s) {
@@ -234,21 +247,21 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
       // v_dot2c_f32_bf16 against (1, 1) per fragment: 16 reads + 32 VALU per K-step, each lane's column its own
       if constexpr (AT) {
         if (rs_tile) {
-          const unsigned char* img = lds + cb * WS_STAGE;
+          const unsigned char* img = lds + cb * C::STAGE;
 #pragma unroll
           for (int c = 0; c < 4; ++c)
 #pragma unroll
-            for (int ks = 0; ks < 2; ++ks) lrs[c] = frag_sum(p4_frag<WS_BM, true>(img, 64 * lw + 16 * c, ks, S), lrs[c]);
+            for (int ks = 0; ks < 2; ++ks) lrs[c] = frag_sum(p4_frag<BM, true>(img, 64 * lw + 16 * c, ks, S), lrs[c]);
         }
       }
       // stage s + 1 landed (visible after the barrier); the stages issued after it stay in flight
       if (s + 1 < nk) {
         if (noload) wait_vmcnt<0>();
-        else wait_stages<WS_INST, 1>(ni - (s + 2));
+        else wait_stages<C::INST, C::NST - 2>(ni - (s + 2));
       }
       __builtin_amdgcn_s_barrier();
-      if (ni < nk) issue(cb);   // stage s + 3 into the buffer step s released
-      cb = cb == WS_NST - 1 ? 0 : cb + 1;
+      if (ni < nk) issue(cb);   // stage s + NST into the buffer step s released
+      cb = cb == C::NST - 1 ? 0 : cb + 1;
     }
     load_resid();   // (before the epilogue barrier: its latency overlaps the compute waves' last k-slice)
     if constexpr (AT) {   // fold the 4 k-groups (lanes l, l ^ 16, l ^ 32, l ^ 48); lanes 0-15 own the columns
@@ -264,7 +277,7 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
       }
     }
   } else {
-    ws_compute<AT, BT>(g, m0, nk, wm, wn, lds);
+    ws_compute<AT, BT, BM>(g, m0, nk, wm, wn, lds);
   }
   __syncthreads();
   if (!loader) load_resid();
@@ -276,7 +289,7 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
       const int r = rb + RS * i, m = m0 + r;
-      f4_t v = *(const f4_t*)(stg + r * WS_SP + cq);
+      f4_t v = *(const f4_t*)(stg + r * C::SP + cq);
       f4_t pr = f4_t{0.f, 0.f, 0.f, 0.f};
       if constexpr (RES) pr = rr[i];
       v = epi_vals<EPI, true>(g, m, n0 + cq, v, b4, uint2{0u, 0u}, pr);
@@ -295,8 +308,8 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
       const int r = rb + RS * i, m = m0 + r;
-      f4_t va = *(const f4_t*)(stg + r * WS_SP + cq);
-      f4_t vb = *(const f4_t*)(stg + r * WS_SP + cq + 4);
+      f4_t va = *(const f4_t*)(stg + r * C::SP + cq);
+      f4_t vb = *(const f4_t*)(stg + r * C::SP + cq + 4);
       if (m < g.M && n0 + cq < g.N) {   // (bf16 C: N % 8 == 0)
         va = epi_vals<EPI>(g, m, n0 + cq, va, ba);
         vb = epi_vals<EPI>(g, m, n0 + cq + 4, vb, bb);
@@ -307,15 +320,15 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
   }
 }
 
-template <bool BT, int EPI>
+template <bool BT, int EPI, int BM>
 __global__ __launch_bounds__(512) void gemm_bf16_ws_kernel(GemmArgs g, int ntiles) {
   g.seed = seed_eff(g.seed);
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[WS_LDS];
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[WsCfg<BM>::LDS];
   const int per8 = (ntiles + 7) / 8;
   const int t = (int)(blockIdx.x % 8) * per8 + (int)(blockIdx.x / 8);
   if (t >= ntiles) return;
   const int ntn = g.N / WS_BN;
-  ws_tile<false, BT, EPI>(g, (t / ntn) * WS_BM, (t % ntn) * WS_BN, false, lds);
+  ws_tile<false, BT, EPI, BM>(g, (t / ntn) * BM, (t % ntn) * WS_BN, false, lds);
 }
 
 // Grouped weight gradients dW (+)= dY^T X of every layer in ONE launch on ws tiles: one 256x128 tile per workgroup,
@@ -550,9 +563,10 @@ void launch_wsp(const GemmArgs& g, bool bt, int epi, int ntiles, hipStream_t st)
 #undef ASRX_CASE
 }
 
-void launch_ws(const GemmArgs& g, bool bt, int epi, int ntiles, hipStream_t st) {
+void launch_ws(const GemmArgs& g, bool bt, int epi, int ntiles, int bm, hipStream_t st) {
   const dim3 grid(8 * ((ntiles + 7) / 8)), blk(512);
-#define ASRX_CASE(E) case (E): hipLaunchKernelGGL((gemm_bf16_ws_kernel<BT_, (E)>), grid, blk, 0, st, g, ntiles); return;
+#define ASRX_CASE(E) case (E): if (bm == 64) hipLaunchKernelGGL((gemm_bf16_ws_kernel<BT_, (E), 64>), grid, blk, 0, st, g, ntiles); \
+                               else hipLaunchKernelGGL((gemm_bf16_ws_kernel<BT_, (E), 256>), grid, blk, 0, st, g, ntiles); return;
   if (!bt) {
     constexpr bool BT_ = false;
     switch (epi) { ASRX_EPIWS_NT(ASRX_CASE) default: break; }

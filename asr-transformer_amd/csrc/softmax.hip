@@ -19,15 +19,22 @@ struct SmArgs {
   uint32_t thr; float dscale; uint64_t seed;
 };
 
-template <int V>
+// NT: non-temporal 16-B accesses (streamed once: no L2 / MALL allocation for the score matrix)
+template <int V, bool NT = false>
 ASRX_DEV void ld_vec(const void* p, int dtype, int64_t off, float* v, int nvalid) {
   if (nvalid >= V && V > 1) {
     if (dtype == ASRX_F32) {
-      if constexpr (V == 4) { f4_t x = *(const f4_t*)((const float*)p + off); v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3]; return; }
+      if constexpr (V == 4) {
+        const f4_t* a = (const f4_t*)((const float*)p + off);
+        f4_t x = NT ? __builtin_nontemporal_load(a) : *a;
+        v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3];
+        return;
+      }
     } else {
       if constexpr (V == 8) {
-        uint4 u = *(const uint4*)((const bf16_t*)p + off);
-        uint32_t w[4] = {u.x, u.y, u.z, u.w};
+        const v4u_t* a = (const v4u_t*)((const bf16_t*)p + off);
+        const v4u_t u = NT ? __builtin_nontemporal_load(a) : *a;
+        uint32_t w[4] = {u[0], u[1], u[2], u[3]};
 #pragma unroll
         for (int i = 0; i < 4; ++i) { v[2 * i] = bf2f(w[i] & 0xffff); v[2 * i + 1] = bf2f(w[i] >> 16); }
         return;
@@ -39,16 +46,21 @@ ASRX_DEV void ld_vec(const void* p, int dtype, int64_t off, float* v, int nvalid
     v[i] = i < nvalid ? (dtype == ASRX_F32 ? ((const float*)p)[off + i] : bf2f(((const bf16_t*)p)[off + i])) : 0.f;
 }
 
-template <int V>
+template <int V, bool NT = false>
 ASRX_DEV void st_vec(void* p, int dtype, int64_t off, const float* v, int nvalid) {
   if (nvalid >= V && V > 1) {
     if (dtype == ASRX_F32) {
-      if constexpr (V == 4) { *(f4_t*)((float*)p + off) = f4_t{v[0], v[1], v[2], v[3]}; return; }
+      if constexpr (V == 4) {
+        const f4_t x = f4_t{v[0], v[1], v[2], v[3]};
+        if (NT) __builtin_nontemporal_store(x, (f4_t*)((float*)p + off));
+        else *(f4_t*)((float*)p + off) = x;
+        return;
+      }
     } else {
       if constexpr (V == 8) {
-        uint4 u;
-        u.x = pack2bf(v[0], v[1]); u.y = pack2bf(v[2], v[3]); u.z = pack2bf(v[4], v[5]); u.w = pack2bf(v[6], v[7]);
-        *(uint4*)((bf16_t*)p + off) = u;
+        const v4u_t u = {pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7])};
+        if (NT) __builtin_nontemporal_store(u, (v4u_t*)((bf16_t*)p + off));
+        else *(v4u_t*)((bf16_t*)p + off) = u;
         return;
       }
     }
@@ -102,8 +114,9 @@ ASRX_DEV bool is_masked(const SmArgs& a, int b, int q, int key) {
 
 // U rows per lane group per block-wave: every row's loads are issued before the first row reduces, so a wave
 // keeps U x 16 B per lane in flight (the one-row version left HBM idle between a row's load and its store).
-template <int V, int LPR, int NJ, int U>
+template <int V, int LPR, int NJ, int U, int NTM>
 __global__ __launch_bounds__(256) void softmax_fwd_kernel(SmArgs a) {
+  constexpr bool NTL = (NTM & 1) != 0, NTS = (NTM & 2) != 0;
   a.seed = seed_eff(a.seed);
   constexpr int RPW = 64 / LPR;
   const int l = threadIdx.x & 63;
@@ -117,7 +130,7 @@ __global__ __launch_bounds__(256) void softmax_fwd_kernel(SmArgs a) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int k0 = (j * LPR + ll) * V;
-      ld_vec<V>(a.s, a.dtype, rr * a.ld + k0, v[u][j], loadable(a, rr, k0, V));
+      ld_vec<V, NTL>(a.s, a.dtype, rr * a.ld + k0, v[u][j], loadable(a, rr, k0, V));
     }
   }
 #pragma unroll
@@ -164,19 +177,20 @@ __global__ __launch_bounds__(256) void softmax_fwd_kernel(SmArgs a) {
       float o[V];
 #pragma unroll
       for (int i = 0; i < V; ++i) o[i] = v[u][j][i] * inv;
-      st_vec<V>(a.p, a.dtype, rr * a.ld + k0, o, nv);
+      st_vec<V, NTS>(a.p, a.dtype, rr * a.ld + k0, o, nv);
       if (a.pd) {
 #pragma unroll
         for (int i = 0; i < V; ++i)
           o[i] = (a.thr == 0u || attn_keep(a.seed, bh, a.lq, a.lk, q, k0 + i, a.thr)) ? o[i] * a.dscale : 0.f;
-        st_vec<V>(a.pd, a.dtype, rr * a.ld + k0, o, nv);
+        st_vec<V, NTS>(a.pd, a.dtype, rr * a.ld + k0, o, nv);
       }
     }
   }
 }
 
-template <int V, int LPR, int NJ, int U>
+template <int V, int LPR, int NJ, int U, int NTM>
 __global__ __launch_bounds__(256) void softmax_bwd_kernel(SmArgs a, void* ds) {
+  constexpr bool NTL = (NTM & 1) != 0, NTS = (NTM & 2) != 0;
   a.seed = seed_eff(a.seed);
   constexpr int RPW = 64 / LPR;
   const int l = threadIdx.x & 63;
@@ -191,8 +205,8 @@ __global__ __launch_bounds__(256) void softmax_bwd_kernel(SmArgs a, void* ds) {
     for (int j = 0; j < NJ; ++j) {
       const int k0 = (j * LPR + ll) * V;
       const int nv = loadable(a, rr, k0, V);
-      ld_vec<V>(a.p, a.dtype, rr * a.ld + k0, pv[u][j], nv);
-      ld_vec<V>(a.pd, a.dtype, rr * a.ld + k0, gv[u][j], nv);
+      ld_vec<V, NTL>(a.p, a.dtype, rr * a.ld + k0, pv[u][j], nv);
+      ld_vec<V, NTL>(a.pd, a.dtype, rr * a.ld + k0, gv[u][j], nv);
     }
   }
 #pragma unroll
@@ -227,9 +241,19 @@ __global__ __launch_bounds__(256) void softmax_bwd_kernel(SmArgs a, void* ds) {
       float o[V];
 #pragma unroll
       for (int i = 0; i < V; ++i) o[i] = pv[u][j][i] * (gv[u][j][i] - dot) * a.scale2;
-      st_vec<V>(ds, a.dtype, rr * a.ld + k0, o, nv);
+      st_vec<V, NTS>(ds, a.dtype, rr * a.ld + k0, o, nv);
     }
   }
+}
+
+// ASRX_SOFTMAX_NT (A/B switch): bit 0 = non-temporal forward loads, bit 2 = forward stores, bit 1 = backward
+// loads and stores.  Default 4: the forward's probabilities are streamed out non-temporally (cold 30.7 -> 28.7 us
+// at 512 x 249^2 bf16, warm unchanged); non-temporal loads cost the warm case (24.7 -> 26-28 us: the scores a
+// preceding GEMM just wrote sit in the Infinity Cache).  ASRX_SOFTMAX_LPR16 (default 1; 0 = off): rows of
+// 129..256 elements on 16 lanes x 2 vectors (4 rows per wave, two 16-B loads per lane in flight).
+int softmax_nt() {
+  const char* e = getenv("ASRX_SOFTMAX_NT");
+  return e ? atoi(e) : 4;
 }
 
 template <int V, int LPR, int NJ, int U>
@@ -238,8 +262,16 @@ bool try_launch(const SmArgs& a, bool bwd, void* ds, hipStream_t st) {
   constexpr int RPW = 64 / LPR;
   const int64_t waves = (a.rows + RPW * U - 1) / (RPW * U);
   const unsigned blocks = (unsigned)((waves + 3) / 4);
-  if (bwd) hipLaunchKernelGGL((softmax_bwd_kernel<V, LPR, NJ, U>), dim3(blocks), dim3(256), 0, st, a, ds);
-  else hipLaunchKernelGGL((softmax_fwd_kernel<V, LPR, NJ, U>), dim3(blocks), dim3(256), 0, st, a);
+  const int nt = softmax_nt();
+  if (bwd) {
+    if (nt & 2) hipLaunchKernelGGL((softmax_bwd_kernel<V, LPR, NJ, U, 3>), dim3(blocks), dim3(256), 0, st, a, ds);
+    else hipLaunchKernelGGL((softmax_bwd_kernel<V, LPR, NJ, U, 0>), dim3(blocks), dim3(256), 0, st, a, ds);
+  } else {
+    const int m = ((nt & 1) ? 1 : 0) | ((nt & 4) ? 2 : 0);
+#define ASRX_SMF(M) hipLaunchKernelGGL((softmax_fwd_kernel<V, LPR, NJ, U, M>), dim3(blocks), dim3(256), 0, st, a)
+    if (m == 0) ASRX_SMF(0); else if (m == 1) ASRX_SMF(1); else if (m == 2) ASRX_SMF(2); else ASRX_SMF(3);
+#undef ASRX_SMF
+  }
   return true;
 }
 
@@ -263,6 +295,8 @@ int softmax_u() {
 template <int V>
 bool dispatch(const SmArgs& a, bool bwd, void* ds, hipStream_t st) {
   const int u = softmax_u();
+  static const bool lpr16 = [] { const char* e = getenv("ASRX_SOFTMAX_LPR16"); return !(e && e[0] == '0'); }();
+  if (lpr16 && !bwd && V == 8 && a.lk > 128 && try_launch<V, 16, 2, 1>(a, bwd, ds, st)) return true;
   const bool shortrow = u == 4 ? dispatch_u<V, 4>(a, bwd, ds, st)
                       : u == 2 ? dispatch_u<V, 2>(a, bwd, ds, st) : dispatch_u<V, 1>(a, bwd, ds, st);
   return shortrow || try_launch<V, 64, 2, 1>(a, bwd, ds, st) ||

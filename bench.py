@@ -340,6 +340,43 @@ def other_configs(names=("c2", "c5"), reps=5):
                                       "shape": f"B*H={B * H} Lq=Lk={T2} dh={dh}, no mask, eval (no dropout)"}
         del fns
         torch.cuda.empty_cache()
+
+        # the training form at the same shape (streamed forward with dropout 0.1 + the O rounding residual, and the
+        # key-block backward: 4 blocks of 256 keys per head, dQ shares added in fp32)
+        gst = ((d, T2 * d), (d, T2 * d), (2 * d, T2 * 2 * d), (2 * d, T2 * 2 * d))
+
+        def make_train():
+            qkv = (torch.randn(rows, 3 * d, device="cuda", generator=gen) * 0.5).bfloat16()
+            o = torch.empty(rows, d, device="cuda", dtype=torch.bfloat16)
+            o_lo = torch.empty_like(o)
+            do = (torch.randn(rows, d, device="cuda", generator=gen) * 0.1).bfloat16()
+            dq = torch.empty(rows, d, device="cuda", dtype=torch.bfloat16)
+            dkv = torch.empty(rows, 2 * d, device="cuda", dtype=torch.bfloat16)
+            dm = K.dropmask_buffer(B, H, T2, T2, dh, 0.1, "cuda")
+            state = {}
+
+            def fwd():
+                state["lse"] = K.attention_fwd(qkv, qkv[:, d:], qkv[:, 2 * d:], o, B, H, T2, T2, dh, st, d ** -0.5,
+                                               MaskSpec(), 0.1, 77, dropmask=dm, o_lo=o_lo)
+
+            def bwd():
+                K.attention_bwd(qkv, qkv[:, d:], qkv[:, 2 * d:], o, state["lse"], do, dq, dkv, dkv[:, d:], B, H, T2,
+                                T2, dh, st, gst, d ** -0.5, MaskSpec(), 0.1, 77, dropmask=dm, o_lo=o_lo)
+            return fwd, bwd
+        nsets = max(2, -(-COLD_BYTES // (rows * d * 14)))
+        pairs = [make_train() for _ in range(nsets)]
+        tf_ms = _graph_time_ms([f for f, _ in pairs])
+        for f, _ in pairs:
+            f()
+        tb_ms = _graph_time_ms([b_ for _, b_ in pairs])
+        for key, t, fl, note in (("attention_fwd_train", tf_ms, flops, "dropout 0.1, O rounding residual"),
+                                 ("attention_bwd", tb_ms, 2.5 * flops, "dropout 0.1; FLOPs counted as 2.5x fwd")):
+            tt = fl / (t * 1e-3) / 1e12
+            out["c5"][key] = {"bound": "mfma", "achieved": round(tt, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                              "frac": round(tt / PEAK_BF16_TFLOPS, 4), "us": round(t * 1e3, 2),
+                              "shape": f"B*H={B * H} Lq=Lk={T2} dh={dh}, no mask, training: {note}"}
+        del pairs
+        torch.cuda.empty_cache()
     return out
 
 

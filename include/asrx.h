@@ -80,7 +80,8 @@ typedef struct asrx_gemm_desc {
   uint32_t* mask_out; int64_t ld_mask;
   /* kernel family (tests / A-B; 0 = auto): 1 = 256x128 LDS-DMA ring (p3), 3 = register-staged tiles, 4 = 64x64
    * LDS-DMA ring, 5 = 128x64 LDS-DMA ring, 6 = 256x256 LDS-DMA ring (p4), 8 = warp-specialised 256x128 tiles
-   * (ws: 4 MFMA waves + 4 LDS-DMA loader waves; A k-contiguous, N % 128 == 0) — honoured where the family's
+   * (ws: 4 MFMA waves + 4 LDS-DMA loader waves; A k-contiguous, N % 128 == 0), 10 = ws on 64x128 tiles (the
+   * 4096-row decoder GEMMs) — honoured where the family's
    * preconditions hold, else auto.  Every family is a hand-written kernel of this library. */
   int32_t kernel;
 } asrx_gemm_desc;
@@ -300,6 +301,18 @@ int asrx_cross_entropy(const float* logits, int64_t rows, int32_t V, int64_t ld,
  * Elementwise utilities.
  * ------------------------------------------------------------------------------------------------- */
 int asrx_cast(int32_t src_dtype, const void* src, int32_t dst_dtype, void* dst, int64_t n, void* stream);
+/* out[i] (dtype_out) = op(a[i], b[i]) over n contiguous elements (any of a, b, out may alias; ASRX_F32 / ASRX_BF16):
+ *   ASRX_EW_RELU_GRAD  b[i] > 0 ? a[i] : 0        ReLU backward gated by its output b (the standalone FrontEnd's
+ *                                                   conv2 ReLU, model.py:170, torch.where in round 2)
+ *   ASRX_EW_DROPOUT    keep(seed, i) ? a[i] / (1 - p) : 0   dropout backward with the element mask of the GEMM
+ *                                                   dropout epilogues (layers.py:40, the standalone MHA's output)
+ *   ASRX_EW_ADD        a[i] + b[i]                  gradient accumulation (the standalone MHA's K/V input, split
+ *                                                   LayerNorm gradients) */
+#define ASRX_EW_RELU_GRAD 0
+#define ASRX_EW_DROPOUT 1
+#define ASRX_EW_ADD 2
+int asrx_ewise(int32_t op, int32_t dtype_a, const void* a, int32_t dtype_b, const void* b, int32_t dtype_out,
+               void* out, int64_t n, float p, uint64_t seed, void* stream);
 
 /* Power spectrogram of a batch of waveforms (the featuriser of modules/dataset.py:34-55:
  * torchaudio.transforms.Spectrogram(n_fft, center=False) -> |STFT|^power):

@@ -261,31 +261,38 @@ def plan_name(M, N, Kd, bt=False, bias=False, c_f32=False, resid=False, dropout=
     return kernel_name(d)
 
 
+@pytest.mark.parametrize("wk", ["ws", "ws64"])
 @pytest.mark.parametrize("M,N,Kd,bt", [(15936, 512, 2048, 1), (15936, 512, 1536, 1), (300, 256, 192, 1),
-                                        (257, 128, 64, 0), (64, 512, 2048, 1), (1000, 384, 640, 0)])
-def test_gemm_ws_plain(M, N, Kd, bt):
-    """The warp-specialised 256x128 kernel (kernel code 8; chosen automatically for the encoder's plain 512-wide data
-    gradients, K >= 1536): C = A . op(B) in bf16 against an fp64 reference, both B layouts, ragged M (rows past M
-    read as zero, stores masked), and identical to the auto plan at the bench shapes."""
+                                        (257, 128, 64, 0), (64, 512, 2048, 1), (1000, 384, 640, 0),
+                                        (4096, 512, 1536, 1), (4096, 512, 512, 0), (4033, 512, 2048, 1)])
+def test_gemm_ws_plain(M, N, Kd, bt, wk):
+    """The warp-specialised kernel on 256x128 tiles (kernel code 8; chosen automatically for the encoder's plain
+    512-wide data gradients) and on 64x128 tiles (code 10; the decoder's 4096-row ones): C = A . op(B) in bf16
+    against an fp64 reference, both B layouts, ragged M (rows past M read as zero, stores masked), and identical to
+    the auto plan at the bench shapes."""
     g = torch.Generator().manual_seed(M + N + Kd)
     a = bf(torch.randn(M, Kd, generator=g))
     b = bf(torch.randn(Kd, N, generator=g) if bt else torch.randn(N, Kd, generator=g))
     c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     ref = a.double() @ (b.double() if bt else b.double().t())
-    assert plan_name(M, N, Kd, bt=bt, kernel="ws").startswith("gemm_bf16_ws_kernel")
-    K().gemm(a.to(dev), b.to(dev), c, M, N, Kd, lda=Kd, ldb=b.shape[1], ldc=N, b_trans=bool(bt), kernel="ws")
+    kn = plan_name(M, N, Kd, bt=bt, kernel=wk)
+    assert kn.startswith("gemm_bf16_ws_kernel") and kn.endswith("64>" if wk == "ws64" else "256>"), kn
+    K().gemm(a.to(dev), b.to(dev), c, M, N, Kd, lda=Kd, ldb=b.shape[1], ldc=N, b_trans=bool(bt), kernel=wk)
     assert relerr(c.float().cpu(), ref) < 1e-2
-    if bt and N == 512 and Kd >= 1536 and M >= 8192:   # the auto plan takes the same path
+    auto_ws = N == 512 and (M >= 8192 if wk == "ws" else 2048 <= M < 8192)
+    if bt and auto_ws:   # the auto plan takes the same path
         c2 = torch.empty_like(c)
         K().gemm(a.to(dev), b.to(dev), c2, M, N, Kd, lda=Kd, ldb=N, ldc=N, b_trans=True)
         assert torch.equal(c, c2)
 
 
+@pytest.mark.parametrize("wk", ["ws", "ws64"])
 @pytest.mark.parametrize("M,N,Kd,f32,resid,drop", [(15936, 512, 2048, 1, 1, 0), (4096, 512, 2048, 1, 1, 0),
                                                    (300, 256, 128, 1, 1, 0), (257, 128, 64, 1, 0, 0),
                                                    (257, 128, 64, 0, 0, 0), (15936, 512, 512, 1, 1, 1),
-                                                   (700, 384, 256, 1, 1, 1)])
-def test_gemm_ws_bias_resid(M, N, Kd, f32, resid, drop):
+                                                   (700, 384, 256, 1, 1, 1), (4096, 512, 512, 1, 1, 1),
+                                                   (4096, 512, 512, 0, 0, 0)])
+def test_gemm_ws_bias_resid(M, N, Kd, f32, resid, drop, wk):
     """The ws kernel's LDS-staged epilogue: out = x . w^T + bias (+ dropout) (+ fp32 residual, ld_resid != ldc) —
     the FFN2 forward (E_BIAS | E_RESID | E_F32) and the out-projection (+ E_DROP) — forced (kernel code 8) against
     an fp64 reference, and element-for-element against the p3 epilogue on the same inputs (same keep bits; fp32
@@ -301,10 +308,10 @@ def test_gemm_ws_bias_resid(M, N, Kd, f32, resid, drop):
     outs = {}
     for kern in ("ws", "p3"):
         c = torch.empty(M, N, device=dev, dtype=torch.float32 if f32 else torch.bfloat16)
-        K().linear(x.to(dev), w.to(dev), c, bias=bias.to(dev), kernel=kern, **kw)
+        K().linear(x.to(dev), w.to(dev), c, bias=bias.to(dev), kernel=wk if kern == "ws" else kern, **kw)
         outs[kern] = c.float().cpu()
-    kn = plan_name(M, N, Kd, bias=True, c_f32=bool(f32), resid=bool(resid), dropout=bool(drop), kernel="ws")
-    assert kn.startswith("gemm_bf16_ws_kernel"), kn
+    kn = plan_name(M, N, Kd, bias=True, c_f32=bool(f32), resid=bool(resid), dropout=bool(drop), kernel=wk)
+    assert kn.startswith("gemm_bf16_ws_kernel") and kn.endswith("64>" if wk == "ws64" else "256>"), kn
     if drop:   # same keep bits in both kernels; the reference is p3's kept pattern
         keep = (outs["p3"] - (r[:, :N] if resid else 0)) != 0
         ref = torch.where(keep, ref / 0.9, torch.zeros_like(ref))
@@ -452,6 +459,26 @@ def test_reduce_rows_grouped(ngroups):
         assert relerr(out, r) < 1e-5
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_ewise(dt):
+    """asrx_ewise vs torch: ReLU gate, dropout backward (the element mask of asrx_dropout_mask / the GEMM dropout
+    epilogues), add; mixed dtypes and in-place outputs."""
+    g = torch.Generator(device=dev).manual_seed(3)
+    n = 100_003
+    a = torch.randn(n, device=dev, generator=g).to(dt)
+    b = torch.randn(n, device=dev, generator=g).to(dt)
+    out = torch.empty(n, device=dev, dtype=torch.float32)
+    K().ewise(K().EW_RELU_GRAD, a, out, b=b)
+    assert torch.equal(out, torch.where(b > 0, a, torch.zeros((), dtype=dt, device=dev)).float())
+    p, seed = 0.1, 12345
+    K().ewise(K().EW_DROPOUT, a, out, p=p, seed=seed)
+    keep = K().dropout_mask(n, p, seed, dev)
+    assert torch.allclose(out, a.float() * keep / (1 - p), rtol=1e-6, atol=0)
+    c = a.clone()
+    K().ewise(K().EW_ADD, c, c, b=b)
+    assert torch.equal(c, (a.float() + b.float()).to(dt))
+
+
 def test_colsum():
     x = torch.randn(10000, 300)
     out = torch.ones(300, device=dev)
@@ -509,7 +536,7 @@ def attn_variant(request):
                                            (2, 2, 256, 256, "decoder"), (1, 1, 5, 17, "none"),
                                            (1, 2, 999, 999, "none"), (1, 2, 300, 300, "decoder"),
                                            (1, 2, 64, 257, "none"), (2, 2, 513, 1031, "none"),
-                                           (2, 2, 100, 200, "none")])
+                                           (2, 2, 100, 200, "none"), (1, 3, 249, 240, "none")])
 def test_attention_fused(dh, B, H, Lq, Lk, kind, attn_variant):
     from asrx.kernels import MaskSpec
     g = torch.Generator().manual_seed(B * 100 + Lq + Lk + dh)
@@ -554,7 +581,8 @@ def test_attention_fused(dh, B, H, Lq, Lk, kind, attn_variant):
     assert relerr(dq_, qh.grad) < 2e-2
 
 
-@pytest.mark.parametrize("Lq,Lk", [(64, 249), (100, 200), (5, 17), (30, 256), (249, 249), (64, 64)])
+@pytest.mark.parametrize("Lq,Lk", [(64, 249), (100, 200), (5, 17), (30, 256), (249, 249), (64, 64), (250, 229),
+                                   (64, 999), (300, 300), (257, 520)])
 @pytest.mark.parametrize("with_lo", [False, True])
 def test_attention_short_query_block_with_dropout(Lq, Lk, with_lo):
     """Short query blocks without a mask (MODE 0, Lq <= 128: the decoder's cross-attention shape) with dropout
@@ -594,7 +622,7 @@ def test_attention_short_query_block_with_dropout(Lq, Lk, with_lo):
 
 
 @pytest.mark.parametrize("attn_variant", ["auto", "tiled"], indirect=True)
-@pytest.mark.parametrize("L", [40, 249])
+@pytest.mark.parametrize("L", [40, 249, 300])
 @pytest.mark.parametrize("bits", [False, True])
 def test_attention_dense_mask_and_dropout_consistency(L, attn_variant, bits):
     """Dense byte mask (mode 2) equals the structured decoder mask; the dropout the kernels apply in forward AND
@@ -624,9 +652,10 @@ def test_attention_dense_mask_and_dropout_consistency(L, attn_variant, bits):
         ka = attn_keep(seed, B * H, L, L, p)
         nq = (L + 31) // 32
         words = dm.cpu().numpy().view(np.uint32)[:B * H * nq * L].reshape(B * H, nq, L)
-        qwords = dm.cpu().numpy().view(np.uint32)[B * H * nq * L:].reshape(B * H, L, nq)
+        qst = K().qmaj_stride(L)
+        qwords = dm.cpu().numpy().view(np.uint32)[B * H * nq * L:].reshape(B * H, L, qst)
         qbits = (qwords[:, :, :, None] >> np.arange(32, dtype=np.uint32)[None, None, None, :]) & 1
-        assert (qbits.reshape(B * H, L, nq * 32)[:, :, :L].astype(bool) == ka).all()   # query-major copy
+        assert (qbits.reshape(B * H, L, qst * 32)[:, :, :L].astype(bool) == ka).all()   # query-major copy
         bits_np = (words[:, :, None, :] >> np.arange(32, dtype=np.uint32)[None, None, :, None]) & 1
         got = bits_np.reshape(B * H, nq * 32, L)[:, :L, :].astype(bool)
         live = ~masked.expand(B, H, L, L).reshape(B * H, L, L).numpy()   # words of masked-out tiles are never read

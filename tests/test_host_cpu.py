@@ -172,25 +172,29 @@ def test_gemm_kernel_plan_names_without_gpu():
     assert kernel_name(ffn1) == "gemm_bf16_p4_kernel<false, false, 3>"
     assert kernel_name(desc(15936, 12288, 512, bias=True)) == "gemm_bf16_p4_kernel<false, false, 1>"
     # the plain 512-wide data gradients with K >= 1536 take the warp-specialised ws kernel, shorter ones stay on p3
-    assert kernel_name(desc(15936, 512, 2048, bt=1)) == "gemm_bf16_ws_kernel<true, 0>"
-    assert kernel_name(desc(15936, 512, 1536, bt=1)) == "gemm_bf16_ws_kernel<true, 0>"
-    assert kernel_name(desc(15936, 512, 512, bt=1)) == "gemm_bf16_ws_kernel<true, 0>"
-    assert kernel_name(desc(4096, 512, 2048, bt=1)).startswith("gemm_bf16_ring_kernel")
-    assert kernel_name(desc(15936, 512, 512, bias=True)) == "gemm_bf16_ws_kernel<false, 1>"
-    # the FFN2 forward (bias + fp32 residual, fp32 out, K = 2048) on ws; the decoder's 4096-row one is not
+    assert kernel_name(desc(15936, 512, 2048, bt=1)) == "gemm_bf16_ws_kernel<true, 0, 256>"
+    assert kernel_name(desc(15936, 512, 1536, bt=1)) == "gemm_bf16_ws_kernel<true, 0, 256>"
+    assert kernel_name(desc(15936, 512, 512, bt=1)) == "gemm_bf16_ws_kernel<true, 0, 256>"
+    # the decoder's 4096-row ones on ws with 64 x 128 tiles (one per CU)
+    assert kernel_name(desc(4096, 512, 2048, bt=1)) == "gemm_bf16_ws_kernel<true, 0, 64>"
+    assert kernel_name(desc(4096, 512, 512, bt=1)) == "gemm_bf16_ws_kernel<true, 0, 64>"
+    assert kernel_name(desc(1024, 512, 2048, bt=1)).startswith("gemm_bf16_ring_kernel")
+    assert kernel_name(desc(15936, 512, 512, bias=True)) == "gemm_bf16_ws_kernel<false, 1, 256>"
+    # the FFN2 forward (bias + fp32 residual, fp32 out, K = 2048) on ws, the decoder's 4096-row one on 64-row tiles
     ff2 = desc(15936, 512, 2048, bias=True, c_dtype=F32)
     ff2.resid, ff2.ld_resid, ff2.resid_dtype = 5 << 20, 512, F32
-    assert kernel_name(ff2) == "gemm_bf16_ws_kernel<false, 81>"
+    assert kernel_name(ff2) == "gemm_bf16_ws_kernel<false, 81, 256>"
     ff2.m = 4096
-    assert kernel_name(ff2).startswith("gemm_bf16_ring_kernel")
+    assert kernel_name(ff2) == "gemm_bf16_ws_kernel<false, 81, 64>"
     wg = desc(2048, 512, 15936, at=1, bt=1, c_dtype=F32)
     wg.tile = 128                     # as kernels.wgrad_plan sets it
     assert kernel_name(wg) == "gemm_bf16_kernel<128, 128, true, true, true>"
     assert kernel_name(desc(64, 64, 64, in_dtype=F32, c_dtype=F32)) == "gemm_f32_kernel<false, false>"
-    for code in (7, 10):              # no library family exists any more: retired codes plan automatically
-        d7 = desc(15936, 512, 2048, bt=1)
-        d7.kernel = code
-        assert kernel_name(d7) == "gemm_bf16_ws_kernel<true, 0>"
+    d7 = desc(15936, 512, 2048, bt=1)
+    d7.kernel = 7                     # no library family exists any more: the retired code plans automatically
+    assert kernel_name(d7) == "gemm_bf16_ws_kernel<true, 0, 256>"
+    d7.kernel = 10                    # ws on 64 x 128 tiles, forced
+    assert kernel_name(d7) == "gemm_bf16_ws_kernel<true, 0, 64>"
     forced = desc(15936, 1536, 512)
     forced.kernel = 3  # noqa                 # asrx_gemm_desc.kernel: register-staged family
     assert kernel_name(forced).startswith("gemm_bf16_kernel<128, 128, false, false, true>")
