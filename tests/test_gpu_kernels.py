@@ -643,7 +643,13 @@ def test_attention_dense_mask_and_dropout_consistency(L, attn_variant, bits):
     o2 = torch.empty_like(o1)
     K().attention_fwd(qd, kvd, kvd[..., d:], o1, B, H, L, L, dh, st, d ** -0.5, s1)
     K().attention_fwd(qd, kvd, kvd[..., d:], o2, B, H, L, L, dh, st, d ** -0.5, s2)
-    assert torch.equal(o1, o2)
+    if L <= 256 or attn_variant == "tiled":   # one kernel for both mask forms
+        assert torch.equal(o1, o2)
+    else:   # past 256 keys the structured mask streams, a dense byte mask takes the tiled kernel
+        assert relerr(o1.float().cpu(), o2.float().cpu()) < 1e-2
+        # padded queries: exact zeros
+        assert torch.all(o1.view(B, L, d).cpu()[valid[:, :L] < 1] == 0)
+        assert torch.all(o2.view(B, L, d).cpu()[valid[:, :L] < 1] == 0)
     p, seed = 0.3, 1234
     o3 = torch.empty_like(o1)
     dm = K().dropmask_buffer(B, H, L, L, dh, p, dev) if bits else None

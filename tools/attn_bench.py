@@ -19,22 +19,25 @@ B, H, DH = 64, 8, 64
 D = H * DH
 
 
-def case(name, Lq, Lk, causal):
+def case(name, Lq, Lk, causal, kv_width=2 * D):
+    """kv_width: row width of the K/V tensor (2 D = a head's rows 2 KB apart; 12 * 2 D = the model's all-layer cross
+    K/V tensor, rows 24 KB apart, this case reading one layer's slice)."""
     g = torch.Generator(device="cuda").manual_seed(0)
     q = torch.randn(B * Lq, D, device="cuda", generator=g).bfloat16()
-    kv = torch.randn(B * Lk, 2 * D, device="cuda", generator=g).bfloat16()
+    kv = torch.randn(B * Lk, kv_width, device="cuda", generator=g).bfloat16()[:, :2 * D]
     o = torch.empty(B * Lq, D, device="cuda", dtype=torch.bfloat16)
     do = torch.randn(B * Lq, D, device="cuda", generator=g).bfloat16()
     dq = torch.empty_like(q)
-    dkv = torch.empty_like(kv)
     if causal:
         valid = torch.ones(B, Lq, device="cuda", dtype=torch.uint8)
         valid[:, Lq - 8:] = 0
         spec = MaskSpec(1, True, valid, valid, valid.stride(0))
     else:
         spec = MaskSpec()
-    st = ((D, Lq * D), (2 * D, Lk * 2 * D), (2 * D, Lk * 2 * D), (D, Lq * D))
-    gst = ((D, Lq * D), (D, Lq * D), (2 * D, Lk * 2 * D), (2 * D, Lk * 2 * D))
+    kw = kv_width
+    st = ((D, Lq * D), (kw, Lk * kw), (kw, Lk * kw), (D, Lq * D))
+    dkv = torch.empty(B * Lk, kw, device="cuda", dtype=torch.bfloat16)[:, :2 * D]
+    gst = ((D, Lq * D), (D, Lq * D), (kw, Lk * kw), (kw, Lk * kw))
     p, seed = 0.1, 77
     dm = K.dropmask_buffer(B, H, Lq, Lk, DH, p, "cuda")
     state = {}
@@ -68,7 +71,7 @@ def main():
     args = ap.parse_args()
     os.environ["ASRX_ATTN_KERNEL"] = args.variant
     cases = {"enc": ("enc_self", 249, 249, False), "cross": ("cross", 64, 249, False),
-             "dec": ("dec_self", 64, 64, True)}
+             "cross24k": ("cross24k", 64, 249, False, 12 * 2 * D), "dec": ("dec_self", 64, 64, True)}
     if args.sweep:
         for lq in (32, 64, 128, 192, 249):
             cases[f"s{lq}"] = (f"lq{lq}", lq, 249, False)
