@@ -1484,6 +1484,12 @@ bool ws64_auto() {
   static const bool on = [] { const char* e = getenv("ASRX_WS64"); return !(e && e[0] == '0'); }();
   return on;
 }
+// ASRX_WS_QKV=0 keeps the 1536-wide Q/K/V projection forwards (bias epilogue) on p3 (A/B switch; default on):
+// tools/blas_ref.py, same box: encoder 42.3 (p3) / 40.8 (p4) -> 37.1 us on ws, decoder (4096 rows) 15.7 -> 12.7 us
+bool ws_qkv_auto() {
+  static const bool on = [] { const char* e = getenv("ASRX_WS_QKV"); return !(e && e[0] == '0'); }();
+  return on;
+}
 // ASRX_WS_MIN_K: shortest reduction planned on ws (A/B; every K from 512 up measured faster than p3 at c3)
 int ws_min_k() {
   static const int k = [] { const char* e = getenv("ASRX_WS_MIN_K"); return e ? atoi(e) : 64; }();
@@ -1576,7 +1582,9 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
   const bool ws_ok = dma_ok && !d->a_trans && batch == 1 && splitk == 1 && d->n % WS_BN == 0 && d->k >= BK &&
                      !d->rowsum_a && !d->mask_out && !d->sc_outer && !d->sc_inner && epi != E_GENERIC &&
                      ws_instantiated(d->b_trans, epi);
-  if (ws_ok && (kvar == 8 || (kvar == 0 && ws_auto() && d->n == 512 && d->m >= 8192 && d->k >= ws_min_k()))) {
+  const bool ws_qkv = ws_qkv_auto() && d->n == 1536 && d->m >= 4096 && !d->b_trans && (epi & E_BIAS) != 0;
+  if (ws_ok && (kvar == 8 || (kvar == 0 && ws_auto() && ((d->n == 512 && d->m >= 8192 && d->k >= ws_min_k()) ||
+                                                          ws_qkv)))) {
     pl.use = 11;
     pl.epi = epi;
     pl.ntiles = ((d->m + WS_BM - 1) / WS_BM) * (d->n / WS_BN);

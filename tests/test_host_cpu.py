@@ -160,9 +160,11 @@ def test_gemm_kernel_plan_names_without_gpu():
             d.bias = 4 << 20
         return d
 
-    # wide outputs (>= 400 256x256 tiles) take p4; the Q/K/V projection (378) p3 (the persistent ws kernel, wsp,
-    # only when forced or with ASRX_WSP)
-    assert kernel_name(desc(15936, 1536, 512, bias=True)) == "gemm_bf16_p3_kernel<false, false, 1>"
+    # wide outputs (>= 400 256x256 tiles) take p4; the Q/K/V projection forward (bias) the ws kernel, encoder and
+    # decoder (the persistent ws kernel, wsp, only when forced or with ASRX_WSP)
+    assert kernel_name(desc(15936, 1536, 512, bias=True)) == "gemm_bf16_ws_kernel<false, 1, 256>"
+    assert kernel_name(desc(4096, 1536, 512, bias=True)) == "gemm_bf16_ws_kernel<false, 1, 256>"
+    assert kernel_name(desc(15936, 1536, 512)) == "gemm_bf16_p3_kernel<false, false, 0>"
     forced = desc(15936, 1536, 512, bias=True)
     forced.kernel = 9
     assert kernel_name(forced) == "gemm_bf16_wsp_kernel<false, 1>"
