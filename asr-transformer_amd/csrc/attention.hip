@@ -805,6 +805,207 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
   }
 }
 
+// Short query blocks without a mask (MODE 0, Lq <= 64, Lk <= 256: the decoder's cross-attention, 64 queries over
+// the encoder's 249 frames).  The resident kernel gives such a head 2 query waves of its 8 — one wave per SIMD walks
+// all 8 key tiles with nothing to hide its dependent softmax chains (phase stamps: ~1.6k cycles per tile).  Here
+// the 8 waves are 2 query groups x 4 key quarters: wave (qg, kq) runs key tiles 2 kq, 2 kq + 1 for queries
+// 32 qg .. + 31 and leaves a partial (max m_j, sum l_j, unnormalised O_j); after a barrier the partials meet in
+// the dead K/V image and the kq = 0 wave of each group combines them,
+//   O = sum_j 2^(m_j - M) O_j / sum_j 2^(m_j - M) l_j,   M = max_j m_j   (scores in the log2 domain),
+// and stores O, its rounding residual and lse.  Dropout keep words: the query-major W8 layout (2 words per query
+// and quarter); the raw-score max and the AND-mask dropout as in the streamed kernel.
+template <bool DROP>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
+void attn_fwd_kq_kernel(AttnArgs a, const uint32_t* qmaj) {
+  __shared__ __attribute__((aligned(1024))) bf16_t sk[R_MAXK * 64];
+  __shared__ __attribute__((aligned(1024))) bf16_t sv[R_MAXK * 64];
+  __shared__ __attribute__((aligned(16))) uint2 smask[16];
+  __shared__ __attribute__((aligned(16))) float sml[8][2][2][16];   // [wave][m | l][qs][query lane]
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, li = l & 15;
+  const int qg = w >> 2, kq = w & 3;
+  const int nkt = (a.Lk + 31) >> 5, nk = nkt * 32, np = (nk + 63) >> 6;
+  const int nkw = nkt;
+  const int qw0 = qg * 32;
+  const bf16_t* Kb = a.k + b * a.kb + h * 64;
+  const bf16_t* Vb = a.v + b * a.vb + h * 64;
+  // loads: Q fragments (4), keep words of this wave's two key tiles (2), then the K/V pieces
+  s8_t qf[2][2];
+  uint32_t dw[2][2];
+#pragma unroll
+  for (int qs = 0; qs < 2; ++qs) {
+    const int qc = min(qw0 + 16 * qs + li, a.Lq - 1);
+    const bf16_t* qp = a.q + b * a.qb + (int64_t)qc * a.qr + h * 64 + 8 * g;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) qf[qs][c] = ld128_asm(qp + 32 * c);
+  }
+#pragma unroll
+  for (int qs = 0; qs < 2; ++qs) {
+    const int qc = min(qw0 + 16 * qs + li, a.Lq - 1);
+    const uint32_t* dp = DROP ? qmaj + ((int64_t)bh * a.Lq + qc) * nkw + min(2 * kq, nkw - 1) : (const uint32_t*)a.q;
+    const uint2 v = ld64_asm(dp);   // words 2 kq, 2 kq + 1 (nkw is 8 when the W8 layout is used)
+    dw[qs][0] = v.x;
+    dw[qs][1] = v.y;
+  }
+  {
+    const asrxg::v4i_t ksrd = asrxg::make_srd(Kb, ((int64_t)(a.Lk - 1) * a.kr + 64) * 2);
+    const asrxg::v4i_t vsrd = asrxg::make_srd(Vb, ((int64_t)(a.Lk - 1) * a.vr + 64) * 2);
+    const int rl = l >> 3, sl = l & 7;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i >= np) break;   // workgroup-uniform
+      const int r = 64 * i + 8 * w + rl;
+      asrxg::dma16_asm(sk + (64 * i + 8 * w) * 64, ksrd, (uint32_t)(r * a.kr + 8 * kslot(r, sl)) * 2u);
+      asrxg::dma16_asm(sv + (64 * i + 8 * w) * 64, vsrd, (uint32_t)(r * a.vr + 8 * vslot(r, sl)) * 2u);
+    }
+  }
+  if (threadIdx.x < 16) {
+    const uint32_t n = threadIdx.x;
+    smask[n] = make_uint2(((n & 1) ? 0xffffu : 0u) | ((n & 2) ? 0xffff0000u : 0u),
+                          ((n & 4) ? 0xffffu : 0u) | ((n & 8) ? 0xffff0000u : 0u));
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int qs = 0; qs < 2; ++qs) {
+    pin(qf[qs][0]);
+    pin(qf[qs][1]);
+    pin(dw[qs][0]);
+    pin(dw[qs][1]);
+    if (!DROP) dw[qs][0] = dw[qs][1] = 0xffffffffu;
+  }
+  lds_barrier();
+
+  const float sc2 = a.scale2;
+  f4_t o[4][2];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) o[u][0] = o[u][1] = f4_t{0.f, 0.f, 0.f, 0.f};
+  float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int kt = 2 * kq + j;
+    if (kt >= nkt) break;   // wave-uniform
+    f4_t sc[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const bf16_t* kr = sk + (kt * 32 + 16 * t + li) * 64;
+      const s8_t k0 = lds_b128(kr + 8 * (g ^ (li & 7))), k1 = lds_b128(kr + 8 * ((g + 4) ^ (li & 7)));
+#pragma unroll
+      for (int qs = 0; qs < 2; ++qs) sc[t][qs] = mfma32(k1, qf[qs][1], mfma32(k0, qf[qs][0], f4_t{0.f, 0.f, 0.f, 0.f}));
+    }
+    if (kt * 32 + 32 > a.Lk) {   // keys past Lk (zero rows of the image)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool bad = kt * 32 + 16 * t + 4 * g + r >= a.Lk;
+          sc[t][0][r] = bad ? -INFINITY : sc[t][0][r];
+          sc[t][1][r] = bad ? -INFINITY : sc[t][1][r];
+        }
+    }
+    s4_t pf[2][2];
+#pragma unroll
+    for (int qs = 0; qs < 2; ++qs) {
+      float mt = fmaxf(fmaxf(fmaxf(sc[0][qs][0], sc[0][qs][1]), fmaxf(sc[0][qs][2], sc[0][qs][3])),
+                       fmaxf(fmaxf(sc[1][qs][0], sc[1][qs][1]), fmaxf(sc[1][qs][2], sc[1][qs][3])));
+      mt = xmax4(mt);
+      const float m_new = fmaxf(m_run[qs], mt);
+      const float m_use = m_new == -INFINITY ? 0.f : m_new;
+      if (__ballot(m_new != m_run[qs])) {
+        const float alpha = exp2_raw((m_run[qs] - m_use) * sc2);
+        l_run[qs] *= alpha;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) o[u][qs] *= alpha;
+        m_run[qs] = m_new;
+      }
+      const float nm = -m_use * sc2;
+      float rs = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        f4_t e;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          e[r] = exp2_raw(fmaf(sc[t][qs][r], sc2, nm));
+          rs += e[r];
+        }
+        s4_t pk = to_bf4(e);
+        if constexpr (DROP) {
+          const uint2 mk = smask[(dw[qs][j] >> (16 * t + 4 * g)) & 15u];
+          u2_t pu = __builtin_bit_cast(u2_t, pk);
+          pu[0] &= mk.x;
+          pu[1] &= mk.y;
+          pk = __builtin_bit_cast(s4_t, pu);
+        }
+        pf[t][qs] = pk;
+      }
+      l_run[qs] += xsum4(rs);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int vr = kt * 32 + 4 * g + (li >> 2);
+      const bf16_t* vp = sv + vr * 64 + 8 * vslot(vr, 2 * u + ((li >> 1) & 1)) + 4 * (li & 1);
+      const s8_t vt = cat8(lds_tr(vp), lds_tr(vp + 16 * 64));
+#pragma unroll
+      for (int qs = 0; qs < 2; ++qs) o[u][qs] = mfma32(vt, cat8(pf[0][qs], pf[1][qs]), o[u][qs]);
+    }
+  }
+  // ---- partials: (m, l) per query in sml, O_j (fp32, this lane's 32 values) in the dead K/V image
+  __syncthreads();   // every wave is done with the K/V image
+  float* spo = (float*)sk;   // [wave][32 values][64 lanes]: 8 KiB per wave, 64 KiB in all (sk + sv)
+  if (g == 0) {
+#pragma unroll
+    for (int qs = 0; qs < 2; ++qs) {
+      sml[w][0][qs][li] = m_run[qs] == -INFINITY ? -INFINITY : m_run[qs] * sc2;
+      sml[w][1][qs][li] = l_run[qs];
+    }
+  }
+  if (kq != 0) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int qs = 0; qs < 2; ++qs)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) spo[(w * 32 + (u * 2 + qs) * 4 + r) * 64 + l] = o[u][qs][r];
+  }
+  __syncthreads();
+  if (kq != 0 || qw0 >= a.Lq) return;
+  const float dsc = DROP ? a.dscale : 1.f;
+#pragma unroll
+  for (int qs = 0; qs < 2; ++qs) {
+    float mj[4], M = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      mj[j] = sml[w + j][0][qs][li];
+      M = fmaxf(M, mj[j]);
+    }
+    const float Mu = M == -INFINITY ? 0.f : M;
+    float L = 0.f, fj[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      fj[j] = exp2_raw(mj[j] - Mu);   // (an empty quarter: 2^-inf = 0)
+      L += fj[j] * sml[w + j][1][qs][li];
+    }
+    f4_t oc[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) oc[u] = o[u][qs] * fj[0];
+#pragma unroll
+    for (int j = 1; j < 4; ++j)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) oc[u][r] += fj[j] * spo[((w + j) * 32 + (u * 2 + qs) * 4 + r) * 64 + l];
+    const int q = qw0 + 16 * qs + li;
+    if (q >= a.Lq) continue;
+    const bool live = L > 0.f;
+    const float inv = live ? dsc / L : 0.f;
+    const int64_t oo = b * a.ob + (int64_t)q * a.orr + h * 64 + 4 * g;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      store_o4(a.o + oo + 16 * u, a.o_lo ? a.o_lo + oo + 16 * u : nullptr, oc[u][0] * inv, oc[u][1] * inv,
+               oc[u][2] * inv, oc[u][3] * inv);
+    if (g == 0 && a.lse) a.lse[(int64_t)bh * a.Lq + q] = live ? Mu + log2f(L) : INFINITY;
+  }
+}
+
 // One 4-byte-per-lane LDS-DMA (buffer_load_dword ... lds: lane l's dword lands at M0 + 4 l), as inline asm like
 // asrxg::dma16_asm (counted by the kernel's own vmcnt waits).
 ASRX_DEV void dma4_asm(const void* lds_dst, asrxg::v4i_t srd, uint32_t voff) {
@@ -1541,6 +1742,14 @@ extern "C" int asrx_attention_fwd(const asrx_attn_desc* d, void* stream) {
     dim3 grid((a.Lq + 255) / 256, a.B * a.H);
     static const bool w8ok = [] { const char* e = getenv("ASRX_ATTN_W8"); return !(e && e[0] == '0'); }();
     const bool w8 = w8ok && qmaj && ((a.Lk + 31) >> 5) == 8 && ((uintptr_t)qmaj % 16) == 0;
+    // short query blocks (the decoder's cross-attention): 2 query groups x 4 key quarters per head
+    static const bool kq_ok = [] { const char* e = getenv("ASRX_ATTN_KQ"); return !(e && e[0] == '0'); }();
+    if (kq_ok && a.mode == 0 && a.Lq <= 64 && (!qmaj || (((a.Lk + 31) >> 5) == 8 && (uintptr_t)qmaj % 8 == 0))) {
+      if (qmaj) hipLaunchKernelGGL((attn_fwd_kq_kernel<true>), grid, dim3(512), 0, st, a, qmaj);
+      else hipLaunchKernelGGL((attn_fwd_kq_kernel<false>), grid, dim3(512), 0, st, a, qmaj);
+      ASRX_CHECK_LAUNCH();
+      return ASRX_OK;
+    }
     if (a.mode == 0 && w8) hipLaunchKernelGGL((attn_fwd_res_kernel<0, true>), grid, dim3(512), 0, st, a, qmaj);
     else if (a.mode == 0) hipLaunchKernelGGL(attn_fwd_res_kernel<0>, grid, dim3(512), 0, st, a, qmaj);
     else if (a.mode == 1) hipLaunchKernelGGL(attn_fwd_res_kernel<1>, grid, dim3(512), 0, st, a, qmaj);

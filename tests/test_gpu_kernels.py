@@ -536,7 +536,8 @@ def attn_variant(request):
                                            (2, 2, 256, 256, "decoder"), (1, 1, 5, 17, "none"),
                                            (1, 2, 999, 999, "none"), (1, 2, 300, 300, "decoder"),
                                            (1, 2, 64, 257, "none"), (2, 2, 513, 1031, "none"),
-                                           (2, 2, 100, 200, "none"), (1, 3, 249, 240, "none")])
+                                           (2, 2, 100, 200, "none"), (1, 3, 249, 240, "none"),
+                                           (2, 2, 64, 100, "none"), (2, 3, 33, 256, "none")])
 def test_attention_fused(dh, B, H, Lq, Lk, kind, attn_variant):
     from asrx.kernels import MaskSpec
     g = torch.Generator().manual_seed(B * 100 + Lq + Lk + dh)
