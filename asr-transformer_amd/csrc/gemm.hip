@@ -715,11 +715,10 @@ ASRX_DEV void p4_body(const GemmArgs& g, const TileSeq tl, int split, int z, uns
     //  no faster with loads and slower without)
     const unsigned char* ln = lds + (cb == NST - 1 ? 0 : cb + 1) * STAGE;
     asm volatile("" : "+v"(S));
-    const bool more = s + 1 < total;
-    if (more) {
+    // (the next step's reads are unconditional: after the last step they read the next ring buffer, unused — a
+    //  guard per fragment split phase B into branch-separated blocks of TN MFMAs)
 #pragma unroll
-      for (int i = 0; i < TN; ++i) fb0[i] = p4_frag<BN, BT>(ln + PA_BYTES, wn + 16 * i, 0, S);
-    }
+    for (int i = 0; i < TN; ++i) fb0[i] = p4_frag<BN, BT>(ln + PA_BYTES, wn + 16 * i, 0, S);
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
 #pragma unroll
@@ -730,7 +729,7 @@ ASRX_DEV void p4_body(const GemmArgs& g, const TileSeq tl, int split, int z, uns
           for (int e = 0; e < 8; ++e) rs[j] += bf2f((bf16_t)fa1[j][e]);
         }
       }
-      if (more) fa0[j] = p4_frag<P_BM, AT>(ln, wm + 16 * j, 0, S);
+      fa0[j] = p4_frag<P_BM, AT>(ln, wm + 16 * j, 0, S);
     }
     P4_ROLL_ORDER();
     if (last) {

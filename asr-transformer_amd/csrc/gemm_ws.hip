@@ -142,16 +142,15 @@ do {                                                                            
     // ---- phase B: k-slice 1 MFMAs of step s | k-slice 0 fragment reads of step s + 1
     const unsigned char* ln = lds + nbo;
     asm volatile("" : "+v"(S));
-    const bool more = s + 1 < nk;
-    if (more) {
+    // (unconditional: after the last step they read the next ring buffer, unused — a guard per fragment split
+    //  this phase into 8 branch-separated blocks of 4 MFMAs)
 #pragma unroll
-      for (int i = 0; i < TN; ++i) fb0[i] = p4_frag<C::BN, BT>(ln + C::PA, wn + 16 * i, 0, S);
-    }
+    for (int i = 0; i < TN; ++i) fb0[i] = p4_frag<C::BN, BT>(ln + C::PA, wn + 16 * i, 0, S);
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
 #pragma unroll
       for (int i = 0; i < TN; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[i], fa1[j], acc[i][j], 0, 0, 0);
-      if (more) fa0[j] = p4_frag<BM, AT>(ln, wm + 16 * j, 0, S);
+      fa0[j] = p4_frag<BM, AT>(ln, wm + 16 * j, 0, S);
     }
     WS_ROLL_ORDER();
     cbo = nbo;
@@ -476,16 +475,13 @@ __global__ __launch_bounds__(512) void gemm_bf16_wsp_kernel(GemmArgs g, int ntil
     }
     const unsigned char* ln = lds + nbo;
     asm volatile("" : "+v"(S));
-    const bool more = s + 1 < total;
-    if (more) {
 #pragma unroll
-      for (int i = 0; i < TN; ++i) fb0[i] = p4_frag<WS_BN, BT>(ln + WS_PA, wn + 16 * i, 0, S);
-    }
+    for (int i = 0; i < TN; ++i) fb0[i] = p4_frag<WS_BN, BT>(ln + WS_PA, wn + 16 * i, 0, S);   // (unconditional, as in ws)
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
 #pragma unroll
       for (int i = 0; i < TN; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[i], fa1[j], acc[i][j], 0, 0, 0);
-      if (more) fa0[j] = p4_frag<WS_BM, false>(ln, wm + 16 * j, 0, S);
+      fa0[j] = p4_frag<WS_BM, false>(ln, wm + 16 * j, 0, S);
     }
     WSP_ROLL_ORDER();
     if (kk == nk - 1) {
