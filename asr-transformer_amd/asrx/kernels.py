@@ -219,6 +219,7 @@ GROUPED_TABLE_KERNEL = "gemm_bf16_grouped_dev_kernel<true, true>"
 GROUPED_P3_KERNELS = ("gemm_bf16_p3g_kernel<64>", "gemm_bf16_p3g_kernel<96>")
 GROUPED_P4_KERNELS = ("gemm_bf16_p4g_kernel<64>", "gemm_bf16_p4g_kernel<96>")
 GROUPED_WS_KERNELS = ("gemm_bf16_wsg_kernel<64>", "gemm_bf16_wsg_kernel<96>")
+GROUPED_WSQ_KERNELS = ("gemm_bf16_wsgq_kernel<64>", "gemm_bf16_wsgq_kernel<96>")
 
 
 def wgrad_groupable(dy, x, wgrad):
@@ -356,7 +357,10 @@ def _grouped_xcd(items, common, kind="p3"):
     common.relu = cvec
     o1 = ents.nbytes
     o2 = o1 + (tmap.nbytes + 63) // 64 * 64
-    n_all = (o2 + block_tile.nbytes + 3) // 4 * 4
+    # ws tiles: 8 per-XCD queue counters after the block map (zeroed by this upload, i.e. on every launch / replay)
+    o3 = (o2 + block_tile.nbytes + 63) // 64 * 64
+    queue = code == 5 and WGRAD_QUEUE and len(block_tile) % 8 == 0
+    n_all = o3 + 64 if queue else (o2 + block_tile.nbytes + 3) // 4 * 4
     host = np.zeros(n_all, dtype=np.uint8)
     host[:o1] = ents.view(np.uint8).reshape(-1)
     host[o1:o1 + tmap.nbytes] = tmap.view(np.uint8)
@@ -364,6 +368,8 @@ def _grouped_xcd(items, common, kind="p3"):
     dev = torch.empty(n_all, dtype=torch.uint8, device=items[0][0].device)
     upload(dev, host)
     base = dev.data_ptr()
+    if queue:
+        common.workspace, common.workspace_elems = base + o3, 16
 
     def launch():
         call("asrx_gemm_grouped_xcd", ctypes.byref(common), base, base + o1, base + o2, len(items), start,
@@ -378,6 +384,9 @@ WGRAD_XCD = os.environ.get("ASRX_WGRAD_XCD", "1") != "0"
 # launch is the cross K/V group (96 long tiles) plus short decoder tiles: whole groups put all 96 on one XCD's 32 CUs
 # (three rounds, modelled makespan 747 K-steps) where packed 32-tile chunks spread them (313)
 WGRAD_PACK = os.environ.get("ASRX_WGRAD_PACK", "1") == "1"
+# ws grouped launch from persistent workgroups on per-XCD tile queues (ASRX_WGRAD_QUEUE=0: one workgroup per tile,
+# started by the in-order dispatcher)
+WGRAD_QUEUE = os.environ.get("ASRX_WGRAD_QUEUE", "1") == "1"
 
 
 def linear_wgrad_grouped(items, *, beta=1.0, kind=None):
@@ -391,7 +400,8 @@ def linear_wgrad_grouped(items, *, beta=1.0, kind=None):
     common.alpha, common.beta = 1.0, beta
     p3 = _grouped_p3_ok(items, beta)
     kind = kind or WGRAD_KIND
-    kname = ({"p4": GROUPED_P4_KERNELS, "ws": GROUPED_WS_KERNELS}.get(kind, GROUPED_P3_KERNELS)[beta == 1.0] if p3
+    wsk = GROUPED_WSQ_KERNELS if WGRAD_QUEUE else GROUPED_WS_KERNELS
+    kname = ({"p4": GROUPED_P4_KERNELS, "ws": wsk}.get(kind, GROUPED_P3_KERNELS)[beta == 1.0] if p3
              else GROUPED_TABLE_KERNEL)
     probe = PROBE
     if probe is not None and probe.active and probe.log is not None:

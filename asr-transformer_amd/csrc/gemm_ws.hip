@@ -1,7 +1,13 @@
 // Warp-specialised bf16 GEMM ("ws") for the one-round N = 512 GEMMs of the encoder (gfx950, MFMA 16x16x32).
 // Replaces the reference's nn.Linear forward of FeedForward.unsqueeze (layers.py:51, + the residual add of
 // model.py:24) and the data gradients of the Q/K/V and FFN1 projections (layers.py:10-12,48 backward, train.py:34).
+#include <algorithm>
+
 #include "gemm_common.h"
+
+// tools only: per-block trace of a grouped weight-gradient launch (ASRX_GEMM_DBG & 128; asrx_ws_trace_read)
+constexpr int WS_TRACE_BLOCKS = 8192;
+__device__ unsigned long long g_ws_trace[4 * WS_TRACE_BLOCKS];
 
 namespace {
 using namespace asrxg;
@@ -334,15 +340,14 @@ __global__ __launch_bounds__(512) void gemm_bf16_ws_kernel(GemmArgs g, int ntile
 // block -> tile through block_tile (the host's XCD-aware layout, kernels.xcd_plan) and tile -> group through
 // tile_group; the bias gradient (row sums of dY^T) fused.  Layout-identical table entries to the p3 / p4 grouped
 // kernels (asrx_gemm_group_dev).
+// One grouped tile (tile index t_all of the table; slot = its position in the block -> tile map, the trace index).
 template <int EPI>
-__global__ __launch_bounds__(512) void gemm_bf16_wsg_kernel(const GroupEnt* __restrict__ ents,
-                                                            const uint16_t* __restrict__ tile_group,
-                                                            const uint16_t* __restrict__ block_tile, int ntiles,
-                                                            int dbg) {
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[WS_LDS];
-  const int tid = block_tile ? (int)block_tile[blockIdx.x] : (int)blockIdx.x;
-  if (tid >= ntiles) return;
-  const int gi = __builtin_amdgcn_readfirstlane((int)tile_group[tid]);
+ASRX_DEV void wsg_tile(const GroupEnt* __restrict__ ents, const uint16_t* __restrict__ tile_group, int t_all, int slot,
+                       int dbg, unsigned char* lds) {
+  // tools only (ASRX_GEMM_DBG & 128): per-tile start / end real time, XCD, CU and tile into g_ws_trace
+  const bool trace = (dbg & 128) && threadIdx.x == 0 && slot < WS_TRACE_BLOCKS;
+  const uint64_t t_start = trace ? __builtin_amdgcn_s_memrealtime() : 0;
+  const int gi = __builtin_amdgcn_readfirstlane((int)tile_group[t_all]);
   const GroupEnt e = ents[gi];
   GemmArgs g = {};
   g.M = e.m; g.N = e.n; g.K = e.k;
@@ -351,9 +356,60 @@ __global__ __launch_bounds__(512) void gemm_bf16_wsg_kernel(const GroupEnt* __re
   g.splitk = 1; g.k_per_split = e.k; g.cvec = 1;
   g.rowsum = e.rowsum;
   g.dbg = dbg & 9;
-  const int t = tid - e.tile_start;
+  const int t = t_all - e.tile_start;
   const int ntn = (e.n + WS_BN - 1) / WS_BN;
   ws_tile<true, true, EPI>(g, (t / ntn) * WS_BM, (t % ntn) * WS_BN, e.rowsum != nullptr && (t % ntn) == 0, lds);
+  if (trace) {
+    const uint32_t xcc = __builtin_amdgcn_s_getreg(20 | (0 << 6) | (15 << 11)) & 15u;   // HW_REG_XCC_ID
+    unsigned long long* r = g_ws_trace + 4 * slot;
+    r[0] = t_start;
+    r[1] = __builtin_amdgcn_s_memrealtime();
+    r[2] = (unsigned long long)xcc | ((unsigned long long)__smid() << 8) | ((unsigned long long)t_all << 32);
+    r[3] = (unsigned long long)e.k | ((unsigned long long)gi << 32) | ((unsigned long long)blockIdx.x << 48);
+  }
+}
+
+// Grouped weight gradients dW (+)= dY^T X of every layer in ONE launch on ws tiles: one 256x128 tile per workgroup,
+// block -> tile through block_tile (the host's XCD-aware layout, kernels.xcd_plan) and tile -> group through
+// tile_group; the bias gradient (row sums of dY^T) fused.  Layout-identical table entries to the p3 / p4 grouped
+// kernels (asrx_gemm_group_dev).
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_bf16_wsg_kernel(const GroupEnt* __restrict__ ents,
+                                                            const uint16_t* __restrict__ tile_group,
+                                                            const uint16_t* __restrict__ block_tile, int ntiles,
+                                                            int dbg) {
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[WS_LDS];
+  const int tid = block_tile ? (int)block_tile[blockIdx.x] : (int)blockIdx.x;
+  if (tid >= ntiles) return;
+  wsg_tile<EPI>(ents, tile_group, tid, (int)blockIdx.x, dbg, lds);
+}
+
+// The same tiles from PERSISTENT workgroups (one per CU) pulling from per-XCD queues: workgroup b runs on XCD
+// x = b % 8 and takes the next slot i of queue x (slot x + 8 i of block_tile, i < depth) by an atomic counter,
+// cnt[x] (zero on entry; the caller re-zeroes it per launch).  The one-tile-per-workgroup launch leaves each
+// workgroup's start to the in-order dispatcher, which hands block b to XCD b % 8 only after block b - 1 found a
+// CU: a slow tile on one XCD holds back the next round of every XCD (c3 trace: CUs idle 15 % of the launch,
+// tools/ws_trace.py).  Here each XCD's 32 workgroups run its queue greedily, independently of the other XCDs.
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_bf16_wsgq_kernel(const GroupEnt* __restrict__ ents,
+                                                             const uint16_t* __restrict__ tile_group,
+                                                             const uint16_t* __restrict__ block_tile, int ntiles,
+                                                             int depth, int* __restrict__ cnt, int dbg) {
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[WS_LDS];
+  __shared__ int s_slot;
+  const int x = (int)(blockIdx.x % 8);
+  for (;;) {
+    if (threadIdx.x == 0) s_slot = atomicAdd(cnt + x, 1);
+    __syncthreads();
+    const int i = s_slot;
+    __syncthreads();   // every wave has read s_slot before the next grab overwrites it
+    if (i >= depth) break;
+    const int slot = x + 8 * i;
+    const int t_all = (int)block_tile[slot];
+    if (t_all >= ntiles) continue;
+    wsg_tile<EPI>(ents, tile_group, t_all, slot, dbg, lds);
+    __syncthreads();   // the epilogue's staging image is dead before the next tile's LDS-DMA
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -525,7 +581,19 @@ bool ws_instantiated(bool bt, int epi) {
 }
 
 int launch_ws_grouped(const GroupEnt* ents, const uint16_t* tile_group, const uint16_t* block_tile, int ntiles,
-                      int blocks, float beta, int dbg, hipStream_t st) {
+                      int blocks, float beta, int dbg, int* queue, hipStream_t st) {
+  if (queue && blocks % 8 == 0) {   // persistent workgroups on per-XCD queues (one per CU, at most 256)
+    const int grid = std::min(blocks, 256), depth = blocks / 8;
+    if (beta == 1.f)
+      hipLaunchKernelGGL((gemm_bf16_wsgq_kernel<E_BETA | E_F32>), dim3(grid), dim3(512), 0, st, ents, tile_group,
+                         block_tile, ntiles, depth, queue, dbg);
+    else if (beta == 0.f)
+      hipLaunchKernelGGL((gemm_bf16_wsgq_kernel<E_F32>), dim3(grid), dim3(512), 0, st, ents, tile_group, block_tile,
+                         ntiles, depth, queue, dbg);
+    else
+      return -1;
+    return 0;
+  }
   if (beta == 1.f)
     hipLaunchKernelGGL((gemm_bf16_wsg_kernel<E_BETA | E_F32>), dim3(blocks), dim3(512), 0, st, ents, tile_group,
                        block_tile, ntiles, dbg);
@@ -577,3 +645,10 @@ void launch_ws(const GemmArgs& g, bool bt, int epi, int ntiles, int bm, hipStrea
 }  // namespace asrxg
 
 ASRX_SEED_OFFSET_SETTER(gemm_ws)
+
+// tools only (not part of include/asrx.h): the per-block trace of the last traced grouped launch
+extern "C" int asrx_ws_trace_read(unsigned long long* host, int n) {
+  if (!host || n < 0 || n > 4 * WS_TRACE_BLOCKS) return ASRX_ERR_ARG;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ws_trace), sizeof(unsigned long long) * n) == hipSuccess
+             ? ASRX_OK : ASRX_ERR_LAUNCH;
+}

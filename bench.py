@@ -191,13 +191,25 @@ def sub_rooflines(B, T2, d, H, ff, p_drop):
                      "frac_warm": round(tfw / PEAK_BF16_TFLOPS, 4), "us_warm": round(tw * 1e3, 2),
                      "buffer_sets": n, "shape": note}
 
+    def make_copy(nbytes):
+        # the same byte count as a plain device copy (half read, half written; torch's vectorised copy kernel, fp32
+        # elements in 16-B vectors): what one launch of this size reaches on this box from HBM — the floor the
+        # kernel's cold fraction is to be read against (a reference point, not product code)
+        src = torch.empty(max(1, nbytes // 8), device="cuda")
+        dst = torch.empty_like(src)
+        return lambda: dst.copy_(src)
+
     def hbm(name, nbytes, make, note):
         t, tw, n = timed(make, nbytes)
         gbs, gbw = nbytes / (t * 1e-3) / 1e9, nbytes / (tw * 1e-3) / 1e9
+        tc, _, _ = timed(lambda: make_copy(nbytes), nbytes)
+        gbc = nbytes / (tc * 1e-3) / 1e9
         out[name] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(gbs / PEAK_HBM_GBS, 4), "us": round(t * 1e3, 2),
                      "frac_warm": round(gbw / PEAK_HBM_GBS, 4), "us_warm": round(tw * 1e3, 2),
-                     "buffer_sets": n, "shape": note}
+                     "buffer_sets": n, "shape": note,
+                     "copy_floor": {"frac": round(gbc / PEAK_HBM_GBS, 4), "us": round(tc * 1e3, 2),
+                                    "kernel_vs_copy": round(tc / t, 3)}}
 
     def rnd(*shape, dtype=torch.float32, scale=1.0):
         return (torch.randn(*shape, device="cuda", generator=gen) * scale).to(dtype)

@@ -169,16 +169,18 @@ def test_gemm_fused_rowsum(tile, splitk, kernel_variant):
 
 
 @pytest.mark.parametrize("wkind,xcd", [("reg", False), ("reg", True), ("p3", False), ("p3", True), ("p4", False),
-                                       ("p4", True), ("ws", False), ("ws", True)])
+                                       ("p4", True), ("ws", False), ("ws", True), ("wsq", False), ("wsq", True)])
 @pytest.mark.parametrize("ngroups", [1, 7, 60])
 def test_gemm_grouped_wgrad(ngroups, wkind, xcd, monkeypatch):
     """Grouped weight gradients (asrx_gemm_grouped_xcd): ragged shapes, K not a multiple of 64, fused bias-grad
     row sums, beta=1 accumulation into existing fp32 grads, 60 problems in one launch (device table written by
-    asrx_upload, > 1 chunk)."""
+    asrx_upload, > 1 chunk).  wsq: the ws tiles from persistent workgroups on per-XCD queues (ws: one workgroup
+    per tile)."""
     g = torch.Generator(device=dev).manual_seed(ngroups)
     shapes = [(1000, 136, 96), (4096, 512, 512), (333, 248, 64), (64, 8, 576), (2500, 1536, 512),
               (77, 40, 1216), (249, 200, 24)]
-    monkeypatch.setattr(K(), "WGRAD_KIND", wkind)
+    monkeypatch.setattr(K(), "WGRAD_KIND", "ws" if wkind == "wsq" else wkind)
+    monkeypatch.setattr(K(), "WGRAD_QUEUE", wkind == "wsq")
     monkeypatch.setattr(K(), "WGRAD_XCD", xcd)
     items, refs = [], []
     for i in range(ngroups):

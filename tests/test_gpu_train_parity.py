@@ -205,7 +205,7 @@ def _assert_bench_plan(log, rows):
     assert by_shape[(rows, 1536, 512)] == {"gemm_bf16_ws_kernel"}, by_shape[(rows, 1536, 512)]   # Q/K/V fwd
     for kk in (512, 1216, 1536, 2048):                                                          # N = 512 outputs
         assert by_shape[(rows, 512, kk)] == {"gemm_bf16_ws_kernel"}, (kk, by_shape[(rows, 512, kk)])
-    assert "gemm_bf16_wsg_kernel" in fam, fam
+    assert fam & {"gemm_bf16_wsg_kernel", "gemm_bf16_wsgq_kernel"}, fam
 
 
 def test_trainer_grads_vs_oracle_bench_batch():
