@@ -1254,7 +1254,8 @@ void attn_fwd_stream_kernel(AttnArgs a, const uint32_t* qmaj) {
 // key validity / padding is a per-lane score bias, query validity is folded into lse (+inf), causality is a
 // compare only in blocks that reach above the diagonal.
 template <int MODE, int NKT>
-ASRX_DEV void attn_bwd_res_head(const AttnArgs& a, const int bh) {
+__global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
+  a.seed = seed_eff(a.seed);
   // NKT 32-key blocks (= waves); keys past Lk are zero rows with a -inf score bias
   constexpr int NK = NKT * 32, NTHR = NKT * 64;
   constexpr int RDT = 32 + 8;                                     // dS^T image [key][32 queries] row stride
@@ -1269,7 +1270,7 @@ ASRX_DEV void attn_bwd_res_head(const AttnArgs& a, const int bh) {
   float* sdel = slse + 64;                                   // [2][32]
   f4_t* slut = (f4_t*)(sdel + 64);                           // [16] dropout factors of a 4-bit keep mask
 
-  const int b = bh / a.H, h = bh % a.H;
+  const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, g = l >> 4, li = l & 15;
   // key block (grid.y > 1 only for Lk > NK: the streamed training path) — kb0 + the wave's local 32-key slice
   const int kb0 = (int)blockIdx.y * NK, nkb = (int)gridDim.y;
@@ -1581,19 +1582,6 @@ ASRX_DEV void attn_bwd_res_head(const AttnArgs& a, const int bh) {
   }
 }
 
-// Persistent over heads: workgroup (x, y) runs heads x, x + gridDim.x, ... of key block y.  With one workgroup per CU
-// (NKT = 8: ~97 KB of LDS) and 512 heads, a grid of one workgroup per head ran as two rounds whose second half the
-// in-order dispatcher released only block by block behind the first round's slowest workgroups.
-template <int MODE, int NKT>
-__global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
-  a.seed = seed_eff(a.seed);
-  const int nbh = a.B * a.H;
-  for (int bh = blockIdx.x; bh < nbh; bh += gridDim.x) {
-    attn_bwd_res_head<MODE, NKT>(a, bh);
-    __syncthreads();   // every LDS image of this head is dead before the next head's staging
-  }
-}
-
 int bwd_res_nkt(int lk) { return lk <= 64 ? 2 : (lk <= 128 ? 4 : 8); }
 
 size_t bwd_res_smem(int lk) {
@@ -1826,19 +1814,8 @@ extern "C" int asrx_attention_bwd(const asrx_attn_desc* d, void* stream) {
       if (!a.dq_acc) return ASRX_ERR_ARG;
       hipMemsetAsync(a.dq_acc, 0, sizeof(float) * (size_t)a.B * a.Lq * a.H * d->dh, st);
     }
-    // resident workgroups: the LDS image bounds them (one per CU at NKT = 8, 256 CUs); ASRX_ATTN_BWD_PERSIST=0: one
-    // workgroup per head
-    static const bool persist = [] { const char* e = getenv("ASRX_ATTN_BWD_PERSIST"); return !(e && e[0] == '0'); }();
-    const int nbh = a.B * a.H;
-    auto gx = [&](const void* fn) {   // resident workgroups of this instantiation x 256 CUs, over the key blocks
-      if (!persist) return nbh;
-      int per_cu = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * nkt, sm) != hipSuccess || per_cu < 1)
-        return nbh;
-      return std::min(nbh, std::max(1, 256 * per_cu / nkb));
-    };
-#define ASRX_BWD_RES(M, N) hipLaunchKernelGGL((attn_bwd_res_kernel<M, N>), \
-                                              dim3(gx((const void*)attn_bwd_res_kernel<M, N>), nkb), dim3(64 * nkt), sm, st, a)
+    const dim3 grid(a.B * a.H, nkb), blk(64 * nkt);
+#define ASRX_BWD_RES(M, N) hipLaunchKernelGGL((attn_bwd_res_kernel<M, N>), grid, blk, sm, st, a)
     if (a.mode == 0) { if (nkt == 2) ASRX_BWD_RES(0, 2); else if (nkt == 4) ASRX_BWD_RES(0, 4); else ASRX_BWD_RES(0, 8); }
     else if (a.mode == 1) { if (nkt == 2) ASRX_BWD_RES(1, 2); else if (nkt == 4) ASRX_BWD_RES(1, 4); else ASRX_BWD_RES(1, 8); }
     else { if (nkt == 2) ASRX_BWD_RES(2, 2); else if (nkt == 4) ASRX_BWD_RES(2, 4); else ASRX_BWD_RES(2, 8); }

@@ -358,13 +358,15 @@ ASRX_DEV void wsg_tile(const GroupEnt* __restrict__ ents, const uint16_t* __rest
   g.dbg = dbg & 9;
   const int t = t_all - e.tile_start;
   const int ntn = (e.n + WS_BN - 1) / WS_BN;
-  ws_tile<true, true, EPI>(g, (t / ntn) * WS_BM, (t % ntn) * WS_BN, e.rowsum != nullptr && (t % ntn) == 0, lds);
+  const bool rs_tile = e.rowsum != nullptr && (t % ntn) == 0;
+  ws_tile<true, true, EPI>(g, (t / ntn) * WS_BM, (t % ntn) * WS_BN, rs_tile, lds);
   if (trace) {
     const uint32_t xcc = __builtin_amdgcn_s_getreg(20 | (0 << 6) | (15 << 11)) & 15u;   // HW_REG_XCC_ID
     unsigned long long* r = g_ws_trace + 4 * slot;
     r[0] = t_start;
     r[1] = __builtin_amdgcn_s_memrealtime();
-    r[2] = (unsigned long long)xcc | ((unsigned long long)__smid() << 8) | ((unsigned long long)t_all << 32);
+    r[2] = (unsigned long long)xcc | (rs_tile ? 0x80ull : 0ull) | ((unsigned long long)__smid() << 8) |
+           ((unsigned long long)t_all << 32);
     r[3] = (unsigned long long)e.k | ((unsigned long long)gi << 32) | ((unsigned long long)blockIdx.x << 48);
   }
 }
@@ -389,7 +391,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_wsg_kernel(const GroupEnt* __re
 // cnt[x] (zero on entry; the caller re-zeroes it per launch).  The one-tile-per-workgroup launch leaves each
 // workgroup's start to the in-order dispatcher, which hands block b to XCD b % 8 only after block b - 1 found a
 // CU: a slow tile on one XCD holds back the next round of every XCD (c3 trace: CUs idle 15 % of the launch,
-// tools/ws_trace.py).  Here each XCD's 32 workgroups run its queue greedily, independently of the other XCDs.
+// tools/ws_trace.py).  Here each XCD's 32 workgroups run its queue greedily, independently of the other XCDs, and a
+// workgroup whose queue is empty takes the remaining tiles of the other XCDs' queues (the launch's tail).
 template <int EPI>
 __global__ __launch_bounds__(512) void gemm_bf16_wsgq_kernel(const GroupEnt* __restrict__ ents,
                                                              const uint16_t* __restrict__ tile_group,
@@ -398,13 +401,18 @@ __global__ __launch_bounds__(512) void gemm_bf16_wsgq_kernel(const GroupEnt* __r
   __shared__ __attribute__((aligned(1024))) unsigned char lds[WS_LDS];
   __shared__ int s_slot;
   const int x = (int)(blockIdx.x % 8);
+  int q = 0;   // queues drained so far: its own XCD's first, then (x + 1) % 8, ... (stealing the other XCDs' last tiles)
   for (;;) {
-    if (threadIdx.x == 0) s_slot = atomicAdd(cnt + x, 1);
+    const int xq = (x + q) & 7;
+    if (threadIdx.x == 0) s_slot = atomicAdd(cnt + xq, 1);
     __syncthreads();
     const int i = s_slot;
     __syncthreads();   // every wave has read s_slot before the next grab overwrites it
-    if (i >= depth) break;
-    const int slot = x + 8 * i;
+    if (i >= depth) {
+      if (++q == 8) break;
+      continue;
+    }
+    const int slot = xq + 8 * i;
     const int t_all = (int)block_tile[slot];
     if (t_all >= ntiles) continue;
     wsg_tile<EPI>(ents, tile_group, t_all, slot, dbg, lds);

@@ -41,7 +41,7 @@ def main():
         t0, t1, w2, w3 = buf[4 * b:4 * b + 4]
         if t0 == 0:
             continue
-        rows.append(dict(b=b, t0=t0, t1=t1, xcc=w2 & 15, cu=(w2 >> 8) & 0xffffff, tile=w2 >> 32, k=w3 & 0xffffffff,
+        rows.append(dict(b=b, t0=t0, t1=t1, xcc=w2 & 15, rs=(w2 >> 7) & 1, cu=(w2 >> 8) & 0xffffff, tile=w2 >> 32, k=w3 & 0xffffffff,
                          g=(w3 >> 32) & 0xffff, wg=w3 >> 48))
     tmin = min(r["t0"] for r in rows)
     tmax = max(r["t1"] for r in rows)
@@ -57,6 +57,13 @@ def main():
         busy = sum(r["t1"] - r["t0"] for r in rs) / 100
         end = (max(r["t1"] for r in rs) - tmin) / 100
         print(f"XCD {x}: {len(rs)} blocks, busy {busy / 32:.1f} us per CU, last end {end:.1f} us")
+    # tile durations by reduction length, with / without the fused bias-gradient row sums (loader waves)
+    for kk in sorted(set(r["k"] for r in rows)):
+        for rs in (0, 1):
+            du = sorted((r["t1"] - r["t0"]) / 100 for r in rows if r["k"] == kk and r["rs"] == rs)
+            if du:
+                print(f"k {kk} row-sum tile {rs}: {len(du)} tiles, duration p10 {du[len(du) // 10]:.1f} "
+                      f"p50 {du[len(du) // 2]:.1f} p90 {du[9 * len(du) // 10]:.1f} us")
     # rounds: consecutive 32 blocks of an XCD in block order
     print("per-XCD rounds (32 consecutive blocks of one XCD): group set, k, start spread, end spread, duration p50")
     for x in sorted(per_x):
