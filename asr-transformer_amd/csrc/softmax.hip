@@ -2,6 +2,7 @@
 // Replaces layers.py:20 (scale), :22-23 (masked_fill(mask>0,-inf)), :25 (softmax + nan_to_num), :26 dropout,
 // and their autograd backward.  HBM-bound: one read + one (or two) writes of the score matrix.
 // LPR lanes per row (rows/wave = 64/LPR), V contiguous elements per lane per step (16-B accesses), NJ steps.
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.h"
@@ -188,6 +189,95 @@ __global__ __launch_bounds__(256) void softmax_fwd_kernel(SmArgs a) {
   }
 }
 
+// Streaming forward for the common case (bf16, no mask, no separate dropout output, 128 < Lk <= 16 NJ x 8): rows on
+// 16 lanes x NJ 16-B vectors (4 rows per wave), PERSISTENT waves that stride over the row groups with the next
+// group's loads in flight while the current one is reduced and stored (the LayerNorm streaming scheme) — the
+// one-group-per-wave kernel above leaves each wave's load latency exposed once per launch and its ~8k short
+// workgroups to the dispatcher.  Probabilities stored non-temporally; padding columns [lk, ld) stored as zeros with
+// the row (except on the last row, whose padding may not be allocated: element-wise there).
+template <int NJ>
+__global__ __launch_bounds__(256) void softmax_fwd_stream_kernel(SmArgs a) {
+  constexpr int V = 8, LPR = 16, PF = 2;
+  const int l = threadIdx.x & 63, sub = l >> 4, ll = l & 15;
+  const int64_t ngroups = (a.rows + 3) / 4;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  float v[PF][NJ][V];
+  // groups wholly before the last row (wave-uniform test) take whole 16-B vectors with no per-vector checks
+  auto load = [&](int p, int64_t grp) {
+    const int64_t row = grp * 4 + sub;
+    if (grp * 4 + 3 < a.rows - 1) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {   // (vectors past the row stride ld hold nothing of this row: skipped)
+        const int k0 = (j * LPR + ll) * V;
+        ld_vec<V, false>(a.s, ASRX_BF16, row * a.ld + k0, v[p][j], k0 < a.ld ? V : 0);
+      }
+    } else {
+      const int64_t rr = row < a.rows ? row : a.rows - 1;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int k0 = (j * LPR + ll) * V;
+        ld_vec<V, false>(a.s, ASRX_BF16, rr * a.ld + k0, v[p][j], loadable(a, rr, k0, V));
+      }
+    }
+  };
+#pragma unroll
+  for (int p = 0; p < PF; ++p)
+    if (gw + p * nw < ngroups) load(p, gw + p * nw);
+  for (int64_t g0 = gw; g0 < ngroups; g0 += PF * nw) {
+#pragma unroll
+    for (int p = 0; p < PF; ++p) {
+      const int64_t grp = g0 + p * nw;
+      if (grp >= ngroups) break;   // wave-uniform
+      const int64_t row = grp * 4 + sub;
+      float x[NJ][V];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int k0 = (j * LPR + ll) * V;
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+          x[j][i] = k0 + i >= a.lk ? -INFINITY : v[p][j][i] * a.scale2;
+          mx = fmaxf(mx, x[j][i]);
+        }
+      }
+      const int64_t nxt = grp + PF * nw;
+      if (nxt < ngroups) load(p, nxt);   // the slot is free: refill it before the reductions
+      mx = group_reduce<LPR, true>(mx);
+      const float mref = mx == -INFINITY ? 0.f : mx;
+      float sum = 0.f;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int i = 0; i < V; ++i) { x[j][i] = exp2_raw(x[j][i] - mref); sum += x[j][i]; }
+      sum = group_reduce<LPR, false>(sum);
+      const float inv = sum > 0.f ? 1.f / sum : 0.f;   // all-masked row -> 0 (nan_to_num, layers.py:25)
+      if (grp * 4 + 3 < a.rows - 1) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int k0 = (j * LPR + ll) * V;
+          if (k0 >= a.ld) continue;
+          float o[V];
+#pragma unroll
+          for (int i = 0; i < V; ++i) o[i] = x[j][i] * inv;
+          st_vec<V, true>(a.p, ASRX_BF16, row * a.ld + k0, o, V);
+        }
+      } else if (row < a.rows) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int k0 = (j * LPR + ll) * V;
+          const int nv = loadable(a, row, k0, V);
+          if (nv <= 0) continue;
+          float o[V];
+#pragma unroll
+          for (int i = 0; i < V; ++i) o[i] = x[j][i] * inv;
+          st_vec<V, true>(a.p, ASRX_BF16, row * a.ld + k0, o, nv);
+        }
+      }
+    }
+  }
+}
+
 template <int V, int LPR, int NJ, int U, int NTM>
 __global__ __launch_bounds__(256) void softmax_bwd_kernel(SmArgs a, void* ds) {
   constexpr bool NTL = (NTM & 1) != 0, NTS = (NTM & 2) != 0;
@@ -292,8 +382,21 @@ int softmax_u() {
   return g_tune_softmax_u ? g_tune_softmax_u : env;
 }
 
+// ASRX_SOFTMAX_STREAM (default 1; 0 = off): the persistent streaming forward for bf16, no mask, no dropout output,
+// 128 < Lk <= 256 (ASRX_SOFTMAX_BPC blocks of 4 waves per CU, default 4)
+bool try_stream(const SmArgs& a, hipStream_t st) {
+  static const bool on = [] { const char* e = getenv("ASRX_SOFTMAX_STREAM"); return !(e && e[0] == '0'); }();
+  static const int bpc = [] { const char* e = getenv("ASRX_SOFTMAX_BPC"); const int v = e ? atoi(e) : 4; return v > 0 ? v : 4; }();
+  if (!on || a.dtype != ASRX_BF16 || a.mode != 0 || a.pd || a.lk <= 128 || a.lk > 256 || a.ld % 8) return false;
+  const int64_t groups = (a.rows + 3) / 4;
+  const unsigned blocks = (unsigned)std::min<int64_t>((groups + 3) / 4, (int64_t)256 * bpc);
+  hipLaunchKernelGGL((softmax_fwd_stream_kernel<2>), dim3(blocks), dim3(256), 0, st, a);
+  return true;
+}
+
 template <int V>
 bool dispatch(const SmArgs& a, bool bwd, void* ds, hipStream_t st) {
+  if (V == 8 && !bwd && try_stream(a, st)) return true;
   const int u = softmax_u();
   static const bool lpr16 = [] { const char* e = getenv("ASRX_SOFTMAX_LPR16"); return !(e && e[0] == '0'); }();
   if (lpr16 && !bwd && V == 8 && a.lk > 128 && try_launch<V, 16, 2, 1>(a, bwd, ds, st)) return true;

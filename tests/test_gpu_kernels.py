@@ -732,6 +732,25 @@ def test_softmax_masked(dtype, Lk, u, tuning):
     assert relerr(ds[..., :Lk].float().cpu(), ref_ds) < tol * 2
 
 
+@pytest.mark.parametrize("Lk", [129, 200, 249, 256])
+@pytest.mark.parametrize("nbh,Lq", [(3, 7), (64, 601)])
+def test_softmax_stream_unmasked(Lk, nbh, Lq):
+    """The persistent streaming forward (bf16, no mask, no dropout output, 128 < Lk <= 256; softmax.hip
+    softmax_fwd_stream_kernel): a row count that is not a multiple of 4 (the last row group), and 38 k rows — several
+    row groups per wave, the prefetch ring — against torch; padding columns stored as zeros."""
+    from asrx.kernels import MaskSpec
+    g = torch.Generator().manual_seed(Lk + Lq)
+    ld = (Lk + 7) // 8 * 8
+    s = torch.randn(nbh, Lq, ld, generator=g) * 3
+    sd = s.to(dev, torch.bfloat16)
+    p = torch.full_like(sd, float("nan"))
+    scale = 0.125
+    K().softmax_fwd(sd, p, None, nbh, 1, Lq, Lk, ld, scale, MaskSpec())
+    ref = torch.softmax(sd[..., :Lk].double().cpu() * scale, -1)
+    assert relerr(p[..., :Lk].float().cpu(), ref) < 1e-2
+    assert (p.reshape(-1, ld)[:-1, Lk:] == 0).all()
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("Lk", [24, 249])
 @pytest.mark.parametrize("u", [0, 4])
