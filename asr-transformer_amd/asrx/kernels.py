@@ -341,7 +341,7 @@ def _grouped_xcd(items, common, kind="p3"):
     cvec = 1
     ents = np.zeros((len(items), 8), dtype=np.int64)
     ints = ents.view(np.int32)
-    start, flops = 0, 0
+    start, flops, panels = 0, 0, 0
     for slot, i in enumerate(group_order):
         dy, x, wgrad, bias_grad = items[i]
         _cuda(dy, x, wgrad, bias_grad)
@@ -349,7 +349,10 @@ def _grouped_xcd(items, common, kind="p3"):
         k = x.shape[1]
         ents[slot, 0], ents[slot, 1], ents[slot, 2] = dy.data_ptr(), x.data_ptr(), wgrad.data_ptr()
         ents[slot, 3] = bias_grad.data_ptr() if bias_grad is not None else 0
-        ints[slot, 8:16] = [dy.stride(0), x.stride(0), wgrad.stride(0), n, k, m, start, 0]
+        # last field: the group's first row-panel counter (ws queue launch: split bias-gradient row sums)
+        ints[slot, 8:16] = [dy.stride(0), x.stride(0), wgrad.stride(0), n, k, m, start, panels]
+        if bias_grad is not None:
+            panels += (n + tile[0] - 1) // tile[0]
         start += nts[i]
         flops += 2 * m * n * k
         if wgrad.stride(0) % 4 or wgrad.data_ptr() % 16:
@@ -357,10 +360,11 @@ def _grouped_xcd(items, common, kind="p3"):
     common.relu = cvec
     o1 = ents.nbytes
     o2 = o1 + (tmap.nbytes + 63) // 64 * 64
-    # ws tiles: 8 per-XCD queue counters after the block map (zeroed by this upload, i.e. on every launch / replay)
+    # ws tiles: 8 per-XCD queue counters (+ 8 spare) and one counter per bias-carrying row panel after the block map,
+    # zeroed by this upload, i.e. on every launch / replay; the row panels' [tiles][256] fp32 row-sum slabs beside
     o3 = (o2 + block_tile.nbytes + 63) // 64 * 64
     queue = code == 5 and WGRAD_QUEUE and len(block_tile) % 8 == 0
-    n_all = o3 + 64 if queue else (o2 + block_tile.nbytes + 3) // 4 * 4
+    n_all = o3 + 4 * (16 + panels) if queue else (o2 + block_tile.nbytes + 3) // 4 * 4
     host = np.zeros(n_all, dtype=np.uint8)
     host[:o1] = ents.view(np.uint8).reshape(-1)
     host[o1:o1 + tmap.nbytes] = tmap.view(np.uint8)
@@ -368,13 +372,16 @@ def _grouped_xcd(items, common, kind="p3"):
     dev = torch.empty(n_all, dtype=torch.uint8, device=items[0][0].device)
     upload(dev, host)
     base = dev.data_ptr()
+    part = None
     if queue:
-        common.workspace, common.workspace_elems = base + o3, 16
+        common.workspace, common.workspace_elems = base + o3, 16 + panels
+        part = torch.empty(start * tile[0], dtype=torch.float32, device=dev.device)
+        common.rowsum_ws = part.data_ptr()
 
     def launch():
         call("asrx_gemm_grouped_xcd", ctypes.byref(common), base, base + o1, base + o2, len(items), start,
              len(block_tile), stream())
-    return flops, launch, dev
+    return flops, launch, (dev, part)
 
 
 # lay each group's tiles on one XCD (ASRX_WGRAD_XCD=0: one table order over all XCDs, A/B)

@@ -1802,7 +1802,8 @@ extern "C" int asrx_gemm_grouped_xcd(const asrx_gemm_desc* common, const asrx_ge
   if (common->tile == 5) {   // ws: warp-specialised 256x128 tiles (fp32 C, 16-B rows, n % 4 == 0, alpha 1, beta 0|1)
     if (common->c_dtype != ASRX_F32 || common->alpha != 1.f ||
         launch_ws_grouped((const GroupEnt*)groups, tile_group, block_tile, tiles, blocks, common->beta, gemm_dbg(),
-                          common->workspace && common->workspace_elems >= 8 ? (int*)common->workspace : nullptr,
+                          common->workspace && common->workspace_elems >= 16 ? (int*)common->workspace : nullptr,
+                          common->workspace && common->workspace_elems >= 16 ? common->rowsum_ws : nullptr,
                           (hipStream_t)stream) != 0)
       return ASRX_ERR_UNSUPPORTED;
   } else if (common->tile == 3 || common->tile == 4) {   // p3 / p4 LDS-DMA ring tiles, 256x128 / 256x256 (fp32 C, 16-B

@@ -519,6 +519,6 @@ void launch_ws(const GemmArgs& g, bool bt, int epi, int ntiles, int bm, hipStrea
 bool wsp_instantiated(bool bt, int epi);
 void launch_wsp(const GemmArgs& g, bool bt, int epi, int ntiles, hipStream_t st);
 int launch_ws_grouped(const GroupEnt* ents, const uint16_t* tile_group, const uint16_t* block_tile, int ntiles,
-                      int blocks, float beta, int dbg, int* queue, hipStream_t st);
+                      int blocks, float beta, int dbg, int* queue, float* part, hipStream_t st);
 
 }  // namespace asrxg

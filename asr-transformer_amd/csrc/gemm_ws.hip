@@ -251,7 +251,9 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
       // compute waves' transposing fragment reads — lane l gets 8 consecutive k of column 16 c + (l & 15) — and 4
       // v_dot2c_f32_bf16 against (1, 1) per fragment: 16 reads + 32 VALU per K-step, each lane's column its own
       if constexpr (AT) {
-        if (rs_tile) {
+        // (split mode, g.rowsum_ws set: this tile sums the K-steps s = k_per_split mod splitk only — the row panel's
+        //  splitk column tiles share the work — into its 256-float slab at g.rowsum_ws)
+        if (rs_tile && (g.splitk <= 1 || s % g.splitk == g.k_per_split)) {
           const unsigned char* img = lds + cb * C::STAGE;
 #pragma unroll
           for (int c = 0; c < 4; ++c)
@@ -277,7 +279,11 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
           v += __shfl_xor(v, 16, 64);
           v += __shfl_xor(v, 32, 64);
           const int m = m0 + 64 * lw + 16 * c + l;
-          if (l < 16 && m < g.M) g.rowsum[m] += v;
+          if (g.rowsum_ws) {   // agent-coherent (write-through) stores: no cache-wide release fence needed
+            if (l < 16) __hip_atomic_store(g.rowsum_ws + 64 * lw + 16 * c + l, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          } else if (l < 16 && m < g.M) {
+            g.rowsum[m] += v;
+          }
         }
       }
     }
@@ -343,7 +349,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_ws_kernel(GemmArgs g, int ntile
 // One grouped tile (tile index t_all of the table; slot = its position in the block -> tile map, the trace index).
 template <int EPI>
 ASRX_DEV void wsg_tile(const GroupEnt* __restrict__ ents, const uint16_t* __restrict__ tile_group, int t_all, int slot,
-                       int dbg, unsigned char* lds) {
+                       int dbg, unsigned char* lds, int* __restrict__ pcnt = nullptr, float* __restrict__ part = nullptr,
+                       int* s_last = nullptr) {
   // tools only (ASRX_GEMM_DBG & 128): per-tile start / end real time, XCD, CU and tile into g_ws_trace
   const bool trace = (dbg & 128) && threadIdx.x == 0 && slot < WS_TRACE_BLOCKS;
   const uint64_t t_start = trace ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -358,8 +365,38 @@ ASRX_DEV void wsg_tile(const GroupEnt* __restrict__ ents, const uint16_t* __rest
   g.dbg = dbg & 9;
   const int t = t_all - e.tile_start;
   const int ntn = (e.n + WS_BN - 1) / WS_BN;
-  const bool rs_tile = e.rowsum != nullptr && (t % ntn) == 0;
+  // bias-gradient row sums: one column tile per row panel sums every K-step into rowsum (one workgroup per tile),
+  // or (queue launch, part / pcnt set) each of the panel's ntn column tiles sums every ntn-th K-step into its own
+  // 256-float slab and the panel's last tile to finish adds the slabs in column order (deterministic) to rowsum:
+  // the row-sum tiles ran ~15 % longer than their round-mates, which then drifted apart in the L2 they share
+  const bool split = part != nullptr && e.rowsum != nullptr;
+  const bool rs_tile = e.rowsum != nullptr && (split || (t % ntn) == 0);
+  if (split) {
+    g.rowsum_ws = part + (int64_t)t_all * WS_BM;
+    g.splitk = ntn;
+    g.k_per_split = t % ntn;
+  }
   ws_tile<true, true, EPI>(g, (t / ntn) * WS_BM, (t % ntn) * WS_BN, rs_tile, lds);
+  if (split) {
+    // the slab stores are agent-coherent write-throughs, complete (vmcnt(0)) before the barrier; the panel counter and
+    // the other slabs are read the same way — a __threadfence here (L2 write-back + invalidate per tile, with the dW
+    // tiles dirty in L2) cost 15 % of the launch
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+      *s_last = __hip_atomic_fetch_add(pcnt + e.pad + t / ntn, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ntn - 1;
+    __syncthreads();
+    if (*s_last) {
+      const int mm = threadIdx.x, m = (t / ntn) * WS_BM + mm;
+      if (mm < WS_BM && m < e.m) {
+        float* sl = part + (int64_t)(e.tile_start + (t / ntn) * ntn) * WS_BM + mm;
+        float v = 0.f;
+        for (int j = 0; j < ntn; ++j)
+          v += __hip_atomic_load(sl + (int64_t)j * WS_BM, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        e.rowsum[m] += v;
+      }
+    }
+  }
   if (trace) {
     const uint32_t xcc = __builtin_amdgcn_s_getreg(20 | (0 << 6) | (15 << 11)) & 15u;   // HW_REG_XCC_ID
     unsigned long long* r = g_ws_trace + 4 * slot;
@@ -397,9 +434,10 @@ template <int EPI>
 __global__ __launch_bounds__(512) void gemm_bf16_wsgq_kernel(const GroupEnt* __restrict__ ents,
                                                              const uint16_t* __restrict__ tile_group,
                                                              const uint16_t* __restrict__ block_tile, int ntiles,
-                                                             int depth, int* __restrict__ cnt, int dbg) {
+                                                             int depth, int* __restrict__ cnt,
+                                                             float* __restrict__ part, int dbg) {
   __shared__ __attribute__((aligned(1024))) unsigned char lds[WS_LDS];
-  __shared__ int s_slot;
+  __shared__ int s_slot, s_last;
   const int x = (int)(blockIdx.x % 8);
   int q = 0;   // queues drained so far: its own XCD's first, then (x + 1) % 8, ... (stealing the other XCDs' last tiles)
   for (;;) {
@@ -415,7 +453,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_wsgq_kernel(const GroupEnt* __r
     const int slot = xq + 8 * i;
     const int t_all = (int)block_tile[slot];
     if (t_all >= ntiles) continue;
-    wsg_tile<EPI>(ents, tile_group, t_all, slot, dbg, lds);
+    wsg_tile<EPI>(ents, tile_group, t_all, slot, dbg, lds, cnt + 16, part, &s_last);
     __syncthreads();   // the epilogue's staging image is dead before the next tile's LDS-DMA
   }
 }
@@ -589,15 +627,15 @@ bool ws_instantiated(bool bt, int epi) {
 }
 
 int launch_ws_grouped(const GroupEnt* ents, const uint16_t* tile_group, const uint16_t* block_tile, int ntiles,
-                      int blocks, float beta, int dbg, int* queue, hipStream_t st) {
+                      int blocks, float beta, int dbg, int* queue, float* part, hipStream_t st) {
   if (queue && blocks % 8 == 0) {   // persistent workgroups on per-XCD queues (one per CU, at most 256)
     const int grid = std::min(blocks, 256), depth = blocks / 8;
     if (beta == 1.f)
       hipLaunchKernelGGL((gemm_bf16_wsgq_kernel<E_BETA | E_F32>), dim3(grid), dim3(512), 0, st, ents, tile_group,
-                         block_tile, ntiles, depth, queue, dbg);
+                         block_tile, ntiles, depth, queue, part, dbg);
     else if (beta == 0.f)
       hipLaunchKernelGGL((gemm_bf16_wsgq_kernel<E_F32>), dim3(grid), dim3(512), 0, st, ents, tile_group, block_tile,
-                         ntiles, depth, queue, dbg);
+                         ntiles, depth, queue, part, dbg);
     else
       return -1;
     return 0;

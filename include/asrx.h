@@ -106,10 +106,13 @@ typedef struct asrx_gemm_group_dev {
  * every tile of the group).  common->tile selects the tile: 3 = the p3 LDS-DMA ring, 256x128 tiles (m x n;
  * fp32 C with 16-byte aligned rows, every group's n % 4 == 0, alpha 1, beta 0 or 1), 4 = the p4 ring, 256x256
  * tiles (same conditions), 5 = the warp-specialised ws kernel, 256x128 tiles (4 MFMA waves + 4 LDS-DMA loader
- * waves, 3-stage ring; same conditions; with common->workspace set and common->workspace_elems >= 8 it is read as
- * 8 int32 queue counters, ZERO on entry, and the launch runs min(blocks, 256) persistent workgroups that take the
- * slots x, x + 8, x + 16, ... of block_tile from per-XCD queues (x = b % 8; blocks % 8 == 0); the counters are left
- * non-zero: zero them before the next launch), 128 = register-staged
+ * waves, 3-stage ring; same conditions; with common->workspace set and common->workspace_elems >= 16 it is read
+ * as int32 counters, ZERO on entry — [0, 8) per-XCD queues, [16, 16 + P) one per 256-row panel of the groups that
+ * carry a rowsum_a (group entry `reserved` = its first panel's index, panels numbered over those groups) — and
+ * common->rowsum_ws as [tiles][256] fp32 scratch: the launch runs min(blocks, 256) persistent workgroups that take
+ * the slots x, x + 8, x + 16, ... of block_tile from per-XCD queues (x = b % 8; blocks % 8 == 0; an empty queue
+ * takes the others' last slots), and each panel's column tiles share its row sums (the last to finish adds them in
+ * column order); the counters are left non-zero: zero them before the next launch), 128 = register-staged
  * 128x128 tiles (any alignment-checked table; common->relu carries its "every C row 16-byte aligned" flag).
  * Replaces the weight/bias-gradient mm + sum of autograd for every nn.Linear (layers.py:10-12,36,48,51). */
 int asrx_gemm_grouped_xcd(const asrx_gemm_desc* common, const asrx_gemm_group_dev* groups,
