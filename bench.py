@@ -233,6 +233,15 @@ def sub_rooflines(B, T2, d, H, ff, p_drop):
                                        MaskSpec(), p_drop, 11, dropmask=dm)
     mfma("attention_fwd", 4.0 * B * H * T2 * T2 * dh, make_attn, rows * d * 8,
          f"B*H={B * H} Lq=Lk={T2} dh={dh}, dropout {p_drop} (incl. the keep-bit generation kernel)")
+    # its memory side: Q, K, V read once, O written once (bf16), keep bits written and read (1 bit per score, two
+    # layouts) — the c3 shape's arithmetic intensity (~100 FLOP/B) is below the MI355X ridge (2.5 PF / 8 TB/s = 312),
+    # so an MFMA fraction near 30% is the HBM roof here
+    a_bytes = 4 * rows * d * 2 + 3 * B * H * T2 * T2 / 8
+    at = out["attention_fwd"]
+    at["algorithmic_bytes"] = int(a_bytes)
+    at["hbm_frac"] = round(a_bytes / (at["us"] * 1e-6) / 1e9 / PEAK_HBM_GBS, 4)
+    at["mfma_roof_at_hbm_peak"] = round(min(1.0, (4.0 * B * H * T2 * T2 * dh / a_bytes) * PEAK_HBM_GBS * 1e9 /
+                                            (PEAK_BF16_TFLOPS * 1e12)), 4)
     gam = torch.rand(d, device="cuda", generator=gen) + 0.5
     bet = rnd(d)
 
