@@ -1307,7 +1307,7 @@ extern "C" int asrx_conv1_bwd_fused(int32_t dcols_dtype, const void* dcols, int3
 // buffer and is capturable in a HIP graph (a replay re-writes the same bytes).  Used for per-launch tables
 // (grouped weight-gradient groups / tile maps) and per-step scalars (Adam hyper-parameters).
 namespace {
-constexpr int UPLOAD_CHUNK = 2048;
+constexpr int UPLOAD_CHUNK = 3968;   // bytes per launch: kernel arguments (4 KiB with the pointer and count)
 struct UploadChunk {
   uint32_t w[UPLOAD_CHUNK / 4];
 };
