@@ -147,6 +147,9 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = argt
             fn.restype = ctypes.c_int
+        # size helper (host arithmetic, int64 result)
+        L.asrx_attn_dropmask_words.argtypes = [c_i32, c_i32, c_i32, c_i32]
+        L.asrx_attn_dropmask_words.restype = c_i64
         _lib = L
     return _lib
 

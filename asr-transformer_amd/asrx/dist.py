@@ -150,6 +150,11 @@ class GradAllReduce:
             w.wait()
         for view, full, work, _bufs in self._post:   # (the side stream's buffers live until here)
             work.wait()
+            if full.is_cuda:
+                # `full` was allocated on the side stream but is read here on the compute stream: tell the caching
+                # allocator, so the block is not handed to a later side-stream allocation before this cast has run
+                # (ordering-independent of _issue_bf16's wait_stream)
+                full.record_stream(torch.cuda.current_stream(full.device))
             _cast(full[:view.numel()], view)
         self._works = []
         self._post = []

@@ -381,7 +381,7 @@ def _grouped_xcd(items, common, kind="p3"):
     def launch():
         call("asrx_gemm_grouped_xcd", ctypes.byref(common), base, base + o1, base + o2, len(items), start,
              len(block_tile), stream())
-    return flops, launch, (dev, part)
+    return flops, launch, (dev, part), queue
 
 
 # lay each group's tiles on one XCD (ASRX_WGRAD_XCD=0: one table order over all XCDs, A/B)
@@ -398,28 +398,32 @@ WGRAD_QUEUE = os.environ.get("ASRX_WGRAD_QUEUE", "1") == "1"
 
 def linear_wgrad_grouped(items, *, beta=1.0, kind=None):
     """Issue many independent weight gradients wgrad[N,K] (+)= dy[M,N]^T . x[M,K] (+ bias_grad[N] += colsum dy)
-    as ONE grouped launch (longest reductions first, tiles of a group on one XCD)."""
+    as ONE grouped launch (longest reductions first, tiles of a group on one XCD).  Returns the name of the kernel
+    instantiation launched (the one rocprofv3 lists)."""
     if not items:
-        return
+        return None
     items = sorted(items, key=lambda it: -it[0].shape[0])
     common = GemmDesc()
     common.in_dtype, common.a_trans, common.b_trans, common.c_dtype = BF16, 1, 1, F32
     common.alpha, common.beta = 1.0, beta
     p3 = _grouped_p3_ok(items, beta)
     kind = kind or WGRAD_KIND
-    wsk = GROUPED_WSQ_KERNELS if WGRAD_QUEUE else GROUPED_WS_KERNELS
+    # the table upload is issued first, so a timed bracket holds the grouped GEMM alone
+    flops, launch, _, queued = _grouped_xcd(items, common, kind if p3 else "reg")
+    # the kernel that actually runs: the ws tiles go to the persistent queue kernel only when _grouped_xcd took it
+    # (its block map must hold whole 8-XCD rounds), else one workgroup per tile
+    wsk = GROUPED_WSQ_KERNELS if queued else GROUPED_WS_KERNELS
     kname = ({"p4": GROUPED_P4_KERNELS, "ws": wsk}.get(kind, GROUPED_P3_KERNELS)[beta == 1.0] if p3
              else GROUPED_TABLE_KERNEL)
     probe = PROBE
     if probe is not None and probe.active and probe.log is not None:
         probe.log.append((kname, len(items), 0,
                           sum(it[0].shape[0] * it[0].shape[1] * it[1].shape[1] for it in items), 1, 1))
-    # the table upload is issued first, so a timed bracket holds the grouped GEMM alone
-    flops, launch, _ = _grouped_xcd(items, common, kind if p3 else "reg")
     if probe is not None and probe.active:
         timed_launch(kname, flops, launch)
     else:
         launch()
+    return kname
 
 
 def colsum(x, out, *, accumulate=True, rows=None, cols=None, ld=None):
@@ -542,7 +546,10 @@ def dropmask_buffer(B, H, Lq, Lk, dh, dropout_p, device):
     [B*H][ceil(Lq/32)][Lk], then query-major words [B*H][Lq][qmaj_stride(Lk)]."""
     if dropout_p <= 0.0 or dh != 64:
         return None
-    return torch.empty(B * H * (((Lq + 31) // 32) * Lk + Lq * qmaj_stride(Lk)), device=device, dtype=torch.int32)
+    from ._lib import lib
+    n = lib().asrx_attn_dropmask_words(B, H, Lq, Lk)   # the C-ABI's own size rule (include/asrx.h)
+    assert n == B * H * (((Lq + 31) // 32) * Lk + Lq * qmaj_stride(Lk)), (n, B, H, Lq, Lk)
+    return torch.empty(n, device=device, dtype=torch.int32)
 
 
 def attention_dropgen(B, H, Lq, Lk, dh, dropout_p, seed, dropmask):
@@ -561,6 +568,12 @@ def layernorm_fwd_dropgen(x, gamma, beta, y, B, H, Lq, Lk, dh, dropout_p, seed, 
     the keep-bit hashing runs beside the HBM-bound LayerNorm.  Returns (mean, rstd)."""
     _cuda(x, gamma, beta, y, dropmask)
     rows, d = x.shape
+    # the fused kernel indexes rows as row * 512 with 16-B vectors: dense [rows, 512] fp32 in, bf16 out only
+    if not (d == 512 and x.dtype == torch.float32 and y.dtype == torch.bfloat16 and x.is_contiguous()
+            and y.is_contiguous() and y.shape == x.shape and gamma.is_contiguous() and beta.is_contiguous()
+            and gamma.numel() == d and beta.numel() == d and gamma.data_ptr() % 16 == 0 and beta.data_ptr() % 16 == 0):
+        raise RuntimeError("asrx.layernorm_fwd_dropgen: needs contiguous [rows, 512] fp32 x / bf16 y and 16-B aligned "
+                           "gamma/beta")
     mean = torch.empty(rows, device=x.device, dtype=torch.float32)
     rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
     a = AttnDesc()

@@ -1684,6 +1684,11 @@ size_t bwd_smem(int nw, int dh) {
 
 ASRX_SEED_OFFSET_SETTER(attention)
 
+extern "C" int64_t asrx_attn_dropmask_words(int32_t batch, int32_t heads, int32_t lq, int32_t lk) {
+  if (batch <= 0 || heads <= 0 || lq <= 0 || lk <= 0) return -1;
+  return (int64_t)batch * heads * ((int64_t)((lq + 31) / 32) * lk + (int64_t)lq * qmaj_stride(lk));
+}
+
 extern "C" int asrx_attn_dropgen(const asrx_attn_desc* d, void* stream) {
   AttnArgs a;
   int rc = fill_args(d, a);

@@ -378,13 +378,31 @@ ASRX_DEV void wsg_tile(const GroupEnt* __restrict__ ents, const uint16_t* __rest
   }
   ws_tile<true, true, EPI>(g, (t / ntn) * WS_BM, (t % ntn) * WS_BN, rs_tile, lds);
   if (split) {
-    // the slab stores are agent-coherent write-throughs, complete (vmcnt(0)) before the barrier; the panel counter and
-    // the other slabs are read the same way — a __threadfence here (L2 write-back + invalidate per tile, with the dW
-    // tiles dirty in L2) cost 15 % of the launch
+    // Slab hand-off between the ntn column tiles of a row panel (workgroups on any XCD):
+    //  producer (every tile): the 256 slab floats are stored by agent-scope atomic stores = `global_store_dword sc1`
+    //    (write-through: the bytes leave the XCD's L2 for memory, no dirty line stays behind); every storing wave
+    //    waits for them (`s_waitcnt vmcnt(0)`, inline asm so the compiler cannot drop it) before the workgroup
+    //    barrier, and only then does ONE lane add to the panel's agent-scope counter.  No release fence: on gfx950
+    //    `__ATOMIC_RELEASE` lowers to `buffer_wbl2 sc1`, a write-back of the whole XCD L2 — with this tile's 128 KiB of
+    //    dW rows dirty in it that cost 15 % of the launch (measured as a __threadfence).  The producer side therefore
+    //    relies on the ISA, not on the HIP memory model: sc1 stores completed by vmcnt(0) are visible at agent scope
+    //    before the counter add that follows them (MI355X_MICROARCH.md, "Workgroup dispatch ... inter-workgroup
+    //    visibility", valid hand-off forms, table row 1: one lane per storing workgroup adds to ONE counter, the last
+    //    adder learns it from the returned value, 4-B sc1 stores and loads).
+    //  consumer (the panel's last tile only, once per panel): an agent-scope ACQUIRE fence after the counter add
+    //    (invalidates this CU's L1, so no stale line can serve the slab loads), its wait, a workgroup barrier, then
+    //    sc1 loads of the slabs — the consumer half is by the memory model.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0)
-      *s_last = __hip_atomic_fetch_add(pcnt + e.pad + t / ntn, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ntn - 1;
+    if (threadIdx.x == 0) {
+      const bool last =
+          __hip_atomic_fetch_add(pcnt + e.pad + t / ntn, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ntn - 1;
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      *s_last = last;
+    }
     __syncthreads();
     if (*s_last) {
       const int mm = threadIdx.x, m = (t / ntn) * WS_BM + mm;

@@ -171,11 +171,14 @@ typedef struct asrx_attn_desc {
   void* dv; int64_t dv_rstride, dv_bstride;
   float* delta;                 /* [batch*heads*lq] workspace */
   float* dq_acc;                /* [batch*lq*heads*dh] fp32 workspace, used when lk > 256 */
-  /* optional dropout keep-bit workspace (dh = 64, lk <= 256, dropout_p > 0): key-major words
+  /* optional dropout keep-bit workspace (dh = 64, dropout_p > 0, any lk): key-major words
    * [batch*heads][ceil(lq/32)][lk] (bit i = query 32c+i) followed by query-major words
-   * [batch*heads][lq][ceil(lk/32)] (bit j = key 32c+j), generated by the forward and read by the backward
-   * instead of re-hashing.  The bits equal the counter-based RNG's decisions, so results do not depend on it;
-   * without it the forward uses the tiled kernel. */
+   * [batch*heads][lq][qmaj_stride(lk)] (bit j = key 32c+j), where qmaj_stride(lk) = ceil(lk/32) for lk <= 256 and
+   * ceil(lk/32) rounded up to a multiple of 4 for lk > 256 (the streamed kernels move 4 words per query and
+   * 128-key chunk).  Total size: batch*heads*(ceil(lq/32)*lk + lq*qmaj_stride(lk)) 32-bit words — the value
+   * asrx_attn_dropmask_words() returns; size the buffer from it.  Generated by the forward (or
+   * asrx_attn_dropgen) and read by the backward instead of re-hashing.  The bits equal the counter-based RNG's
+   * decisions, so results do not depend on it; without it the forward uses the tiled kernel. */
   uint32_t* dropmask;
   int32_t dropmask_ready;       /* nonzero: the forward finds the bits already generated (asrx_attn_dropgen) */
   /* optional (training): bf16 buffer with o's strides; the forward writes the rounding residual O - bf16(O)
@@ -186,6 +189,9 @@ typedef struct asrx_attn_desc {
 } asrx_attn_desc;
 
 int asrx_attention_fwd(const asrx_attn_desc* d, void* stream);
+/* Number of 32-bit words of the dropmask workspace for these shapes (see asrx_attn_desc.dropmask); -1 on bad
+ * arguments.  Host-only arithmetic, no device access. */
+int64_t asrx_attn_dropmask_words(int32_t batch, int32_t heads, int32_t lq, int32_t lk);
 /* Fill d->dropmask with the dropout keep bits of (seed, dropout_p, shapes) — both layouts (see dropmask).  Only
  * the shape/dropout fields of d are read; independent of the Q/K/V data, so it can run ahead on another stream. */
 int asrx_attn_dropgen(const asrx_attn_desc* d, void* stream);

@@ -255,3 +255,67 @@ def test_bench_gpus_flag_launches_ranks_on_cpu():
     r = subprocess.run([sys.executable, bench, "--gpus", "2", "--cpu-dist-selftest"], env=env_bad,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode != 0
+
+
+def _release_worker(rank, world, port, q):
+    """One rank of the multi-GPU backward's release schedule over the product's flat gradient layout (c2 model):
+    decoder spans first, then each encoder release group, then finish() — as asrx.functions.encoder_bwd issues
+    them — with gradients that differ per rank."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    import asrx
+    from asrx.dist import GradAllReduce
+    from asrx.functions import _spans, param_order, release_groups
+    from asrx.params import FlatParams
+    cfg = CONFIGS["c2"]["cfg"]
+    model = asrx.Transformer(cfg.vocab_size, cfg.input_dim, cfg.d_model, cfg.dec_len, cfg.enc_len, cfg.n_enc,
+                             cfg.n_dec, cfg.n_heads, cfg.ff_dim, dropout=0.0, precision="bf16")
+    store = FlatParams(param_order(model), torch.device("cpu"))
+
+    class _C:
+        pass
+    C = _C()
+    C.store = store
+    enc, n = model.encoder, len(model.encoder._layers)
+    out = {}
+    for every in (0, 1, 4, n):
+        flat = store.grad
+        flat.copy_(torch.arange(flat.numel(), dtype=torch.float32).remainder_(977.0) * (rank + 1) + rank)
+        # 0.37 MB buckets: ragged against every span, so each rank count cuts the released ranges differently
+        r = GradAllReduce(flat, bucket_mb=0.37)
+        for a, b in _spans(C, list(model.decoder.parameters())):
+            r.ready(a, b)
+        for lo, hi in release_groups(n, every):
+            ps = [p for l in enc._layers[lo:hi] for p in l.parameters()]
+            if hi == n:
+                ps += list(enc._norm_out.parameters())
+            for a, b in _spans(C, ps):
+                r.ready(a, b)
+        r.finish()
+        base = torch.arange(flat.numel(), dtype=torch.float32).remainder_(977.0)
+        want = base * sum(w + 1 for w in range(world)) + sum(range(world))
+        out[every] = (bool(torch.equal(flat, want)), float(flat.double().sum()))
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_ws4_release_schedule_sums_every_element_once():
+    """World size 4 (beyond the 2- and 3-rank cases): the released ranges plus finish() leave every rank holding
+    the exact sum over ranks of every gradient element, for the default and fixed release granularities."""
+    world, port = 4, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_release_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=600) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for every in res[0]:
+        for r in range(world):
+            assert res[r][every][0], (r, every)                  # exact sum over ranks, every element once
+            assert res[r][every][1] == res[0][every][1], (r, every)

@@ -191,8 +191,13 @@ def test_gemm_grouped_wgrad(ngroups, wkind, xcd, monkeypatch):
         bg = torch.randn(N, device=dev, generator=g) if i % 2 == 0 else None
         refs.append((wg + dy.float().t() @ x.float(), None if bg is None else bg + dy.float().sum(0)))
         items.append((dy, x, wg, bg))
-    K().linear_wgrad_grouped(items)
+    kname = K().linear_wgrad_grouped(items)
     torch.cuda.synchronize()
+    if wkind == "wsq" and xcd:
+        assert kname.startswith("gemm_bf16_wsgq_kernel"), kname     # the queue kernel ran (8-XCD block map)
+    elif wkind in ("ws", "wsq"):
+        assert kname.startswith(("gemm_bf16_wsg_kernel", "gemm_bf16_wsgq_kernel")), kname
+        assert wkind == "wsq" or kname.startswith("gemm_bf16_wsg_kernel"), kname
     odd = bf(torch.randn(10, 250, device=dev))      # rows not 16-byte aligned: not groupable (C.wgrad runs it alone)
     assert not K().wgrad_groupable(odd, bf(torch.randn(10, 64, device=dev)), torch.zeros(250, 64, device=dev))
     for (dy, x, wg, bg), (rw, rb) in zip(items, refs):

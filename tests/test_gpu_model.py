@@ -1,8 +1,9 @@
 """Model-level parity of the drop-in asrx modules against the reference's golden vectors and the oracle.
 
 Tolerances: fp32 path <= 1e-3 relative (max-norm) on logits — we hold it to 1e-4;
-bf16 path <= 1.5e-2 relative with >= 98% argmax agreement (the reference under bf16 autocast itself deviates
-3.5e-3..4.4e-3 from fp64)."""
+bf16 path at the bench model dims (c3, c5): within BF16_FACTOR = 1.5x the error of the reference's own bf16 path
+(the oracle under torch's bf16 autocast) against the fp32 oracle, in the max norm, with >= 98% argmax agreement;
+small golden configs: <= 1.5e-2 relative with >= 98% argmax agreement."""
 import os
 
 import numpy as np
@@ -10,6 +11,7 @@ import pytest
 import torch
 
 from oracle.ref_model import CONFIGS, det_params, forward as oracle_forward, synthetic_batch
+from tests.bf16_check import check_bf16_forward
 
 pytestmark = pytest.mark.gpu
 dev = "cuda"
@@ -82,30 +84,30 @@ def test_forward_c2_fp32_vs_oracle():
 
 
 def test_forward_c3_bf16_vs_oracle():
-    """Paper config (d=512, h=8, 12+12) at T=1000 with a 2-utterance batch, bf16 fused path."""
+    """Paper config (d=512, h=8, 12+12) at T=1000 with a 2-utterance batch, bf16 fused path, bounded by the
+    reference's own bf16-autocast error."""
     m, cfg = build("c3", "bf16")
     m.eval()
     s, t, k = synthetic_batch(cfg, 2, 1000, 65, seed=1234)
     P = det_params(cfg, 0)
     with torch.no_grad():
-        ref = oracle_forward(P, s, t[:, :-1], k[:, :-1], cfg, False)
-        logits = m(s.to(dev), t[:, :-1].to(dev), k[:, :-1].to(dev))
-    assert relerr(logits, ref) < 1.5e-2
-    assert float((logits.cpu().argmax(-1) == ref.argmax(-1)).double().mean()) >= 0.98
+        logits = m(s.to(dev), t[:, :-1].to(dev), k[:, :-1].to(dev)).cpu()
+    check_bf16_forward(logits, P, s, t[:, :-1], k[:, :-1], cfg, "c3 B=2")
 
 
 def test_forward_c5_long_utterance_bf16_vs_oracle():
-    """c5 long-utterance stress geometry (T = 4000 frames -> T' = 999 encoder positions, O(T'^2) attention on the
-    tiled LDS K/V path since T' > 256), one utterance, bf16 fused path vs the oracle on the host."""
+    """c5 long-utterance stress geometry at the bench's decoder length: T = 4000 frames -> T' = 999 encoder
+    positions (O(T'^2) attention on the streamed LDS K/V path since T' > 256), L = 256 text positions (the
+    256-key causal decoder self-attention and the 256-query x 999-key cross-attention), two utterances, bf16 fused
+    path vs the oracle on the host, bounded by the reference's own bf16-autocast error."""
     m, cfg = build("c5", "bf16")
     m.eval()
-    s, t, k = synthetic_batch(cfg, 1, 4000, 65, seed=4321)
+    s, t, k = synthetic_batch(cfg, 2, 4000, 257, seed=4321)
+    assert int(k[:, :-1].sum(-1).max()) > 128 and int(k[:, :-1].sum(-1).min()) < 256   # long and padded rows
     P = det_params(cfg, 0)
     with torch.no_grad():
-        ref = oracle_forward(P, s, t[:, :-1], k[:, :-1], cfg, False)
-        logits = m(s.to(dev), t[:, :-1].to(dev), k[:, :-1].to(dev))
-    assert relerr(logits, ref) < 1.5e-2
-    assert float((logits.cpu().argmax(-1) == ref.argmax(-1)).double().mean()) >= 0.98
+        logits = m(s.to(dev), t[:, :-1].to(dev), k[:, :-1].to(dev)).cpu()
+    check_bf16_forward(logits, P, s, t[:, :-1], k[:, :-1], cfg, "c5 B=2 L=256")
 
 
 @pytest.mark.parametrize("precision,tol", [("fp32", 1e-3), ("bf16", 5e-2)])

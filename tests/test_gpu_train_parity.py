@@ -235,8 +235,5 @@ def test_trainer_grads_vs_oracle_bench_batch():
     names = [kk for kk, v in ref.items() if v is not None]
     check_grads(gsd, ref, names, "c3 B=64", ref_bf16=ref16)
     del P, P16, ref, ref16
-    from oracle.ref_model import forward as oracle_forward
-    with torch.no_grad():
-        ref_logits = oracle_forward(det_params(cfg, 0), s, t[:, :-1], k[:, :-1], cfg, False)
-    assert relerr(logits, ref_logits) < 1.5e-2
-    assert float((logits.argmax(-1) == ref_logits.argmax(-1)).double().mean()) >= 0.98
+    from tests.bf16_check import check_bf16_forward
+    check_bf16_forward(logits, det_params(cfg, 0), s, t[:, :-1], k[:, :-1], cfg, "c3 B=64")

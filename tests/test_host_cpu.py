@@ -16,7 +16,11 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _declared_symbols():
     src = open(os.path.join(REPO, "include", "asrx.h")).read()
-    return sorted(set(re.findall(r"\bint\s+(asrx_\w+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(?:int|int64_t)\s+(asrx_\w+)\s*\(", src)))
+
+
+# entry points with a non-int result, bound separately in asrx._lib.lib()
+_NON_INT = {"asrx_attn_dropmask_words"}
 
 
 def test_library_exports_every_declared_symbol():
@@ -27,9 +31,24 @@ def test_library_exports_every_declared_symbol():
     assert len(syms) >= 20
     for s in syms:
         assert hasattr(lib, s), s
-        assert s in SIGNATURES, s
-    assert set(SIGNATURES) == set(syms)
+        assert s in SIGNATURES or s in _NON_INT, s
+    assert set(SIGNATURES) | _NON_INT == set(syms)
     assert lib.asrx_version() >= 1
+
+
+@pytest.mark.parametrize("B,H,Lq,Lk", [(64, 8, 249, 249), (16, 8, 999, 999), (2, 8, 64, 300), (1, 1, 1, 257),
+                                       (3, 4, 33, 256)])
+def test_dropmask_size_rule(B, H, Lq, Lk):
+    """The header's dropmask size rule (asrx_attn_dropmask_words): key-major [B*H][ceil(Lq/32)][Lk] words, then
+    query-major [B*H][Lq][qmaj_stride(Lk)] with the stride rounded up to a multiple of 4 past 256 keys."""
+    import asrx
+    from asrx.kernels import qmaj_stride
+    lib = asrx.native()
+    nkw = (Lk + 31) // 32
+    stride = nkw if Lk <= 256 else (nkw + 3) // 4 * 4
+    assert qmaj_stride(Lk) == stride
+    assert lib.asrx_attn_dropmask_words(B, H, Lq, Lk) == B * H * (((Lq + 31) // 32) * Lk + Lq * stride)
+    assert lib.asrx_attn_dropmask_words(0, H, Lq, Lk) == -1
 
 
 def test_abi_rejects_bad_arguments_without_gpu():
