@@ -128,6 +128,8 @@ SIGNATURES = {
     "asrx_upload": [c_vp, c_vp, c_i64, c_vp],
     "asrx_set_seed_offset": [c_u64, c_vp],
     "asrx_dropout_mask": [c_vp, c_i64, c_f32, c_u64, c_vp],
+    "asrx_zero_spans": [c_vp, c_vp, c_i32, c_vp],
+    "asrx_step_tokens": [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp],
 }
 
 ERRORS = {-1: "bad argument", -2: "launch failure", -3: "unsupported shape/layout"}

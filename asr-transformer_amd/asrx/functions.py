@@ -323,8 +323,9 @@ def decoder_bwd(C, dec, S, dlogits_c):
     return denc
 
 
-def model_forward(C, model, spectrum, text, mask):
-    """Transformer.forward (model.py:194-198) as one native program. Returns (logits [B*L, Vp] fp32, S)."""
+def model_forward(C, model, spectrum, text, mask, spec=None):
+    """Transformer.forward (model.py:194-198) as one native program. Returns (logits [B*L, Vp] fp32, S).  spec:
+    the decoder's self-attention mask when the caller already built it (mask is then unused)."""
     dev = C.store.device
     spectrum = spectrum.to(dev)
     feats, Sf = Bk.frontend_fwd(C, spectrum, model.input_layer[0], model.input_layer[2])
@@ -332,7 +333,7 @@ def model_forward(C, model, spectrum, text, mask):
     T2 = Sf["dims"][-1]
     enc, Se = encoder_fwd(C, model.encoder, feats, B, T2)
     L = text.shape[1]
-    logits, Sd = decoder_fwd(C, model.decoder, text, mask, enc, B, L, T2)
+    logits, Sd = decoder_fwd(C, model.decoder, text, mask, enc, B, L, T2, spec=spec)
     return logits, dict(f=Sf, e=Se, d=Sd)
 
 

@@ -109,7 +109,8 @@ def kernel_name(d):
 PROBE = None
 
 # asrx_gemm_desc.kernel: forced kernel family (0 = auto).  ASRX_GEMM_KERNEL picks a process-wide default (A/B).
-KERNEL_CODES = {"auto": 0, "p3": 1, "reg": 3, "ring": 4, "ring128": 5, "p4": 6, "ws": 8, "wsp": 9, "ws64": 10}
+KERNEL_CODES = {"auto": 0, "p3": 1, "reg": 3, "ring": 4, "ring128": 5, "p4": 6, "ws": 8, "wsp": 9, "ws64": 10,
+                "wse": 11}
 GEMM_KERNEL = KERNEL_CODES.get(os.environ.get("ASRX_GEMM_KERNEL", "auto"), 0)
 
 
@@ -670,6 +671,28 @@ def sum_chunks_bf16(recv, world, chunk, out):
     """out[i] = bf16(sum_w recv[w * chunk + i]) with an fp32 sum (bf16-wire gradient exchange, asrx.dist)."""
     _cuda(recv, out)
     call("asrx_sum_chunks_bf16", recv.data_ptr(), world, chunk, out.data_ptr(), stream())
+
+
+def zero_spans(buf, spans):
+    """buf[a:b] = 0 for every row (a, b) of the device int64 table `spans` [n, 2] (asrx_zero_spans)."""
+    _cuda(buf, spans)
+    assert buf.dtype == torch.float32 and spans.dtype == torch.int64 and spans.is_contiguous()
+    call("asrx_zero_spans", buf.data_ptr(), spans.data_ptr(), spans.shape[0], stream())
+
+
+def step_tokens(text, inp, mask):
+    """(dec_in int64 [B*L], tgt int64 [B*L], valid uint8 [B, L]) of a teacher-forced step from (B, L+1) token rows
+    and the float pad mask (asrx_step_tokens): inp[:, :-1], text[:, 1:], mask[:, :-1] >= 1."""
+    _cuda(text, inp, mask)
+    assert text.dtype == torch.int64 and inp.dtype == torch.int64 and mask.dtype == torch.float32
+    assert text.stride(1) == 1 and inp.stride(1) == 1 and mask.stride(1) == 1 and text.shape == inp.shape == mask.shape
+    B, L = text.shape[0], text.shape[1] - 1
+    dec_in = torch.empty(B * L, dtype=torch.int64, device=text.device)
+    tgt = torch.empty(B * L, dtype=torch.int64, device=text.device)
+    valid = torch.empty(B, L, dtype=torch.uint8, device=text.device)
+    call("asrx_step_tokens", text.data_ptr(), text.stride(0), inp.data_ptr(), inp.stride(0), mask.data_ptr(),
+         mask.stride(0), B, L, dec_in.data_ptr(), tgt.data_ptr(), valid.data_ptr(), stream())
+    return dec_in, tgt, valid
 
 
 def dropout_mask(n, p, seed, device):

@@ -125,7 +125,12 @@ def wgrad_only_params(model):
     from .layers import MHA, _Lin
     from .model import _Classifier
     out = []
+    # (input_encoding is built but unused by the reference, model.py:173: no GEMM writes its gradient, so it stays in
+    #  the zeroed spans instead of being drained by a torch fill every step)
+    unused = {id(m) for m in (getattr(model, "input_encoding", None),) if m is not None}
     for m in model.modules():
+        if id(m) in unused:
+            continue
         if isinstance(m, (_Lin, _Classifier)):
             out.append(m.weight)
         elif isinstance(m, MHA):
@@ -259,12 +264,15 @@ class Trainer:
         # captured buffer, overwritten by the next step)
         self.want_preds = bool(preds)
         self.last_preds = None
-        if self._wonly:   # flat indices of everything else (zeroed each step by one index_fill)
-            keep = torch.ones(self.store.grad.numel(), dtype=torch.bool)
-            for p in self._wonly:
-                o = self.store.offset(p)
-                keep[o:o + p.numel()] = False
-            self._zero_idx = keep.nonzero().squeeze(1).to(self.store.grad.device)
+        if self._wonly:   # the spans of everything else, zeroed each step by one asrx_zero_spans launch
+            n, spans, pos = self.store.grad.numel(), [], 0
+            for o, k in sorted((self.store.offset(p), p.numel()) for p in self._wonly):
+                if o > pos:
+                    spans.append((pos, o))
+                pos = max(pos, o + k)
+            if pos < n:
+                spans.append((pos, n))
+            self._zero_spans = torch.tensor(spans, dtype=torch.int64).reshape(-1, 2).to(self.store.grad.device)
 
     def forward_backward(self, spectrum, text, mask, ready=None, capture=False, input_text=None):
         """text: (B, L+1) with BOS ... ; inputs text[:, :-1], targets text[:, 1:] (train.py:24,32).  input_text
@@ -274,13 +282,21 @@ class Trainer:
         model = self.model
         C = make_ctx(model, model.decoder.p)
         inp = text if input_text is None else input_text
-        logits, S = model_forward(C, model, spectrum, inp[:, :-1], mask[:, :-1])
+        if (text.is_cuda and text.dtype == torch.int64 and inp.dtype == torch.int64 and mask.dtype == torch.float32
+                and text.stride(1) == 1 and inp.stride(1) == 1 and mask.stride(1) == 1):
+            # the shifted inputs, targets and decoder mask in one native launch (no torch copies in the step)
+            B, L = text.shape[0], text.shape[1] - 1
+            dec_in, tgt, valid = K.step_tokens(text, inp, mask)
+            spec = K.MaskSpec(1, True, valid, valid, valid.stride(0))
+            logits, S = model_forward(C, model, spectrum, dec_in.view(B, L), None, spec=spec)
+        else:
+            logits, S = model_forward(C, model, spectrum, inp[:, :-1], mask[:, :-1])
+            tgt = text[:, 1:].reshape(-1).contiguous()
         V = model.decoder._classifier.V
-        tgt = text[:, 1:].reshape(-1).contiguous()
         loss, dl, am = K.cross_entropy(logits, V, tgt, ignore_index=self.ignore_index, want_argmax=self.want_preds)
         self.last_preds = am
         if self._wonly and C.cd == torch.bfloat16 and all(p.grad is not None for p in self.store.params):
-            self.store.grad.index_fill_(0, self._zero_idx, 0.0)
+            K.zero_spans(self.store.grad, self._zero_spans)
             C.fresh = FreshGrads(self.store, self._wonly)
         else:
             self.store.grad.zero_()

@@ -1350,3 +1350,62 @@ extern "C" int asrx_set_seed_offset(uint64_t offset, void* stream) {
   ASRX_CHECK_LAUNCH();
   return ASRX_OK;
 }
+
+// ------------------------------------------------------------------------------------------------
+// Training-step bookkeeping that round 3 left to torch kernels inside the captured step (asrx.train.Trainer):
+//   * asrx_zero_spans: zero the accumulating regions of the flat gradient buffer (biases, LayerNorm, embedding,
+//     conv, unused modules) — every span [start, end) of a static device table, one workgroup per span; the
+//     Linear-weight regions (FreshGrads) are left alone.  Replaces grad.index_fill_(0, idx, 0) (an 8-byte index
+//     per element read, 4-byte scattered writes).
+//   * asrx_step_tokens: the teacher-forced inputs of train.py:22-24,32 from the (B, L+1) token rows: decoder input
+//     tokens inp[:, :-1], targets text[:, 1:] (contiguous int64) and the decoder's key/query validity mask[:, :-1] >= 1
+//     (uint8, model.py:108-115: pad = mask < 1) in one launch.  Replaces two strided int64 copies and the mask
+//     compare + cast.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void zero_spans_kernel(float* __restrict__ base, const int64_t* __restrict__ spans) {
+  const int64_t a = spans[2 * blockIdx.x], b = spans[2 * blockIdx.x + 1];
+  // 16-B stores over the aligned middle, scalar ends
+  const int64_t a4 = (a + 3) & ~(int64_t)3, b4 = b & ~(int64_t)3;
+  if (a4 >= b4) {
+    for (int64_t i = a + threadIdx.x; i < b; i += 256) base[i] = 0.f;
+    return;
+  }
+  for (int64_t i = a + threadIdx.x; i < a4; i += 256) base[i] = 0.f;
+  for (int64_t i = b4 + threadIdx.x; i < b; i += 256) base[i] = 0.f;
+  for (int64_t i = a4 + 4 * (int64_t)threadIdx.x; i < b4; i += 1024) *(f4_t*)(base + i) = f4_t{0.f, 0.f, 0.f, 0.f};
+}
+
+extern "C" int asrx_zero_spans(float* base, const int64_t* spans, int32_t nspans, void* stream) {
+  if (nspans < 0 || (nspans > 0 && (!base || !spans))) return ASRX_ERR_ARG;
+  if (((uintptr_t)base & 15) != 0) return ASRX_ERR_ARG;
+  if (nspans == 0) return ASRX_OK;
+  hipLaunchKernelGGL(zero_spans_kernel, dim3(nspans), dim3(256), 0, (hipStream_t)stream, base, spans);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
+__global__ __launch_bounds__(256) void step_tokens_kernel(const int64_t* __restrict__ text, const int64_t* __restrict__ inp,
+                                                          const float* __restrict__ mask, int64_t ld_text, int64_t ld_inp,
+                                                          int64_t ld_mask, int B, int L, int64_t* __restrict__ dec_in,
+                                                          int64_t* __restrict__ tgt, uint8_t* __restrict__ valid) {
+  const int64_t n = (int64_t)B * L;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int b = (int)(i / L), t = (int)(i % L);
+    dec_in[i] = inp[(int64_t)b * ld_inp + t];
+    tgt[i] = text[(int64_t)b * ld_text + t + 1];
+    valid[i] = mask[(int64_t)b * ld_mask + t] >= 1.f ? 1 : 0;
+  }
+}
+
+extern "C" int asrx_step_tokens(const int64_t* text, int64_t ld_text, const int64_t* inp, int64_t ld_inp,
+                                const float* mask, int64_t ld_mask, int32_t B, int32_t L, int64_t* dec_in, int64_t* tgt,
+                                uint8_t* valid, void* stream) {
+  if (!text || !inp || !mask || !dec_in || !tgt || !valid || B <= 0 || L <= 0) return ASRX_ERR_ARG;
+  if (ld_text < L + 1 || ld_inp < L || ld_mask < L) return ASRX_ERR_ARG;
+  const int64_t n = (int64_t)B * L;
+  const int grid = (int)std::min<int64_t>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(step_tokens_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, text, inp, mask, ld_text, ld_inp,
+                     ld_mask, B, L, dec_in, tgt, valid);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}

@@ -1477,6 +1477,11 @@ int wsp_min_rows() {
   static const int m = [] { const char* e = getenv("ASRX_WSP_M"); return e ? atoi(e) : 4096; }();
   return m;
 }
+// ASRX_WSE=0 keeps the wide projections on p4 / ws / p3 (A/B switch; default on)
+bool wse_auto() {
+  static const bool on = [] { const char* e = getenv("ASRX_WSE"); return !(e && e[0] == '0'); }();
+  return on;
+}
 // ASRX_WS64=0 keeps the decoder's 4096-row N = 512 GEMMs on the ring kernels (A/B switch; default on): ws with
 // 64 x 128 tiles (64 x 4 = 256 tiles = one per CU) for 2048 <= M < 8192
 bool ws64_auto() {
@@ -1512,7 +1517,8 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
     tile = t128 >= 400 ? 128 : 64;
   }
   const int kvar = d->kernel == 1 ? 1 : d->kernel == 3 ? 3 : d->kernel == 4 ? 4 : d->kernel == 5 ? 5 :
-                   d->kernel == 6 ? 6 : d->kernel == 8 ? 8 : d->kernel == 9 ? 9 : d->kernel == 10 ? 10 : 0;
+                   d->kernel == 6 ? 6 : d->kernel == 8 ? 8 : d->kernel == 9 ? 9 : d->kernel == 10 ? 10 :
+                   d->kernel == 11 ? 11 : 0;
   const bool dma_ok = pl.vec && d->k % BK == 0 && (!d->a_trans || d->m % 8 == 0) && (!d->b_trans || d->n % 8 == 0) &&
                       d->m >= 8 && d->n >= 8;
   const int nt_p3 = ((d->m + P_BM - 1) / P_BM) * ((d->n + P_BN - 1) / P_BN);
@@ -1609,7 +1615,19 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
     pl.epi = epi;
     pl.ntiles = ((d->m + WS_BM - 1) / WS_BM) * (d->n / WS_BN);
   }
-    return pl;
+  // wse (use 14, round 4): the persistent ws walk with the epilogue on the loader waves (gemm_ws.hip) — every wide
+  // projection of >= 2 rounds of 256x128 tiles: the encoder Q/K/V and all-layer cross K/V forwards, the FFN1 forward
+  // (ReLU / dropout / mask bits) and the gated FFN2 data gradient; kernel code 11 forces it (K >= 128)
+  const bool wse_ok = dma_ok && !d->a_trans && batch == 1 && splitk == 1 && d->n % WS_BN == 0 && d->k >= 2 * BK &&
+                      !d->rowsum_a && !d->sc_outer && !d->sc_inner && epi != E_GENERIC && d->c_dtype == ASRX_BF16 &&
+                      wse_instantiated(d->b_trans, epi);
+  const long nt_ws = (long)((d->m + WS_BM - 1) / WS_BM) * (d->n / WS_BN);
+  if (wse_ok && (kvar == 11 || (kvar == 0 && wse_auto() && nt_ws >= 512))) {
+    pl.use = 14;
+    pl.epi = epi;
+    pl.ntiles = (int)nt_ws;
+  }
+  return pl;
 }
 
 }  // namespace
@@ -1635,6 +1653,8 @@ extern "C" int asrx_gemm_kernel_name(const asrx_gemm_desc* d, char* buf, int len
     snprintf(buf, len, "gemm_bf16_ws_kernel<%s, %d, %d>", tf[!!d->b_trans], pl.epi, pl.use == 13 ? 64 : 256);
   else if (pl.use == 12)
     snprintf(buf, len, "gemm_bf16_wsp_kernel<%s, %d>", tf[!!d->b_trans], pl.epi);
+  else if (pl.use == 14)
+    snprintf(buf, len, "gemm_bf16_wse_kernel<%s, %d>", tf[!!d->b_trans], pl.epi);
   else if (pl.use == 9)
     snprintf(buf, len, "gemm_bf16_tallk_kernel");
   else if (pl.use == 1 || pl.use == 2)
@@ -1682,6 +1702,8 @@ int gemm_bf16_run(const asrx_gemm_desc* d, const GemmArgs& g, const GemmPlan& pl
     launch_ws(g, d->b_trans, epi, pl.ntiles, pl.use == 13 ? 64 : 256, st);
   } else if (pl.use == 12) {
     launch_wsp(g, d->b_trans, epi, pl.ntiles, st);
+  } else if (pl.use == 14) {
+    launch_wse(g, d->b_trans, epi, pl.ntiles, st);
   } else if (pl.use == 9) {
     hipLaunchKernelGGL(gemm_bf16_tallk_kernel, dim3(splitk), dim3(512), 0, st, g, TallkConv{0, 0, 0, 0, 0, 0});
   } else if (pl.use == 2) {

@@ -268,6 +268,7 @@ ASRX_DEV int epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int
       // serialised one load latency per fragment row (FFN2 data gradient 57 -> see DESIGN §4)
       constexpr bool GPL = !PRE && (EPI & E_GBITS) != 0 && (EPI & (E_RESID | E_ROWADD | E_GATE)) == 0;
       uint32_t gwl[GPL ? TN / 2 : 1][GPL ? TM : 1];
+
       if constexpr (GPL) {
 #pragma unroll
         for (int i = 0; i < TN; i += 2)
@@ -324,8 +325,15 @@ ASRX_DEV int epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int
             const uint32_t mc = ((bx & lo) + lo) & hi, md = ((by & lo) + lo) & hi;
             const uint32_t r = (ma >> 15) | (mb >> 13) | (mc >> 11) | (md >> 9);
             const uint32_t byte = (r | (r >> 15)) & 0xffu;
-            if (m < g.M && na < g.N)
-              ((uint8_t*)g.mask_out)[((int64_t)m * g.ld_mask + (na >> 5)) * 4 + gq] = (uint8_t)byte;
+            // the 4 lanes l, l ^ 16, l ^ 32, l ^ 48 hold the 4 bytes of the row's 32-column word: OR-ed together by two
+            // permlane swaps (no register held across the loop), stored as one dword by lane group 0 (16 lanes, one
+            // dword store per fragment pair and row block instead of a byte store per lane)
+            uint32_t wv = byte << (8 * gq);
+            const auto x16 = __builtin_amdgcn_permlane16_swap(wv, wv, false, false);
+            wv = x16[0] | x16[1];
+            const auto x32 = __builtin_amdgcn_permlane32_swap(wv, wv, false, false);
+            wv = x32[0] | x32[1];
+            if (gq == 0 && m < g.M && na < g.N) ((uint32_t*)g.mask_out)[(int64_t)m * g.ld_mask + (na >> 5)] = wv;
           }
         }
       }
@@ -518,6 +526,8 @@ bool ws_instantiated(bool bt, int epi);
 void launch_ws(const GemmArgs& g, bool bt, int epi, int ntiles, int bm, hipStream_t st);
 bool wsp_instantiated(bool bt, int epi);
 void launch_wsp(const GemmArgs& g, bool bt, int epi, int ntiles, hipStream_t st);
+bool wse_instantiated(bool bt, int epi);
+void launch_wse(const GemmArgs& g, bool bt, int epi, int ntiles, hipStream_t st);
 int launch_ws_grouped(const GroupEnt* ents, const uint16_t* tile_group, const uint16_t* block_tile, int ntiles,
                       int blocks, float beta, int dbg, int* queue, float* part, hipStream_t st);
 

@@ -620,6 +620,284 @@ __global__ __launch_bounds__(512) void gemm_bf16_wsp_kernel(GemmArgs g, int ntil
 #undef WSP_ROLL_ORDER
 }
 
+// ------------------------------------------------------------------------------------------------
+// "wse": the wsp tile walk with the EPILOGUE moved off the MFMA waves (round 4).  In wsp / p4 the waves that run
+// the MFMAs also run each tile's epilogue: bias / ReLU / dropout hash / mask bits / gate bits and 64-128 KiB of
+// stores per tile, during which the matrix pipe idles (c3 FFN1 forward: 28.7 us of K-loop became 58.2 us).  Here
+// the compute waves only finish the fp32 arithmetic that has no memory operand (alpha, bias, ReLU, the dropout
+// scale 1/(1-p)), round ONCE to bf16 and hand the 256x128 tile to the loader waves through a 64 KiB LDS image,
+// then go straight on with the next tile's K-loop.  The loader waves ("service" waves) apply what remains — the
+// dropout zeroing (the counter-based hash), the gate bits of the FFN2 data gradient, the 1-bit ReLU mask of the FFN1
+// forward — and store the tile in 16-row passes spread over the next tile's K-steps, beside their LDS-DMA issue.
+// Values are bit-identical to the fused epilogue: zeroing commutes with the one rounding.
+//   LDS: a 2-stage ring (2 x 48 KiB) + the hand-off image H (64 KiB) = 160 KiB.  H holds the tile row-major as bf16,
+//   8-byte units XOR-swizzled by the row (conflict-free ds_write_b64 from the accumulator layout, whole-row
+//   ds_read_b128 for the passes).
+//   Schedule (one barrier per K-step, as ws): H(t) is written after the mid-step barrier of tile t's last K-step and
+//   is visible from the next barrier; the service waves read it in the nk - 1 following intervals (quota passes
+//   each) and have finished before the barrier after which H(t + 1) is written; the last tile drains after one
+//   extra barrier.  Needs nk >= 2 (K >= 128).  The service waves' stores and gate loads sit in their vmcnt ledger:
+//   the wait for stage s + 1 leaves exactly the stores issued after it in flight.
+// ------------------------------------------------------------------------------------------------
+constexpr int WSE_NST = 2;
+constexpr int WSE_H = WS_BM * WS_BN * 2;
+constexpr int WSE_LDS = WSE_NST * WS_STAGE + WSE_H;
+static_assert(WSE_LDS <= 163840, "wse: ring + hand-off image fit the CU's LDS");
+
+// byte offset in H of the 8-byte unit u (columns 4u .. 4u + 3) / the 16-byte unit v (columns 8v .. 8v + 7) of row r
+ASRX_DEV uint32_t wse_h8(int r, int u) { return (uint32_t)(r * 256 + ((u ^ ((r & 15) << 1)) << 3)); }
+ASRX_DEV uint32_t wse_h16(int r, int v) { return (uint32_t)(r * 256 + ((v ^ (r & 15)) << 4)); }
+
+// keep mask of a packed bf16 pair: low half kept if k0, high half if k1
+ASRX_DEV uint32_t keep2(bool k0, bool k1) { return (k0 ? 0x0000ffffu : 0u) | (k1 ? 0xffff0000u : 0u); }
+
+template <bool BT, int EPI>
+__global__ __launch_bounds__(512) void gemm_bf16_wse_kernel(GemmArgs g, int ntiles) {
+  g.seed = seed_eff(g.seed);
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[WSE_LDS];
+  constexpr int TM = 8, TN = 4, PASSES = WS_BM / 16;
+  constexpr bool DROP = (EPI & E_DROP) != 0, GB = (EPI & E_GBITS) != 0, MO = (EPI & E_MASKOUT) != 0;
+  static_assert((EPI & (E_F32 | E_RESID | E_ROWADD | E_GATE | E_BETA)) == 0, "wse: bf16 outputs, no memory operand but gate bits");
+  const TileSeq tl = TileSeq::persistent(ntiles, 1, blockIdx.x, gridDim.x);
+  if (tl.count == 0) return;
+  const int ntn = g.N / WS_BN;
+  const int nk = g.K / BK;
+  const int total = tl.count * nk;
+  const bf16_t* A = (const bf16_t*)g.a;
+  const bf16_t* B = (const bf16_t*)g.b;
+  const int64_t a_bytes = ((int64_t)(g.M - 1) * g.lda + g.K) * 2;
+  const int64_t b_bytes = BT ? ((int64_t)(g.K - 1) * g.ldb + g.N) * 2 : ((int64_t)(g.N - 1) * g.ldb + g.K) * 2;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int l = threadIdx.x & 63;
+  const int lw = wave & 3;
+  const int wm = (lw >> 1) * 128, wn = (lw & 1) * 64;
+  const bool noload = (g.dbg & 8) != 0, noepi = (g.dbg & 1) != 0;
+  unsigned char* H = lds + WSE_NST * WS_STAGE;
+  if (wave >= 4) {
+    // ---------------- service waves: the ring's LDS-DMA, then the hand-off passes
+    WsStage<WS_BM, false> sa;
+    WsStage<WS_BN, BT> sb;
+    int ni = 0, iv = 0, ik = 0;   // stages issued; tile / k-step of the next one
+    auto issue = [&](int buf) {
+      if (ik == 0) {
+        const int t = tl(iv);
+        sa.set_tile(lw, (t / ntn) * WS_BM, g.lda);
+        sb.set_tile(lw, (t % ntn) * WS_BN, g.ldb);
+      }
+      if (!noload) {
+        unsigned char* img = lds + buf * WS_STAGE;
+        sa.issue(img, sa.srd(A, g.lda, a_bytes, ik * BK), lw);
+        sb.issue(img + WS_PA, sb.srd(B, g.ldb, b_bytes, ik * BK), lw);
+      }
+      ++ni;
+      if (++ik == nk) { ik = 0; ++iv; }
+    };
+    const int t = threadIdx.x - 256;          // service thread: row (t >> 4) of a 16-row pass, 16-byte unit t & 15
+    const int pr = t >> 4, pv = t & 15;
+    const int quota = (PASSES + nk - 2) / (nk - 1);
+    // one 16-row pass p of the tile (m0, n0): returns the number of store instructions it issued (per wave)
+    uint32_t gw[PASSES];   // gate words of this interval's passes (E_GBITS)
+    auto gate_load = [&](int m0, int n0, int p0, int np) {
+      if constexpr (GB) {
+#pragma unroll
+        for (int q = 0; q < PASSES; ++q) {
+          if (q < np) {
+            const int m = m0 + 16 * (p0 + q) + pr, n = n0 + 8 * pv;
+            gw[q] = m < g.M ? ((const uint32_t*)g.gate)[(int64_t)m * g.ld_gate + (n >> 5)] : 0u;
+          }
+        }
+      }
+    };
+    auto pass = [&](int m0, int n0, int p, int q) -> int {
+      const int r = 16 * p + pr, m = m0 + r, n = n0 + 8 * pv;
+      v4u_t x = *(const v4u_t*)(H + wse_h16(r, pv));
+      if constexpr (DROP) {
+        const uint32_t pb = (uint32_t)((int64_t)m * g.N + n) >> 1;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t h = rng_hash(g.seed, pb + k);
+          x[k] &= keep2(rng_half(h, 0) >= g.drop_thr, rng_half(h, 1) >= g.drop_thr);
+        }
+      }
+      if constexpr (GB) {
+        const uint32_t b0 = gw[q] >> mask_bit_pos(n), b1 = gw[q] >> mask_bit_pos(n + 4);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t bb = k < 2 ? b0 >> (2 * k) : b1 >> (2 * k - 4);
+          x[k] &= keep2(bb & 1u, (bb >> 1) & 1u);
+        }
+      }
+      int nst = 0;
+      if (m < g.M) {
+        *(v4u_t*)((bf16_t*)g.c + (int64_t)m * g.ldc + n) = x;
+        nst = 1;
+      }
+      if constexpr (MO) {
+        // columns n + e: bit mask_bit_pos(n) + e (e < 4), mask_bit_pos(n + 4) + e - 4; "> 0" of a ReLU output =
+        // low 15 bits nonzero.  The 4 lanes of a quad hold the 4 parts of one 32-column word: OR by DPP.
+        const uint32_t lo = 0x7fff7fffu, hi = 0x80008000u;
+        uint32_t nz[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) nz[k] = ((x[k] & lo) + lo) & hi;   // bit 15: col 2k, bit 31: col 2k + 1
+        const uint32_t n4a = (nz[0] >> 15) | (nz[0] >> 30) | (nz[1] >> 13) | (nz[1] >> 28);
+        const uint32_t n4b = (nz[2] >> 15) | (nz[2] >> 30) | (nz[3] >> 13) | (nz[3] >> 28);
+        uint32_t w = ((n4a & 15u) << mask_bit_pos(n)) | ((n4b & 15u) << mask_bit_pos(n + 4));
+        w |= (uint32_t)__builtin_amdgcn_mov_dpp((int)w, 0xB1, 0xF, 0xF, true);   // quad_perm [1,0,3,2]
+        w |= (uint32_t)__builtin_amdgcn_mov_dpp((int)w, 0x4E, 0xF, 0xF, true);   // quad_perm [2,3,0,1]
+        if ((pv & 3) == 0 && m < g.M) ((uint32_t*)g.mask_out)[(int64_t)m * g.ld_mask + (n >> 5)] = w;
+        nst += 1;
+      }
+      return nst;
+    };
+    issue(0);
+    if (total > 1) issue(1);
+    if (noload) wait_vmcnt<0>();
+    else if (total > 1) wait_vmcnt<WS_INST>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    int ptile = -1, done = PASSES;   // hand-off image being stored: tile index (in tl) and passes done
+    for (int s = 0; s < total; ++s) {
+      // interval between the barriers of steps s - 1 and s: H(tile tau) became visible at its start if
+      // s == (tau + 1) nk + 1
+      if (s > nk && (s - 1) % nk == 0) { ptile = (s - 1) / nk - 1; done = 0; }
+      const int np = (ptile >= 0 && !noepi) ? min(quota, PASSES - done) : 0;
+      const int tt = ptile >= 0 ? tl(ptile) : 0;
+      const int m0 = (tt / ntn) * WS_BM, n0 = (tt % ntn) * WS_BN;
+      const bool iss = s >= 1 && s + 1 < total;
+      if (np > 0) gate_load(m0, n0, done, np);   // (issued before the stage: their wait leaves the stage in flight)
+      if (iss) issue((s + 1) & 1);
+      if constexpr (GB) {
+        if (np > 0) {
+          if (iss && !noload) wait_vmcnt<WS_INST>();
+          else wait_vmcnt<0>();
+        }
+      }
+      int nst = 0;
+      for (int q = 0; q < np; ++q) nst += pass(m0, n0, done + q, q);
+      done += np;
+      if (s + 1 < total) {
+        if (noload) wait_vmcnt<0>();
+        else wait_vmcnt_rt(nst);   // stage s + 1 landed; this interval's stores stay in flight
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    // the last tile's image: visible after one more barrier
+    __builtin_amdgcn_s_barrier();
+    if (!noepi) {
+      const int tt = tl(tl.count - 1);
+      const int m0 = (tt / ntn) * WS_BM, n0 = (tt % ntn) * WS_BN;
+      for (int p0 = 0; p0 < PASSES; p0 += quota) {
+        const int np = min(quota, PASSES - p0);
+        gate_load(m0, n0, p0, np);
+        if constexpr (GB) wait_vmcnt<0>();
+        for (int q = 0; q < np; ++q) pass(m0, n0, p0 + q, q);
+      }
+    }
+    return;
+  }
+  // ---------------- compute waves: the p4 pipeline on a 128x64 wave tile (as wsp), then the tile into H
+  f4_t acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+  s8_t fa0[TM], fb0[TN], fa1[TM], fb1[TN];
+  uint32_t S = p4_swz_bytes();
+#define WSE_ROLL_ORDER()                                                                      \
+  do {                                                                                        \
+    __builtin_amdgcn_sched_group_barrier(0x100, TN * (BT ? 2 : 1), 0);                        \
+    _Pragma("unroll") for (int j_ = 0; j_ < TM; ++j_) {                                       \
+      __builtin_amdgcn_sched_group_barrier(0x008, TN, 0);                                     \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                      \
+    }                                                                                         \
+  } while (0)
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int j = 0; j < TM; ++j) fa0[j] = p4_frag<WS_BM, false>(lds, wm + 16 * j, 0, S);
+#pragma unroll
+  for (int i = 0; i < TN; ++i) fb0[i] = p4_frag<WS_BN, BT>(lds + WS_PA, wn + 16 * i, 0, S);
+  uint32_t cbo = 0;
+  int vc = 0, kk = 0;   // tile / k-step of step s
+  const int gq = l >> 4;
+  for (int s = 0; s < total; ++s) {
+    asm volatile("" : "+s"(cbo));
+    const uint32_t nbo = cbo == 0 ? (uint32_t)WS_STAGE : 0u;
+    const unsigned char* la = lds + cbo;
+    // the tile's bias columns, loaded at its last K-step (the compute waves issue no other vector-memory operation)
+    f4_t b4[TN];
+    if constexpr ((EPI & E_BIAS) != 0) {
+      if (kk == nk - 1) {
+        const int n0 = (tl(vc) % ntn) * WS_BN;
+#pragma unroll
+        for (int i = 0; i < TN; ++i) b4[i] = *(const f4_t*)(g.bias + n0 + wn + 16 * i + 4 * gq);
+      }
+    }
+    asm volatile("" : "+v"(S));
+#pragma unroll
+    for (int i = 0; i < TN; ++i) fb1[i] = p4_frag<WS_BN, BT>(la + WS_PA, wn + 16 * i, 1, S);
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+#pragma unroll
+      for (int i = 0; i < TN; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[i], fa0[j], acc[i][j], 0, 0, 0);
+      fa1[j] = p4_frag<WS_BM, false>(la, wm + 16 * j, 1, S);
+    }
+    WSE_ROLL_ORDER();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const unsigned char* ln = lds + nbo;
+    asm volatile("" : "+v"(S));
+#pragma unroll
+    for (int i = 0; i < TN; ++i) fb0[i] = p4_frag<WS_BN, BT>(ln + WS_PA, wn + 16 * i, 0, S);   // (unconditional, as in ws)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+#pragma unroll
+      for (int i = 0; i < TN; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[i], fa1[j], acc[i][j], 0, 0, 0);
+      fa0[j] = p4_frag<WS_BM, false>(ln, wm + 16 * j, 0, S);
+    }
+    WSE_ROLL_ORDER();
+    if (kk == nk - 1) {
+      if (noepi) {
+        keep_live(acc);
+      } else {
+        // the memory-free part of the epilogue (epi_vals order: alpha, bias, ReLU, dropout scale), ONE rounding,
+        // into H (lane: row wm + 16 j + (l & 15), columns wn + 16 i + 4 gq .. + 3 = 8-byte unit (wn >> 2) + 4 i + gq)
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int j = 0; j < TM; ++j) {
+            f4_t v = acc[i][j];
+            if constexpr ((EPI & E_ALPHA) != 0) v *= g.alpha;
+            if constexpr ((EPI & E_BIAS) != 0) v += b4[i];
+            if constexpr ((EPI & E_RELU) != 0) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+            }
+            if constexpr (DROP) v *= g.drop_scale;
+            const uint2 u = {pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+            *(uint2*)(H + wse_h8(wm + 16 * j + (l & 15), (wn >> 2) + 4 * i + gq)) = u;
+          }
+      }
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+    }
+    if (++kk == nk) { kk = 0; ++vc; }
+    cbo = nbo;
+  }
+#undef WSE_ROLL_ORDER
+  // the last tile's image complete before the service waves' drain
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+// wse instantiations: the step's wide projections — Q/K/V and cross K/V forwards (bias), the FFN1 forward (bias, ReLU,
+// dropout, 1-bit mask), the FFN2 data gradient gated by those bits (alpha = 1/(1-p)), plain forwards
+#define ASRX_EPIWSE_NT(X) X(0) X(E_BIAS) X(E_BIAS | E_RELU) X(E_BIAS | E_RELU | E_DROP) X(E_BIAS | E_RELU | E_MASKOUT) \
+  X(E_BIAS | E_RELU | E_DROP | E_MASKOUT)
+#define ASRX_EPIWSE_NN(X) X(0) X(E_GBITS) X(E_GBITS | E_ALPHA)
+
 // wsp instantiations: the wide projections of the training step (Q/K/V and cross K/V forwards with bias, the FFN1
 // forward's ReLU / dropout / 1-bit mask epilogue, the FFN2 data gradient gated by those bits) and plain GEMMs
 #define ASRX_EPIWSP_NT(X) X(0) X(E_BIAS) X(E_BIAS | E_RELU) X(E_BIAS | E_RELU | E_DROP) X(E_BIAS | E_RELU | E_MASKOUT) \
@@ -687,6 +965,28 @@ void launch_wsp(const GemmArgs& g, bool bt, int epi, int ntiles, hipStream_t st)
   } else {
     constexpr bool BT_ = true;
     switch (epi) { ASRX_EPIWSP_NN(ASRX_CASE) default: break; }
+  }
+#undef ASRX_CASE
+}
+
+bool wse_instantiated(bool bt, int epi) {
+#define ASRX_HAS(E) if (epi == (E)) return true;
+  if (!bt) { ASRX_EPIWSE_NT(ASRX_HAS) }
+  else { ASRX_EPIWSE_NN(ASRX_HAS) }
+#undef ASRX_HAS
+  return false;
+}
+
+void launch_wse(const GemmArgs& g, bool bt, int epi, int ntiles, hipStream_t st) {
+  const int G = ntiles >= 256 ? 256 : 8 * ((ntiles + 7) / 8);
+  const dim3 grid(G), blk(512);
+#define ASRX_CASE(E) case (E): hipLaunchKernelGGL((gemm_bf16_wse_kernel<BT_, (E)>), grid, blk, 0, st, g, ntiles); return;
+  if (!bt) {
+    constexpr bool BT_ = false;
+    switch (epi) { ASRX_EPIWSE_NT(ASRX_CASE) default: break; }
+  } else {
+    constexpr bool BT_ = true;
+    switch (epi) { ASRX_EPIWSE_NN(ASRX_CASE) default: break; }
   }
 #undef ASRX_CASE
 }

@@ -80,8 +80,9 @@ typedef struct asrx_gemm_desc {
   uint32_t* mask_out; int64_t ld_mask;
   /* kernel family (tests / A-B; 0 = auto): 1 = 256x128 LDS-DMA ring (p3), 3 = register-staged tiles, 4 = 64x64
    * LDS-DMA ring, 5 = 128x64 LDS-DMA ring, 6 = 256x256 LDS-DMA ring (p4), 8 = warp-specialised 256x128 tiles
-   * (ws: 4 MFMA waves + 4 LDS-DMA loader waves; A k-contiguous, N % 128 == 0), 10 = ws on 64x128 tiles (the
-   * 4096-row decoder GEMMs) — honoured where the family's
+   * (ws: 4 MFMA waves + 4 LDS-DMA loader waves; A k-contiguous, N % 128 == 0), 9 = ws over a persistent tile walk
+   * (wsp), 10 = ws on 64x128 tiles (the 4096-row decoder GEMMs), 11 = wsp with the epilogue on the loader waves
+   * (wse: bf16 C, K % 64 == 0, K >= 128) — honoured where the family's
    * preconditions hold, else auto.  Every family is a hand-written kernel of this library. */
   int32_t kernel;
 } asrx_gemm_desc;
@@ -354,6 +355,16 @@ int asrx_sum_chunks_bf16(const void* in, int32_t world, int64_t chunk, void* out
 int asrx_adam(float* p, const float* g, float* m, float* v, void* p_bf16, int64_t n, float lr, float beta1,
               float beta2, float eps, float weight_decay, float bias_corr1, float bias_corr2, float grad_scale,
               int32_t decoupled, const float* hyp, void* stream);
+/* Zero the spans [spans[2i], spans[2i+1]) (element offsets, device int64 table of nspans pairs) of an fp32 buffer
+ * (16-B aligned base), one workgroup per span.  The training step zeroes the accumulating gradient regions with it
+ * (optimizer.zero_grad, train.py:27, for everything a weight-gradient GEMM does not overwrite). */
+int asrx_zero_spans(float* base, const int64_t* spans, int32_t nspans, void* stream);
+/* Teacher-forced step inputs (train.py:22-24,32 without the index_put quirk; model.py:108-115): from the (B, L+1)
+ * token rows `text` (targets) and `inp` (decoder input; = text unless shifted), row strides in elements, and the
+ * float pad mask (B, L+1): dec_in[b*L+t] = inp[b][t], tgt[b*L+t] = text[b][t+1], valid[b*L+t] = mask[b][t] >= 1. */
+int asrx_step_tokens(const int64_t* text, int64_t ld_text, const int64_t* inp, int64_t ld_inp, const float* mask,
+                     int64_t ld_mask, int32_t B, int32_t L, int64_t* dec_in, int64_t* tgt, uint8_t* valid,
+                     void* stream);
 /* delta[(b*heads+h)*lq+q] = sum_d dO*O (attention backward prologue). */
 int asrx_attn_delta(const asrx_attn_desc* d, void* stream);
 /* y = dropout(x) with the library RNG (idx = element index); used for tests of the RNG stream. */

@@ -35,7 +35,7 @@ def bf(x):
 
 # ------------------------------------------------------------------------------------------------ GEMM
 
-VARIANTS = ["auto", "p3", "p4", "reg", "ring", "ring128"]   # kernel families the auto plan can select (gemm.hip plan_bf16)
+VARIANTS = ["auto", "p3", "p4", "reg", "ring", "ring128", "wse"]   # kernel families the auto plan can select (gemm.hip plan_bf16)
 
 
 @pytest.fixture
@@ -84,7 +84,7 @@ def test_gemm_epilogue(tile, kernel_variant):
     assert relerr(out.cpu(), ref) < 2e-3
 
 
-@pytest.mark.parametrize("kernel_variant", ["auto", "p3", "p4", "ring", "ring128"], indirect=True)
+@pytest.mark.parametrize("kernel_variant", ["auto", "p3", "p4", "ring", "ring128", "wse"], indirect=True)
 @pytest.mark.parametrize("m,n,p", [(300, 512, 0.1), (1000, 4160, 0.0), (4096, 2048, 0.1)])
 def test_gemm_relu_mask_bits(m, n, p, kernel_variant):
     """FFN hidden layer: the ReLU/dropout epilogue also writes the 1-bit mask C > 0 (mask_out), and the data
@@ -357,6 +357,44 @@ def test_gemm_wsp_epilogues(M, N, Kd):
         assert torch.equal(a, b)
     ref = x.double() @ w.double().t() + bias.double()
     assert relerr(outs["wsp"][0].float(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,Kd", [(15936, 1536, 512), (15936, 2048, 512), (4096, 2048, 512), (1000, 384, 192),
+                                    (700, 256, 128), (15936, 1024, 128), (2500, 4096, 512)])
+def test_gemm_wse_epilogues(M, N, Kd):
+    """The persistent warp-specialised kernel with the epilogue on the loader waves (kernel code 11, wse): bias
+    (Q/K/V, cross K/V), bias + ReLU + dropout + 1-bit mask out (FFN1 forward), bias + ReLU + mask without dropout,
+    and the data gradient gated by the bits with alpha (FFN2 dX) — bit for bit equal to the p4 kernel's fused
+    epilogue (same MFMA accumulation order; the hand-off rounds once, zeroing commutes with it), incl. ragged M,
+    the shortest reduction (K = 128: two K-steps per tile, the whole hand-off in one interval), one tile per
+    workgroup (the drain only) and many; the plain product against fp64."""
+    g = torch.Generator(device=dev).manual_seed(M + N + Kd)
+    x = bf(torch.randn(M, Kd, device=dev, generator=g))
+    w = bf(torch.randn(N, Kd, device=dev, generator=g))
+    bias = torch.randn(N, device=dev, generator=g)
+    assert plan_name(M, N, Kd, bias=True, kernel="wse").startswith("gemm_bf16_wse_kernel")
+    outs = {}
+    for kern in ("wse", "p4"):
+        y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        K().linear(x, w, y, bias=bias, kernel=kern)
+        yr = torch.empty_like(y)
+        bits = torch.full((M, N // 32 + 1), -1, device=dev, dtype=torch.int32)   # odd row stride, pad must survive
+        K().linear(x, w, yr, bias=bias, relu=True, dropout_p=0.1, seed=9, mask_out=bits, ld_mask=N // 32 + 1,
+                   kernel=kern)
+        y0 = torch.empty_like(y)
+        bits0 = torch.zeros(M, N // 32, device=dev, dtype=torch.int32)
+        K().linear(x, w, y0, bias=bias, relu=True, mask_out=bits0, ld_mask=N // 32, kernel=kern)
+        dy = bf(torch.randn(M, Kd, device=dev, generator=torch.Generator(device=dev).manual_seed(5)))
+        wt = bf(torch.randn(Kd, N, device=dev, generator=torch.Generator(device=dev).manual_seed(6)))
+        dx = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        K().linear_dgrad(dy, wt, dx, alpha=1 / 0.9, gate=bits, ld_gate=N // 32 + 1, gate_bits=True, kernel=kern)
+        outs[kern] = (y, yr, bits, y0, bits0, dx)
+    torch.cuda.synchronize()
+    for name, a, b in zip(("bias", "relu+drop", "bits", "relu", "bits0", "gated dX"), outs["wse"], outs["p4"]):
+        assert torch.equal(a, b), name
+    assert bool((outs["wse"][2][:, N // 32:] == -1).all())
+    ref = x.double() @ w.double().t() + bias.double()
+    assert relerr(outs["wse"][0].float(), ref) < 1e-2
 
 
 def test_gemm_ws_rowadd():
@@ -935,3 +973,27 @@ def test_sum_chunks_bf16(world, chunk):
     K().sum_chunks_bf16(recv, world, chunk, out)
     want = recv.view(world, chunk).float().sum(0).to(torch.bfloat16) if chunk else out
     assert torch.equal(out, want)
+
+
+def test_zero_spans_and_step_tokens():
+    """asrx_zero_spans (the step's gradient zeroing: ragged, unaligned and adjacent spans, nothing outside them
+    touched) and asrx_step_tokens (decoder input, targets and validity mask of train.py:22-24,32 / model.py:108-115)
+    against torch."""
+    g = torch.Generator(device=dev).manual_seed(3)
+    buf = torch.randn(100003, device=dev, generator=g)
+    ref = buf.clone()
+    spans = [(0, 5), (5, 64), (70, 71), (77, 4099), (5000, 5003), (9001, 70001), (99999, 100003)]
+    for a, b in spans:
+        ref[a:b] = 0
+    K().zero_spans(buf, torch.tensor(spans, dtype=torch.int64, device=dev))
+    torch.cuda.synchronize()
+    assert torch.equal(buf, ref)
+    B, L1 = 5, 17
+    text = torch.randint(0, 250, (B, L1), device=dev, generator=g)
+    inp = torch.randint(0, 250, (B, L1), device=dev, generator=g)
+    mask = (torch.rand(B, L1, device=dev, generator=g) > 0.3).float()
+    dec_in, tgt, valid = K().step_tokens(text, inp, mask)
+    torch.cuda.synchronize()
+    assert torch.equal(dec_in.view(B, L1 - 1), inp[:, :-1])
+    assert torch.equal(tgt, text[:, 1:].reshape(-1))
+    assert torch.equal(valid, (mask[:, :-1] >= 1).to(torch.uint8))
