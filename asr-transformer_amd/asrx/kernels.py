@@ -680,6 +680,29 @@ def zero_spans(buf, spans):
     call("asrx_zero_spans", buf.data_ptr(), spans.data_ptr(), spans.shape[0], stream())
 
 
+ROW_SCALE, ROW_ADD = 0, 1
+
+
+def rowwise(op, a, b, out, period=1):
+    """fp32 [rows, d]: ROW_SCALE out = a * b[:, None] (b [rows]); ROW_ADD out = a + b[r % period] (b [period, d])
+    (asrx_rowwise; out may alias a)."""
+    _cuda(a, b, out)
+    assert a.dtype == b.dtype == out.dtype == torch.float32 and a.is_contiguous() and out.is_contiguous()
+    assert b.is_contiguous() and out.shape == a.shape and a.dim() == 2
+    rows, d = a.shape
+    assert (b.numel() == rows) if op == ROW_SCALE else (b.shape[-1] == d and b.numel() >= period * d)
+    call("asrx_rowwise", op, a.data_ptr(), b.data_ptr(), out.data_ptr(), rows, d, period, stream())
+
+
+def transpose_last2(x, out):
+    """out[b] = x[b]^T for fp32 x (B, R, C) contiguous -> out (B, C, R) (asrx_transpose_last2)."""
+    _cuda(x, out)
+    assert x.dtype == out.dtype == torch.float32 and x.is_contiguous() and out.is_contiguous() and x.dim() == 3
+    B, R, C = x.shape
+    assert out.shape == (B, C, R)
+    call("asrx_transpose_last2", x.data_ptr(), B, R, C, out.data_ptr(), stream())
+
+
 def step_tokens(text, inp, mask):
     """(dec_in int64 [B*L], tgt int64 [B*L], valid uint8 [B, L]) of a teacher-forced step from (B, L+1) token rows
     and the float pad mask (asrx_step_tokens): inp[:, :-1], text[:, 1:], mask[:, :-1] >= 1."""

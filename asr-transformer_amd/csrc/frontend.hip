@@ -1409,3 +1409,57 @@ extern "C" int asrx_step_tokens(const int64_t* text, int64_t ld_text, const int6
   ASRX_CHECK_LAUNCH();
   return ASRX_OK;
 }
+
+// ------------------------------------------------------------------------------------------------
+// Row-wise fp32 ops of the post-LN model family (asrx.new: modules/Transformer/new/model.py):
+//   ROWSCALE: out[r][c] = a[r][c] * b[r]            (x *= non_pad_mask, new/model.py:25,28,83,86,89)
+//   ROWADD:   out[r][c] = a[r][c] + b[r % period][c] (+ pe(x), new/model.py:60)
+// and the (B, R, C) -> (B, C, R) transpose of the encoder input (new/model.py:55).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rowwise_kernel(int op, const float* __restrict__ a, const float* __restrict__ b,
+                                                      float* __restrict__ out, int64_t rows, int d, int64_t period) {
+  const int64_t n = rows * d;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / d;
+    const int c = (int)(i - r * d);
+    out[i] = op == 0 ? a[i] * b[r] : a[i] + b[(r % period) * d + c];
+  }
+}
+
+extern "C" int asrx_rowwise(int32_t op, const float* a, const float* b, float* out, int64_t rows, int32_t d,
+                            int64_t period, void* stream) {
+  if (!a || !b || !out || rows < 0 || d <= 0 || (op != 0 && op != 1) || (op == 1 && period <= 0)) return ASRX_ERR_ARG;
+  if (rows == 0) return ASRX_OK;
+  hipLaunchKernelGGL(rowwise_kernel, dim3(grid_for(rows * d)), dim3(256), 0, (hipStream_t)stream, (int)op, a, b, out,
+                     rows, (int)d, period);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
+// out[b][c][r] = x[b][r][c] through a 32x33 LDS tile
+__global__ __launch_bounds__(256) void transpose_kernel(const float* __restrict__ x, int R, int C, float* __restrict__ out) {
+  __shared__ float tile[32][33];
+  const int64_t b = blockIdx.z;
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const float* xb = x + b * (int64_t)R * C;
+  float* ob = out + b * (int64_t)R * C;
+  for (int k = ty; k < 32; k += 8) {
+    const int r = r0 + k, c = c0 + tx;
+    tile[k][tx] = (r < R && c < C) ? xb[(int64_t)r * C + c] : 0.f;
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    const int c = c0 + k, r = r0 + tx;
+    if (r < R && c < C) ob[(int64_t)c * R + r] = tile[tx][k];
+  }
+}
+
+extern "C" int asrx_transpose_last2(const float* x, int64_t batch, int32_t R, int32_t C, float* out, void* stream) {
+  if (!x || !out || batch < 0 || R < 0 || C < 0 || batch > 65535) return ASRX_ERR_ARG;
+  if (batch == 0 || R == 0 || C == 0) return ASRX_OK;
+  hipLaunchKernelGGL(transpose_kernel, dim3((C + 31) / 32, (R + 31) / 32, (unsigned)batch), dim3(256), 0,
+                     (hipStream_t)stream, x, (int)R, (int)C, out);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}

@@ -383,6 +383,109 @@ bool ln_bwd_launch(int x_dtype, const void* x, int dy_dtype, const void* dy, con
   return true;
 }
 
+// Any width d <= LNA_MAXD (the widths the CH x NJ kernels do not cover, e.g. the post-LN family's d = n_mels = 80,
+// asrx.new): one row per wave, lane l owns columns l + 64 k; two-pass mean / variance from registers.
+constexpr int LNA_K = 32, LNA_MAXD = 64 * LNA_K;
+ASRX_DEV float lna_ld(const void* p, int dtype, int64_t i) {
+  return dtype == ASRX_BF16 ? bf2f(((const bf16_t*)p)[i]) : ((const float*)p)[i];
+}
+
+__global__ __launch_bounds__(256) void ln_fwd_any_kernel(int x_dtype, const void* __restrict__ x, int y_dtype,
+                                                         void* __restrict__ y, const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, float* __restrict__ mean,
+                                                         float* __restrict__ rstd, int64_t rows, int d, float eps) {
+  const int l = threadIdx.x & 63;
+  const int nk = (d + 63) / 64;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += (int64_t)gridDim.x * 4) {
+    float v[LNA_K];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < LNA_K; ++k) {
+      const int c = l + 64 * k;
+      v[k] = (k < nk && c < d) ? lna_ld(x, x_dtype, row * d + c) : 0.f;
+      s += v[k];
+    }
+    const float mu = wave_sum(s) / d;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < LNA_K; ++k) {
+      const int c = l + 64 * k;
+      const float t = (k < nk && c < d) ? v[k] - mu : 0.f;
+      q += t * t;
+    }
+    const float rs = rsqrtf(wave_sum(q) / d + eps);
+#pragma unroll
+    for (int k = 0; k < LNA_K; ++k) {
+      const int c = l + 64 * k;
+      if (k < nk && c < d) {
+        const float o = (v[k] - mu) * rs * gamma[c] + beta[c];
+        if (y_dtype == ASRX_F32) ((float*)y)[row * d + c] = o;
+        else ((bf16_t*)y)[row * d + c] = f2bf(o);
+      }
+    }
+    if (l == 0) { mean[row] = mu; rstd[row] = rs; }
+  }
+}
+
+// backward for any width: dx = rstd (g - mean(g) - xhat mean(g xhat)) + dres, g = dy gamma; dgamma | dbeta partials per
+// block into part[block][2 d] (LDS: 4 waves x 2 d floats, dynamic)
+__global__ __launch_bounds__(256) void ln_bwd_any_kernel(int x_dtype, const void* __restrict__ x, int dy_dtype,
+                                                         const void* __restrict__ dy, const float* __restrict__ gamma,
+                                                         const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                         const float* __restrict__ dres, float* __restrict__ dx_out,
+                                                         void* __restrict__ dx_drop, int drop_dtype, uint32_t thr,
+                                                         float dscale, uint64_t seed, float* __restrict__ part,
+                                                         int64_t rows, int d) {
+  seed = seed_eff(seed);
+  extern __shared__ float red[];   // [4][2 d]
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nk = (d + 63) / 64;
+  float pg[LNA_K], pb[LNA_K];
+#pragma unroll
+  for (int k = 0; k < LNA_K; ++k) { pg[k] = 0.f; pb[k] = 0.f; }
+  for (int64_t row = (int64_t)blockIdx.x * 4 + w; row < rows; row += (int64_t)gridDim.x * 4) {
+    const float mu = mean[row], rs = rstd[row];
+    float xh[LNA_K], g[LNA_K], sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int k = 0; k < LNA_K; ++k) {
+      const int c = l + 64 * k;
+      const bool ok = k < nk && c < d;
+      const float xv = ok ? lna_ld(x, x_dtype, row * d + c) : 0.f;
+      const float dv = ok ? lna_ld(dy, dy_dtype, row * d + c) : 0.f;
+      xh[k] = (xv - mu) * rs;
+      g[k] = ok ? dv * gamma[c] : 0.f;
+      sg += g[k];
+      sgx += g[k] * xh[k];
+      pg[k] += dv * xh[k];
+      pb[k] += dv;
+    }
+    sg = wave_sum(sg) / d;
+    sgx = wave_sum(sgx) / d;
+#pragma unroll
+    for (int k = 0; k < LNA_K; ++k) {
+      const int c = l + 64 * k;
+      if (k < nk && c < d) {
+        const int64_t off = row * d + c;
+        const float o = rs * (g[k] - sg - xh[k] * sgx) + (dres ? dres[off] : 0.f);
+        dx_out[off] = o;
+        if (dx_drop) {
+          const float od = (thr == 0u || rng_keep(seed, (uint32_t)off, thr)) ? o * dscale : 0.f;
+          if (drop_dtype == ASRX_F32) ((float*)dx_drop)[off] = od;
+          else ((bf16_t*)dx_drop)[off] = f2bf(od);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < LNA_K; ++k) {
+    const int c = l + 64 * k;
+    if (k < nk && c < d) { red[w * 2 * d + c] = pg[k]; red[w * 2 * d + d + c] = pb[k]; }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 2 * d; c += 256)
+    part[(int64_t)blockIdx.x * 2 * d + c] = red[c] + red[2 * d + c] + red[4 * d + c] + red[6 * d + c];
+}
+
 }  // namespace
 
 ASRX_SEED_OFFSET_SETTER(norm)
@@ -412,7 +515,12 @@ extern "C" int asrx_layernorm_fwd(int32_t x_dtype, const void* x, int32_t y_dtyp
             ln_fwd_launch<4, 3>(x_dtype, x, y_dtype, y, gamma, beta, mean, rstd, rows, d, eps, st) ||
             ln_fwd_launch<4, 4>(x_dtype, x, y_dtype, y, gamma, beta, mean, rstd, rows, d, eps, st) ||
             ln_fwd_launch<4, 8>(x_dtype, x, y_dtype, y, gamma, beta, mean, rstd, rows, d, eps, st);
-  if (!ok) return ASRX_ERR_UNSUPPORTED;
+  if (!ok) {
+    if (d <= 0 || d > LNA_MAXD) return ASRX_ERR_UNSUPPORTED;
+    const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((rows + 3) / 4, 2048));
+    hipLaunchKernelGGL(ln_fwd_any_kernel, dim3(blocks), dim3(256), 0, st, x_dtype, x, y_dtype, y, gamma, beta, mean,
+                       rstd, rows, d, eps);
+  }
   ASRX_CHECK_LAUNCH();
   return ASRX_OK;
 }
@@ -444,7 +552,13 @@ extern "C" int asrx_layernorm_bwd(int32_t x_dtype, const void* x, int32_t dy_dty
             ln_bwd_launch<4, 2>(x_dtype, x, dy_dtype, dy, gamma, mean, rstd, dres, dx_out, dx_drop, drop_dtype, dropout_p, seed, part, nblocks, rows, d, st) ||
             ln_bwd_launch<4, 3>(x_dtype, x, dy_dtype, dy, gamma, mean, rstd, dres, dx_out, dx_drop, drop_dtype, dropout_p, seed, part, nblocks, rows, d, st) ||
             ln_bwd_launch<4, 4>(x_dtype, x, dy_dtype, dy, gamma, mean, rstd, dres, dx_out, dx_drop, drop_dtype, dropout_p, seed, part, nblocks, rows, d, st);
-  if (!ok) return ASRX_ERR_UNSUPPORTED;
+  if (!ok) {
+    if (d <= 0 || d > LNA_MAXD) return ASRX_ERR_UNSUPPORTED;
+    const uint32_t thr = drop_threshold(dropout_p);
+    const float sc = (dropout_p > 0.f && dropout_p < 1.f) ? 1.f / (1.f - dropout_p) : 1.f;
+    hipLaunchKernelGGL(ln_bwd_any_kernel, dim3(nblocks), dim3(256), (size_t)8 * d * sizeof(float), st, x_dtype, x,
+                       dy_dtype, dy, gamma, mean, rstd, dres, dx_out, dx_drop, drop_dtype, thr, sc, seed, part, rows, d);
+  }
   ASRX_CHECK_LAUNCH();
   return ASRX_OK;
 }

@@ -87,7 +87,11 @@ def cpu_baseline(cfg, frames, text_len, batch, steps, extra=True):
            "sample": f"oracle fp32 train step (fwd+CE+bwd, dropout {cfg.dropout}) {cfg.n_enc}+{cfg.n_dec} layers "
                      f"d{cfg.d_model}, B={batch}, T={frames}, L={text_len}, {steps} steps after 1 warmup, "
                      f"{dt:.1f}s",
-           "cpu_model": model, "affinity_cpus": aff, "threads": threads}
+           "cpu_model": model, "affinity_cpus": aff, "threads": threads,
+           "frames_per_s_per_thread": round(batch * frames * steps / dt / threads, 1),
+           # the GPU pool grants each GPU a share of the host (OMP_NUM_THREADS, 16 per GPU) and asks worker pools to
+           # stay within it; the affinity set is the whole shared machine, so the baseline runs at the share
+           "threads_rule": "OMP_NUM_THREADS share of the box (the pool's per-GPU CPU share), not the affinity set"}
     if extra:
         fw = {}
         for name, b in (("c2", CONFIGS["c2"]["batch"]), ("c3", 64), ("c5", 2)):

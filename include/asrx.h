@@ -365,6 +365,13 @@ int asrx_zero_spans(float* base, const int64_t* spans, int32_t nspans, void* str
 int asrx_step_tokens(const int64_t* text, int64_t ld_text, const int64_t* inp, int64_t ld_inp, const float* mask,
                      int64_t ld_mask, int32_t B, int32_t L, int64_t* dec_in, int64_t* tgt, uint8_t* valid,
                      void* stream);
+/* Row-wise fp32 ops of the post-LN model family (modules/Transformer/new/model.py, asrx.new): op 0 (ROWSCALE)
+ * out[r][c] = a[r][c] * b[r] (the non_pad_mask products, new/model.py:25,28,83-89); op 1 (ROWADD) out[r][c] =
+ * a[r][c] + b[r % period][c] (the positional table, new/model.py:60).  out may alias a. */
+int asrx_rowwise(int32_t op, const float* a, const float* b, float* out, int64_t rows, int32_t d, int64_t period,
+                 void* stream);
+/* out[b][c][r] = x[b][r][c] (fp32, batch <= 65535): the encoder input's view/transpose (new/model.py:53-55). */
+int asrx_transpose_last2(const float* x, int64_t batch, int32_t R, int32_t C, float* out, void* stream);
 /* delta[(b*heads+h)*lq+q] = sum_d dO*O (attention backward prologue). */
 int asrx_attn_delta(const asrx_attn_desc* d, void* stream);
 /* y = dropout(x) with the library RNG (idx = element index); used for tests of the RNG stream. */

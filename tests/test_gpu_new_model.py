@@ -1,0 +1,173 @@
+"""Parity of the post-LN model family (asrx.new, the drop-in for modules/Transformer/new/) against the reference's own
+outputs (tests/golden/new_model.npz, made by tests/golden/make_golden_new.py from the variant run with its own
+layers / masking) and against the pinned oracle (oracle/ref_model_new.py).
+
+Tolerances: fp32 path — logits and encoder output <= 1e-4 relative (max norm), loss <= 1e-5 relative, every
+parameter gradient <= 1e-3 relative, greedy evaluate tokens / EOS steps exact; bf16 path — logits within 1.5x the
+error of the oracle under torch's bf16 autocast (the reference's own bf16 path) against fp32."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_model_new as N
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def relerr(a, b):
+    a, b = torch.as_tensor(a).double().cpu(), torch.as_tensor(b).double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def build(name, precision="fp32", dropout=None, seed=0):
+    import asrx.new
+    c = N.NEW_CONFIGS[name]
+    m = asrx.new.Transformer(c.vocab_size, c.n_mels, c.enc_seq_len, c.dec_seq_len, c.hidden_dim, c.n_enc, c.n_dec,
+                             c.n_heads, c.ff_dim, dev, dropout=c.dropout if dropout is None else dropout, sr=c.sr,
+                             n_fft=c.n_fft, padding_idx=c.pad_id, eos_token=c.eos_id, bos_token=c.bos_id,
+                             precision=precision)
+    sd = m.state_dict()
+    sd.update(N.det_params(c, seed))
+    m.load_state_dict(sd)
+    return m.to(dev), c
+
+
+def golden_batch(golden_dir, name):
+    g = np.load(os.path.join(golden_dir, "new_model.npz"))
+    p = name + "/"
+    batch = {"spectre": torch.from_numpy(g[p + "spectre"]).to(dev),
+             "spectrogram_len": torch.from_numpy(g[p + "lens"]).to(dev),
+             "encoded_text": torch.from_numpy(g[p + "text"]).to(dev)}
+    return g, p, batch
+
+
+def targets(text, eos):
+    t = torch.full_like(text, eos)
+    t[:, :-1] = text[:, 1:]
+    return t
+
+
+@pytest.mark.parametrize("name", ["new_micro", "new_small"])
+def test_new_forward_grads_fp32_golden(golden_dir, name):
+    """fp32: eval logits and encoder output, the dropout-0 training loss and every parameter gradient (the unused
+    VGG front-end none) against the reference's own values."""
+    g, p, batch = golden_batch(golden_dir, name)
+    m, c = build(name)
+    m.eval()
+    with torch.no_grad():
+        logits = m(batch)
+        enc = m.encoder(batch["spectre"], batch["spectrogram_len"])
+    assert relerr(logits, g[p + "logits"]) < 1e-4
+    assert relerr(enc, g[p + "enc"]) < 1e-4
+    m.train()
+    m.zero_grad()
+    lg = m(batch)
+    loss = torch.nn.functional.cross_entropy(lg.transpose(1, 2), targets(batch["encoded_text"], c.eos_id))
+    loss.backward()
+    assert abs(float(loss) - float(g[p + "loss"])) < 1e-5 * abs(float(g[p + "loss"]))
+    named = {}
+    for k, prm in m.named_parameters():
+        named[k] = prm
+    # gradients under the reference keys: load them as weights into a twin (the state_dict hooks split the fused
+    # q / k / v storage back into per-head keys)
+    twin, _ = build(name)
+    with torch.no_grad():
+        for (k1, p1), (k2, p2) in zip(m.named_parameters(), twin.named_parameters()):
+            assert k1 == k2
+            p2.copy_(p1.grad if p1.grad is not None else torch.zeros_like(p2))
+    gsd = twin.state_dict()
+    for k in g[p + "grad_names"]:
+        assert relerr(gsd[k], g[p + "grad/" + k]) < 1e-3, k
+    for k in g[p + "nograd_names"]:
+        assert named[k].grad is None or float(named[k].grad.abs().max()) == 0.0, k
+
+
+@pytest.mark.parametrize("name", ["new_micro", "new_small"])
+def test_new_evaluate_fp32_golden(golden_dir, name):
+    """Greedy evaluate (new/model.py:125-142): token rows, EOS steps exact, last-step logits."""
+    g, p, batch = golden_batch(golden_dir, name)
+    m, c = build(name)
+    m.eval()
+    with torch.no_grad():
+        toks, last, eoses = m.evaluate(batch)
+    np.testing.assert_array_equal(toks.cpu().numpy(), g[p + "eval_tokens"])
+    np.testing.assert_array_equal(eoses.numpy(), g[p + "eval_eoses"])
+    assert toks.dtype == torch.int32
+    assert relerr(last, g[p + "eval_last"]) < 1e-4
+
+
+def test_new_forward_bf16_vs_oracle_autocast_bound():
+    """bf16 operands (fp32 accumulation and residual stream): logits within 1.5x the error of the oracle under
+    torch's bf16 autocast against the fp32 oracle."""
+    m, c = build("new_small", "bf16")
+    m.eval()
+    s, lens, text = N.synthetic_batch(c, 4, seed=7)
+    batch = {"spectre": s.to(dev), "spectrogram_len": lens.to(dev), "encoded_text": text.to(dev)}
+    with torch.no_grad():
+        logits = m(batch).cpu()
+    P = N.det_params(c, 0)
+    with torch.no_grad():
+        ref = N.forward(P, s, lens, text, c, False)
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            ref16 = N.forward(P, s, lens, text, c, False).float()
+    e, e16 = relerr(logits, ref), relerr(ref16, ref)
+    print(f"\nnew_small bf16: logits rel err {e:.3e} (autocast path {e16:.3e})")
+    assert e <= 1.5 * e16, (e, e16)
+
+
+def test_new_layers_standalone_dense_masks():
+    """The drop-in EncoderLayer / DecoderLayer called as the reference calls them — dense boolean masks, a
+    (B, L, 1) non_pad_mask — against the oracle's layer functions (fp32)."""
+    m, c = build("new_micro")
+    m.eval()
+    P = N.det_params(c, 0)
+    g = torch.Generator().manual_seed(3)
+    B, T, L, d = 2, c.enc_len, c.dec_seq_len, c.n_mels
+    x = torch.randn(B, T, d, generator=g)
+    lens = torch.tensor([T, T - 7])
+    npm = N.valid_rows(lens, T)
+    mask = npm.lt(1).unsqueeze(1).expand(-1, T, -1)
+    with torch.no_grad():
+        y = m.encoder.layers[0](x.to(dev), mask.to(dev), npm.unsqueeze(-1).to(dev))
+    k = "encoder.layers.0"
+    want = N._ln(P, k + ".norm1", N.mha(P, k + ".attention", x, None, mask, c, False)) * npm.unsqueeze(-1)
+    want = N._ln(P, k + ".norm2", N.ffn(P, k + ".ff", want, c, False)) * npm.unsqueeze(-1)
+    assert relerr(y, want) < 1e-4
+    xd = torch.randn(B, L, d, generator=g)
+    text = torch.tensor([[1, 9, 8, 2, 2, 2, 2, 2], [1, 7, 6, 5, 11, 12, 13, 2]])
+    npm_d = text.ne(c.eos_id).float().unsqueeze(-1)
+    causal = torch.triu(torch.ones((L, L), dtype=torch.uint8), diagonal=1).unsqueeze(0).expand(B, -1, -1)
+    amask = (causal + text.eq(c.eos_id).unsqueeze(1).expand(-1, L, -1)).gt(0)
+    emask = npm.lt(1).unsqueeze(1).expand(-1, L, -1)
+    with torch.no_grad():
+        yd = m.decoder.layers[1](xd.to(dev), amask.to(dev), x.to(dev), emask.to(dev), npm_d.to(dev))
+    want_d = N.decoder_layer(P, "decoder.layers.1", xd, amask, x, emask, npm_d, c, False)
+    assert relerr(yd, want_d) < 1e-4
+
+
+def test_new_training_steps_reduce_loss():
+    """Dropout 0.1, bf16: a few AdamW steps on one batch drive the loss down (finite gradients throughout)."""
+    m, c = build("new_small", "bf16", dropout=0.1)
+    m.train()
+    s, lens, text = N.synthetic_batch(c, 4, seed=9)
+    batch = {"spectre": s.to(dev), "spectrogram_len": lens.to(dev), "encoded_text": text.to(dev)}
+    tgt = targets(batch["encoded_text"], c.eos_id)
+    opt = torch.optim.AdamW(m.parameters(), lr=2e-3)
+    losses = []
+    for _ in range(8):
+        opt.zero_grad()
+        loss = torch.nn.functional.cross_entropy(m(batch).transpose(1, 2), tgt)
+        loss.backward()
+        assert all(torch.isfinite(p.grad).all() for p in m.parameters() if p.grad is not None)
+        opt.step()
+        losses.append(float(loss))
+    assert losses[-1] < 0.8 * losses[0], losses

@@ -179,19 +179,22 @@ def test_gemm_kernel_plan_names_without_gpu():
             d.bias = 4 << 20
         return d
 
-    # wide outputs (>= 400 256x256 tiles) take p4; the Q/K/V projection forward (bias) the ws kernel, encoder and
-    # decoder (the persistent ws kernel, wsp, only when forced or with ASRX_WSP)
-    assert kernel_name(desc(15936, 1536, 512, bias=True)) == "gemm_bf16_ws_kernel<false, 1, 256>"
+    # wide outputs of >= 2 rounds of 256x128 tiles take wse (the persistent ws walk with the epilogue on the loader
+    # waves): the encoder Q/K/V projection, FFN1 forward, FFN2 data gradient, all-layer cross K/V; the decoder's
+    # 4096-row Q/K/V (192 tiles) the one-round ws kernel (the persistent ws kernel, wsp, only when forced)
+    assert kernel_name(desc(15936, 1536, 512, bias=True)) == "gemm_bf16_wse_kernel<false, 1>"
     assert kernel_name(desc(4096, 1536, 512, bias=True)) == "gemm_bf16_ws_kernel<false, 1, 256>"
-    assert kernel_name(desc(15936, 1536, 512)) == "gemm_bf16_p3_kernel<false, false, 0>"
+    assert kernel_name(desc(15936, 1536, 512)) == "gemm_bf16_wse_kernel<false, 0>"
     forced = desc(15936, 1536, 512, bias=True)
     forced.kernel = 9
     assert kernel_name(forced) == "gemm_bf16_wsp_kernel<false, 1>"
-    assert kernel_name(desc(15936, 2048, 512, bt=1)) == "gemm_bf16_p4_kernel<false, true, 0>"
+    assert kernel_name(desc(15936, 2048, 512, bt=1)) == "gemm_bf16_wse_kernel<true, 0>"
     ffn1 = desc(15936, 2048, 512, bias=True)
     ffn1.relu = 1
-    assert kernel_name(ffn1) == "gemm_bf16_p4_kernel<false, false, 3>"
-    assert kernel_name(desc(15936, 12288, 512, bias=True)) == "gemm_bf16_p4_kernel<false, false, 1>"
+    assert kernel_name(ffn1) == "gemm_bf16_wse_kernel<false, 3>"
+    assert kernel_name(desc(15936, 12288, 512, bias=True)) == "gemm_bf16_wse_kernel<false, 1>"
+    forced.kernel = 6                 # p4 forced: the 256x256 ring
+    assert kernel_name(forced) == "gemm_bf16_p4_kernel<false, false, 1>"
     # the plain 512-wide data gradients with K >= 1536 take the warp-specialised ws kernel, shorter ones stay on p3
     assert kernel_name(desc(15936, 512, 2048, bt=1)) == "gemm_bf16_ws_kernel<true, 0, 256>"
     assert kernel_name(desc(15936, 512, 1536, bt=1)) == "gemm_bf16_ws_kernel<true, 0, 256>"
@@ -330,3 +333,32 @@ def test_early_adam_spans_cover_the_buffer_once():
         assert cover == [1] * n
         released = set(i for a, b in spans for i in range(a, b))
         assert all(i in released for a, b in early for i in range(a, b))
+
+
+def _build_new(name):
+    import asrx.new
+    from oracle.ref_model_new import NEW_CONFIGS
+    c = NEW_CONFIGS[name]
+    m = asrx.new.Transformer(c.vocab_size, c.n_mels, c.enc_seq_len, c.dec_seq_len, c.hidden_dim, c.n_enc, c.n_dec,
+                             c.n_heads, c.ff_dim, "cpu", dropout=c.dropout, sr=c.sr, n_fft=c.n_fft, padding_idx=c.pad_id,
+                             eos_token=c.eos_id, bos_token=c.bos_id)
+    return m, c
+
+
+@pytest.mark.parametrize("name", ["new_micro", "new_small"])
+def test_new_state_dict_schema_matches_reference(golden_dir, name):
+    """asrx.new.Transformer (the post-LN family, modules/Transformer/new/) has the reference's state_dict keys,
+    order and shapes (tests/golden/make_golden_new.py records them from the reference), and its fused per-head
+    q / k / v storage round-trips a reference state_dict losslessly."""
+    from oracle.ref_model_new import det_params
+    ref = json.load(open(os.path.join(golden_dir, "ref_new_state_dict_schema.json")))
+    m, c = _build_new(name)
+    sd = m.state_dict()
+    assert [[k, list(v.shape)] for k, v in sd.items()] == ref[name]
+    assert sum(p.numel() for p in m.parameters()) == ref[name + "_nparams"]
+    P = det_params(c, 0)
+    sd.update(P)
+    m.load_state_dict(sd)
+    back = m.state_dict()
+    for k, v in P.items():
+        assert torch.equal(back[k], v), k

@@ -139,3 +139,38 @@ def test_decoder_mask_semantics():
     assert m[0, 0].tolist() == [False, True, True, True]
     assert m[0, 3].tolist() == [True, True, True, True]     # query pad -> whole row masked
     assert m[1, 0].tolist() == [False, True, True, True]
+
+
+# ---- the second model family, modules/Transformer/new/ (tests/golden/make_golden_new.py)
+
+@pytest.mark.parametrize("name", ["new_micro", "new_small"])
+def test_oracle_new_forward_grads_evaluate(golden_dir, name):
+    """oracle.ref_model_new against the reference's new/ variant run with its own layers / masking: eval logits and
+    encoder output, the dropout-0 loss and every parameter gradient (cross-entropy against the left-shifted tokens),
+    the unused VGG front-end without gradients, and the greedy evaluate() tokens, EOS steps and last logits."""
+    from oracle import ref_model_new as N
+    g = load(golden_dir, "new_model.npz")
+    cfg = N.NEW_CONFIGS[name]
+    p = name + "/"
+    s, lens, text = (torch.from_numpy(g[p + k]) for k in ("spectre", "lens", "text"))
+    spec, lens2, text2 = N.synthetic_batch(cfg, 3, seed=99)
+    assert torch.equal(spec, s) and torch.equal(lens2, lens) and torch.equal(text2, text)
+    P = {k: v.clone().requires_grad_(True) for k, v in N.det_params(cfg).items()}
+    logits = N.forward(P, s, lens, text, cfg, False)
+    assert rel(logits.detach(), g[p + "logits"]) < 1e-5
+    with torch.no_grad():
+        assert rel(N.encoder(P, s, lens, cfg), g[p + "enc"]) < 1e-5
+    tgt = torch.full_like(text, cfg.eos_id)
+    tgt[:, :-1] = text[:, 1:]
+    loss = torch.nn.functional.cross_entropy(logits.transpose(1, 2), tgt)
+    loss.backward()
+    assert abs(float(loss) - float(g[p + "loss"])) < 1e-5 * abs(float(g[p + "loss"]))
+    for k in g[p + "grad_names"]:
+        assert rel(P[k].grad, g[p + "grad/" + k]) < 1e-4, k
+    for k in g[p + "nograd_names"]:
+        assert P[k].grad is None, k
+    with torch.no_grad():
+        toks, last, eoses = N.evaluate(P, s, lens, cfg)
+    np.testing.assert_array_equal(toks.numpy(), g[p + "eval_tokens"])
+    np.testing.assert_array_equal(eoses.numpy(), g[p + "eval_eoses"])
+    assert rel(last, g[p + "eval_last"]) < 1e-5

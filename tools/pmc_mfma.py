@@ -58,6 +58,25 @@ def summarise(per):
             rec["mfma_tflops"] = round(mops * 512 / dur / 1e12, 1)
             rec["mfma_frac_of_peak"] = round(mops * 512 / dur / 1e12 / PEAK_TF, 4)
         out[name] = rec
+    return normalise_short(out)
+
+
+def normalise_short(out, min_us=300.0):
+    """GRBM_GUI_ACTIVE over-reads on dispatches shorter than ~0.3 ms (implied clocks of 3.6-4.8 GHz, above the
+    chip's 2.4 GHz), which under-states their busy fraction.  For those, also report the busy fraction over the
+    dispatch's DURATION at the clock the long dispatches of the same pass held (their GUI_ACTIVE / duration, weighted
+    by duration): mfma_busy_frac_dur = busy cycles / (dur * clock_ref * 1024 SIMDs)."""
+    long_ = [r for r in out.values() if r.get("dur_us") and r["dur_us"] >= min_us and r.get("clock_ghz")]
+    if not long_:
+        return out
+    w = sum(r["dur_us"] * r["launches"] for r in long_)
+    clk = sum(r["clock_ghz"] * r["dur_us"] * r["launches"] for r in long_) / w
+    for r in out.values():
+        r.pop("mfma_busy_frac_dur", None)
+        if r.get("dur_us") and r["dur_us"] < min_us and r.get("mfma_busy_frac") is not None:
+            busy = r["mfma_busy_frac"] * r["gui_cycles"] * SIMDS
+            r["mfma_busy_frac_dur"] = round(busy / (r["dur_us"] * 1e-6 * clk * 1e9 * SIMDS), 4)
+            r["clock_ref_ghz"] = round(clk, 3)
     return out
 
 
@@ -69,14 +88,15 @@ def main():
     args = ap.parse_args()
     res = summarise(load(args.csv))
     for name, r in sorted(res.items(), key=lambda kv: -kv[1]["mfma_flop_per_launch"] * kv[1]["launches"]):
-        print(f"{name[:60]:60s} n={r['launches']:4d} busy={r['mfma_busy_frac']} "
+        print(f"{name[:60]:60s} n={r['launches']:4d} busy={r['mfma_busy_frac']} busy_dur={r.get('mfma_busy_frac_dur')} "
               f"clk={r.get('clock_ghz')} TF={r.get('mfma_tflops')} dur={r.get('dur_us')}")
     if args.out:
         with open(args.out, "w") as f:
             json.dump({"config": args.config, "source": args.csv,
                        "counters": "SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE",
                        "formula": "mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs); "
-                                  "mfma_flop = MOPS_BF16 * 512",
+                                  "mfma_flop = MOPS_BF16 * 512; dispatches < 0.3 ms also mfma_busy_frac_dur = "
+                                  "busy cycles / (duration * clock_ref * 1024), clock_ref = the long dispatches' clock",
                        "kernels": res}, f, indent=1)
 
 
