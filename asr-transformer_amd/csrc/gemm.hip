@@ -1534,7 +1534,8 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
     // whose grid fills the chip; smaller grids (the decoder's 4096-row GEMMs) take the 4-stage ring kernel; the
     // register path wins the weight-gradient (A^T, reduction over B*T rows) and very long-K GEMMs.
     // (with the inline-asm LDS-DMA, p3 also wins the long-K cross-attention K/V data gradient, K = 12 288)
-    else if (kvar == 0 && !d->a_trans) {
+    // (a forced ws-family code, 8 .. 11, on a GEMM that family cannot take plans as auto)
+    else if ((kvar == 0 || kvar >= 8) && !d->a_trans) {
       // wide outputs whose 256x256 tiles still fill the chip (>= 1.25 tiles per CU; the c3 FFN1 forward, the gated
       // FFN2 data gradient, the Q/K/V and cross K/V projections) take p4: half the operand ingest per FLOP
       // (tools/blas_ref.py: FFN1 forward 47 -> 39 us, FFN2 data gradient 52 -> 41 us); the N = 512 outputs (126

@@ -203,6 +203,31 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
   const int rb = F32 ? tid >> 5 : tid >> 4;
   constexpr int RS = F32 ? 16 : 32;
   f4_t rr[RES ? NR : 1];
+  // PRER (round 4): the fp32 residual / row-add epilogues without dropout (FFN2 forward, _lin_in + PE) take their
+  // memory operand on the LOADER waves, issued right after the ring's last stage, so its HBM latency hides under the
+  // last K-steps; the loader waves then run the whole epilogue (thread lt = tid - 256: columns 4 (lt & 31) .. +3 of
+  // rows (lt >> 5) + 8 i) while the compute waves are done after the staging image.  ASRX_GEMM_DBG & 32: the
+  // round-3 split (A/B).
+  constexpr bool PRER = RES && (EPI & E_DROP) == 0 && BM == 256;
+  constexpr int NRL = PRER ? BM / 8 : 1;
+  const bool prer = PRER && !(g.dbg & 32);
+  f4_t rl[NRL];
+  auto load_resid_all = [&]() {
+    if constexpr (PRER) {
+      const int lt = tid - 256;
+#pragma unroll
+      for (int i = 0; i < NRL; ++i) {
+        const int m = m0 + (lt >> 5) + 8 * i;
+        rl[i] = f4_t{0.f, 0.f, 0.f, 0.f};
+        if (m < g.M) {
+          if constexpr ((EPI & E_RESID) != 0)
+            rl[i] = *(const f4_t*)((const float*)g.resid + (int64_t)m * g.ld_resid + n0 + (lt & 31) * 4);
+          else
+            rl[i] = *(const f4_t*)(g.rowadd + (int64_t)(m % g.rowadd_mod) * g.ld_rowadd + n0 + (lt & 31) * 4);
+        }
+      }
+    }
+  };
   auto load_resid = [&]() {
     if constexpr (RES) {
 #pragma unroll
@@ -241,8 +266,13 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
 #pragma unroll
     for (int i = 0; i < C::NST; ++i)
       if (i < nk) issue(i);
+    int extra = 0;   // vector-memory operations issued after the last stage (the PRER residual loads)
     if (noload) wait_vmcnt<0>();
     else wait_stages<C::INST, C::NST - 1>(min(nk, C::NST) - 1);
+    if (prer && ni == nk) {   // every stage issued in the prologue: the residual right away
+      load_resid_all();
+      extra = NRL;
+    }
     __builtin_amdgcn_s_barrier();
     int cb = 0;
     for (int s = 0; s < nk; ++s) {
@@ -264,13 +294,20 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
       // stage s + 1 landed (visible after the barrier); the stages issued after it stay in flight
       if (s + 1 < nk) {
         if (noload) wait_vmcnt<0>();
+        else if (extra) wait_vmcnt_rt(min(ni - (s + 2), C::NST - 2) * C::INST + extra);
         else wait_stages<C::INST, C::NST - 2>(ni - (s + 2));
       }
       __builtin_amdgcn_s_barrier();
-      if (ni < nk) issue(cb);   // stage s + NST into the buffer step s released
+      if (ni < nk) {
+        issue(cb);   // stage s + NST into the buffer step s released
+        if (prer && ni == nk) {
+          load_resid_all();
+          extra = NRL;
+        }
+      }
       cb = cb == C::NST - 1 ? 0 : cb + 1;
     }
-    load_resid();   // (before the epilogue barrier: its latency overlaps the compute waves' last k-slice)
+    if (!prer) load_resid();   // (before the epilogue barrier: its latency overlaps the compute waves' last k-slice)
     if constexpr (AT) {   // fold the 4 k-groups (lanes l, l ^ 16, l ^ 32, l ^ 48); lanes 0-15 own the columns
       if (rs_tile) {
 #pragma unroll
@@ -291,8 +328,29 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
     ws_compute<AT, BT, BM>(g, m0, nk, wm, wn, lds);
   }
   __syncthreads();
-  if (!loader) load_resid();
   if (g.dbg & 1) return;
+  if constexpr (PRER) {
+    if (prer) {   // the loader waves store every row; the compute waves are done
+      if (!loader) return;
+      const int lt = tid - 256, cl = (lt & 31) * 4;
+      f4_t b4 = f4_t{0.f, 0.f, 0.f, 0.f};
+      if constexpr ((EPI & E_BIAS) != 0) b4 = *(const f4_t*)(g.bias + n0 + cl);
+      const bool ncol = n0 + cl < g.N;
+#pragma unroll
+      for (int i = 0; i < NRL; ++i) {
+        const int r = (lt >> 5) + 8 * i, m = m0 + r;
+        f4_t v = *(const f4_t*)(stg + r * C::SP + cl);
+        v = epi_vals<EPI, true>(g, m, n0 + cl, v, b4, uint2{0u, 0u}, rl[i]);
+        if (m < g.M && ncol) {
+          float* c = (float*)g.c + (int64_t)m * g.ldc + n0 + cl;
+          if constexpr ((EPI & E_BETA) != 0) v += *(const f4_t*)c;
+          *(f4_t*)c = v;
+        }
+      }
+      return;
+    }
+  }
+  if (!loader) load_resid();
   if constexpr (F32) {
     f4_t b4 = f4_t{0.f, 0.f, 0.f, 0.f};
     if constexpr ((EPI & E_BIAS) != 0) b4 = *(const f4_t*)(g.bias + n0 + cq);

@@ -194,15 +194,18 @@ def _plan_log(fn):
 
 
 def _assert_bench_plan(log, rows):
-    """The GEMM kernels of a c3 step at B = 64 (bench.py's workload): the wide encoder projections on p4 (FFN1
-    forward, the gated FFN2 data gradient, the all-layer cross K/V), the Q/K/V projection forward and every 512-wide
-    encoder output on the warp-specialised ws kernel, the weight gradients in one grouped ws launch."""
+    """The GEMM kernels of a c3 step at B = 64 (bench.py's workload): the wide encoder projections (FFN1 forward,
+    the gated FFN2 data gradient, the Q/K/V projection forward, the all-layer cross K/V) on the warp-specialised
+    kernel with the epilogue on its loader waves (wse; p4 / ws with ASRX_WSE=0), every 512-wide encoder output on
+    the ws kernel, the weight gradients in one grouped ws launch."""
     by_shape = {}
     for name, m, n, k, *_ in log:
         by_shape.setdefault((m, n, k), set()).add(name.split("<")[0])
     fam = {nm for names in by_shape.values() for nm in names}
-    assert by_shape[(rows, 2048, 512)] == {"gemm_bf16_p4_kernel"}, by_shape[(rows, 2048, 512)]   # FFN1 fwd + FFN2 dX
-    assert by_shape[(rows, 1536, 512)] == {"gemm_bf16_ws_kernel"}, by_shape[(rows, 1536, 512)]   # Q/K/V fwd
+    wse = os.environ.get("ASRX_WSE", "1") != "0"
+    want_ffn, want_qkv = ({"gemm_bf16_wse_kernel"},) * 2 if wse else ({"gemm_bf16_p4_kernel"}, {"gemm_bf16_ws_kernel"})
+    assert by_shape[(rows, 2048, 512)] == want_ffn, by_shape[(rows, 2048, 512)]   # FFN1 fwd + FFN2 dX
+    assert by_shape[(rows, 1536, 512)] == want_qkv, by_shape[(rows, 1536, 512)]   # Q/K/V fwd
     for kk in (512, 1216, 1536, 2048):                                                          # N = 512 outputs
         assert by_shape[(rows, 512, kk)] == {"gemm_bf16_ws_kernel"}, (kk, by_shape[(rows, 512, kk)])
     assert fam & {"gemm_bf16_wsg_kernel", "gemm_bf16_wsgq_kernel"}, fam
