@@ -1477,9 +1477,11 @@ int wsp_min_rows() {
   static const int m = [] { const char* e = getenv("ASRX_WSP_M"); return e ? atoi(e) : 4096; }();
   return m;
 }
-// ASRX_WSE=0 keeps the wide projections on p4 / ws / p3 (A/B switch; default on)
+// ASRX_WSE=1 puts the wide projections on wse (A/B switch; default off: in the c3 step (profiles/r04_*) the FFN1
+// forward 61.9 -> 64.6 us and the gated FFN2 data gradient 50.3 -> 70.4 us against p4, the Q/K/V forward 40 us
+// either way against the multi-round ws kernel — 256x128 tiles ingest 1.5x the operand bytes of p4's 256x256)
 bool wse_auto() {
-  static const bool on = [] { const char* e = getenv("ASRX_WSE"); return !(e && e[0] == '0'); }();
+  static const bool on = [] { const char* e = getenv("ASRX_WSE"); return e && e[0] == '1'; }();
   return on;
 }
 // ASRX_WS64=0 keeps the decoder's 4096-row N = 512 GEMMs on the ring kernels (A/B switch; default on): ws with

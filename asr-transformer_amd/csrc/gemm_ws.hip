@@ -121,7 +121,9 @@ do {                                                                            
     __builtin_amdgcn_sched_group_barrier(0x100, AT ? 2 : 1, 0);                             \
   }                                                                                         \
 } while (0)
-  __builtin_amdgcn_s_barrier();
+  // ASRX_GEMM_DBG & 64 (diagnostic, garbage results): no loads, no ring barriers — the compute waves' own stream
+  const bool nobar = (g.dbg & 64) != 0;
+  if (!nobar) __builtin_amdgcn_s_barrier();
 #pragma unroll
   for (int j = 0; j < TM; ++j) fa0[j] = p4_frag<BM, AT>(lds, wm + 16 * j, 0, S);
 #pragma unroll
@@ -142,9 +144,11 @@ do {                                                                            
       fa1[j] = p4_frag<BM, AT>(la, wm + 16 * j, 1, S);
     }
     WS_ROLL_ORDER();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    // ---- mid-step barrier: stage s + 1 visible, buffer s dead (every k-slice-1 read of step s returned)
-    __builtin_amdgcn_s_barrier();
+    if (!nobar) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // ---- mid-step barrier: stage s + 1 visible, buffer s dead (every k-slice-1 read of step s returned)
+      __builtin_amdgcn_s_barrier();
+    }
     // ---- phase B: k-slice 1 MFMAs of step s | k-slice 0 fragment reads of step s + 1
     const unsigned char* ln = lds + nbo;
     asm volatile("" : "+v"(S));
@@ -246,7 +250,9 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
 
   // The two roles run separate loops with the same barrier count (1 + nk): a shared loop with role branches made
   // the compiler merge the accumulators through phi copies (and spill them).
-  if (loader) {
+  if (loader && (g.dbg & 64)) {
+    // (diagnostic: the compute waves run their stream alone; see ws_compute)
+  } else if (loader) {
     // ---------------- loader waves: 3-stage ring, stage s + 3 issued once step s has released its buffer
     float lrs[4] = {0.f, 0.f, 0.f, 0.f};
     const uint32_t S = p4_swz_bytes();

@@ -85,8 +85,14 @@ def test_new_forward_grads_fp32_golden(golden_dir, name):
             assert k1 == k2
             p2.copy_(p1.grad if p1.grad is not None else torch.zeros_like(p2))
     gsd = twin.state_dict()
+    # a gradient that is zero in exact arithmetic (the key bias: softmax is shift-invariant along the keys) holds
+    # only rounding noise in either implementation (~1e-11): its error is measured against the largest gradient
+    gmax = max(float(np.abs(g[p + "grad/" + k]).max()) for k in g[p + "grad_names"])
     for k in g[p + "grad_names"]:
-        assert relerr(gsd[k], g[p + "grad/" + k]) < 1e-3, k
+        want = g[p + "grad/" + k]
+        den = max(float(np.abs(want).max()), 1e-6 * gmax)
+        err = float((gsd[k].double().cpu() - torch.from_numpy(want).double()).abs().max()) / den
+        assert err < 1e-3, (k, err)
     for k in g[p + "nograd_names"]:
         assert named[k].grad is None or float(named[k].grad.abs().max()) == 0.0, k
 

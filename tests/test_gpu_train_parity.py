@@ -196,13 +196,13 @@ def _plan_log(fn):
 def _assert_bench_plan(log, rows):
     """The GEMM kernels of a c3 step at B = 64 (bench.py's workload): the wide encoder projections (FFN1 forward,
     the gated FFN2 data gradient, the Q/K/V projection forward, the all-layer cross K/V) on the warp-specialised
-    kernel with the epilogue on its loader waves (wse; p4 / ws with ASRX_WSE=0), every 512-wide encoder output on
+    kernel family p4 (FFN) / ws (Q/K/V; with ASRX_WSE=1 both on wse, the epilogue on the loader waves), every 512-wide encoder output on
     the ws kernel, the weight gradients in one grouped ws launch."""
     by_shape = {}
     for name, m, n, k, *_ in log:
         by_shape.setdefault((m, n, k), set()).add(name.split("<")[0])
     fam = {nm for names in by_shape.values() for nm in names}
-    wse = os.environ.get("ASRX_WSE", "1") != "0"
+    wse = os.environ.get("ASRX_WSE", "0") == "1"
     want_ffn, want_qkv = ({"gemm_bf16_wse_kernel"},) * 2 if wse else ({"gemm_bf16_p4_kernel"}, {"gemm_bf16_ws_kernel"})
     assert by_shape[(rows, 2048, 512)] == want_ffn, by_shape[(rows, 2048, 512)]   # FFN1 fwd + FFN2 dX
     assert by_shape[(rows, 1536, 512)] == want_qkv, by_shape[(rows, 1536, 512)]   # Q/K/V fwd

@@ -179,20 +179,27 @@ def test_gemm_kernel_plan_names_without_gpu():
             d.bias = 4 << 20
         return d
 
-    # wide outputs of >= 2 rounds of 256x128 tiles take wse (the persistent ws walk with the epilogue on the loader
-    # waves): the encoder Q/K/V projection, FFN1 forward, FFN2 data gradient, all-layer cross K/V; the decoder's
-    # 4096-row Q/K/V (192 tiles) the one-round ws kernel (the persistent ws kernel, wsp, only when forced)
-    assert kernel_name(desc(15936, 1536, 512, bias=True)) == "gemm_bf16_wse_kernel<false, 1>"
+    # wide outputs (>= 400 256x256 tiles) take p4; the Q/K/V projection forward (bias) the ws kernel, encoder and
+    # decoder; the persistent ws kernels (wsp; wse, the epilogue on the loader waves) only when forced or with
+    # ASRX_WSP / ASRX_WSE=1 (round 4: wse measured no faster in the step)
+    assert kernel_name(desc(15936, 1536, 512, bias=True)) == "gemm_bf16_ws_kernel<false, 1, 256>"
     assert kernel_name(desc(4096, 1536, 512, bias=True)) == "gemm_bf16_ws_kernel<false, 1, 256>"
-    assert kernel_name(desc(15936, 1536, 512)) == "gemm_bf16_wse_kernel<false, 0>"
+    assert kernel_name(desc(15936, 1536, 512)) == "gemm_bf16_p3_kernel<false, false, 0>"
     forced = desc(15936, 1536, 512, bias=True)
     forced.kernel = 9
     assert kernel_name(forced) == "gemm_bf16_wsp_kernel<false, 1>"
-    assert kernel_name(desc(15936, 2048, 512, bt=1)) == "gemm_bf16_wse_kernel<true, 0>"
+    forced.kernel = 11
+    assert kernel_name(forced) == "gemm_bf16_wse_kernel<false, 1>"
+    assert kernel_name(desc(15936, 2048, 512, bt=1)) == "gemm_bf16_p4_kernel<false, true, 0>"
     ffn1 = desc(15936, 2048, 512, bias=True)
     ffn1.relu = 1
+    assert kernel_name(ffn1) == "gemm_bf16_p4_kernel<false, false, 3>"
+    ffn1.kernel = 11
     assert kernel_name(ffn1) == "gemm_bf16_wse_kernel<false, 3>"
-    assert kernel_name(desc(15936, 12288, 512, bias=True)) == "gemm_bf16_wse_kernel<false, 1>"
+    ragged = desc(1000, 4160, 256, bias=True)   # N % 128 != 0: a forced ws-family code plans as auto
+    ragged.kernel = 11
+    assert kernel_name(ragged) == kernel_name(desc(1000, 4160, 256, bias=True))
+    assert kernel_name(desc(15936, 12288, 512, bias=True)) == "gemm_bf16_p4_kernel<false, false, 1>"
     forced.kernel = 6                 # p4 forced: the 256x256 ring
     assert kernel_name(forced) == "gemm_bf16_p4_kernel<false, false, 1>"
     # the plain 512-wide data gradients with K >= 1536 take the warp-specialised ws kernel, shorter ones stay on p3
