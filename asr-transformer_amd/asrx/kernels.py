@@ -219,8 +219,9 @@ GROUPED_TABLE_KERNEL = "gemm_bf16_grouped_dev_kernel<true, true>"
 # (beta != 1, beta == 1) instantiations (96 = E_BETA | E_F32: accumulate into the fp32 grads)
 GROUPED_P3_KERNELS = ("gemm_bf16_p3g_kernel<64>", "gemm_bf16_p3g_kernel<96>")
 GROUPED_P4_KERNELS = ("gemm_bf16_p4g_kernel<64>", "gemm_bf16_p4g_kernel<96>")
-GROUPED_WS_KERNELS = ("gemm_bf16_wsg_kernel<64>", "gemm_bf16_wsg_kernel<96>")
-GROUPED_WSQ_KERNELS = ("gemm_bf16_wsgq_kernel<64>", "gemm_bf16_wsgq_kernel<96>")
+_WS8 = "8" if int(os.environ.get("ASRX_WS8", "0") or 0) & 1 else ""   # (read once by the library too)
+GROUPED_WS_KERNELS = (f"gemm_bf16_wsg{_WS8}_kernel<64>", f"gemm_bf16_wsg{_WS8}_kernel<96>")
+GROUPED_WSQ_KERNELS = (f"gemm_bf16_wsgq{_WS8}_kernel<64>", f"gemm_bf16_wsgq{_WS8}_kernel<96>")
 
 
 def wgrad_groupable(dy, x, wgrad):

@@ -1653,7 +1653,8 @@ extern "C" int asrx_gemm_kernel_name(const asrx_gemm_desc* d, char* buf, int len
   }
   const GemmPlan pl = plan_bf16(d, batch, splitk);
   if (pl.use == 11 || pl.use == 13)
-    snprintf(buf, len, "gemm_bf16_ws_kernel<%s, %d, %d>", tf[!!d->b_trans], pl.epi, pl.use == 13 ? 64 : 256);
+    snprintf(buf, len, "gemm_bf16_ws%s_kernel<%s, %d, %d>", (ws8_mode() & (pl.use == 13 ? 2 : 1)) ? "8" : "",
+             tf[!!d->b_trans], pl.epi, pl.use == 13 ? 64 : 256);
   else if (pl.use == 12)
     snprintf(buf, len, "gemm_bf16_wsp_kernel<%s, %d>", tf[!!d->b_trans], pl.epi);
   else if (pl.use == 14)

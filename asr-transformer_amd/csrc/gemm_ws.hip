@@ -99,10 +99,22 @@ struct WsStage {
 // staging image.  (No row sums here: the bias gradient's column sums are the loader waves' — a per-wave branch in
 // this MFMA stream split it into small blocks, 1.68 vs 1.29 ms for the 12 encoder layers' weight gradients, and a
 // branch-free sum needs registers these waves do not have.)
-template <bool AT, bool BT, int BM = 256>
+// NCW (round 4): compute waves per workgroup — 4 (one per SIMD, (BM / 2) x 64 wave tiles) or 8 (two per SIMD,
+// (BM / 4) x 64 wave tiles, so one wave's fragment-read and barrier bubbles are filled by its SIMD partner's MFMAs;
+// 12 waves = 768 threads per workgroup with the 4 loader waves).
+template <int BM, int NCW>
+struct WsWave {
+  static_assert(NCW == 4 || NCW == 8, "ws: 4 or 8 compute waves");
+  static constexpr int TM = BM * 2 / (16 * NCW), TN = 4;   // (NCW / 2) x 2 wave tiles of (16 TM) x 64
+  static constexpr int NTHR = 64 * (NCW + 4);
+  ASRX_DEV static int wm(int cw) { return (cw >> 1) * (16 * TM); }
+  ASRX_DEV static int wn(int cw) { return (cw & 1) * 64; }
+};
+
+template <bool AT, bool BT, int BM = 256, int NCW = 4>
 ASRX_DEV void ws_compute(const GemmArgs& g, int m0, int nk, int wm, int wn, unsigned char* lds) {
   using C = WsCfg<BM>;
-  constexpr int TM = C::TM, TN = C::TN;
+  constexpr int TM = WsWave<BM, NCW>::TM, TN = WsWave<BM, NCW>::TN;
   const int l = threadIdx.x & 63;
   float* stg = (float*)lds;
   // ---------------- compute waves: the p4 pipeline on a 128x64 wave tile
@@ -178,7 +190,7 @@ do {                                                                            
 // weight gradient's dY); BT: B stored k-strided ([K][N]).  Ragged K only with both operands k-strided (rows past K
 // read as zero through the descriptor range); ragged M / N tiles: rows / column groups past them are not stored.
 // g.rowsum (AT only): += the row sums of op(A) (the fused bias gradient), by the compute waves of column block 0.
-template <bool AT, bool BT, int EPI, int BM = 256>
+template <bool AT, bool BT, int EPI, int BM = 256, int NCW = 4>
 ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned char* lds) {
   using C = WsCfg<BM>;
   const bf16_t* A = (const bf16_t*)g.a;
@@ -188,9 +200,9 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
   const int nk = (g.K + BK - 1) / BK;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int l = threadIdx.x & 63;
-  const bool loader = wave >= 4;
-  const int lw = wave & 3;
-  const int wm = (lw >> 1) * (16 * C::TM), wn = (lw & 1) * 64;
+  const bool loader = wave >= NCW;
+  const int lw = loader ? wave - NCW : wave & 3;   // loader index (loaders) / compute index (NCW = 4)
+  const int wm = WsWave<BM, NCW>::wm(wave), wn = WsWave<BM, NCW>::wn(wave);
   const bool noload = (g.dbg & 8) != 0;
 
   float* stg = (float*)lds;
@@ -210,11 +222,11 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
   // PRER (round 4): the fp32 residual / row-add epilogues without dropout (FFN2 forward, _lin_in + PE) take their
   // memory operand on the LOADER waves, issued right after the ring's last stage, so its HBM latency hides under the
   // last K-steps; the loader waves then run the whole epilogue (thread lt = tid - 256: columns 4 (lt & 31) .. +3 of
-  // rows (lt >> 5) + 8 i) while the compute waves are done after the staging image.  ASRX_GEMM_DBG & 32: the
-  // round-3 split (A/B).
-  constexpr bool PRER = RES && (EPI & E_DROP) == 0 && BM == 256;
+  // rows (lt >> 5) + 8 i) while the compute waves are done after the staging image.  Opt-in (ASRX_GEMM_DBG & 32):
+  // measured 2-3 us SLOWER in the c3 step (FFN2 forward 46.2 -> 48.4-48.7 us, _lin_in 34.8 -> 35.9-37.9).
+  constexpr bool PRER = RES && (EPI & E_DROP) == 0 && BM == 256 && NCW == 4;
   constexpr int NRL = PRER ? BM / 8 : 1;
-  const bool prer = PRER && !(g.dbg & 32);
+  const bool prer = PRER && (g.dbg & 32);
   f4_t rl[NRL];
   auto load_resid_all = [&]() {
     if constexpr (PRER) {
@@ -313,7 +325,7 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
       }
       cb = cb == C::NST - 1 ? 0 : cb + 1;
     }
-    if (!prer) load_resid();   // (before the epilogue barrier: its latency overlaps the compute waves' last k-slice)
+    if (!prer && NCW == 4) load_resid();   // (before the epilogue barrier: overlaps the compute waves' last k-slice)
     if constexpr (AT) {   // fold the 4 k-groups (lanes l, l ^ 16, l ^ 32, l ^ 48); lanes 0-15 own the columns
       if (rs_tile) {
 #pragma unroll
@@ -331,10 +343,11 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
       }
     }
   } else {
-    ws_compute<AT, BT, BM>(g, m0, nk, wm, wn, lds);
+    ws_compute<AT, BT, BM, NCW>(g, m0, nk, wm, wn, lds);
   }
   __syncthreads();
   if (g.dbg & 1) return;
+  if (NCW == 8 && tid >= 512) return;   // (8 compute waves: they alone run the 512-thread epilogue below)
   if constexpr (PRER) {
     if (prer) {   // the loader waves store every row; the compute waves are done
       if (!loader) return;
@@ -356,7 +369,7 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
       return;
     }
   }
-  if (!loader) load_resid();
+  if (!loader || NCW == 8) load_resid();
   if constexpr (F32) {
     f4_t b4 = f4_t{0.f, 0.f, 0.f, 0.f};
     if constexpr ((EPI & E_BIAS) != 0) b4 = *(const f4_t*)(g.bias + n0 + cq);
@@ -395,15 +408,24 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
   }
 }
 
-template <bool BT, int EPI, int BM>
-__global__ __launch_bounds__(512) void gemm_bf16_ws_kernel(GemmArgs g, int ntiles) {
+template <bool BT, int EPI, int BM, int NCW>
+ASRX_DEV void ws_kernel_body(GemmArgs& g, int ntiles) {
   g.seed = seed_eff(g.seed);
   __shared__ __attribute__((aligned(1024))) unsigned char lds[WsCfg<BM>::LDS];
   const int per8 = (ntiles + 7) / 8;
   const int t = (int)(blockIdx.x % 8) * per8 + (int)(blockIdx.x / 8);
   if (t >= ntiles) return;
   const int ntn = g.N / WS_BN;
-  ws_tile<false, BT, EPI, BM>(g, (t / ntn) * BM, (t % ntn) * WS_BN, false, lds);
+  ws_tile<false, BT, EPI, BM, NCW>(g, (t / ntn) * BM, (t % ntn) * WS_BN, false, lds);
+}
+template <bool BT, int EPI, int BM>
+__global__ __launch_bounds__(512) void gemm_bf16_ws_kernel(GemmArgs g, int ntiles) {
+  ws_kernel_body<BT, EPI, BM, 4>(g, ntiles);
+}
+// (ASRX_WS8) the same tiles with 8 compute waves
+template <bool BT, int EPI, int BM>
+__global__ __launch_bounds__(768) void gemm_bf16_ws8_kernel(GemmArgs g, int ntiles) {
+  ws_kernel_body<BT, EPI, BM, 8>(g, ntiles);
 }
 
 // Grouped weight gradients dW (+)= dY^T X of every layer in ONE launch on ws tiles: one 256x128 tile per workgroup,
@@ -411,7 +433,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_ws_kernel(GemmArgs g, int ntile
 // tile_group; the bias gradient (row sums of dY^T) fused.  Layout-identical table entries to the p3 / p4 grouped
 // kernels (asrx_gemm_group_dev).
 // One grouped tile (tile index t_all of the table; slot = its position in the block -> tile map, the trace index).
-template <int EPI>
+template <int EPI, int NCW = 4>
 ASRX_DEV void wsg_tile(const GroupEnt* __restrict__ ents, const uint16_t* __restrict__ tile_group, int t_all, int slot,
                        int dbg, unsigned char* lds, int* __restrict__ pcnt = nullptr, float* __restrict__ part = nullptr,
                        int* s_last = nullptr) {
@@ -440,7 +462,7 @@ ASRX_DEV void wsg_tile(const GroupEnt* __restrict__ ents, const uint16_t* __rest
     g.splitk = ntn;
     g.k_per_split = t % ntn;
   }
-  ws_tile<true, true, EPI>(g, (t / ntn) * WS_BM, (t % ntn) * WS_BN, rs_tile, lds);
+  ws_tile<true, true, EPI, WS_BM, NCW>(g, (t / ntn) * WS_BM, (t % ntn) * WS_BN, rs_tile, lds);
   if (split) {
     // Slab hand-off between the ntn column tiles of a row panel (workgroups on any XCD):
     //  producer (every tile): the 256 slab floats are stored by agent-scope atomic stores = `global_store_dword sc1`
@@ -494,15 +516,27 @@ ASRX_DEV void wsg_tile(const GroupEnt* __restrict__ ents, const uint16_t* __rest
 // block -> tile through block_tile (the host's XCD-aware layout, kernels.xcd_plan) and tile -> group through
 // tile_group; the bias gradient (row sums of dY^T) fused.  Layout-identical table entries to the p3 / p4 grouped
 // kernels (asrx_gemm_group_dev).
+template <int EPI, int NCW>
+ASRX_DEV void wsg_body(const GroupEnt* __restrict__ ents, const uint16_t* __restrict__ tile_group,
+                       const uint16_t* __restrict__ block_tile, int ntiles, int dbg) {
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[WS_LDS];
+  const int tid = block_tile ? (int)block_tile[blockIdx.x] : (int)blockIdx.x;
+  if (tid >= ntiles) return;
+  wsg_tile<EPI, NCW>(ents, tile_group, tid, (int)blockIdx.x, dbg, lds);
+}
 template <int EPI>
 __global__ __launch_bounds__(512) void gemm_bf16_wsg_kernel(const GroupEnt* __restrict__ ents,
                                                             const uint16_t* __restrict__ tile_group,
                                                             const uint16_t* __restrict__ block_tile, int ntiles,
                                                             int dbg) {
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[WS_LDS];
-  const int tid = block_tile ? (int)block_tile[blockIdx.x] : (int)blockIdx.x;
-  if (tid >= ntiles) return;
-  wsg_tile<EPI>(ents, tile_group, tid, (int)blockIdx.x, dbg, lds);
+  wsg_body<EPI, 4>(ents, tile_group, block_tile, ntiles, dbg);
+}
+template <int EPI>
+__global__ __launch_bounds__(768) void gemm_bf16_wsg8_kernel(const GroupEnt* __restrict__ ents,
+                                                             const uint16_t* __restrict__ tile_group,
+                                                             const uint16_t* __restrict__ block_tile, int ntiles,
+                                                             int dbg) {
+  wsg_body<EPI, 8>(ents, tile_group, block_tile, ntiles, dbg);
 }
 
 // The same tiles from PERSISTENT workgroups (one per CU) pulling from per-XCD queues: workgroup b runs on XCD
@@ -512,12 +546,10 @@ __global__ __launch_bounds__(512) void gemm_bf16_wsg_kernel(const GroupEnt* __re
 // CU: a slow tile on one XCD holds back the next round of every XCD (c3 trace: CUs idle 15 % of the launch,
 // tools/ws_trace.py).  Here each XCD's 32 workgroups run its queue greedily, independently of the other XCDs, and a
 // workgroup whose queue is empty takes the remaining tiles of the other XCDs' queues (the launch's tail).
-template <int EPI>
-__global__ __launch_bounds__(512) void gemm_bf16_wsgq_kernel(const GroupEnt* __restrict__ ents,
-                                                             const uint16_t* __restrict__ tile_group,
-                                                             const uint16_t* __restrict__ block_tile, int ntiles,
-                                                             int depth, int* __restrict__ cnt,
-                                                             float* __restrict__ part, int dbg) {
+template <int EPI, int NCW>
+ASRX_DEV void wsgq_body(const GroupEnt* __restrict__ ents, const uint16_t* __restrict__ tile_group,
+                        const uint16_t* __restrict__ block_tile, int ntiles, int depth, int* __restrict__ cnt,
+                        float* __restrict__ part, int dbg) {
   __shared__ __attribute__((aligned(1024))) unsigned char lds[WS_LDS];
   __shared__ int s_slot, s_last;
   const int x = (int)(blockIdx.x % 8);
@@ -535,9 +567,25 @@ __global__ __launch_bounds__(512) void gemm_bf16_wsgq_kernel(const GroupEnt* __r
     const int slot = xq + 8 * i;
     const int t_all = (int)block_tile[slot];
     if (t_all >= ntiles) continue;
-    wsg_tile<EPI>(ents, tile_group, t_all, slot, dbg, lds, cnt + 16, part, &s_last);
+    wsg_tile<EPI, NCW>(ents, tile_group, t_all, slot, dbg, lds, cnt + 16, part, &s_last);
     __syncthreads();   // the epilogue's staging image is dead before the next tile's LDS-DMA
   }
+}
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_bf16_wsgq_kernel(const GroupEnt* __restrict__ ents,
+                                                             const uint16_t* __restrict__ tile_group,
+                                                             const uint16_t* __restrict__ block_tile, int ntiles,
+                                                             int depth, int* __restrict__ cnt,
+                                                             float* __restrict__ part, int dbg) {
+  wsgq_body<EPI, 4>(ents, tile_group, block_tile, ntiles, depth, cnt, part, dbg);
+}
+template <int EPI>
+__global__ __launch_bounds__(768) void gemm_bf16_wsgq8_kernel(const GroupEnt* __restrict__ ents,
+                                                              const uint16_t* __restrict__ tile_group,
+                                                              const uint16_t* __restrict__ block_tile, int ntiles,
+                                                              int depth, int* __restrict__ cnt,
+                                                              float* __restrict__ part, int dbg) {
+  wsgq_body<EPI, 8>(ents, tile_group, block_tile, ntiles, depth, cnt, part, dbg);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -986,29 +1034,46 @@ bool ws_instantiated(bool bt, int epi) {
   return false;
 }
 
-int launch_ws_grouped(const GroupEnt* ents, const uint16_t* tile_group, const uint16_t* block_tile, int ntiles,
-                      int blocks, float beta, int dbg, int* queue, float* part, hipStream_t st) {
+// ASRX_WS8=1: the 256-row ws tiles (one-round encoder GEMMs, grouped weight gradients) with 8 compute waves
+// (WsWave; A/B switch)
+//   (bit 0: the 256-row tiles; bit 1: the decoder's 64-row tiles)
+int ws8_mode() {
+  static const int m = [] { const char* e = getenv("ASRX_WS8"); return e ? atoi(e) & 3 : 0; }();
+  return m;
+}
+bool ws8_on() { return (ws8_mode() & 1) != 0; }
+
+template <int NCW>
+int launch_ws_grouped_n(const GroupEnt* ents, const uint16_t* tile_group, const uint16_t* block_tile, int ntiles,
+                        int blocks, float beta, int dbg, int* queue, float* part, hipStream_t st) {
+  const dim3 blk(WsWave<256, NCW>::NTHR);
   if (queue && blocks % 8 == 0) {   // persistent workgroups on per-XCD queues (one per CU, at most 256)
     const int grid = std::min(blocks, 256), depth = blocks / 8;
     if (beta == 1.f)
-      hipLaunchKernelGGL((gemm_bf16_wsgq_kernel<E_BETA | E_F32>), dim3(grid), dim3(512), 0, st, ents, tile_group,
+      hipLaunchKernelGGL((NCW == 8 ? gemm_bf16_wsgq8_kernel<E_BETA | E_F32> : gemm_bf16_wsgq_kernel<E_BETA | E_F32>), dim3(grid), blk, 0, st, ents, tile_group,
                          block_tile, ntiles, depth, queue, part, dbg);
     else if (beta == 0.f)
-      hipLaunchKernelGGL((gemm_bf16_wsgq_kernel<E_F32>), dim3(grid), dim3(512), 0, st, ents, tile_group, block_tile,
+      hipLaunchKernelGGL((NCW == 8 ? gemm_bf16_wsgq8_kernel<E_F32> : gemm_bf16_wsgq_kernel<E_F32>), dim3(grid), blk, 0, st, ents, tile_group, block_tile,
                          ntiles, depth, queue, part, dbg);
     else
       return -1;
     return 0;
   }
   if (beta == 1.f)
-    hipLaunchKernelGGL((gemm_bf16_wsg_kernel<E_BETA | E_F32>), dim3(blocks), dim3(512), 0, st, ents, tile_group,
+    hipLaunchKernelGGL((NCW == 8 ? gemm_bf16_wsg8_kernel<E_BETA | E_F32> : gemm_bf16_wsg_kernel<E_BETA | E_F32>), dim3(blocks), blk, 0, st, ents, tile_group,
                        block_tile, ntiles, dbg);
   else if (beta == 0.f)
-    hipLaunchKernelGGL((gemm_bf16_wsg_kernel<E_F32>), dim3(blocks), dim3(512), 0, st, ents, tile_group, block_tile,
+    hipLaunchKernelGGL((NCW == 8 ? gemm_bf16_wsg8_kernel<E_F32> : gemm_bf16_wsg_kernel<E_F32>), dim3(blocks), blk, 0, st, ents, tile_group, block_tile,
                        ntiles, dbg);
   else
     return -1;
   return 0;
+}
+
+int launch_ws_grouped(const GroupEnt* ents, const uint16_t* tile_group, const uint16_t* block_tile, int ntiles,
+                      int blocks, float beta, int dbg, int* queue, float* part, hipStream_t st) {
+  return ws8_on() ? launch_ws_grouped_n<8>(ents, tile_group, block_tile, ntiles, blocks, beta, dbg, queue, part, st)
+                  : launch_ws_grouped_n<4>(ents, tile_group, block_tile, ntiles, blocks, beta, dbg, queue, part, st);
 }
 
 bool wsp_instantiated(bool bt, int epi) {
@@ -1056,8 +1121,10 @@ void launch_wse(const GemmArgs& g, bool bt, int epi, int ntiles, hipStream_t st)
 }
 
 void launch_ws(const GemmArgs& g, bool bt, int epi, int ntiles, int bm, hipStream_t st) {
-  const dim3 grid(8 * ((ntiles + 7) / 8)), blk(512);
-#define ASRX_CASE(E) case (E): if (bm == 64) hipLaunchKernelGGL((gemm_bf16_ws_kernel<BT_, (E), 64>), grid, blk, 0, st, g, ntiles); \
+  const dim3 grid(8 * ((ntiles + 7) / 8)), blk(512), blk8(WsWave<256, 8>::NTHR);
+#define ASRX_CASE(E) case (E): if (bm == 64 && (ws8_mode() & 2)) hipLaunchKernelGGL((gemm_bf16_ws8_kernel<BT_, (E), 64>), grid, blk8, 0, st, g, ntiles); \
+                               else if (bm == 64) hipLaunchKernelGGL((gemm_bf16_ws_kernel<BT_, (E), 64>), grid, blk, 0, st, g, ntiles); \
+                               else if (ws8_on()) hipLaunchKernelGGL((gemm_bf16_ws8_kernel<BT_, (E), 256>), grid, blk8, 0, st, g, ntiles); \
                                else hipLaunchKernelGGL((gemm_bf16_ws_kernel<BT_, (E), 256>), grid, blk, 0, st, g, ntiles); return;
   if (!bt) {
     constexpr bool BT_ = false;

@@ -194,10 +194,11 @@ def test_gemm_grouped_wgrad(ngroups, wkind, xcd, monkeypatch):
     kname = K().linear_wgrad_grouped(items)
     torch.cuda.synchronize()
     if wkind == "wsq" and xcd:
-        assert kname.startswith("gemm_bf16_wsgq_kernel"), kname     # the queue kernel ran (8-XCD block map)
+        assert kname.startswith(("gemm_bf16_wsgq_kernel", "gemm_bf16_wsgq8_kernel")), kname   # the queue kernel ran
     elif wkind in ("ws", "wsq"):
-        assert kname.startswith(("gemm_bf16_wsg_kernel", "gemm_bf16_wsgq_kernel")), kname
-        assert wkind == "wsq" or kname.startswith("gemm_bf16_wsg_kernel"), kname
+        assert kname.startswith(("gemm_bf16_wsg_kernel", "gemm_bf16_wsgq_kernel", "gemm_bf16_wsg8_kernel",
+                                  "gemm_bf16_wsgq8_kernel")), kname
+        assert wkind == "wsq" or kname.startswith(("gemm_bf16_wsg_kernel", "gemm_bf16_wsg8_kernel")), kname
     odd = bf(torch.randn(10, 250, device=dev))      # rows not 16-byte aligned: not groupable (C.wgrad runs it alone)
     assert not K().wgrad_groupable(odd, bf(torch.randn(10, 64, device=dev)), torch.zeros(250, 64, device=dev))
     for (dy, x, wg, bg), (rw, rb) in zip(items, refs):
@@ -283,7 +284,7 @@ def test_gemm_ws_plain(M, N, Kd, bt, wk):
     c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     ref = a.double() @ (b.double() if bt else b.double().t())
     kn = plan_name(M, N, Kd, bt=bt, kernel=wk)
-    assert kn.startswith("gemm_bf16_ws_kernel") and kn.endswith("64>" if wk == "ws64" else "256>"), kn
+    assert kn.startswith(("gemm_bf16_ws_kernel", "gemm_bf16_ws8_kernel")) and kn.endswith("64>" if wk == "ws64" else "256>"), kn
     K().gemm(a.to(dev), b.to(dev), c, M, N, Kd, lda=Kd, ldb=b.shape[1], ldc=N, b_trans=bool(bt), kernel=wk)
     assert relerr(c.float().cpu(), ref) < 1e-2
     auto_ws = N == 512 and (M >= 8192 if wk == "ws" else 2048 <= M < 8192)
@@ -318,7 +319,7 @@ def test_gemm_ws_bias_resid(M, N, Kd, f32, resid, drop, wk):
         K().linear(x.to(dev), w.to(dev), c, bias=bias.to(dev), kernel=wk if kern == "ws" else kern, **kw)
         outs[kern] = c.float().cpu()
     kn = plan_name(M, N, Kd, bias=True, c_f32=bool(f32), resid=bool(resid), dropout=bool(drop), kernel=wk)
-    assert kn.startswith("gemm_bf16_ws_kernel") and kn.endswith("64>" if wk == "ws64" else "256>"), kn
+    assert kn.startswith(("gemm_bf16_ws_kernel", "gemm_bf16_ws8_kernel")) and kn.endswith("64>" if wk == "ws64" else "256>"), kn
     if drop:   # same keep bits in both kernels; the reference is p3's kept pattern
         keep = (outs["p3"] - (r[:, :N] if resid else 0)) != 0
         ref = torch.where(keep, ref / 0.9, torch.zeros_like(ref))
