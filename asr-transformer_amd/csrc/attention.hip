@@ -1447,11 +1447,13 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
       for (int kc = 0; kc < NKT; ++kc) acc = mfma32(ka[kc], da[kc], acc);
       const int q = min(q0 + 16 * qs + li, a.Lq - 1);   // rows past Lq: duplicate store of the last row's
       if (nkb > 1) {                                     // (zero-dS) value would be wrong -> guarded below
-        // several key blocks: this block's share of dQ into the fp32 accumulator (dq_finish scales and casts)
+        // several key blocks: this block's share of dQ into ITS fp32 partial (plain 16-B stores; dq_finish adds the
+        // nkb partials in block order, scales and casts — round 3 added the shares by fp32 atomics into one
+        // accumulator, which serialised on the L2 at c5: 4 key blocks x 128 heads, 477 us per backward)
         if (q0 + 16 * qs + li < a.Lq) {
-          float* dst = a.dq_acc + (((int64_t)b * a.Lq + q) * a.H + h) * 64 + 16 * u + 4 * g;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) unsafeAtomicAdd(dst + e, acc[e]);
+          float* dst = a.dq_acc + (int64_t)blockIdx.y * ((int64_t)a.B * a.Lq * a.H * 64) +
+                       (((int64_t)b * a.Lq + q) * a.H + h) * 64 + 16 * u + 4 * g;
+          *(f4_t*)dst = acc;
         }
       } else {
         uint2 x;
@@ -1639,8 +1641,8 @@ int bwd_res_opt() {   // ASRX_ATTN_BWD_OPT: bits of attn_bwd_res_kernel's OPT (A
   return o;
 }
 
-// dq (bf16, strided) = scale * dq_acc (fp32 [B][Lq][H][DH])
-__global__ __launch_bounds__(256) void dq_finish_kernel(AttnArgs a, int dh) {
+// dq (bf16, strided) = scale * sum of the nparts fp32 partials dq_acc[p] ([nparts][B][Lq][H][DH], added in order)
+__global__ __launch_bounds__(256) void dq_finish_kernel(AttnArgs a, int dh, int nparts) {
   const int64_t total = (int64_t)a.B * a.Lq * a.H * dh;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
     const int d = (int)(i % dh);
@@ -1649,7 +1651,9 @@ __global__ __launch_bounds__(256) void dq_finish_kernel(AttnArgs a, int dh) {
     const int64_t r2 = r / a.H;
     const int q = (int)(r2 % a.Lq);
     const int b = (int)(r2 / a.Lq);
-    a.dq[b * a.dqb + (int64_t)q * a.dqr + h * dh + d] = f2bf(a.dq_acc[i] * a.scale);
+    float acc = a.dq_acc[i];
+    for (int p = 1; p < nparts; ++p) acc += a.dq_acc[(int64_t)p * total + i];
+    a.dq[b * a.dqb + (int64_t)q * a.dqr + h * dh + d] = f2bf(acc * a.scale);
   }
 }
 
@@ -1866,10 +1870,7 @@ extern "C" int asrx_attention_bwd(const asrx_attn_desc* d, void* stream) {
     const int nkb = (a.Lk + R_MAXK - 1) / R_MAXK;
     const int opt = (nkt == 8 && nkb == 1) ? bwd_res_opt() : 0;
     const size_t sm = bwd_res_smem(a.Lk, opt);
-    if (nkb > 1) {   // key blocks add their dQ shares into dq_acc
-      if (!a.dq_acc) return ASRX_ERR_ARG;
-      hipMemsetAsync(a.dq_acc, 0, sizeof(float) * (size_t)a.B * a.Lq * a.H * d->dh, st);
-    }
+    if (nkb > 1 && !a.dq_acc) return ASRX_ERR_ARG;   // key blocks store their dQ partials into dq_acc[blockIdx.y]
     const dim3 grid(a.B * a.H, nkb), blk(64 * nkt);
 #define ASRX_BWD_RES(M, N) hipLaunchKernelGGL((attn_bwd_res_kernel<M, N>), grid, blk, sm, st, a)
 #define ASRX_BWD_RES8(M)                                                                                           \
@@ -1892,7 +1893,7 @@ extern "C" int asrx_attention_bwd(const asrx_attn_desc* d, void* stream) {
     if (nkb > 1) {
       const int64_t total = (int64_t)a.B * a.Lq * a.H * d->dh;
       const unsigned blocks = (unsigned)std::min<int64_t>((total + 255) / 256, 8192);
-      hipLaunchKernelGGL(dq_finish_kernel, dim3(blocks), dim3(256), 0, st, a, d->dh);
+      hipLaunchKernelGGL(dq_finish_kernel, dim3(blocks), dim3(256), 0, st, a, d->dh, nkb);
       ASRX_CHECK_LAUNCH();
     }
     return ASRX_OK;
@@ -1915,7 +1916,7 @@ extern "C" int asrx_attention_bwd(const asrx_attn_desc* d, void* stream) {
   if (!single) {
     const int64_t total = (int64_t)a.B * a.Lq * a.H * d->dh;
     unsigned blocks = (unsigned)std::min<int64_t>((total + 255) / 256, 8192);
-    hipLaunchKernelGGL(dq_finish_kernel, dim3(blocks), dim3(256), 0, st, a, d->dh);
+    hipLaunchKernelGGL(dq_finish_kernel, dim3(blocks), dim3(256), 0, st, a, d->dh, 1);
     ASRX_CHECK_LAUNCH();
   }
   return ASRX_OK;

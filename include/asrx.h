@@ -171,7 +171,9 @@ typedef struct asrx_attn_desc {
   void* dk; int64_t dk_rstride, dk_bstride;
   void* dv; int64_t dv_rstride, dv_bstride;
   float* delta;                 /* [batch*heads*lq] workspace */
-  float* dq_acc;                /* [batch*lq*heads*dh] fp32 workspace, used when lk > 256 */
+  float* dq_acc;                /* fp32 workspace, used when lk > 256: ceil(lk/256) partials of [batch*lq*heads*dh]
+                                 * (one per 256-key block of the resident / streamed kernels; the tiled fallback
+                                 * accumulates into the first) — ceil(lk/256)*batch*lq*heads*dh floats */
   /* optional dropout keep-bit workspace (dh = 64, dropout_p > 0, any lk): key-major words
    * [batch*heads][ceil(lq/32)][lk] (bit i = query 32c+i) followed by query-major words
    * [batch*heads][lq][qmaj_stride(lk)] (bit j = key 32c+j), where qmaj_stride(lk) = ceil(lk/32) for lk <= 256 and

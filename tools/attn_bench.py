@@ -19,7 +19,7 @@ B, H, DH = 64, 8, 64
 D = H * DH
 
 
-def case(name, Lq, Lk, causal, kv_width=2 * D):
+def case(name, Lq, Lk, causal, kv_width=2 * D, B=B):
     """kv_width: row width of the K/V tensor (2 D = a head's rows 2 KB apart; 12 * 2 D = the model's all-layer cross
     K/V tensor, rows 24 KB apart, this case reading one layer's slice)."""
     g = torch.Generator(device="cuda").manual_seed(0)
@@ -71,7 +71,8 @@ def main():
     args = ap.parse_args()
     os.environ["ASRX_ATTN_KERNEL"] = args.variant
     cases = {"enc": ("enc_self", 249, 249, False), "cross": ("cross", 64, 249, False),
-             "cross24k": ("cross24k", 64, 249, False, 12 * 2 * D), "dec": ("dec_self", 64, 64, True)}
+             "cross24k": ("cross24k", 64, 249, False, 12 * 2 * D), "dec": ("dec_self", 64, 64, True),
+             "c5": ("c5_self", 999, 999, False, 2 * D, 16)}   # c5: B = 16, T' = 999 (the streamed kernels)
     if args.sweep:
         for lq in (32, 64, 128, 192, 249):
             cases[f"s{lq}"] = (f"lq{lq}", lq, 249, False)
