@@ -618,8 +618,8 @@ def attention_bwd(q, k, v, o, lse, do, dq, dk, dv, B, H, Lq, Lk, dh, strides, gs
     delta = torch.empty(B * H * Lq, device=q.device, dtype=torch.float32)
     d.delta = delta.data_ptr()
     acc = None
-    if Lk > 256:   # one fp32 dQ partial per 256-key block (asrx.h dq_acc)
-        acc = torch.empty((Lk + 255) // 256 * B * Lq * H * dh, device=q.device, dtype=torch.float32)
+    if Lk > 128:   # fp32 dQ partials, one per key block of the kernel (asrx.h dq_acc)
+        acc = torch.empty((Lk + 127) // 128 * B * Lq * H * dh, device=q.device, dtype=torch.float32)
         d.dq_acc = acc.data_ptr()
     call("asrx_attention_bwd", ctypes.byref(d), stream())
 

@@ -1632,8 +1632,8 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
 
 int bwd_res_nkt(int lk) { return lk <= 64 ? 2 : (lk <= 128 ? 4 : 8); }
 
-size_t bwd_res_smem(int lk, int opt = 0) {
-  const int nk = bwd_res_nkt(lk) * 32, nqb = (opt & 4) ? 3 : 2;
+size_t bwd_res_smem(int nkt, int opt = 0) {
+  const int nk = nkt * 32, nqb = (opt & 4) ? 3 : 2;
   return (size_t)(nk * R_VS + 2 * nqb * 32 * R_CS + 2 * nk * (32 + 8)) * 2 + 128 * 4 + 16 * 16;
 }
 int bwd_res_opt() {   // ASRX_ATTN_BWD_OPT: bits of attn_bwd_res_kernel's OPT (A/B; default 0)
@@ -1866,10 +1866,15 @@ extern "C" int asrx_attention_bwd(const asrx_attn_desc* d, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const bool longk = stream_ok(d, a) && (!a.thr || a.dropmask);
   if ((resident_ok(d, a) || longk) && a.dqr % 4 == 0 && a.dqb % 4 == 0 && (uintptr_t)a.dq % 8 == 0) {   // forms delta itself
-    const int nkt = bwd_res_nkt(a.Lk);
-    const int nkb = (a.Lk + R_MAXK - 1) / R_MAXK;
+    // ASRX_ATTN_XSPLIT=1 (A/B): short query blocks over 129..256 keys (the decoder's cross-attention, 64 x 249) as
+    // two 128-key blocks of 4 waves (1024 workgroups, two per CU) with per-block dQ partials, instead of one
+    // 256-key block of 8 waves per head
+    static const bool xsplit_on = [] { const char* e = getenv("ASRX_ATTN_XSPLIT"); return e && e[0] == '1'; }();
+    const bool xsplit = xsplit_on && a.Lq <= 64 && a.Lk > 128 && a.Lk <= R_MAXK && a.dq_acc;
+    const int nkt = xsplit ? 4 : bwd_res_nkt(a.Lk);
+    const int nkb = (a.Lk + 32 * nkt - 1) / (32 * nkt);
     const int opt = (nkt == 8 && nkb == 1) ? bwd_res_opt() : 0;
-    const size_t sm = bwd_res_smem(a.Lk, opt);
+    const size_t sm = bwd_res_smem(nkt, opt);
     if (nkb > 1 && !a.dq_acc) return ASRX_ERR_ARG;   // key blocks store their dQ partials into dq_acc[blockIdx.y]
     const dim3 grid(a.B * a.H, nkb), blk(64 * nkt);
 #define ASRX_BWD_RES(M, N) hipLaunchKernelGGL((attn_bwd_res_kernel<M, N>), grid, blk, sm, st, a)

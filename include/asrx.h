@@ -171,9 +171,10 @@ typedef struct asrx_attn_desc {
   void* dk; int64_t dk_rstride, dk_bstride;
   void* dv; int64_t dv_rstride, dv_bstride;
   float* delta;                 /* [batch*heads*lq] workspace */
-  float* dq_acc;                /* fp32 workspace, used when lk > 256: ceil(lk/256) partials of [batch*lq*heads*dh]
-                                 * (one per 256-key block of the resident / streamed kernels; the tiled fallback
-                                 * accumulates into the first) — ceil(lk/256)*batch*lq*heads*dh floats */
+  float* dq_acc;                /* optional fp32 workspace of ceil(lk/128)*batch*lq*heads*dh floats: dQ partials,
+                                 * one [batch*lq*heads*dh] slab per key block of the kernel (required for lk > 256;
+                                 * used for 128 < lk <= 256 by ASRX_ATTN_XSPLIT; the tiled fallback accumulates into
+                                 * the first slab) */
   /* optional dropout keep-bit workspace (dh = 64, dropout_p > 0, any lk): key-major words
    * [batch*heads][ceil(lq/32)][lk] (bit i = query 32c+i) followed by query-major words
    * [batch*heads][lq][qmaj_stride(lk)] (bit j = key 32c+j), where qmaj_stride(lk) = ceil(lk/32) for lk <= 256 and
