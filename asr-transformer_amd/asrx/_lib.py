@@ -83,6 +83,15 @@ class AttnDesc(ctypes.Structure):
     ]
 
 
+class AdamDesc(ctypes.Structure):
+    _fields_ = [
+        ("p", c_vp), ("m", c_vp), ("v", c_vp), ("p_bf16", c_vp), ("g_base", c_vp), ("hyp", c_vp),
+        ("lr", c_f32), ("beta1", c_f32), ("beta2", c_f32), ("eps", c_f32), ("weight_decay", c_f32),
+        ("bias_corr1", c_f32), ("bias_corr2", c_f32), ("grad_scale", c_f32),
+        ("decoupled", c_i32), ("reserved", c_i32),
+    ]
+
+
 # name -> argtypes (restype is int for all)
 SIGNATURES = {
     "asrx_version": [],
@@ -92,6 +101,10 @@ SIGNATURES = {
     "asrx_gemm_set_debug": [c_i32],
     "asrx_set_tuning": [c_i32, c_i32],
     "asrx_gemm_grouped_xcd": [ctypes.POINTER(GemmDesc), c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp],
+    "asrx_gemm_grouped_xcd_adam": [ctypes.POINTER(GemmDesc), c_vp, c_vp, c_vp, c_i32, c_i32, c_i32,
+                                   ctypes.POINTER(AdamDesc), c_vp],
+    "asrx_adam_spans": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32,
+                        c_f32, c_i32, c_vp, c_vp],
     "asrx_reduce_rows_grouped": [ctypes.POINTER(RowsumGroup), c_i32, c_vp],
     "asrx_attention_fwd": [ctypes.POINTER(AttnDesc), c_vp],
     "asrx_attn_dropgen": [ctypes.POINTER(AttnDesc), c_vp],

@@ -80,6 +80,8 @@ class Ctx:
         self.wq = None                  # list -> weight gradients are queued and issued grouped (flush_wgrad)
         self.lnq = None                 # list -> LayerNorm dgamma|dbeta partials queued for one grouped reduce
         self.fresh = None               # FreshGrads of a Trainer step (unzeroed weight-gradient regions)
+        self.adam = None                # AdamDesc -> the optimizer step fused into the grouped weight gradients
+        self.adam_cover = []            # (offset, numel) of the flat-gradient ranges whose AdamW ran fused
 
     def W(self, p):
         return self.store.w16(p) if self.cd == torch.bfloat16 else self.store.w32(p)
@@ -114,7 +116,16 @@ class Ctx:
         q0, q1 = [], []
         for it in q:
             (q0 if self.fresh.take(it[2]) else q1).append(it)
-        K.linear_wgrad_grouped(q0, beta=0.0)
+        # fused AdamW only where every written gradient is final in this launch: first writers (beta 0), no second
+        # writer in the step (the Trainer enables it for a single end-of-backward flush only)
+        adam = self.adam if not q1 else None
+        kname = K.linear_wgrad_grouped(q0, beta=0.0, adam=adam)
+        if adam is not None and kname in K.GROUPED_WSQA_KERNELS:
+            base = self.store.grad.data_ptr()
+            for _, _, gw, gb in q0:
+                for t in (gw, gb):
+                    if t is not None:
+                        self.adam_cover.append(((t.data_ptr() - base) // 4, t.numel()))
         K.linear_wgrad_grouped(q1)
 
     def defer_wgrad(self):

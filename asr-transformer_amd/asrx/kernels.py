@@ -222,6 +222,7 @@ GROUPED_P4_KERNELS = ("gemm_bf16_p4g_kernel<64>", "gemm_bf16_p4g_kernel<96>")
 _WS8 = "8" if int(os.environ.get("ASRX_WS8", "0") or 0) & 1 else ""   # (read once by the library too)
 GROUPED_WS_KERNELS = (f"gemm_bf16_wsg{_WS8}_kernel<64>", f"gemm_bf16_wsg{_WS8}_kernel<96>")
 GROUPED_WSQ_KERNELS = (f"gemm_bf16_wsgq{_WS8}_kernel<64>", f"gemm_bf16_wsgq{_WS8}_kernel<96>")
+GROUPED_WSQA_KERNELS = ("gemm_bf16_wsgqa_kernel<64>", None)   # AdamW fused (beta 0 only)
 
 
 def wgrad_groupable(dy, x, wgrad):
@@ -330,7 +331,7 @@ def upload(dst, host_bytes):
     call("asrx_upload", dst.data_ptr(), buf.ctypes.data, buf.nbytes, stream())
 
 
-def _grouped_xcd(items, common, kind="p3"):
+def _grouped_xcd(items, common, kind="p3", adam=None):
     """Grouped weight gradients with an XCD-aware workgroup -> tile map (asrx_gemm_grouped_xcd): 64-B group
     entries (operand pointers: per call), then the tile -> group and block -> tile maps (per shape set, cached on
     the host), written into one device buffer by asrx_upload.  Returns (flops, launch(), table buffer): the
@@ -380,10 +381,16 @@ def _grouped_xcd(items, common, kind="p3"):
         part = torch.empty(start * tile[0], dtype=torch.float32, device=dev.device)
         common.rowsum_ws = part.data_ptr()
 
+    fused = adam is not None and queue and common.beta == 0.0
+
     def launch():
-        call("asrx_gemm_grouped_xcd", ctypes.byref(common), base, base + o1, base + o2, len(items), start,
-             len(block_tile), stream())
-    return flops, launch, (dev, part), queue
+        if fused:   # (the AdamDesc is held by this closure until the call)
+            call("asrx_gemm_grouped_xcd_adam", ctypes.byref(common), base, base + o1, base + o2, len(items), start,
+                 len(block_tile), ctypes.byref(adam), stream())
+        else:
+            call("asrx_gemm_grouped_xcd", ctypes.byref(common), base, base + o1, base + o2, len(items), start,
+                 len(block_tile), stream())
+    return flops, launch, (dev, part), (queue, fused)
 
 
 # lay each group's tiles on one XCD (ASRX_WGRAD_XCD=0: one table order over all XCDs, A/B)
@@ -398,10 +405,12 @@ WGRAD_PACK = os.environ.get("ASRX_WGRAD_PACK", "1") == "1"
 WGRAD_QUEUE = os.environ.get("ASRX_WGRAD_QUEUE", "1") == "1"
 
 
-def linear_wgrad_grouped(items, *, beta=1.0, kind=None):
+def linear_wgrad_grouped(items, *, beta=1.0, kind=None, adam=None):
     """Issue many independent weight gradients wgrad[N,K] (+)= dy[M,N]^T . x[M,K] (+ bias_grad[N] += colsum dy)
-    as ONE grouped launch (longest reductions first, tiles of a group on one XCD).  Returns the name of the kernel
-    instantiation launched (the one rocprofv3 lists)."""
+    as ONE grouped launch (longest reductions first, tiles of a group on one XCD).  adam (AdamDesc, optional): the
+    AdamW step of every written element fused into the launch (asrx_gemm_grouped_xcd_adam) where the launch can take
+    it (ws queue launch, beta 0).  Returns the name of the kernel instantiation launched (the one rocprofv3 lists);
+    it is a GROUPED_WSQA_KERNELS name exactly when the optimizer step was fused."""
     if not items:
         return None
     items = sorted(items, key=lambda it: -it[0].shape[0])
@@ -411,10 +420,11 @@ def linear_wgrad_grouped(items, *, beta=1.0, kind=None):
     p3 = _grouped_p3_ok(items, beta)
     kind = kind or WGRAD_KIND
     # the table upload is issued first, so a timed bracket holds the grouped GEMM alone
-    flops, launch, _, queued = _grouped_xcd(items, common, kind if p3 else "reg")
+    flops, launch, _, (queued, fused) = _grouped_xcd(items, common, kind if p3 else "reg",
+                                                     adam if p3 and (kind or WGRAD_KIND) == "ws" else None)
     # the kernel that actually runs: the ws tiles go to the persistent queue kernel only when _grouped_xcd took it
     # (its block map must hold whole 8-XCD rounds), else one workgroup per tile
-    wsk = GROUPED_WSQ_KERNELS if queued else GROUPED_WS_KERNELS
+    wsk = GROUPED_WSQA_KERNELS if fused else GROUPED_WSQ_KERNELS if queued else GROUPED_WS_KERNELS
     kname = ({"p4": GROUPED_P4_KERNELS, "ws": wsk}.get(kind, GROUPED_P3_KERNELS)[beta == 1.0] if p3
              else GROUPED_TABLE_KERNEL)
     probe = PROBE
@@ -833,6 +843,29 @@ def adam(p, g, m, v, p_bf16, lr, beta1, beta2, eps, weight_decay, step, grad_sca
     bc2 = 1.0 - beta2 ** step
     call("asrx_adam", p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), _p(p_bf16), p.numel(), lr, beta1,
          beta2, eps, weight_decay, bc1, bc2, grad_scale, int(decoupled), _p(hyp), stream())
+
+
+def adam_desc(p, m, v, p_bf16, g, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0, decoupled=False,
+              hyp=None):
+    """The AdamW state of flat buffers p / m / v (+ bf16 shadow) laid out like the gradient buffer g, for a fused
+    grouped weight-gradient launch (linear_wgrad_grouped(adam=...))."""
+    from ._lib import AdamDesc
+    _cuda(p, m, v, p_bf16, g, hyp)
+    d = AdamDesc()
+    d.p, d.m, d.v, d.p_bf16, d.g_base, d.hyp = p.data_ptr(), m.data_ptr(), v.data_ptr(), _p(p_bf16), g.data_ptr(), _p(hyp)
+    d.lr, d.beta1, d.beta2, d.eps, d.weight_decay = lr, beta1, beta2, eps, weight_decay
+    d.bias_corr1, d.bias_corr2 = 1.0 - beta1 ** step, 1.0 - beta2 ** step
+    d.grad_scale, d.decoupled = grad_scale, int(decoupled)
+    return d
+
+
+def adam_spans(p, g, m, v, p_bf16, spans, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0, decoupled=False,
+               hyp=None):
+    """AdamW over the element ranges of a device int64 [n, 2] table (bounds multiples of 4; asrx_adam_spans)."""
+    _cuda(p, g, m, v, p_bf16, spans, hyp)
+    call("asrx_adam_spans", p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), _p(p_bf16), spans.data_ptr(),
+         spans.shape[0], lr, beta1, beta2, eps, weight_decay, 1.0 - beta1 ** step, 1.0 - beta2 ** step, grad_scale,
+         int(decoupled), _p(hyp), stream())
 
 
 def adam_hyper(hyp, lr, beta1, beta2, step):

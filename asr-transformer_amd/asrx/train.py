@@ -32,6 +32,10 @@ GRAPH_WARMUP = 2
 # one-rank RCCL rehearsal it was slower (14.35 / 14.26 vs 14.12 / 14.13 ms, ABAB) — the side AdamW starts right at
 # the release point and takes HBM bandwidth from the HBM-bound encoder backward it runs beside
 EARLY_ADAM = os.environ.get("ASRX_DP_EARLY_ADAM", "0") == "1"
+# single-GPU steps: AdamW of every nn.Linear parameter fused into the grouped weight-gradient launch, the rest by
+# one span-table launch (ASRX_FUSED_ADAM=0: the separate optimizer launch over the flat buffers)
+FUSED_ADAM = os.environ.get("ASRX_FUSED_ADAM", "1") == "1"
+ADAM_SPAN = 8192   # elements per workgroup of the residual span-table launch
 
 
 def _aligned_spans(spans, n, q=4):
@@ -264,6 +268,9 @@ class Trainer:
         # captured buffer, overwritten by the next step)
         self.want_preds = bool(preds)
         self.last_preds = None
+        self._cover = None       # flat-gradient ranges whose AdamW the last backward ran fused (None: none)
+        self._rspans = {}        # residual-range tables by cover
+        self._fuse_next = False  # the next forward_backward fuses AdamW (set by step(), which owns the optimizer)
         if self._wonly:   # the spans of everything else, zeroed each step by one asrx_zero_spans launch
             n, spans, pos = self.store.grad.numel(), [], 0
             for o, k in sorted((self.store.offset(p), p.numel()) for p in self._wonly):
@@ -273,6 +280,36 @@ class Trainer:
             if pos < n:
                 spans.append((pos, n))
             self._zero_spans = torch.tensor(spans, dtype=torch.int64).reshape(-1, 2).to(self.store.grad.device)
+
+    def _fused_adam_ok(self):
+        """AdamW fused into the grouped weight-gradient launch: single GPU (no gradient exchange before the step),
+        bf16, FreshGrads, one end-of-backward flush (ASRX_FUSED_ADAM=0: the separate optimizer launch)."""
+        from .blocks import WGRAD_OVERLAP
+        return (FUSED_ADAM and not self.reducer.active and self.model.precision == "bf16" and bool(self._wonly)
+                and not WGRAD_OVERLAP)
+
+    def _residual_spans(self, cover):
+        """Device [n, 2] table of the flat ranges NOT covered by the fused launch, cut into pieces of at most
+        ADAM_SPAN elements (one workgroup each); cached per cover (built in the eager step that precedes a capture)."""
+        key = tuple(sorted(cover))
+        tab = self._rspans.get(key)
+        if tab is None:
+            n = self.store.flat.numel()
+            spans, pos = [], 0
+            for o, k in key:
+                if o > pos:
+                    spans.append((pos, o))
+                pos = max(pos, o + k)
+            if pos < n:
+                spans.append((pos, n))
+            pieces = []
+            for a, b in spans:
+                a4, b4 = a // 4 * 4, -(-b // 4) * 4   # (every parameter is 64-aligned: no cut shares a quad)
+                for c in range(a4, b4, ADAM_SPAN):
+                    pieces.append((c, min(b4, c + ADAM_SPAN)))
+            tab = torch.tensor(pieces, dtype=torch.int64).reshape(-1, 2).to(self.store.flat.device)
+            self._rspans[key] = tab
+        return tab
 
     def forward_backward(self, spectrum, text, mask, ready=None, capture=False, input_text=None):
         """text: (B, L+1) with BOS ... ; inputs text[:, :-1], targets text[:, 1:] (train.py:24,32).  input_text
@@ -300,15 +337,29 @@ class Trainer:
             C.fresh = FreshGrads(self.store, self._wonly)
         else:
             self.store.grad.zero_()
+        self._cover = None
+        if self._fuse_next and C.fresh is not None:
+            sh = self.store.shadow
+            C.adam = K.adam_desc(self.store.flat, self.m, self.v, sh, self.store.grad, self.lr, self.betas[0],
+                                 self.betas[1], self.eps, self.wd, max(1, self.step_count + 1),
+                                 grad_scale=1.0 / self.reducer.world, decoupled=self.decoupled, hyp=self._hyp)
         if ready is None and not capture and self.reducer.active:
             ready = self.reducer.ready
         model_backward(C, model, S, dl.to(C.cd) if dl.dtype != C.cd else dl, ready=ready)
         if C.fresh is not None:
             C.fresh.drain()
             C.fresh = None
+        if C.adam is not None and C.adam_cover:
+            self._cover = list(C.adam_cover)
         return loss
 
     def _adam(self, hyp=None, span=None):
+        if span is None and self._cover is not None:   # the fused launch updated its ranges: AdamW for the rest
+            sh = self.store.shadow
+            K.adam_spans(self.store.flat, self.store.grad, self.m, self.v, sh, self._residual_spans(self._cover),
+                         self.lr, self.betas[0], self.betas[1], self.eps, self.wd, max(1, self.step_count),
+                         grad_scale=1.0 / self.reducer.world, decoupled=self.decoupled, hyp=hyp)
+            return
         a, b = span if span is not None else (0, self.store.flat.numel())
         sh = self.store.shadow[a:b] if self.store.shadow is not None else None
         K.adam(self.store.flat[a:b], self.store.grad[a:b], self.m[a:b], self.v[a:b], sh, self.lr, self.betas[0],
@@ -360,9 +411,15 @@ class Trainer:
             if self._cap is not None:
                 return self._replay(spectrum, text, mask, input_text)
             self._eager_keys.add(key)
-        loss = self.forward_backward(spectrum, text, mask, input_text=input_text)
+        self._fuse_next = self._fused_adam_ok()
+        if self._fuse_next:   # the fused launch reads this step's lr / bias corrections from the device
+            K.adam_hyper(self._hyp, self.lr, self.betas[0], self.betas[1], self.step_count + 1)
+        try:
+            loss = self.forward_backward(spectrum, text, mask, input_text=input_text)
+        finally:
+            self._fuse_next = False
         self.step_count += 1
-        self._reduce_and_adam()
+        self._reduce_and_adam(self._hyp if self._cover is not None else None)
         self.store.mark_shadow_fresh()
         return loss
 
@@ -394,12 +451,14 @@ class Trainer:
         with torch.cuda.stream(side):
             seg = _Segments(pool)
             K.CAPTURE = seg
+            self._fuse_next = self._fused_adam_ok()
             try:
                 loss = self.forward_backward(*ins[:3], ready=seg if self.reducer.active else None, capture=True,
                                              input_text=ins[3])
                 if not self.reducer.active:
                     self._adam(self._hyp)
             finally:
+                self._fuse_next = False
                 K.CAPTURE = None
                 seg.close()
         torch.cuda.current_stream(dev).wait_stream(side)

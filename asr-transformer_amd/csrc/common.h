@@ -25,6 +25,68 @@ ASRX_DEV uint32_t pack2bf(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector((f2_t){a, b}, bf2_t));
 }
 
+// ---- AdamW (asrx_adam; fused into the grouped weight-gradient epilogue, asrx_gemm_grouped_xcd_adam; asrx_adam_spans)
+// One element: the reference's torch.optim.AdamW / Adam step (train.py:35) in fp32.  Contraction is off so the
+// element math rounds identically in every kernel that inlines it (the fused epilogue, the streaming kernel).
+ASRX_DEV float adam_elem(float g, float& p, float& m, float& v, float lr, float b1, float b2, float eps, float wd,
+                         float bc1, float rbc2, float gs, int decoupled) {
+#pragma clang fp contract(off)
+  float gr = g * gs;
+  float pv = p;
+  if (decoupled) pv *= (1.f - lr * wd);
+  else gr += wd * pv;
+  m = b1 * m + (1.f - b1) * gr;
+  v = b2 * v + (1.f - b2) * gr * gr;
+  const float denom = sqrtf(v) * rbc2 + eps;
+  pv -= (lr / bc1) * m / denom;
+  p = pv;
+  return pv;
+}
+
+// The optimizer state a fused epilogue updates: parameter, moments and bf16 shadow share the gradient buffer's
+// element offsets (flat stores of one layout), g0 = the gradient buffer's base.  hyp (device, optional): the
+// step's {lr, bias_corr1, bias_corr2} (a replayed HIP graph), overriding lr / bc1 / rbc2.
+struct AdamFused {
+  float* p; float* m; float* v; bf16_t* pb; const float* g0; const float* hyp;
+  float lr, b1, b2, eps, wd, bc1, rbc2, gs; int decoupled;
+};
+ASRX_DEV void adam_hyp(const AdamFused& a, float& lr, float& bc1, float& rbc2) {
+  lr = a.lr; bc1 = a.bc1; rbc2 = a.rbc2;
+  if (a.hyp) { lr = a.hyp[0]; bc1 = a.hyp[1]; rbc2 = 1.f / sqrtf(a.hyp[2]); }
+}
+// the 4 elements at gradient address ga (16-B aligned) with final gradient values g4
+ASRX_DEV void adam_apply4(const AdamFused& a, const float* ga, f4_t g4, float lr, float bc1, float rbc2) {
+  const int64_t off = ga - a.g0;
+  f4_t p4 = *(const f4_t*)(a.p + off), m4 = *(const f4_t*)(a.m + off), v4 = *(const f4_t*)(a.v + off);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float pe = p4[k], me = m4[k], ve = v4[k];
+    adam_elem(g4[k], pe, me, ve, lr, a.b1, a.b2, a.eps, a.wd, bc1, rbc2, a.gs, a.decoupled);
+    p4[k] = pe;
+    m4[k] = me;
+    v4[k] = ve;
+  }
+  *(f4_t*)(a.p + off) = p4;
+  *(f4_t*)(a.m + off) = m4;
+  *(f4_t*)(a.v + off) = v4;
+  if (a.pb) {
+    typedef uint32_t au2_t __attribute__((ext_vector_type(2)));
+    au2_t u;
+    u.x = pack2bf(p4[0], p4[1]);
+    u.y = pack2bf(p4[2], p4[3]);
+    *(au2_t*)(a.pb + off) = u;
+  }
+}
+ASRX_DEV void adam_apply1(const AdamFused& a, const float* ga, float g, float lr, float bc1, float rbc2) {
+  const int64_t off = ga - a.g0;
+  float p = a.p[off], m = a.m[off], v = a.v[off];
+  adam_elem(g, p, m, v, lr, a.b1, a.b2, a.eps, a.wd, bc1, rbc2, a.gs, a.decoupled);
+  a.p[off] = p;
+  a.m[off] = m;
+  a.v[off] = v;
+  if (a.pb) a.pb[off] = f2bf(p);
+}
+
 // raw v_exp_f32 (2^x; -inf -> 0): the softmax arguments are <= 0, so no range reduction is needed
 ASRX_DEV float exp2_raw(float x) { return __builtin_amdgcn_exp2f(x); }
 

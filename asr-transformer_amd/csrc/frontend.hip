@@ -891,15 +891,11 @@ ASRX_DEV void adam_f4(f4_t& pp, const f4_t gg, f4_t& mm, f4_t& vv, float lr, flo
                       float wd, float bc1, float rbc2, float gs, int decoupled) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    float gr = gg[k] * gs;
-    float pv = pp[k];
-    if (decoupled) pv *= (1.f - lr * wd);
-    else gr += wd * pv;
-    mm[k] = b1 * mm[k] + (1.f - b1) * gr;
-    vv[k] = b2 * vv[k] + (1.f - b2) * gr * gr;
-    const float denom = sqrtf(vv[k]) * rbc2 + eps;
-    pv -= (lr / bc1) * mm[k] / denom;
-    pp[k] = pv;
+    float pe = pp[k], me = mm[k], ve = vv[k];
+    adam_elem(gg[k], pe, me, ve, lr, b1, b2, eps, wd, bc1, rbc2, gs, decoupled);
+    pp[k] = pe;
+    mm[k] = me;
+    vv[k] = ve;
   }
 }
 
@@ -951,15 +947,34 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
   // tail
   if (blockIdx.x == 0) {
     for (int64_t i = n4 * 4 + threadIdx.x; i < n; i += 256) {
-      float gr = g[i] * gs, pv = p[i];
-      if (decoupled) pv *= (1.f - lr * wd);
-      else gr += wd * pv;
-      m[i] = b1 * m[i] + (1.f - b1) * gr;
-      v[i] = b2 * v[i] + (1.f - b2) * gr * gr;
-      pv -= (lr / bc1) * m[i] / (sqrtf(v[i]) * rbc2 + eps);
+      float pv = p[i], mv = m[i], vv = v[i];
+      adam_elem(g[i], pv, mv, vv, lr, b1, b2, eps, wd, bc1, rbc2, gs, decoupled);
       p[i] = pv;
+      m[i] = mv;
+      v[i] = vv;
       if (pb) pb[i] = f2bf(pv);
     }
+  }
+}
+
+// AdamW over a table of element ranges of the flat buffers (the parameters a fused weight-gradient launch did not
+// update): block b takes range b; every range is 4-aligned and a multiple of 4 long (host-checked).
+__global__ __launch_bounds__(256) void adam_spans_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                         float* __restrict__ m, float* __restrict__ v,
+                                                         bf16_t* __restrict__ pb, const int64_t* __restrict__ spans,
+                                                         float lr, float b1, float b2, float eps, float wd, float bc1,
+                                                         float rbc2, float gs, int decoupled,
+                                                         const float* __restrict__ hyp) {
+  if (hyp) {
+    lr = hyp[0];
+    bc1 = hyp[1];
+    rbc2 = 1.f / sqrtf(hyp[2]);
+  }
+  const int64_t a = spans[2 * blockIdx.x] / 4, e = spans[2 * blockIdx.x + 1] / 4;
+  for (int64_t i = a + threadIdx.x; i < e; i += 256) {
+    f4_t pp = ((const f4_t*)p)[i], mm = ((const f4_t*)m)[i], vv = ((const f4_t*)v)[i];
+    adam_f4(pp, ((const f4_t*)g)[i], mm, vv, lr, b1, b2, eps, wd, bc1, rbc2, gs, decoupled);
+    adam_store(p, m, v, pb, i, pp, mm, vv);
   }
 }
 
@@ -1001,9 +1016,10 @@ extern "C" int asrx_version(void) { return 2; }
 
 extern "C" int asrx_struct_sizes(int64_t* out, int32_t n) {
   if (!out || n < 0) return ASRX_ERR_ARG;
-  const int64_t s[4] = {(int64_t)sizeof(asrx_gemm_desc), (int64_t)sizeof(asrx_attn_desc),
-                        (int64_t)sizeof(asrx_gemm_group_dev), (int64_t)sizeof(asrx_rowsum_group)};
-  const int k = n < 4 ? n : 4;
+  const int64_t s[5] = {(int64_t)sizeof(asrx_gemm_desc), (int64_t)sizeof(asrx_attn_desc),
+                        (int64_t)sizeof(asrx_gemm_group_dev), (int64_t)sizeof(asrx_rowsum_group),
+                        (int64_t)sizeof(asrx_adam_desc)};
+  const int k = n < 5 ? n : 5;
   for (int i = 0; i < k; ++i) out[i] = s[i];
   return k;
 }
@@ -1243,6 +1259,21 @@ extern "C" int asrx_adam(float* p, const float* g, float* m, float* v, void* p_b
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1)), dim3(256), 0, (hipStream_t)stream, p, g, m, v,
                      (bf16_t*)p_bf16, n, lr, beta1, beta2, eps, weight_decay, bias_corr1, 1.f / sqrtf(bias_corr2),
                      grad_scale, decoupled, hyp);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
+extern "C" int asrx_adam_spans(float* p, const float* g, float* m, float* v, void* p_bf16, const int64_t* spans,
+                               int32_t nspans, float lr, float beta1, float beta2, float eps, float weight_decay,
+                               float bias_corr1, float bias_corr2, float grad_scale, int32_t decoupled,
+                               const float* hyp, void* stream) {
+  if (!p || !g || !m || !v || nspans < 0 || (nspans > 0 && !spans)) return ASRX_ERR_ARG;
+  if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16) return ASRX_ERR_ARG;
+  if (p_bf16 && (uintptr_t)p_bf16 % 8) return ASRX_ERR_ARG;
+  if (nspans == 0) return ASRX_OK;
+  hipLaunchKernelGGL(adam_spans_kernel, dim3(nspans), dim3(256), 0, (hipStream_t)stream, p, g, m, v, (bf16_t*)p_bf16,
+                     spans, lr, beta1, beta2, eps, weight_decay, bias_corr1, 1.f / sqrtf(bias_corr2), grad_scale,
+                     decoupled, hyp);
   ASRX_CHECK_LAUNCH();
   return ASRX_OK;
 }

@@ -1816,6 +1816,35 @@ extern "C" int asrx_gemm(const asrx_gemm_desc* d, void* stream) {
   return ASRX_OK;
 }
 
+// The grouped weight gradients of a single-GPU step with AdamW fused into the epilogue (the ws queue launch only:
+// tile 5, fp32 C, beta 0, the counters / slabs of common->workspace / rowsum_ws): every dW and bias-gradient element
+// is stored AND its parameter, moments and bf16 shadow updated at the same element offset (asrx.h).
+extern "C" int asrx_gemm_grouped_xcd_adam(const asrx_gemm_desc* common, const asrx_gemm_group_dev* groups,
+                                          const uint16_t* tile_group, const uint16_t* block_tile, int32_t count,
+                                          int32_t tiles, int32_t blocks, const asrx_adam_desc* adam, void* stream) {
+  if (!common || !groups || !tile_group || !block_tile || !adam || count <= 0 || count > 65535 || tiles < 0 ||
+      blocks < 0 || tiles > 65535)
+    return ASRX_ERR_ARG;
+  if (!adam->p || !adam->m || !adam->v || !adam->g_base || (((uintptr_t)adam->p | (uintptr_t)adam->m |
+      (uintptr_t)adam->v | (uintptr_t)adam->g_base) % 16) || (adam->p_bf16 && (uintptr_t)adam->p_bf16 % 8))
+    return ASRX_ERR_ARG;
+  if (tiles == 0 || blocks == 0) return ASRX_OK;
+  if (common->in_dtype != ASRX_BF16 || !common->a_trans || !common->b_trans || common->tile != 5 ||
+      common->c_dtype != ASRX_F32 || common->alpha != 1.f || common->beta != 0.f || !common->workspace ||
+      common->workspace_elems < 16 || !common->rowsum_ws)
+    return ASRX_ERR_UNSUPPORTED;
+  AdamFused ad;
+  ad.p = adam->p; ad.m = adam->m; ad.v = adam->v; ad.pb = (bf16_t*)adam->p_bf16; ad.g0 = adam->g_base;
+  ad.hyp = adam->hyp; ad.lr = adam->lr; ad.b1 = adam->beta1; ad.b2 = adam->beta2; ad.eps = adam->eps;
+  ad.wd = adam->weight_decay; ad.bc1 = adam->bias_corr1; ad.rbc2 = 1.f / sqrtf(adam->bias_corr2);
+  ad.gs = adam->grad_scale; ad.decoupled = adam->decoupled;
+  if (launch_ws_grouped_adam((const GroupEnt*)groups, tile_group, block_tile, tiles, blocks, gemm_dbg(),
+                             (int*)common->workspace, common->rowsum_ws, ad, (hipStream_t)stream) != 0)
+    return ASRX_ERR_UNSUPPORTED;
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
 extern "C" int asrx_gemm_grouped_xcd(const asrx_gemm_desc* common, const asrx_gemm_group_dev* groups,
                                      const uint16_t* tile_group, const uint16_t* block_tile, int32_t count,
                                      int32_t tiles, int32_t blocks, void* stream) {

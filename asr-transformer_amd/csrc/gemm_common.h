@@ -135,7 +135,7 @@ typedef const __attribute__((address_space(1))) void gbl_void_t;
 // specialising them removes the per-element runtime branches of epilogue4 (the generic fallback).
 enum : int {
   E_BIAS = 1, E_RELU = 2, E_DROP = 4, E_GATE = 8, E_RESID = 16, E_BETA = 32, E_F32 = 64, E_ALPHA = 128,
-  E_ROWADD = 256, E_GBITS = 512, E_MASKOUT = 1024, E_GENERIC = 1 << 30
+  E_ROWADD = 256, E_GBITS = 512, E_MASKOUT = 1024, E_ADAM = 2048, E_GENERIC = 1 << 30
 };
 
 // The fused element-wise epilogue of the fast path for the 4 consecutive columns n..n+3 of row m (valid
@@ -531,5 +531,7 @@ bool wse_instantiated(bool bt, int epi);
 void launch_wse(const GemmArgs& g, bool bt, int epi, int ntiles, hipStream_t st);
 int launch_ws_grouped(const GroupEnt* ents, const uint16_t* tile_group, const uint16_t* block_tile, int ntiles,
                       int blocks, float beta, int dbg, int* queue, float* part, hipStream_t st);
+int launch_ws_grouped_adam(const GroupEnt* ents, const uint16_t* tile_group, const uint16_t* block_tile, int ntiles,
+                           int blocks, int dbg, int* queue, float* part, const AdamFused& ad, hipStream_t st);
 
 }  // namespace asrxg

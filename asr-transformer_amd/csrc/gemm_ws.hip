@@ -191,7 +191,8 @@ do {                                                                            
 // read as zero through the descriptor range); ragged M / N tiles: rows / column groups past them are not stored.
 // g.rowsum (AT only): += the row sums of op(A) (the fused bias gradient), by the compute waves of column block 0.
 template <bool AT, bool BT, int EPI, int BM = 256, int NCW = 4>
-ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned char* lds) {
+ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned char* lds,
+                      const AdamFused* ad = nullptr) {
   using C = WsCfg<BM>;
   const bf16_t* A = (const bf16_t*)g.a;
   const bf16_t* B = (const bf16_t*)g.b;
@@ -370,7 +371,56 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
     }
   }
   if (!loader || NCW == 8) load_resid();
-  if constexpr (F32) {
+  if constexpr ((EPI & E_ADAM) != 0) {
+    // E_ADAM (the grouped weight gradients of a single-GPU step, asrx_gemm_grouped_xcd_adam): each thread's rows in
+    // groups of 4 — the dW values stored, then the AdamW update of the same elements (parameter, moments, bf16
+    // shadow at the gradient's offsets), the 12 operand loads of a group issued before its arithmetic
+    static_assert((EPI & (E_BETA | E_BIAS | E_RESID | E_ROWADD | E_DROP | E_RELU)) == 0 && F32, "ws: E_ADAM is plain dW");
+    float alr, abc1, arbc2;
+    adam_hyp(*ad, alr, abc1, arbc2);
+    const bool ncol = n0 + cq < g.N;
+#pragma unroll
+    for (int i0 = 0; i0 < NR; i0 += 4) {
+      f4_t dv[4], pa[4], ma[4], va[4];
+      float* cp[4];
+      bool ok[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int r = rb + RS * (i0 + u), m = m0 + r;
+        dv[u] = *(const f4_t*)(stg + r * C::SP + cq);
+        ok[u] = m < g.M && ncol;
+        cp[u] = (float*)g.c + (int64_t)(ok[u] ? m : m0) * g.ldc + n0 + (ok[u] ? cq : 0);
+        const int64_t off = cp[u] - ad->g0;
+        pa[u] = *(const f4_t*)(ad->p + off);
+        ma[u] = *(const f4_t*)(ad->m + off);
+        va[u] = *(const f4_t*)(ad->v + off);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (!ok[u]) continue;
+        *(f4_t*)cp[u] = dv[u];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float pe = pa[u][k], me = ma[u][k], ve = va[u][k];
+          adam_elem(dv[u][k], pe, me, ve, alr, ad->b1, ad->b2, ad->eps, ad->wd, abc1, arbc2, ad->gs, ad->decoupled);
+          pa[u][k] = pe;
+          ma[u][k] = me;
+          va[u][k] = ve;
+        }
+        const int64_t off = cp[u] - ad->g0;
+        *(f4_t*)(ad->p + off) = pa[u];
+        *(f4_t*)(ad->m + off) = ma[u];
+        *(f4_t*)(ad->v + off) = va[u];
+        if (ad->pb) {
+          typedef uint32_t au2_t __attribute__((ext_vector_type(2)));
+          au2_t w;
+          w.x = pack2bf(pa[u][0], pa[u][1]);
+          w.y = pack2bf(pa[u][2], pa[u][3]);
+          *(au2_t*)(ad->pb + off) = w;
+        }
+      }
+    }
+  } else if constexpr (F32) {
     f4_t b4 = f4_t{0.f, 0.f, 0.f, 0.f};
     if constexpr ((EPI & E_BIAS) != 0) b4 = *(const f4_t*)(g.bias + n0 + cq);
     const bool ncol = n0 + cq < g.N;   // (N % 4 == 0: a column group is wholly in or out)
@@ -436,7 +486,7 @@ __global__ __launch_bounds__(768) void gemm_bf16_ws8_kernel(GemmArgs g, int ntil
 template <int EPI, int NCW = 4>
 ASRX_DEV void wsg_tile(const GroupEnt* __restrict__ ents, const uint16_t* __restrict__ tile_group, int t_all, int slot,
                        int dbg, unsigned char* lds, int* __restrict__ pcnt = nullptr, float* __restrict__ part = nullptr,
-                       int* s_last = nullptr) {
+                       int* s_last = nullptr, const AdamFused* ad = nullptr) {
   // tools only (ASRX_GEMM_DBG & 128): per-tile start / end real time, XCD, CU and tile into g_ws_trace
   const bool trace = (dbg & 128) && threadIdx.x == 0 && slot < WS_TRACE_BLOCKS;
   const uint64_t t_start = trace ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -462,7 +512,7 @@ ASRX_DEV void wsg_tile(const GroupEnt* __restrict__ ents, const uint16_t* __rest
     g.splitk = ntn;
     g.k_per_split = t % ntn;
   }
-  ws_tile<true, true, EPI, WS_BM, NCW>(g, (t / ntn) * WS_BM, (t % ntn) * WS_BN, rs_tile, lds);
+  ws_tile<true, true, EPI, WS_BM, NCW>(g, (t / ntn) * WS_BM, (t % ntn) * WS_BN, rs_tile, lds, ad);
   if (split) {
     // Slab hand-off between the ntn column tiles of a row panel (workgroups on any XCD):
     //  producer (every tile): the 256 slab floats are stored by agent-scope atomic stores = `global_store_dword sc1`
@@ -497,7 +547,13 @@ ASRX_DEV void wsg_tile(const GroupEnt* __restrict__ ents, const uint16_t* __rest
         float v = 0.f;
         for (int j = 0; j < ntn; ++j)
           v += __hip_atomic_load(sl + (int64_t)j * WS_BM, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        e.rowsum[m] += v;
+        const float gb = e.rowsum[m] + v;   // the bias gradient is final here (every column tile's share added)
+        e.rowsum[m] = gb;
+        if constexpr ((EPI & E_ADAM) != 0) {
+          float alr, abc1, arbc2;
+          adam_hyp(*ad, alr, abc1, arbc2);
+          adam_apply1(*ad, e.rowsum + m, gb, alr, abc1, arbc2);
+        }
       }
     }
   }
@@ -549,7 +605,7 @@ __global__ __launch_bounds__(768) void gemm_bf16_wsg8_kernel(const GroupEnt* __r
 template <int EPI, int NCW>
 ASRX_DEV void wsgq_body(const GroupEnt* __restrict__ ents, const uint16_t* __restrict__ tile_group,
                         const uint16_t* __restrict__ block_tile, int ntiles, int depth, int* __restrict__ cnt,
-                        float* __restrict__ part, int dbg) {
+                        float* __restrict__ part, int dbg, const AdamFused* ad = nullptr) {
   __shared__ __attribute__((aligned(1024))) unsigned char lds[WS_LDS];
   __shared__ int s_slot, s_last;
   const int x = (int)(blockIdx.x % 8);
@@ -567,7 +623,7 @@ ASRX_DEV void wsgq_body(const GroupEnt* __restrict__ ents, const uint16_t* __res
     const int slot = xq + 8 * i;
     const int t_all = (int)block_tile[slot];
     if (t_all >= ntiles) continue;
-    wsg_tile<EPI, NCW>(ents, tile_group, t_all, slot, dbg, lds, cnt + 16, part, &s_last);
+    wsg_tile<EPI, NCW>(ents, tile_group, t_all, slot, dbg, lds, cnt + 16, part, &s_last, ad);
     __syncthreads();   // the epilogue's staging image is dead before the next tile's LDS-DMA
   }
 }
@@ -578,6 +634,16 @@ __global__ __launch_bounds__(512) void gemm_bf16_wsgq_kernel(const GroupEnt* __r
                                                              int depth, int* __restrict__ cnt,
                                                              float* __restrict__ part, int dbg) {
   wsgq_body<EPI, 4>(ents, tile_group, block_tile, ntiles, depth, cnt, part, dbg);
+}
+// (asrx_gemm_grouped_xcd_adam) the same launch with the AdamW update of every dW / bias element fused into the
+// epilogue (the optimizer state by value: the kernel-argument segment)
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_bf16_wsgqa_kernel(const GroupEnt* __restrict__ ents,
+                                                              const uint16_t* __restrict__ tile_group,
+                                                              const uint16_t* __restrict__ block_tile, int ntiles,
+                                                              int depth, int* __restrict__ cnt,
+                                                              float* __restrict__ part, int dbg, AdamFused ad) {
+  wsgq_body<EPI | E_ADAM, 4>(ents, tile_group, block_tile, ntiles, depth, cnt, part, dbg, &ad);
 }
 template <int EPI>
 __global__ __launch_bounds__(768) void gemm_bf16_wsgq8_kernel(const GroupEnt* __restrict__ ents,
@@ -1067,6 +1133,15 @@ int launch_ws_grouped_n(const GroupEnt* ents, const uint16_t* tile_group, const 
                        ntiles, dbg);
   else
     return -1;
+  return 0;
+}
+
+int launch_ws_grouped_adam(const GroupEnt* ents, const uint16_t* tile_group, const uint16_t* block_tile, int ntiles,
+                           int blocks, int dbg, int* queue, float* part, const AdamFused& ad, hipStream_t st) {
+  if (!queue || !part || blocks % 8 != 0) return -1;   // the queue launch only: its slab hand-off finalises the bias
+  const int grid = std::min(blocks, 256), depth = blocks / 8;
+  hipLaunchKernelGGL((gemm_bf16_wsgqa_kernel<E_F32>), dim3(grid), dim3(512), 0, st, ents, tile_group, block_tile, ntiles,
+                     depth, queue, part, dbg, ad);
   return 0;
 }
 

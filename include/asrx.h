@@ -36,7 +36,8 @@ int asrx_version(void);
 
 /* sizeof of the descriptor structs as this library was compiled (binding check: a ctypes / cgo mirror of a
  * struct must have the same size): out[0] = asrx_gemm_desc, out[1] = asrx_attn_desc, out[2] =
- * asrx_gemm_group_dev, out[3] = asrx_rowsum_group.  Returns the number of entries written (<= n). */
+ * asrx_gemm_group_dev, out[3] = asrx_rowsum_group, out[4] = asrx_adam_desc.  Returns the number of entries written
+ * (<= n). */
 int asrx_struct_sizes(int64_t* out, int32_t n);
 
 /* ---------------------------------------------------------------------------------------------------
@@ -119,6 +120,24 @@ typedef struct asrx_gemm_group_dev {
 int asrx_gemm_grouped_xcd(const asrx_gemm_desc* common, const asrx_gemm_group_dev* groups,
                           const uint16_t* tile_group, const uint16_t* block_tile, int32_t count, int32_t tiles,
                           int32_t blocks, void* stream);
+
+/* AdamW state for asrx_gemm_grouped_xcd_adam: flat fp32 parameter / moment buffers (and the optional bf16 shadow)
+ * laid out like the gradient buffer whose base is g_base — the update of gradient element g_base[i] goes to
+ * p[i], m[i], v[i], p_bf16[i].  Hyper-parameters as asrx_adam (hyp: device {lr, bias_corr1, bias_corr2} or null). */
+typedef struct asrx_adam_desc {
+  float* p; float* m; float* v; void* p_bf16; const float* g_base; const float* hyp;
+  float lr, beta1, beta2, eps, weight_decay, bias_corr1, bias_corr2, grad_scale;
+  int32_t decoupled, reserved;
+} asrx_adam_desc;
+
+/* asrx_gemm_grouped_xcd (tile 5, the persistent queue launch: fp32 C, beta 0, workspace counters and rowsum_ws
+ * slabs) with the optimizer step fused into the epilogue: each dW element and each group's bias gradient (rowsum_a)
+ * is stored and the AdamW update of its parameter applied at once, the parameter / moment / shadow bytes moving
+ * while the other tiles compute (single-GPU training: the gradients need no exchange first).  Replaces the
+ * optimizer.step() (train.py:35) of every nn.Linear parameter together with its gradient mm + sum. */
+int asrx_gemm_grouped_xcd_adam(const asrx_gemm_desc* common, const asrx_gemm_group_dev* groups,
+                               const uint16_t* tile_group, const uint16_t* block_tile, int32_t count, int32_t tiles,
+                               int32_t blocks, const asrx_adam_desc* adam, void* stream);
 
 /* Name of the kernel instantiation asrx_gemm would launch for d (as rocprofv3 lists it, without the
  * namespace/argument list), e.g. "gemm_bf16_p3_kernel<false, false, 1>".  Host-only: no launch, no GPU
@@ -358,6 +377,12 @@ int asrx_sum_chunks_bf16(const void* in, int32_t world, int64_t chunk, void* out
 int asrx_adam(float* p, const float* g, float* m, float* v, void* p_bf16, int64_t n, float lr, float beta1,
               float beta2, float eps, float weight_decay, float bias_corr1, float bias_corr2, float grad_scale,
               int32_t decoupled, const float* hyp, void* stream);
+/* AdamW (as asrx_adam) over the element ranges [spans[2i], spans[2i+1]) of the flat buffers, one workgroup per
+ * range (device int64 table, nspans pairs, every bound a multiple of 4): the parameters a fused weight-gradient
+ * launch (asrx_gemm_grouped_xcd_adam) did not update. */
+int asrx_adam_spans(float* p, const float* g, float* m, float* v, void* p_bf16, const int64_t* spans, int32_t nspans,
+                    float lr, float beta1, float beta2, float eps, float weight_decay, float bias_corr1,
+                    float bias_corr2, float grad_scale, int32_t decoupled, const float* hyp, void* stream);
 /* Zero the spans [spans[2i], spans[2i+1]) (element offsets, device int64 table of nspans pairs) of an fp32 buffer
  * (16-B aligned base), one workgroup per span.  The training step zeroes the accumulating gradient regions with it
  * (optimizer.zero_grad, train.py:27, for everything a weight-gradient GEMM does not overwrite). */

@@ -65,12 +65,12 @@ def test_ctypes_struct_sizes_match_the_library():
     (asrx_struct_sizes): a stale mirror would make the library read past the caller's struct."""
     import ctypes
     import asrx
-    from asrx._lib import AttnDesc, GemmDesc, GemmGroupDev, RowsumGroup
+    from asrx._lib import AdamDesc, AttnDesc, GemmDesc, GemmGroupDev, RowsumGroup
     lib = asrx.native()
-    out = (ctypes.c_int64 * 4)()
-    assert lib.asrx_struct_sizes(out, 4) == 4
+    out = (ctypes.c_int64 * 5)()
+    assert lib.asrx_struct_sizes(out, 5) == 5
     assert list(out) == [ctypes.sizeof(GemmDesc), ctypes.sizeof(AttnDesc), ctypes.sizeof(GemmGroupDev),
-                         ctypes.sizeof(RowsumGroup)]
+                         ctypes.sizeof(RowsumGroup), ctypes.sizeof(AdamDesc)]
     assert ctypes.sizeof(GemmGroupDev) == 64
 
 
