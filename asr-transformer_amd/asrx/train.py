@@ -412,14 +412,15 @@ class Trainer:
                 return self._replay(spectrum, text, mask, input_text)
             self._eager_keys.add(key)
         self._fuse_next = self._fused_adam_ok()
-        if self._fuse_next:   # the fused launch reads this step's lr / bias corrections from the device
-            K.adam_hyper(self._hyp, self.lr, self.betas[0], self.betas[1], self.step_count + 1)
+        # this step's lr / bias corrections from the device, as in a replayed graph (and the fused launch): every
+        # AdamW of the trainer takes 1/sqrt(bias_corr2) from the same device arithmetic
+        K.adam_hyper(self._hyp, self.lr, self.betas[0], self.betas[1], self.step_count + 1)
         try:
             loss = self.forward_backward(spectrum, text, mask, input_text=input_text)
         finally:
             self._fuse_next = False
         self.step_count += 1
-        self._reduce_and_adam(self._hyp if self._cover is not None else None)
+        self._reduce_and_adam(self._hyp)
         self.store.mark_shadow_fresh()
         return loss
 
