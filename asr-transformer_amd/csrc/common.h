@@ -26,19 +26,25 @@ ASRX_DEV uint32_t pack2bf(float a, float b) {
 }
 
 // ---- AdamW (asrx_adam; fused into the grouped weight-gradient epilogue, asrx_gemm_grouped_xcd_adam; asrx_adam_spans)
-// One element: the reference's torch.optim.AdamW / Adam step (train.py:35) in fp32.  Contraction is off so the
-// element math rounds identically in every kernel that inlines it (the fused epilogue, the streaming kernel).
+// One element: the reference's torch.optim.AdamW / Adam step (train.py:35) in fp32.  The library is compiled with
+// -ffp-contract=fast, which fuses multiply-adds across statements and ignores FP_CONTRACT pragmas, so each kernel
+// that inlines this (the fused weight-gradient epilogue, the streaming kernels) could round it differently: the
+// multiply-adds are explicit fmaf and every other product is pinned (an empty asm on its register), which leaves the
+// compiler nothing to fuse — one rounding sequence wherever it is inlined.
+ASRX_DEV float adam_pin(float x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
 ASRX_DEV float adam_elem(float g, float& p, float& m, float& v, float lr, float b1, float b2, float eps, float wd,
                          float bc1, float rbc2, float gs, int decoupled) {
-#pragma clang fp contract(off)
-  float gr = g * gs;
+  float gr = adam_pin(g * gs);
   float pv = p;
-  if (decoupled) pv *= (1.f - lr * wd);
-  else gr += wd * pv;
-  m = b1 * m + (1.f - b1) * gr;
-  v = b2 * v + (1.f - b2) * gr * gr;
-  const float denom = sqrtf(v) * rbc2 + eps;
-  pv -= (lr / bc1) * m / denom;
+  if (decoupled) pv = adam_pin(pv * __builtin_fmaf(-lr, wd, 1.f));
+  else gr = __builtin_fmaf(wd, pv, gr);
+  m = __builtin_fmaf(b1, m, adam_pin((1.f - b1) * gr));
+  v = __builtin_fmaf(b2, v, adam_pin(adam_pin((1.f - b2) * gr) * gr));
+  const float denom = __builtin_fmaf(sqrtf(v), rbc2, eps);
+  pv -= adam_pin(adam_pin(lr / bc1) * m) / denom;
   p = pv;
   return pv;
 }

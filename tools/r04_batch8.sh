@@ -13,6 +13,7 @@ run() {   # name seconds cmd...
   case $rc in 0|1) ;; *) echo "stopping after rc=$rc"; exit "$rc";; esac
   return $rc
 }
+timeout -k 10 300 python tools/fadam_diag.py > gpurun_out/fadam_diag.log 2>&1; grep -E "losses|differing" gpurun_out/fadam_diag.log
 run t_fadam 500 python -u -m pytest tests/test_gpu_fused_adam.py tests/test_gpu_graph.py tests/test_gpu_train_epoch.py \
     -x -q --timeout 300 --timeout-method thread -m gpu || exit 1
 bash tools/prof_step.sh b8 ASRX_NONE=0 ASRX_FUSED_ADAM=0 || exit $?
