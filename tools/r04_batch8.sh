@@ -18,3 +18,4 @@ run t_fadam 500 python -u -m pytest tests/test_gpu_fused_adam.py tests/test_gpu_
     -x -q --timeout 300 --timeout-method thread -m gpu || exit 1
 bash tools/prof_step.sh b8 ASRX_NONE=0 ASRX_FUSED_ADAM=0 || exit $?
 run bench_b8 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-sub --no-other
+run dualmb 300 python tools/dualmb_probe.py --reps 10
