@@ -1,5 +1,6 @@
 """Per-kernel table of ONE steady-state training step from a rocprofv3 kernel trace: the launches between two
-consecutive adam_kernel launches (one per step), so warm-up and setup launches are excluded.
+consecutive optimizer launches (adam_kernel, or adam_spans_kernel when AdamW runs fused into the grouped weight
+gradients: one per step), so warm-up and setup launches are excluded.
 
     python tools/step_table.py gpurun_out/prof/run_kernel_trace.csv [--step -1]
 """
@@ -15,9 +16,9 @@ def main():
     ap.add_argument("--step", type=int, default=-1, help="which adam-to-adam interval (default: the last)")
     args = ap.parse_args()
     rows = sorted(csv.DictReader(open(args.trace)), key=lambda r: int(r["Start_Timestamp"]))
-    adam = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"]]
+    adam = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"] or "adam_spans_kernel" in r["Kernel_Name"]]
     if len(adam) < 2:
-        raise SystemExit("need two adam_kernel launches in the trace")
+        raise SystemExit("need two optimizer launches (adam_kernel / adam_spans_kernel) in the trace")
     pairs = list(zip(adam[:-1], adam[1:]))
     a, b = pairs[args.step]
     seg = rows[a + 1:b + 1]
