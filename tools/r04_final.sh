@@ -1,6 +1,7 @@
 #!/bin/bash
-# round-4 measurement on one box: GPU tests, smoke, PMC passes (traffic + MFMA, copied into profiles/ so
-# the bench line reads them), the full default bench line, and the rocprofv3 kernel trace of the graph-mode step.
+# round-4 closing measurement on one box: GPU tests, smoke, PMC passes (traffic + MFMA, copied into profiles/ so
+# the bench line reads them), the full default bench line, the rocprofv3 kernel trace of the graph-mode step and
+# its step table, and the fused-AdamW step A/B.
 set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
@@ -17,3 +18,4 @@ cp gpurun_out/c3_pmc_traffic.json gpurun_out/c3_pmc_mfma.json profiles/   # (the
 step bench 900 python bench.py
 step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 3 --no-cpu-baseline --no-probe --no-sub --no-other
 step steptab 120 python3 tools/step_table.py gpurun_out/prof/run_kernel_trace.csv
+bash tools/prof_step.sh fin ASRX_FUSED_ADAM=0 ASRX_NONE=0 || exit $?
