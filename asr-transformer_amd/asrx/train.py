@@ -122,6 +122,26 @@ class _Segments:
                 reducer.ready(a, b)
 
 
+def residual_pieces(n, cover, piece=None):
+    """The [start, end) ranges of a flat buffer of n elements NOT covered by the (offset, numel) ranges `cover`, cut
+    into pieces of at most `piece` elements (default ADAM_SPAN), bounds on multiples of 4 (every parameter starts
+    64-aligned, so a cover range never shares a quad with an uncovered one)."""
+    piece = piece or ADAM_SPAN
+    spans, pos = [], 0
+    for o, k in sorted(cover):
+        if o > pos:
+            spans.append((pos, o))
+        pos = max(pos, o + k)
+    if pos < n:
+        spans.append((pos, n))
+    out = []
+    for a, b in spans:
+        a4, b4 = a // 4 * 4, -(-b // 4) * 4
+        for c in range(a4, b4, piece):
+            out.append((c, min(b4, c + piece)))
+    return out
+
+
 def wgrad_only_params(model):
     """Parameters written only by a weight-gradient GEMM: the Linear weights (incl. the packed Q/K/V and K/V
     projections and the classifier).  Biases (fused row sums accumulate), LayerNorm, embedding and conv
@@ -294,19 +314,7 @@ class Trainer:
         key = tuple(sorted(cover))
         tab = self._rspans.get(key)
         if tab is None:
-            n = self.store.flat.numel()
-            spans, pos = [], 0
-            for o, k in key:
-                if o > pos:
-                    spans.append((pos, o))
-                pos = max(pos, o + k)
-            if pos < n:
-                spans.append((pos, n))
-            pieces = []
-            for a, b in spans:
-                a4, b4 = a // 4 * 4, -(-b // 4) * 4   # (every parameter is 64-aligned: no cut shares a quad)
-                for c in range(a4, b4, ADAM_SPAN):
-                    pieces.append((c, min(b4, c + ADAM_SPAN)))
+            pieces = residual_pieces(self.store.flat.numel(), key)
             tab = torch.tensor(pieces, dtype=torch.int64).reshape(-1, 2).to(self.store.flat.device)
             self._rspans[key] = tab
         return tab

@@ -28,7 +28,7 @@ def build(name, dropout):
     return m.to(dev).train(), cfg
 
 
-def run(name, fused, graph, steps, batch, dropout=0.0, wd=0.0):
+def run(name, fused, graph, steps, batch, dropout=0.0, wd=0.0, decoupled=True):
     import asrx.train as T
     old = T.FUSED_ADAM
     T.FUSED_ADAM = fused
@@ -39,7 +39,7 @@ def run(name, fused, graph, steps, batch, dropout=0.0, wd=0.0):
         for i in range(steps):
             s, t, k = synthetic_batch(cfg, batch, spec["frames"], spec["text_len"] + 1, seed=300 + i)
             data.append((s.to(dev), t.to(dev), k.to(dev)))
-        tr = T.Trainer(m, lr=2e-3, weight_decay=wd, graph=graph)
+        tr = T.Trainer(m, lr=2e-3, weight_decay=wd, decoupled=decoupled, graph=graph)
         losses = [float(tr.step(*b)) for b in data]
         torch.cuda.synchronize()
         return tr, losses
@@ -47,12 +47,12 @@ def run(name, fused, graph, steps, batch, dropout=0.0, wd=0.0):
         T.FUSED_ADAM = old
 
 
-@pytest.mark.parametrize("wd", [0.0, 0.01])
-def test_fused_adam_equals_separate_adam_eager(wd):
+@pytest.mark.parametrize("wd,decoupled", [(0.0, True), (0.01, True), (0.01, False)])
+def test_fused_adam_equals_separate_adam_eager(wd, decoupled):
     """c3 dimensions at B = 2 (the bench's GEMM shapes per row, the ws queue launch): 4 eager AdamW steps; from the
     second (FreshGrads) on the fused path runs, covering every nn.Linear weight and bias gradient."""
-    ref, l0 = run("c3", False, False, 4, 2, wd=wd)
-    tr, l1 = run("c3", True, False, 4, 2, wd=wd)
+    ref, l0 = run("c3", False, False, 4, 2, wd=wd, decoupled=decoupled)
+    tr, l1 = run("c3", True, False, 4, 2, wd=wd, decoupled=decoupled)
     assert tr._cover, "the fused launch did not run"
     assert ref._cover is None
     covered = sum(k for _, k in tr._cover)

@@ -369,3 +369,22 @@ def test_new_state_dict_schema_matches_reference(golden_dir, name):
     back = m.state_dict()
     for k, v in P.items():
         assert torch.equal(back[k], v), k
+
+
+def test_fused_adam_residual_pieces():
+    """The ranges the span-table AdamW steps after a fused weight-gradient launch: the complement of the covered
+    parameters, cut into bounded pieces, every element of the buffer stepped exactly once over cover + pieces."""
+    from asrx.train import residual_pieces
+    n = 10_000
+    cover = [(64, 256), (1024, 512), (320, 64), (9_984, 16)]
+    pieces = residual_pieces(n, cover, piece=1000)
+    assert all(b - a <= 1000 and a % 4 == 0 and b % 4 == 0 for a, b in pieces)
+    hits = [0] * n
+    for o, k in cover:
+        for i in range(o, o + k):
+            hits[i] += 1
+    for a, b in pieces:
+        for i in range(a, b):
+            hits[i] += 1
+    assert hits == [1] * n
+    assert residual_pieces(128, [(0, 128)]) == []
