@@ -249,7 +249,8 @@ __global__ __launch_bounds__(256) void gemm_bf16_grouped_dev_kernel(float alpha,
 }
 
 // diagnostics switch (ASRX_GEMM_DBG, or asrx_gemm_set_debug for interleaved A/B in one process): 1 = skip the
-// epilogue stores, 4 = issue each LDS-DMA stage in one block, 8 = no operand loads (compute on stale LDS)
+// epilogue stores, 4 = issue each LDS-DMA stage in one block, 8 = no operand loads (compute on stale LDS), 256 =
+// the fused AdamW epilogue without its load look-ahead
 int g_gemm_dbg = -1;
 int gemm_dbg() {
   if (g_gemm_dbg < 0) { const char* e = getenv("ASRX_GEMM_DBG"); g_gemm_dbg = e ? atoi(e) : 0; }
@@ -1653,7 +1654,8 @@ extern "C" int asrx_gemm_kernel_name(const asrx_gemm_desc* d, char* buf, int len
   }
   const GemmPlan pl = plan_bf16(d, batch, splitk);
   if (pl.use == 11 || pl.use == 13)
-    snprintf(buf, len, "gemm_bf16_ws%s_kernel<%s, %d, %d>", (ws8_mode() & (pl.use == 13 ? 2 : 1)) ? "8" : "",
+    snprintf(buf, len, "gemm_bf16_ws%s_kernel<%s, %d, %d>",
+             ((pl.epi & E_F32) == 0 && wsr_on()) ? "r" : (ws8_mode() & (pl.use == 13 ? 2 : 1)) ? "8" : "",
              tf[!!d->b_trans], pl.epi, pl.use == 13 ? 64 : 256);
   else if (pl.use == 12)
     snprintf(buf, len, "gemm_bf16_wsp_kernel<%s, %d>", tf[!!d->b_trans], pl.epi);

@@ -524,6 +524,7 @@ ASRX_DEV s8_t p4_frag(const unsigned char* img, int i0, int ks, uint32_t S) {
 constexpr int WS_BM = 256, WS_BN = 128;
 bool ws_instantiated(bool bt, int epi);
 int ws8_mode();   // ASRX_WS8 bits: 1 the 256-row ws tiles, 2 the 64-row ones, on 8 compute waves (gemm_bf16_ws8_kernel)
+bool wsr_on();    // ASRX_WSR: bf16-output ws tiles stored from registers (gemm_bf16_wsr_kernel)
 void launch_ws(const GemmArgs& g, bool bt, int epi, int ntiles, int bm, hipStream_t st);
 bool wsp_instantiated(bool bt, int epi);
 void launch_wsp(const GemmArgs& g, bool bt, int epi, int ntiles, hipStream_t st);

@@ -111,8 +111,10 @@ struct WsWave {
   ASRX_DEV static int wn(int cw) { return (cw & 1) * 64; }
 };
 
-template <bool AT, bool BT, int BM = 256, int NCW = 4>
-ASRX_DEV void ws_compute(const GemmArgs& g, int m0, int nk, int wm, int wn, unsigned char* lds) {
+// REPI >= 0 (the wsr kernels, bf16 C): the finished tile is stored from registers with epilogue REPI
+// (gemm_common.h epilogue_tile) instead of going through the LDS staging image
+template <bool AT, bool BT, int BM = 256, int NCW = 4, int REPI = -1>
+ASRX_DEV void ws_compute(const GemmArgs& g, int m0, int n0, int nk, int wm, int wn, unsigned char* lds) {
   using C = WsCfg<BM>;
   constexpr int TM = WsWave<BM, NCW>::TM, TN = WsWave<BM, NCW>::TN;
   const int l = threadIdx.x & 63;
@@ -178,6 +180,10 @@ do {                                                                            
     cbo = nbo;
   }
 #undef WS_ROLL_ORDER
+  if constexpr (REPI >= 0) {
+    epilogue_tile<REPI, TN, TM>(g, 0, m0, n0, wm, wn, acc);
+    return;
+  }
   // every ring buffer is dead after the last mid-step barrier: the fp32 tile goes to the staging image
 #pragma unroll
   for (int i = 0; i < TN; ++i)
@@ -190,7 +196,7 @@ do {                                                                            
 // weight gradient's dY); BT: B stored k-strided ([K][N]).  Ragged K only with both operands k-strided (rows past K
 // read as zero through the descriptor range); ragged M / N tiles: rows / column groups past them are not stored.
 // g.rowsum (AT only): += the row sums of op(A) (the fused bias gradient), by the compute waves of column block 0.
-template <bool AT, bool BT, int EPI, int BM = 256, int NCW = 4>
+template <bool AT, bool BT, int EPI, int BM = 256, int NCW = 4, bool REG = false>
 ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned char* lds,
                       const AdamFused* ad = nullptr) {
   using C = WsCfg<BM>;
@@ -344,7 +350,36 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
       }
     }
   } else {
-    ws_compute<AT, BT, BM, NCW>(g, m0, nk, wm, wn, lds);
+    ws_compute<AT, BT, BM, NCW, REG ? EPI : -1>(g, m0, n0, nk, wm, wn, lds);
+  }
+  if constexpr (REG) {
+    static_assert((EPI & (E_F32 | E_ADAM)) == 0 && NCW == 4, "ws: register epilogue for bf16 C");
+    return;   // (the compute waves stored their wave tiles; the loader waves are done)
+  }
+  // E_ADAM: the optimizer operands of the thread's first row group are loaded before the epilogue barrier (their HBM
+  // latency under the other role's tail), every later group's while the previous group computes (adam_rows below)
+  constexpr int AG = 4;   // rows per Adam group
+  constexpr int NAG = (EPI & E_ADAM) != 0 ? NR / AG : 1;
+  f4_t apa[2][AG], ama[2][AG], ava[2][AG];
+  auto adam_off = [&](int i, bool& ok) {   // element offset of the thread's row i from the gradient base
+    const int m = m0 + rb + RS * i;
+    ok = m < g.M && n0 + cq < g.N;
+    return ((float*)g.c + (int64_t)(ok ? m : m0) * g.ldc + n0 + (ok ? cq : 0)) - ad->g0;
+  };
+  auto adam_load = [&](int grp, int b) {
+#pragma unroll
+    for (int u = 0; u < AG; ++u) {
+      bool ok;
+      const int64_t off = adam_off(grp * AG + u, ok);
+      apa[b][u] = *(const f4_t*)(ad->p + off);
+      ama[b][u] = *(const f4_t*)(ad->m + off);
+      ava[b][u] = *(const f4_t*)(ad->v + off);
+    }
+  };
+  // (ASRX_GEMM_DBG & 256: no look-ahead — each group's loads issued at its start, the first cut's schedule; A/B)
+  const bool apf = !(g.dbg & 256);
+  if constexpr ((EPI & E_ADAM) != 0) {
+    if (apf && !(g.dbg & 1) && !(NCW == 8 && tid >= 512)) adam_load(0, 0);
   }
   __syncthreads();
   if (g.dbg & 1) return;
@@ -373,49 +408,41 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
   if (!loader || NCW == 8) load_resid();
   if constexpr ((EPI & E_ADAM) != 0) {
     // E_ADAM (the grouped weight gradients of a single-GPU step, asrx_gemm_grouped_xcd_adam): each thread's rows in
-    // groups of 4 — the dW values stored, then the AdamW update of the same elements (parameter, moments, bf16
-    // shadow at the gradient's offsets), the 12 operand loads of a group issued before its arithmetic
+    // groups of AG — the dW values stored, then the AdamW update of the same elements (parameter, moments, bf16
+    // shadow at the gradient's offsets); group grp + 1's 3·AG operand loads are in flight during group grp
     static_assert((EPI & (E_BETA | E_BIAS | E_RESID | E_ROWADD | E_DROP | E_RELU)) == 0 && F32, "ws: E_ADAM is plain dW");
     float alr, abc1, arbc2;
     adam_hyp(*ad, alr, abc1, arbc2);
-    const bool ncol = n0 + cq < g.N;
 #pragma unroll
-    for (int i0 = 0; i0 < NR; i0 += 4) {
-      f4_t dv[4], pa[4], ma[4], va[4];
-      float* cp[4];
-      bool ok[4];
+    for (int grp = 0; grp < NAG; ++grp) {
+      const int b = grp & 1;
+      if (!apf) adam_load(grp, b);
+      else if (grp + 1 < NAG) adam_load(grp + 1, b ^ 1);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int r = rb + RS * (i0 + u), m = m0 + r;
-        dv[u] = *(const f4_t*)(stg + r * C::SP + cq);
-        ok[u] = m < g.M && ncol;
-        cp[u] = (float*)g.c + (int64_t)(ok[u] ? m : m0) * g.ldc + n0 + (ok[u] ? cq : 0);
-        const int64_t off = cp[u] - ad->g0;
-        pa[u] = *(const f4_t*)(ad->p + off);
-        ma[u] = *(const f4_t*)(ad->m + off);
-        va[u] = *(const f4_t*)(ad->v + off);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (!ok[u]) continue;
-        *(f4_t*)cp[u] = dv[u];
+      for (int u = 0; u < AG; ++u) {
+        const int i = grp * AG + u;
+        bool ok;
+        const int64_t off = adam_off(i, ok);
+        if (!ok) continue;
+        const f4_t dv = *(const f4_t*)(stg + (rb + RS * i) * C::SP + cq);
+        *(f4_t*)(const_cast<float*>(ad->g0) + off) = dv;   // (= the tile of g.c)
+        f4_t pv = apa[b][u], mv = ama[b][u], vv = ava[b][u];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          float pe = pa[u][k], me = ma[u][k], ve = va[u][k];
-          adam_elem(dv[u][k], pe, me, ve, alr, ad->b1, ad->b2, ad->eps, ad->wd, abc1, arbc2, ad->gs, ad->decoupled);
-          pa[u][k] = pe;
-          ma[u][k] = me;
-          va[u][k] = ve;
+          float pe = pv[k], me = mv[k], ve = vv[k];
+          adam_elem(dv[k], pe, me, ve, alr, ad->b1, ad->b2, ad->eps, ad->wd, abc1, arbc2, ad->gs, ad->decoupled);
+          pv[k] = pe;
+          mv[k] = me;
+          vv[k] = ve;
         }
-        const int64_t off = cp[u] - ad->g0;
-        *(f4_t*)(ad->p + off) = pa[u];
-        *(f4_t*)(ad->m + off) = ma[u];
-        *(f4_t*)(ad->v + off) = va[u];
+        *(f4_t*)(ad->p + off) = pv;
+        *(f4_t*)(ad->m + off) = mv;
+        *(f4_t*)(ad->v + off) = vv;
         if (ad->pb) {
           typedef uint32_t au2_t __attribute__((ext_vector_type(2)));
           au2_t w;
-          w.x = pack2bf(pa[u][0], pa[u][1]);
-          w.y = pack2bf(pa[u][2], pa[u][3]);
+          w.x = pack2bf(pv[0], pv[1]);
+          w.y = pack2bf(pv[2], pv[3]);
           *(au2_t*)(ad->pb + off) = w;
         }
       }
@@ -458,7 +485,7 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
   }
 }
 
-template <bool BT, int EPI, int BM, int NCW>
+template <bool BT, int EPI, int BM, int NCW, bool REG = false>
 ASRX_DEV void ws_kernel_body(GemmArgs& g, int ntiles) {
   g.seed = seed_eff(g.seed);
   __shared__ __attribute__((aligned(1024))) unsigned char lds[WsCfg<BM>::LDS];
@@ -466,11 +493,16 @@ ASRX_DEV void ws_kernel_body(GemmArgs& g, int ntiles) {
   const int t = (int)(blockIdx.x % 8) * per8 + (int)(blockIdx.x / 8);
   if (t >= ntiles) return;
   const int ntn = g.N / WS_BN;
-  ws_tile<false, BT, EPI, BM, NCW>(g, (t / ntn) * BM, (t % ntn) * WS_BN, false, lds);
+  ws_tile<false, BT, EPI, BM, NCW, REG>(g, (t / ntn) * BM, (t % ntn) * WS_BN, false, lds);
 }
 template <bool BT, int EPI, int BM>
 __global__ __launch_bounds__(512) void gemm_bf16_ws_kernel(GemmArgs g, int ntiles) {
   ws_kernel_body<BT, EPI, BM, 4>(g, ntiles);
+}
+// (ASRX_WSR) the bf16-output tiles stored from the compute waves' registers (no staging image, no epilogue barrier)
+template <bool BT, int EPI, int BM>
+__global__ __launch_bounds__(512) void gemm_bf16_wsr_kernel(GemmArgs g, int ntiles) {
+  ws_kernel_body<BT, EPI, BM, 4, true>(g, ntiles);
 }
 // (ASRX_WS8) the same tiles with 8 compute waves
 template <bool BT, int EPI, int BM>
@@ -498,7 +530,7 @@ ASRX_DEV void wsg_tile(const GroupEnt* __restrict__ ents, const uint16_t* __rest
   g.batch_inner = 1; g.alpha = 1.f; g.beta = (EPI & E_BETA) ? 1.f : 0.f; g.rowadd_mod = 1;
   g.splitk = 1; g.k_per_split = e.k; g.cvec = 1;
   g.rowsum = e.rowsum;
-  g.dbg = dbg & 9;
+  g.dbg = dbg & (9 | 256);
   const int t = t_all - e.tile_start;
   const int ntn = (e.n + WS_BN - 1) / WS_BN;
   // bias-gradient row sums: one column tile per row panel sums every K-step into rowsum (one workgroup per tile),
@@ -1108,6 +1140,11 @@ int ws8_mode() {
   return m;
 }
 bool ws8_on() { return (ws8_mode() & 1) != 0; }
+// ASRX_WSR=1: bf16-output ws GEMMs through gemm_bf16_wsr_kernel (A/B switch)
+bool wsr_on() {
+  static const bool on = [] { const char* e = getenv("ASRX_WSR"); return e && atoi(e) != 0; }();
+  return on;
+}
 
 template <int NCW>
 int launch_ws_grouped_n(const GroupEnt* ents, const uint16_t* tile_group, const uint16_t* block_tile, int ntiles,
@@ -1197,7 +1234,10 @@ void launch_wse(const GemmArgs& g, bool bt, int epi, int ntiles, hipStream_t st)
 
 void launch_ws(const GemmArgs& g, bool bt, int epi, int ntiles, int bm, hipStream_t st) {
   const dim3 grid(8 * ((ntiles + 7) / 8)), blk(512), blk8(WsWave<256, 8>::NTHR);
-#define ASRX_CASE(E) case (E): if (bm == 64 && (ws8_mode() & 2)) hipLaunchKernelGGL((gemm_bf16_ws8_kernel<BT_, (E), 64>), grid, blk8, 0, st, g, ntiles); \
+#define ASRX_CASE(E) case (E): if (((E) & E_F32) == 0 && wsr_on()) { \
+                                 if (bm == 64) hipLaunchKernelGGL((gemm_bf16_wsr_kernel<BT_, ((E) & E_F32) ? 0 : (E), 64>), grid, blk, 0, st, g, ntiles); \
+                                 else hipLaunchKernelGGL((gemm_bf16_wsr_kernel<BT_, ((E) & E_F32) ? 0 : (E), 256>), grid, blk, 0, st, g, ntiles); \
+                               } else if (bm == 64 && (ws8_mode() & 2)) hipLaunchKernelGGL((gemm_bf16_ws8_kernel<BT_, (E), 64>), grid, blk8, 0, st, g, ntiles); \
                                else if (bm == 64) hipLaunchKernelGGL((gemm_bf16_ws_kernel<BT_, (E), 64>), grid, blk, 0, st, g, ntiles); \
                                else if (ws8_on()) hipLaunchKernelGGL((gemm_bf16_ws8_kernel<BT_, (E), 256>), grid, blk8, 0, st, g, ntiles); \
                                else hipLaunchKernelGGL((gemm_bf16_ws_kernel<BT_, (E), 256>), grid, blk, 0, st, g, ntiles); return;

@@ -284,7 +284,7 @@ def test_gemm_ws_plain(M, N, Kd, bt, wk):
     c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     ref = a.double() @ (b.double() if bt else b.double().t())
     kn = plan_name(M, N, Kd, bt=bt, kernel=wk)
-    assert kn.startswith(("gemm_bf16_ws_kernel", "gemm_bf16_ws8_kernel")) and kn.endswith("64>" if wk == "ws64" else "256>"), kn
+    assert kn.startswith(("gemm_bf16_ws_kernel", "gemm_bf16_ws8_kernel", "gemm_bf16_wsr_kernel")) and kn.endswith("64>" if wk == "ws64" else "256>"), kn
     K().gemm(a.to(dev), b.to(dev), c, M, N, Kd, lda=Kd, ldb=b.shape[1], ldc=N, b_trans=bool(bt), kernel=wk)
     assert relerr(c.float().cpu(), ref) < 1e-2
     auto_ws = N == 512 and (M >= 8192 if wk == "ws" else 2048 <= M < 8192)
@@ -319,7 +319,7 @@ def test_gemm_ws_bias_resid(M, N, Kd, f32, resid, drop, wk):
         K().linear(x.to(dev), w.to(dev), c, bias=bias.to(dev), kernel=wk if kern == "ws" else kern, **kw)
         outs[kern] = c.float().cpu()
     kn = plan_name(M, N, Kd, bias=True, c_f32=bool(f32), resid=bool(resid), dropout=bool(drop), kernel=wk)
-    assert kn.startswith(("gemm_bf16_ws_kernel", "gemm_bf16_ws8_kernel")) and kn.endswith("64>" if wk == "ws64" else "256>"), kn
+    assert kn.startswith(("gemm_bf16_ws_kernel", "gemm_bf16_ws8_kernel", "gemm_bf16_wsr_kernel")) and kn.endswith("64>" if wk == "ws64" else "256>"), kn
     if drop:   # same keep bits in both kernels; the reference is p3's kept pattern
         keep = (outs["p3"] - (r[:, :N] if resid else 0)) != 0
         ref = torch.where(keep, ref / 0.9, torch.zeros_like(ref))
