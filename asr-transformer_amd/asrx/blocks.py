@@ -184,6 +184,8 @@ _SIDE_DROPGEN = os.environ.get("ASRX_DROPGEN_SIDE", "0") == "1"
 # the attention keep bits generated inside the preceding LayerNorm's launch (ASRX_LN_DROPGEN=0: by the attention
 # forward's own launch)
 LN_DROPGEN = os.environ.get("ASRX_LN_DROPGEN", "1") == "1"
+# ... also for the decoder's cross-attention (round 4; ASRX_LN_DROPGEN_CROSS=0: its own keep-bit launch, A/B)
+LN_DROPGEN_CROSS = os.environ.get("ASRX_LN_DROPGEN_CROSS", "1") == "1"
 
 
 def _side_stream(device):
@@ -313,20 +315,27 @@ def attn_bwd(C, S, q, k, v, o, do, dq, dk, dv, gstrides):
 
 # ------------------------------------------------------------------------------------------------ sublayers
 
+def ln_fwd_attn(C, x, ln, prep, B, H, Lq, Lk, dh, on=True):
+    """The sublayer's LayerNorm; where the fused attention will take dropout keep bits, they are generated in the
+    same launch (asrx_layernorm_fwd_attn_dropgen) and handed to the attention through prep."""
+    d = x.shape[1]
+    dm = (K.dropmask_buffer(B, H, Lq, Lk, dh, C.p, x.device)
+          if on and LN_DROPGEN and prep["dropmask"] is None and C.cd == torch.bfloat16 and C.attn_impl == "fused"
+          and d == 512 and x.dtype == torch.float32 else None)
+    if dm is None:
+        return ln_fwd(C, x, ln)
+    h = _empty(x.shape, C.cd, x)
+    mean, rstd = K.layernorm_fwd_dropgen(x, ln.weight.data, ln.bias.data, h, B, H, Lq, Lk, dh, C.p, prep["seed"], dm)
+    prep["dropmask"], prep["ready"] = dm, True
+    return h, mean, rstd
+
+
 def self_attn_fwd(C, x, ln, mha, B, T, H, spec):
     """x + Drop(MHA(LN(x))) with fused per-head projections (layers.py:10-12 -> one N=3d GEMM)."""
     M, d = x.shape
     dh = d // H
     prep = attn_prepare(C, B, H, T, T, dh, x.device)
-    dm = (K.dropmask_buffer(B, H, T, T, dh, C.p, x.device)
-          if LN_DROPGEN and prep["dropmask"] is None and C.cd == torch.bfloat16 and C.attn_impl == "fused"
-          and d == 512 and x.dtype == torch.float32 else None)
-    if dm is not None:   # the LayerNorm and the attention's keep bits in one launch (asrx_layernorm_fwd_attn_dropgen)
-        h = _empty(x.shape, C.cd, x)
-        mean, rstd = K.layernorm_fwd_dropgen(x, ln.weight.data, ln.bias.data, h, B, H, T, T, dh, C.p, prep["seed"], dm)
-        prep["dropmask"], prep["ready"] = dm, True
-    else:
-        h, mean, rstd = ln_fwd(C, x, ln)
+    h, mean, rstd = ln_fwd_attn(C, x, ln, prep, B, H, T, T, dh)
     qkv = _empty((M, 3 * d), C.cd, x)
     K.linear(h, C.W(mha.wqkv), qkv, bias=mha.bqkv.data)
     o = _empty((M, d), C.cd, x)
@@ -364,7 +373,7 @@ def cross_attn_fwd(C, x, ln, mha, kv, kv_ld, B, L, Te, H):
     M, d = x.shape
     dh = d // H
     prep = attn_prepare(C, B, H, L, Te, dh, x.device)
-    h, mean, rstd = ln_fwd(C, x, ln)
+    h, mean, rstd = ln_fwd_attn(C, x, ln, prep, B, H, L, Te, dh, on=LN_DROPGEN_CROSS)
     q = _empty((M, d), C.cd, x)
     K.linear(h, C.W(mha.wq), q, bias=mha.bq.data)
     o = _empty((M, d), C.cd, x)

@@ -200,7 +200,9 @@ ASRX_DEV f4_t epi_vals(const GemmArgs& g, int m, int n, f4_t v, f4_t b4, uint2 p
   }
   if constexpr ((EPI & E_DROP) != 0) {   // n % 4 == 0 and N even: two pair hashes cover the 4 elements
     const uint32_t pb = (uint32_t)((int64_t)m * g.N + n) >> 1;
-    const uint32_t h0 = rng_hash(g.seed, pb), h1 = rng_hash(g.seed, pb + 1);
+    // (ASRX_GEMM_DBG & 512, diagnostics only: the index itself instead of its hash — wrong masks, hash cost A/B)
+    const bool nohash = (g.dbg & 512) != 0;
+    const uint32_t h0 = nohash ? pb * 0x10001u : rng_hash(g.seed, pb), h1 = nohash ? (pb + 1) * 0x10001u : rng_hash(g.seed, pb + 1);
     v[0] = rng_half(h0, 0) >= g.drop_thr ? v[0] * g.drop_scale : 0.f;
     v[1] = rng_half(h0, 1) >= g.drop_thr ? v[1] * g.drop_scale : 0.f;
     v[2] = rng_half(h1, 0) >= g.drop_thr ? v[2] * g.drop_scale : 0.f;

@@ -572,6 +572,14 @@ def main():
                 "pmc_mfma": pm if same else None}
         if not same:
             roof["pmc_note"] = "traffic / pmc_mfma omitted: no committed PMC profile of a launch of this size"
+        cover = getattr(trainer, "_cover", None)
+        if probe.target in K.GROUPED_WSQA_KERNELS and cover:
+            n_opt = sum(k for _, k in cover)
+            roof["fused_optimizer"] = {
+                "op": "AdamW", "params": n_opt, "bytes_per_launch": 26 * n_opt,
+                "note": "the launch also runs the optimizer step of these parameters in its epilogue (fp32 master, "
+                        "both moments, bf16 shadow: 26 B each beyond the GEMM's own dW store); achieved / frac count "
+                        "the GEMM FLOPs only, traffic includes the optimizer bytes"}
     out = {"metric": "encoder+decoder frames/sec/GPU at d_model=512 T=1000; 1->8 GPU scaling",
            "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,

@@ -416,10 +416,12 @@ def test_gemm_ws_rowadd():
     assert (outs["ws"] - outs["p3"]).abs().max() <= 1e-4 * ref.abs().max()
 
 
-@pytest.mark.parametrize("B,H,L,rows_extra", [(64, 8, 249, 0), (64, 8, 64, 0), (3, 2, 37, 0)])
-def test_layernorm_fused_with_keep_bits(B, H, L, rows_extra):
+@pytest.mark.parametrize("B,H,L,Lk", [(64, 8, 249, 249), (64, 8, 64, 64), (64, 8, 64, 249), (3, 2, 37, 37),
+                                      (3, 2, 37, 300)])
+def test_layernorm_fused_with_keep_bits(B, H, L, Lk):
     """asrx_layernorm_fwd_attn_dropgen: the LayerNorm part equals asrx_layernorm_fwd bit for bit and the keep bits
-    (both layouts) equal asrx_attn_dropgen's, for the encoder (249 keys), decoder (64) and a ragged shape."""
+    (both layouts) equal asrx_attn_dropgen's, for the encoder (249 keys), the decoder self (64) and cross (64
+    queries over the 249 encoder frames: rows = B x queries) attention, and ragged shapes."""
     d = 512
     rows = B * L
     g = torch.Generator(device=dev).manual_seed(rows)
@@ -429,10 +431,10 @@ def test_layernorm_fused_with_keep_bits(B, H, L, rows_extra):
     y1 = torch.empty(rows, d, device=dev, dtype=torch.bfloat16)
     y2 = torch.empty_like(y1)
     m1, r1 = K().layernorm_fwd(x, gam, bet, y1)
-    dm1 = K().dropmask_buffer(B, H, L, L, 64, 0.1, dev)
-    dm2 = K().dropmask_buffer(B, H, L, L, 64, 0.1, dev)
-    K().attention_dropgen(B, H, L, L, 64, 0.1, 1234567, dm1)
-    m2, r2 = K().layernorm_fwd_dropgen(x, gam, bet, y2, B, H, L, L, 64, 0.1, 1234567, dm2)
+    dm1 = K().dropmask_buffer(B, H, L, Lk, 64, 0.1, dev)
+    dm2 = K().dropmask_buffer(B, H, L, Lk, 64, 0.1, dev)
+    K().attention_dropgen(B, H, L, Lk, 64, 0.1, 1234567, dm1)
+    m2, r2 = K().layernorm_fwd_dropgen(x, gam, bet, y2, B, H, L, Lk, 64, 0.1, 1234567, dm2)
     torch.cuda.synchronize()
     assert torch.equal(y1, y2) and torch.equal(m1, m2) and torch.equal(r1, r2)
     assert torch.equal(dm1, dm2)
