@@ -280,6 +280,10 @@ ASRX_DEV int epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int
             gwl[i / 2][j] = (m < g.M && na < g.N) ? ((const uint32_t*)g.gate)[(int64_t)m * g.ld_gate + (na >> 5)] : 0u;
           }
       }
+      // row-major store order (round 4): per row block j, both fragment pairs i — the two 64-byte halves of each
+      // row's 128-byte line leave back to back (column-pair-major order wrote every first half of the wave's 128
+      // rows before any second half)
+      f4_t bav[TN / 2], bbv[TN / 2];
 #pragma unroll
       for (int i = 0; i < TN; i += 2) {
         const int na = n0 + wn + 16 * i + 4 * gq, nb = na + 16;
@@ -293,9 +297,16 @@ ASRX_DEV int epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int
             if (nb < g.N) bb = *(const f4_t*)(g.bias + nb);
           }
         }
-        const int ncol = n0 + wn + 16 * (i + (gq & 1)) + 8 * (gq >> 1);
+        bav[i / 2] = ba;
+        bbv[i / 2] = bb;
+      }
 #pragma unroll
-        for (int j = 0; j < TM; ++j) {
+      for (int j = 0; j < TM; ++j) {
+#pragma unroll
+        for (int i = 0; i < TN; i += 2) {
+          const int na = n0 + wn + 16 * i + 4 * gq, nb = na + 16;
+          const f4_t ba = bav[i / 2], bb = bbv[i / 2];
+          const int ncol = n0 + wn + 16 * (i + (gq & 1)) + 8 * (gq >> 1);
           const int m = m0 + wm + 16 * j + (l & 15);
           f4_t va = acc[i][j], vb = acc[i + 1][j];
           if (m < g.M) {
