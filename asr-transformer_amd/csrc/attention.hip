@@ -1716,9 +1716,9 @@ bool resident_ok(const asrx_attn_desc* d, const AttnArgs& a) {
 // Lk > 256, dh = 64, no mask or the structured mask -> the streamed forward / key-block backward
 // (ASRX_ATTN_KERNEL=tiled: the general tiled kernels): 16-B aligned K/V rows for the LDS-DMA, 32-bit byte offsets of every K/V row of the padded last chunk,
 // and the backward's 24-bit query-row products
-bool stream_ok(const asrx_attn_desc* d, const AttnArgs& a) {
+bool stream_ok(const asrx_attn_desc* d, const AttnArgs& a, bool any_lk = false) {
   if (force_tiled()) return false;
-  if (d->dh != 64 || a.Lk <= R_MAXK || a.mode == 2) return false;
+  if (d->dh != 64 || (a.Lk <= R_MAXK && !any_lk) || a.mode == 2) return false;
   constexpr int64_t L24 = 1 << 23, L31 = (int64_t)1 << 31;
   const bool s24 = a.qr < L24 && a.orr < L24 && a.Lq < L24 && (!a.dout || (a.dor < L24 && a.dqr < L24));
   const int64_t qs = std::max({(int64_t)a.qr, (int64_t)a.orr, a.dout ? (int64_t)a.dor : 0, a.dout ? (int64_t)a.dqr : 0});
@@ -1786,7 +1786,12 @@ extern "C" int asrx_attention_fwd(const asrx_attn_desc* d, void* stream) {
   if (rc) return rc;
   if (!a.o || (a.orr % 4) || (a.ob % 4) || ((uintptr_t)a.o % 8)) return ASRX_ERR_UNSUPPORTED;
   hipStream_t st = (hipStream_t)stream;
-  if (resident_ok(d, a) && (!a.thr || a.dropmask)) {
+  // 128 < Lk <= 256 with more than 64 queries (the c3 encoder self-attention) on the streamed forward too: its K/V
+  // arrive in two 128-key chunks, the first computed on while the second lands — in the c3 step 28.7 vs 30.3 us on
+  // the resident kernel, alone 40.4 vs 41.2 (round 4, same box; ASRX_ATTN_STREAM_FWD=0 keeps the resident kernel)
+  static const bool sfwd = [] { const char* e = getenv("ASRX_ATTN_STREAM_FWD"); return !(e && e[0] == '0'); }();
+  const bool take_stream = sfwd && a.Lk > 128 && a.Lk <= R_MAXK && a.Lq > 64 && stream_ok(d, a, true);
+  if (!take_stream && resident_ok(d, a) && (!a.thr || a.dropmask)) {
     // dropout: keep bits (key-major for the backward, query-major for this kernel), generated here unless the
     // caller already did (asrx_attn_dropgen, e.g. on a side stream while the Q/K/V projection runs)
     const uint32_t* qmaj = nullptr;
@@ -1816,7 +1821,7 @@ extern "C" int asrx_attention_fwd(const asrx_attn_desc* d, void* stream) {
     ASRX_CHECK_LAUNCH();
     return ASRX_OK;
   }
-  if (stream_ok(d, a) && (!a.thr || a.dropmask)) {   // Lk > 256: K/V streamed through LDS, training or inference
+  if ((take_stream || stream_ok(d, a)) && (!a.thr || a.dropmask)) {   // Lk > 256: K/V streamed through LDS
     const uint32_t* qmaj = nullptr;
     if (a.thr) {
       if (!d->dropmask_ready) {
