@@ -233,6 +233,16 @@ ASRX_DEV f4_t epi_vals(const GemmArgs& g, int m, int n, f4_t v, f4_t b4, uint2 p
   return v;
 }
 
+// GEMM output stores (C, mask bits, the fused optimizer's state) are non-temporal (round 4): a one-round GEMM's
+// output otherwise sits dirty in L2 until the end-of-kernel write-back.  c3 step 12.13-12.14 -> 12.07-12.08 ms
+// (same box, both orders); ASRX_GEMM_DBG & 1024 restores ordinary stores (A/B)
+typedef uint32_t epi_u2_t __attribute__((ext_vector_type(2)));
+template <typename T>
+ASRX_DEV void epi_store(const GemmArgs& g, T* p, T v) {
+  if (g.dbg & 1024) *p = v;
+  else __builtin_nontemporal_store(v, p);
+}
+
 typedef __attribute__((address_space(3))) const float lds_cfloat_t;
 
 // Returns a lower bound on the vector-memory instructions it issued (the 16-byte stores of a full tile on the
@@ -327,7 +337,7 @@ ASRX_DEV int epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int
           const auto sy = __builtin_amdgcn_permlane16_swap(ay, by, false, false);
           if (m < g.M && ncol < g.N) {
             v4u_t u = {sx[0], sy[0], sx[1], sy[1]};
-            *(v4u_t*)((bf16_t*)g.c + (int64_t)m * g.ldc + ncol) = u;
+            epi_store(g, (v4u_t*)((bf16_t*)g.c + (int64_t)m * g.ldc + ncol), u);
           }
           if constexpr ((EPI & E_MASKOUT) != 0) {
             // ReLU outputs are >= 0, so "> 0" is "low 15 bits nonzero": adding 0x7fff to each 15-bit half sets
@@ -346,7 +356,7 @@ ASRX_DEV int epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int
             wv = x16[0] | x16[1];
             const auto x32 = __builtin_amdgcn_permlane32_swap(wv, wv, false, false);
             wv = x32[0] | x32[1];
-            if (gq == 0 && m < g.M && na < g.N) ((uint32_t*)g.mask_out)[(int64_t)m * g.ld_mask + (na >> 5)] = wv;
+            if (gq == 0 && m < g.M && na < g.N) epi_store(g, (uint32_t*)g.mask_out + (int64_t)m * g.ld_mask + (na >> 5), wv);
           }
         }
       }
@@ -377,7 +387,7 @@ ASRX_DEV int epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int
         uint2 u;
         u.x = pack2bf(v[0], v[1]);
         u.y = pack2bf(v[2], v[3]);
-        *(uint2*)((bf16_t*)g.c + (int64_t)m * g.ldc + n) = u;
+        epi_store(g, (epi_u2_t*)((bf16_t*)g.c + (int64_t)m * g.ldc + n), epi_u2_t{u.x, u.y});
       }
     }
   }

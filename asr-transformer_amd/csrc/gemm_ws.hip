@@ -399,7 +399,7 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
         if (m < g.M && ncol) {
           float* c = (float*)g.c + (int64_t)m * g.ldc + n0 + cl;
           if constexpr ((EPI & E_BETA) != 0) v += *(const f4_t*)c;
-          *(f4_t*)c = v;
+          epi_store(g, (f4_t*)c, v);
         }
       }
       return;
@@ -425,7 +425,7 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
         const int64_t off = adam_off(i, ok);
         if (!ok) continue;
         const f4_t dv = *(const f4_t*)(stg + (rb + RS * i) * C::SP + cq);
-        *(f4_t*)(const_cast<float*>(ad->g0) + off) = dv;   // (= the tile of g.c)
+        epi_store(g, (f4_t*)(const_cast<float*>(ad->g0) + off), dv);   // (= the tile of g.c)
         f4_t pv = apa[b][u], mv = ama[b][u], vv = ava[b][u];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -435,15 +435,15 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
           mv[k] = me;
           vv[k] = ve;
         }
-        *(f4_t*)(ad->p + off) = pv;
-        *(f4_t*)(ad->m + off) = mv;
-        *(f4_t*)(ad->v + off) = vv;
+        epi_store(g, (f4_t*)(ad->p + off), pv);
+        epi_store(g, (f4_t*)(ad->m + off), mv);
+        epi_store(g, (f4_t*)(ad->v + off), vv);
         if (ad->pb) {
           typedef uint32_t au2_t __attribute__((ext_vector_type(2)));
           au2_t w;
           w.x = pack2bf(pv[0], pv[1]);
           w.y = pack2bf(pv[2], pv[3]);
-          *(au2_t*)(ad->pb + off) = w;
+          epi_store(g, (au2_t*)(ad->pb + off), w);
         }
       }
     }
@@ -461,7 +461,7 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
       if (m < g.M && ncol) {
         float* c = (float*)g.c + (int64_t)m * g.ldc + n0 + cq;
         if constexpr ((EPI & E_BETA) != 0) v += *(const f4_t*)c;
-        *(f4_t*)c = v;
+        epi_store(g, (f4_t*)c, v);
       }
     }
   } else {
@@ -479,7 +479,7 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
         va = epi_vals<EPI>(g, m, n0 + cq, va, ba);
         vb = epi_vals<EPI>(g, m, n0 + cq + 4, vb, bb);
         v4u_t u = {pack2bf(va[0], va[1]), pack2bf(va[2], va[3]), pack2bf(vb[0], vb[1]), pack2bf(vb[2], vb[3])};
-        *(v4u_t*)((bf16_t*)g.c + (int64_t)m * g.ldc + n0 + cq) = u;
+        epi_store(g, (v4u_t*)((bf16_t*)g.c + (int64_t)m * g.ldc + n0 + cq), u);
       }
     }
   }
@@ -530,7 +530,7 @@ ASRX_DEV void wsg_tile(const GroupEnt* __restrict__ ents, const uint16_t* __rest
   g.batch_inner = 1; g.alpha = 1.f; g.beta = (EPI & E_BETA) ? 1.f : 0.f; g.rowadd_mod = 1;
   g.splitk = 1; g.k_per_split = e.k; g.cvec = 1;
   g.rowsum = e.rowsum;
-  g.dbg = dbg & (9 | 256);
+  g.dbg = dbg & (9 | 256 | 1024);
   const int t = t_all - e.tile_start;
   const int ntn = (e.n + WS_BN - 1) / WS_BN;
   // bias-gradient row sums: one column tile per row panel sums every K-step into rowsum (one workgroup per tile),
