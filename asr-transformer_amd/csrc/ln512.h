@@ -20,14 +20,16 @@ ASRX_DEV void ld8b(const bf16_t* p, float* v) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) { v[2 * i] = __uint_as_float(w[i] << 16); v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u); }
 }
+// (stores non-temporal, round 4: the outputs stream past L2 instead of sitting dirty there until the end-of-kernel
+//  write-back, as the GEMM epilogues' do)
+typedef uint32_t ln_u4_t __attribute__((ext_vector_type(4)));
 ASRX_DEV void st8b(bf16_t* p, const float* v) {
-  uint4 u;
-  u.x = pack2bf(v[0], v[1]); u.y = pack2bf(v[2], v[3]); u.z = pack2bf(v[4], v[5]); u.w = pack2bf(v[6], v[7]);
-  *(uint4*)p = u;
+  const ln_u4_t u = {pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7])};
+  __builtin_nontemporal_store(u, (ln_u4_t*)p);
 }
 ASRX_DEV void st8f(float* p, const float* v) {
-  *(f4_t*)p = f4_t{v[0], v[1], v[2], v[3]};
-  *(f4_t*)(p + 4) = f4_t{v[4], v[5], v[6], v[7]};
+  __builtin_nontemporal_store(f4_t{v[0], v[1], v[2], v[3]}, (f4_t*)p);
+  __builtin_nontemporal_store(f4_t{v[4], v[5], v[6], v[7]}, (f4_t*)(p + 4));
 }
 
 // The rows of wave gw of nw (rows gw, gw + nw, ...); a kernel body (ln_fwd512_kernel) or one block type of a
