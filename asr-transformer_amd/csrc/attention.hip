@@ -1789,8 +1789,11 @@ extern "C" int asrx_attention_fwd(const asrx_attn_desc* d, void* stream) {
   // 128 < Lk <= 256 with more than 64 queries (the c3 encoder self-attention) on the streamed forward too: its K/V
   // arrive in two 128-key chunks, the first computed on while the second lands — in the c3 step 28.7 vs 30.3 us on
   // the resident kernel, alone 40.4 vs 41.2 (round 4, same box; ASRX_ATTN_STREAM_FWD=0 keeps the resident kernel)
+  // (ASRX_ATTN_KERNEL=resident, read per call like =tiled: the resident kernel, for tests of both paths)
   static const bool sfwd = [] { const char* e = getenv("ASRX_ATTN_STREAM_FWD"); return !(e && e[0] == '0'); }();
-  const bool take_stream = sfwd && a.Lk > 128 && a.Lk <= R_MAXK && a.Lq > 64 && stream_ok(d, a, true);
+  const char* ak = getenv("ASRX_ATTN_KERNEL");
+  const bool take_stream = sfwd && !(ak && !strcmp(ak, "resident")) && a.Lk > 128 && a.Lk <= R_MAXK && a.Lq > 64 &&
+                           stream_ok(d, a, true);
   if (!take_stream && resident_ok(d, a) && (!a.thr || a.dropmask)) {
     // dropout: keep bits (key-major for the backward, query-major for this kernel), generated here unless the
     // caller already did (asrx_attn_dropgen, e.g. on a side stream while the Q/K/V projection runs)

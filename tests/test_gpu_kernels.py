@@ -576,7 +576,7 @@ def attn_variant(request):
         os.environ["ASRX_ATTN_KERNEL"] = old
 
 
-@pytest.mark.parametrize("attn_variant", ["auto", "tiled"], indirect=True)
+@pytest.mark.parametrize("attn_variant", ["auto", "tiled", "resident"], indirect=True)
 @pytest.mark.parametrize("dh", [32, 64])
 @pytest.mark.parametrize("B,H,Lq,Lk,kind", [(2, 4, 70, 70, "decoder"), (3, 2, 64, 249, "none"),
                                            (2, 2, 249, 249, "none"), (1, 2, 100, 300, "none"),
