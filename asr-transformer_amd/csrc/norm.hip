@@ -262,10 +262,11 @@ __global__ __launch_bounds__(256) void ln_bwd512_kernel(const float* __restrict_
 }
 
 // LN variant selection (asrx_set_tuning ASRX_TUNE_LN_PF / ASRX_LN_PF: rows in flight per wave of the d = 512
-// kernels, 8 (ASRX_LN_PF=0) = the general CH x NJ kernels; ASRX_TUNE_LN_BPC / ASRX_LN_BPC: blocks of 4 waves per
+// kernels, default 2 (round 4, c3 step: ln_fwd512 7.49 -> 7.13 us, ln_dropgen 11.27 -> 11.08, ln_bwd512 equal
+// against 1), 8 (ASRX_LN_PF=0) = the general CH x NJ kernels; ASRX_TUNE_LN_BPC / ASRX_LN_BPC: blocks of 4 waves per
 // CU of the forward)
 int ln_pf() {
-  static const int env = [] { const char* e = getenv("ASRX_LN_PF"); return e ? atoi(e) : 1; }();
+  static const int env = [] { const char* e = getenv("ASRX_LN_PF"); return e ? atoi(e) : 2; }();
   return g_tune_ln_pf == 8 ? 0 : g_tune_ln_pf > 0 ? g_tune_ln_pf : env;
 }
 int ln_bpc() {
