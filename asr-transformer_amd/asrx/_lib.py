@@ -167,6 +167,8 @@ def lib():
         # size helper (host arithmetic, int64 result)
         L.asrx_attn_dropmask_words.argtypes = [c_i32, c_i32, c_i32, c_i32]
         L.asrx_attn_dropmask_words.restype = c_i64
+        L.asrx_attn_dq_acc_elems.argtypes = [c_i32, c_i32, c_i32, c_i32, c_i32]
+        L.asrx_attn_dq_acc_elems.restype = c_i64
         _lib = L
     return _lib
 

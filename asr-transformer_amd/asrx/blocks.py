@@ -82,6 +82,7 @@ class Ctx:
         self.fresh = None               # FreshGrads of a Trainer step (unzeroed weight-gradient regions)
         self.adam = None                # AdamDesc -> the optimizer step fused into the grouped weight gradients
         self.adam_cover = []            # (offset, numel) of the flat-gradient ranges whose AdamW ran fused
+        self._gwritten = set()          # data_ptr of every dW / db this step has written so far (fused-AdamW guard)
 
     def W(self, p):
         return self.store.w16(p) if self.cd == torch.bfloat16 else self.store.w32(p)
@@ -105,20 +106,48 @@ class Ctx:
             self.wq.append((dy, x, gw, gb))
         else:
             first = self.fresh is not None and self.fresh.take(gw)
+            self._note_writes(gw, gb)
             K.linear_wgrad(dy, x, gw, bias_grad=gb, beta=0.0 if first else 1.0)
+
+    def _note_writes(self, *ts):
+        cov = {o for o, _ in self.adam_cover}
+        base = self.store.grad.data_ptr()
+        for t in ts:
+            if t is not None:
+                # a gradient whose AdamW already ran fused must never be written again in the step
+                assert (t.data_ptr() - base) // 4 not in cov, "asrx: write to a gradient after its fused AdamW"
+                self._gwritten.add(t.data_ptr())
+
+    def _adam_safe(self, q0):
+        """Fused AdamW is correct only if the grouped launch is the sole and final writer of every dW / db it covers:
+        each target appears once in q0 and nothing wrote it before in this step (a second bias contributor, e.g. a
+        colsum in a data-gradient epilogue, or an earlier flush).  FreshGrads.take already claimed every dW of q0."""
+        seen = set()
+        for _, _, gw, gb in q0:
+            for t in (gw, gb):
+                if t is None:
+                    continue
+                if t.data_ptr() in seen or t.data_ptr() in self._gwritten:
+                    return False
+                seen.add(t.data_ptr())
+        return True
 
     def _issue_wgrads(self, q):
         """One grouped launch for the queued weight gradients; with fresh (unzeroed) targets the first writes go
         in a beta = 0 launch ahead of the accumulating one."""
         if self.fresh is None:
+            for _, _, gw, gb in q:
+                self._note_writes(gw, gb)
             K.linear_wgrad_grouped(q)
             return
         q0, q1 = [], []
         for it in q:
             (q0 if self.fresh.take(it[2]) else q1).append(it)
         # fused AdamW only where every written gradient is final in this launch: first writers (beta 0), no second
-        # writer in the step (the Trainer enables it for a single end-of-backward flush only)
-        adam = self.adam if not q1 else None
+        # writer in the step (the Trainer enables it for a single end-of-backward flush only; _adam_safe checks it)
+        adam = self.adam if not q1 and self._adam_safe(q0) else None
+        for _, _, gw, gb in q0 + q1:
+            self._note_writes(gw, gb)
         kname = K.linear_wgrad_grouped(q0, beta=0.0, adam=adam)
         if adam is not None and kname in K.GROUPED_WSQA_KERNELS:
             base = self.store.grad.data_ptr()

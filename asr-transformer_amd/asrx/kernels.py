@@ -628,8 +628,12 @@ def attention_bwd(q, k, v, o, lse, do, dq, dk, dv, B, H, Lq, Lk, dh, strides, gs
     delta = torch.empty(B * H * Lq, device=q.device, dtype=torch.float32)
     d.delta = delta.data_ptr()
     acc = None
-    if Lk > 128:   # fp32 dQ partials, one per key block of the kernel (asrx.h dq_acc)
-        acc = torch.empty((Lk + 127) // 128 * B * Lq * H * dh, device=q.device, dtype=torch.float32)
+    from ._lib import lib
+    nacc = lib().asrx_attn_dq_acc_elems(B, H, Lq, Lk, dh)   # fp32 dQ partials, one per key block (asrx.h dq_acc)
+    if nacc < 0:
+        raise RuntimeError(f"asrx.attention_bwd: bad shapes {(B, H, Lq, Lk, dh)}")
+    if nacc > 0:
+        acc = torch.empty(nacc, device=q.device, dtype=torch.float32)
         d.dq_acc = acc.data_ptr()
     call("asrx_attention_bwd", ctypes.byref(d), stream())
 

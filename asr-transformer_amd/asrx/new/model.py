@@ -107,9 +107,12 @@ class Encoder(nn.Module):
         self.layers = nn.ModuleList([EncoderLayer(emb_dim, num_heads, ff_dim, dropout) for _ in range(num_layers)])
 
     def forward(self, x, lens, cfg=None):
-        cfg = cfg or _cfg(self, self.dropout)
         B, C, Fm, T = x.shape
         d = self.emb_dim
+        if T > self.pe.pe.shape[1]:
+            # the reference's `x + self.pe[:, :T]` fails to broadcast there (new/layers.py:79-80)
+            raise ValueError(f"asrx.new.Encoder: {T} frames exceed the positional table's {self.pe.pe.shape[1]}")
+        cfg = cfg or _cfg(self, self.dropout)
         xt = torch.empty(B, T, C * Fm, dtype=torch.float32, device=x.device)
         K.transpose_last2(x.reshape(B, C * Fm, T).float().contiguous(), xt)
         valid = torch.arange(T, device=x.device).unsqueeze(0) < lens.to(x.device).reshape(-1, 1)   # mask glue
@@ -162,9 +165,16 @@ class Decoder(nn.Module):
         self.layers = nn.ModuleList([DecoderLayer(emb_dim, num_heads, ff_dim, dropout) for _ in range(num_layers)])
         self.classifier = _Lin(emb_dim, vocab_size, bias=False)
 
+    def _check_len(self, L):
+        if L > self.pe.pe.shape[1]:
+            # embed_fwd reads pe[t] for every t < L: past the table is past its allocation (the reference's broadcast
+            # of pe[:, :L] raises, new/layers.py:79-80)
+            raise ValueError(f"asrx.new.Decoder: {L} tokens exceed the positional table's {self.pe.pe.shape[1]}")
+
     def _run(self, x, enc_x, self_spec, enc_spec, rows, cfg):
         B, L = x.shape
         d = self.emb_dim
+        self._check_len(L)
         h = O.EmbedFn.apply(self.emb.weight, x, self.pe.pe[0, :L].contiguous(), L, self.padding_idx, cfg)
         h = h.view(B, L, d)
         enc_x = enc_x.float()
@@ -173,8 +183,9 @@ class Decoder(nn.Module):
         return O.LinearFn.apply(h.reshape(B * L, d), self.classifier.weight, None, cfg).view(B, L, self.vocab_size)
 
     def forward(self, x, enc_x, enc_lens, cfg=None):
-        cfg = cfg or _cfg(self, self.p)
         B, L = x.shape
+        self._check_len(L)
+        cfg = cfg or _cfg(self, self.p)
         dev = enc_x.device
         x = x.to(dev)
         valid = x.ne(self.eos_token)                                                           # mask glue

@@ -124,21 +124,38 @@ class _Segments:
 
 def residual_pieces(n, cover, piece=None):
     """The [start, end) ranges of a flat buffer of n elements NOT covered by the (offset, numel) ranges `cover`, cut
-    into pieces of at most `piece` elements (default ADAM_SPAN), bounds on multiples of 4 (every parameter starts
-    64-aligned, so a cover range never shares a quad with an uncovered one)."""
+    into pieces of at most `piece` elements (default ADAM_SPAN).  Every parameter starts 64-aligned, so with whole
+    parameters as cover the bounds are multiples of 4; others are kept exact (never rounded into a covered quad)."""
     piece = piece or ADAM_SPAN
-    spans, pos = [], 0
-    for o, k in sorted(cover):
-        if o > pos:
-            spans.append((pos, o))
-        pos = max(pos, o + k)
-    if pos < n:
-        spans.append((pos, n))
     out = []
-    for a, b in spans:
-        a4, b4 = a // 4 * 4, -(-b // 4) * 4
-        for c in range(a4, b4, piece):
-            out.append((c, min(b4, c + piece)))
+    for a, b in _minus(0, n, sorted(cover)):
+        # exact bounds (asrx_adam_spans steps unaligned heads / tails one element at a time), inner cuts on quads
+        cuts = [a] + list(range(a // 4 * 4 + piece, b, piece)) + [b]
+        out += [(c0, c1) for c0, c1 in zip(cuts[:-1], cuts[1:]) if c1 > c0]
+    return out
+
+
+def _minus(a, b, holes):
+    """[a, b) without the (offset, numel) ranges `holes` (sorted): the remaining non-empty runs, in order."""
+    out, pos = [], a
+    for o, k in holes:
+        if o + k <= pos or o >= b:
+            continue
+        if o > pos:
+            out.append((pos, o))
+        pos = max(pos, o + k)
+    if pos < b:
+        out.append((pos, b))
+    return out
+
+
+def unused_params(model):
+    """Parameters the reference's forward never uses, so they never get a gradient there (their .grad stays None and
+    torch's optimizers skip them): input_encoding (model.py:173) and Encoder._norm_in (model.py:12)."""
+    out = []
+    for m in (getattr(model, "input_encoding", None), getattr(getattr(model, "encoder", None), "_norm_in", None)):
+        if m is not None:
+            out += list(m.parameters())
     return out
 
 
@@ -291,6 +308,11 @@ class Trainer:
         self._cover = None       # flat-gradient ranges whose AdamW the last backward ran fused (None: none)
         self._rspans = {}        # residual-range tables by cover
         self._fuse_next = False  # the next forward_backward fuses AdamW (set by step(), which owns the optimizer)
+        # parameters the reference never gives a gradient (input_encoding, model.py:173; Encoder._norm_in, model.py:12):
+        # torch's AdamW skips a parameter whose grad is None, so every AdamW launch here leaves their ranges alone
+        # (a zero-gradient step would still apply weight decay to them)
+        self._frozen = sorted((self.store.offset(p), p.numel()) for p in unused_params(model)
+                              if self.store.owns(p))
         if self._wonly:   # the spans of everything else, zeroed each step by one asrx_zero_spans launch
             n, spans, pos = self.store.grad.numel(), [], 0
             for o, k in sorted((self.store.offset(p), p.numel()) for p in self._wonly):
@@ -314,7 +336,7 @@ class Trainer:
         key = tuple(sorted(cover))
         tab = self._rspans.get(key)
         if tab is None:
-            pieces = residual_pieces(self.store.flat.numel(), key)
+            pieces = residual_pieces(self.store.flat.numel(), sorted(key + tuple(self._frozen)))
             tab = torch.tensor(pieces, dtype=torch.int64).reshape(-1, 2).to(self.store.flat.device)
             self._rspans[key] = tab
         return tab
@@ -368,11 +390,12 @@ class Trainer:
                          self.lr, self.betas[0], self.betas[1], self.eps, self.wd, max(1, self.step_count),
                          grad_scale=1.0 / self.reducer.world, decoupled=self.decoupled, hyp=hyp)
             return
-        a, b = span if span is not None else (0, self.store.flat.numel())
-        sh = self.store.shadow[a:b] if self.store.shadow is not None else None
-        K.adam(self.store.flat[a:b], self.store.grad[a:b], self.m[a:b], self.v[a:b], sh, self.lr, self.betas[0],
-               self.betas[1], self.eps, self.wd, max(1, self.step_count), grad_scale=1.0 / self.reducer.world,
-               decoupled=self.decoupled, hyp=hyp)
+        a0, b0 = span if span is not None else (0, self.store.flat.numel())
+        for a, b in _minus(a0, b0, self._frozen):
+            sh = self.store.shadow[a:b] if self.store.shadow is not None else None
+            K.adam(self.store.flat[a:b], self.store.grad[a:b], self.m[a:b], self.v[a:b], sh, self.lr, self.betas[0],
+                   self.betas[1], self.eps, self.wd, max(1, self.step_count), grad_scale=1.0 / self.reducer.world,
+                   decoupled=self.decoupled, hyp=hyp)
 
     def _reduce_and_adam(self, hyp=None):
         """finish() the gradient exchange and run AdamW.  Multi-GPU over RCCL (fp32 wire): the ranges released

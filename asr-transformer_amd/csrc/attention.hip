@@ -1743,6 +1743,12 @@ extern "C" int64_t asrx_attn_dropmask_words(int32_t batch, int32_t heads, int32_
   return (int64_t)batch * heads * ((int64_t)((lq + 31) / 32) * lk + (int64_t)lq * qmaj_stride(lk));
 }
 
+extern "C" int64_t asrx_attn_dq_acc_elems(int32_t batch, int32_t heads, int32_t lq, int32_t lk, int32_t dh) {
+  if (batch <= 0 || heads <= 0 || lq <= 0 || lk <= 0 || (dh != 32 && dh != 64)) return -1;
+  if (lk <= 128) return 0;
+  return (int64_t)((lk + 127) / 128) * batch * lq * heads * dh;
+}
+
 extern "C" int asrx_attn_dropgen(const asrx_attn_desc* d, void* stream) {
   AttnArgs a;
   int rc = fill_args(d, a);

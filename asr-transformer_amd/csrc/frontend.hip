@@ -957,8 +957,10 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
   }
 }
 
-// AdamW over a table of element ranges of the flat buffers (the parameters a fused weight-gradient launch did not
-// update): block b takes range b; every range is 4-aligned and a multiple of 4 long (host-checked).
+// AdamW over a table of element ranges [a, e) of the flat buffers (the parameters a fused weight-gradient launch did
+// not update): block b takes range b.  The 16-B body covers [roundup4(a), rounddown4(e)); a bound that is not a
+// multiple of 4 (the table the trainer builds has none) gets its head / tail elements stepped one at a time, so no
+// element is skipped or stepped twice whatever the table holds.
 __global__ __launch_bounds__(256) void adam_spans_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                          float* __restrict__ m, float* __restrict__ v,
                                                          bf16_t* __restrict__ pb, const int64_t* __restrict__ spans,
@@ -970,11 +972,23 @@ __global__ __launch_bounds__(256) void adam_spans_kernel(float* __restrict__ p, 
     bc1 = hyp[1];
     rbc2 = 1.f / sqrtf(hyp[2]);
   }
-  const int64_t a = spans[2 * blockIdx.x] / 4, e = spans[2 * blockIdx.x + 1] / 4;
+  const int64_t a0 = spans[2 * blockIdx.x], e0 = spans[2 * blockIdx.x + 1];
+  const int64_t a = (a0 + 3) / 4, e = e0 / 4;
   for (int64_t i = a + threadIdx.x; i < e; i += 256) {
     f4_t pp = ((const f4_t*)p)[i], mm = ((const f4_t*)m)[i], vv = ((const f4_t*)v)[i];
     adam_f4(pp, ((const f4_t*)g)[i], mm, vv, lr, b1, b2, eps, wd, bc1, rbc2, gs, decoupled);
     adam_store(p, m, v, pb, i, pp, mm, vv);
+  }
+  // unaligned head [a0, 4a) and tail [4e, e0) (at most 3 elements each; a span inside one 4-group: [a0, e0))
+  const int64_t hb = min(4 * a, e0), tb = max(4 * e, hb);
+  const int64_t j = threadIdx.x < 3 ? a0 + threadIdx.x : tb + (threadIdx.x - 3);
+  if ((threadIdx.x < 3 && j < hb) || (threadIdx.x >= 3 && threadIdx.x < 6 && j >= tb && j < e0)) {
+    float pe = p[j], me = m[j], ve = v[j];
+    adam_elem(g[j], pe, me, ve, lr, b1, b2, eps, wd, bc1, rbc2, gs, decoupled);
+    p[j] = pe;
+    m[j] = me;
+    v[j] = ve;
+    if (pb) pb[j] = f2bf(pe);
   }
 }
 
@@ -1012,7 +1026,7 @@ inline unsigned grid_for(int64_t work, int cap = 8192) {
 
 ASRX_SEED_OFFSET_SETTER(frontend)
 
-extern "C" int asrx_version(void) { return 2; }
+extern "C" int asrx_version(void) { return 3; }
 
 extern "C" int asrx_struct_sizes(int64_t* out, int32_t n) {
   if (!out || n < 0) return ASRX_ERR_ARG;

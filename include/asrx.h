@@ -31,7 +31,8 @@ extern "C" {
 #define ASRX_F32 1
 #define ASRX_BITS 2   /* gate operand only: 1 bit per element, uint32 words (ld in words; see mask_out) */
 
-/* Library version / build identification. */
+/* Library version / build identification (3: dq_acc holds one slab per key block, asrx_attn_dq_acc_elems;
+ * asrx_adam_spans takes bounds that are not multiples of 4). */
 int asrx_version(void);
 
 /* sizeof of the descriptor structs as this library was compiled (binding check: a ctypes / cgo mirror of a
@@ -190,10 +191,11 @@ typedef struct asrx_attn_desc {
   void* dk; int64_t dk_rstride, dk_bstride;
   void* dv; int64_t dv_rstride, dv_bstride;
   float* delta;                 /* [batch*heads*lq] workspace */
-  float* dq_acc;                /* optional fp32 workspace of ceil(lk/128)*batch*lq*heads*dh floats: dQ partials,
-                                 * one [batch*lq*heads*dh] slab per key block of the kernel (required for lk > 256;
-                                 * used for 128 < lk <= 256 by ASRX_ATTN_XSPLIT; the tiled fallback accumulates into
-                                 * the first slab) */
+  float* dq_acc;                /* optional fp32 workspace of asrx_attn_dq_acc_elems() floats (version >= 3:
+                                 * ceil(lk/128)*batch*lq*heads*dh): dQ partials, one [batch*lq*heads*dh] slab per key
+                                 * block of the kernel (required for lk > 256; version 2 and earlier took ONE slab, a
+                                 * caller sized by that rule overflows it; the tiled fallback accumulates into the
+                                 * first slab) */
   /* optional dropout keep-bit workspace (dh = 64, dropout_p > 0, any lk): key-major words
    * [batch*heads][ceil(lq/32)][lk] (bit i = query 32c+i) followed by query-major words
    * [batch*heads][lq][qmaj_stride(lk)] (bit j = key 32c+j), where qmaj_stride(lk) = ceil(lk/32) for lk <= 256 and
@@ -215,6 +217,9 @@ int asrx_attention_fwd(const asrx_attn_desc* d, void* stream);
 /* Number of 32-bit words of the dropmask workspace for these shapes (see asrx_attn_desc.dropmask); -1 on bad
  * arguments.  Host-only arithmetic, no device access. */
 int64_t asrx_attn_dropmask_words(int32_t batch, int32_t heads, int32_t lq, int32_t lk);
+/* Number of fp32 elements of the dq_acc workspace asrx_attention_bwd needs for these shapes (0: none needed, lk <=
+ * 128; -1 on bad arguments).  Host-only arithmetic.  Size dq_acc from it (the rule changed in version 3). */
+int64_t asrx_attn_dq_acc_elems(int32_t batch, int32_t heads, int32_t lq, int32_t lk, int32_t dh);
 /* Fill d->dropmask with the dropout keep bits of (seed, dropout_p, shapes) — both layouts (see dropmask).  Only
  * the shape/dropout fields of d are read; independent of the Q/K/V data, so it can run ahead on another stream. */
 int asrx_attn_dropgen(const asrx_attn_desc* d, void* stream);
@@ -378,8 +383,9 @@ int asrx_adam(float* p, const float* g, float* m, float* v, void* p_bf16, int64_
               float beta2, float eps, float weight_decay, float bias_corr1, float bias_corr2, float grad_scale,
               int32_t decoupled, const float* hyp, void* stream);
 /* AdamW (as asrx_adam) over the element ranges [spans[2i], spans[2i+1]) of the flat buffers, one workgroup per
- * range (device int64 table, nspans pairs, every bound a multiple of 4): the parameters a fused weight-gradient
- * launch (asrx_gemm_grouped_xcd_adam) did not update. */
+ * range (device int64 table, nspans pairs): the parameters a fused weight-gradient launch
+ * (asrx_gemm_grouped_xcd_adam) did not update.  Bounds that are multiples of 4 take the 16-B path only; since
+ * version 3 any other bound is handled too (head / tail elements one at a time; version 2 skipped them). */
 int asrx_adam_spans(float* p, const float* g, float* m, float* v, void* p_bf16, const int64_t* spans, int32_t nspans,
                     float lr, float beta1, float beta2, float eps, float weight_decay, float bias_corr1,
                     float bias_corr2, float grad_scale, int32_t decoupled, const float* hyp, void* stream);

@@ -20,7 +20,7 @@ def _declared_symbols():
 
 
 # entry points with a non-int result, bound separately in asrx._lib.lib()
-_NON_INT = {"asrx_attn_dropmask_words"}
+_NON_INT = {"asrx_attn_dropmask_words", "asrx_attn_dq_acc_elems"}
 
 
 def test_library_exports_every_declared_symbol():
@@ -49,6 +49,10 @@ def test_dropmask_size_rule(B, H, Lq, Lk):
     assert qmaj_stride(Lk) == stride
     assert lib.asrx_attn_dropmask_words(B, H, Lq, Lk) == B * H * (((Lq + 31) // 32) * Lk + Lq * stride)
     assert lib.asrx_attn_dropmask_words(0, H, Lq, Lk) == -1
+    # dq_acc (version 3): one [B*Lq*H*dh] fp32 slab per 128 keys past 128 keys, none below
+    assert lib.asrx_version() >= 3
+    assert lib.asrx_attn_dq_acc_elems(B, H, Lq, Lk, 64) == (0 if Lk <= 128 else (Lk + 127) // 128 * B * Lq * H * 64)
+    assert lib.asrx_attn_dq_acc_elems(B, H, Lq, Lk, 48) == -1
 
 
 def test_abi_rejects_bad_arguments_without_gpu():
@@ -388,3 +392,15 @@ def test_fused_adam_residual_pieces():
             hits[i] += 1
     assert hits == [1] * n
     assert residual_pieces(128, [(0, 128)]) == []
+
+
+def test_new_over_length_inputs_raise():
+    """asrx.new: frames past the encoder's positional table, or tokens past the decoder's, raise ValueError before
+    any device work (the reference's `x + pe[:, :T]` fails to broadcast there; embed_fwd would read past the table)."""
+    m, c = _build_new("new_micro")
+    T = m.encoder.pe.pe.shape[1] + 1
+    with pytest.raises(ValueError):
+        m.encoder(torch.zeros(1, 1, c.n_mels, T), torch.tensor([T]))
+    L = m.decoder.pe.pe.shape[1] + 1
+    with pytest.raises(ValueError):
+        m.decoder(torch.zeros(1, L, dtype=torch.int64), torch.zeros(1, 4, c.n_mels), torch.tensor([4]))
