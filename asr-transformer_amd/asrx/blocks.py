@@ -149,7 +149,7 @@ class Ctx:
         for _, _, gw, gb in q0 + q1:
             self._note_writes(gw, gb)
         kname = K.linear_wgrad_grouped(q0, beta=0.0, adam=adam)
-        if adam is not None and kname in K.GROUPED_WSQA_KERNELS:
+        if adam is not None and kname in K.GROUPED_FUSED_KERNELS:
             base = self.store.grad.data_ptr()
             for _, _, gw, gb in q0:
                 for t in (gw, gb):

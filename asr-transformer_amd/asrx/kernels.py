@@ -109,8 +109,7 @@ def kernel_name(d):
 PROBE = None
 
 # asrx_gemm_desc.kernel: forced kernel family (0 = auto).  ASRX_GEMM_KERNEL picks a process-wide default (A/B).
-KERNEL_CODES = {"auto": 0, "p3": 1, "reg": 3, "ring": 4, "ring128": 5, "p4": 6, "ws": 8, "wsp": 9, "ws64": 10,
-                "wse": 11}
+KERNEL_CODES = {"auto": 0, "p3": 1, "reg": 3, "ring": 4, "ring128": 5, "p4": 6, "ws": 8, "ws64": 10}
 GEMM_KERNEL = KERNEL_CODES.get(os.environ.get("ASRX_GEMM_KERNEL", "auto"), 0)
 
 
@@ -219,10 +218,17 @@ GROUPED_TABLE_KERNEL = "gemm_bf16_grouped_dev_kernel<true, true>"
 # (beta != 1, beta == 1) instantiations (96 = E_BETA | E_F32: accumulate into the fp32 grads)
 GROUPED_P3_KERNELS = ("gemm_bf16_p3g_kernel<64>", "gemm_bf16_p3g_kernel<96>")
 GROUPED_P4_KERNELS = ("gemm_bf16_p4g_kernel<64>", "gemm_bf16_p4g_kernel<96>")
-_WS8 = "8" if int(os.environ.get("ASRX_WS8", "0") or 0) & 1 else ""   # (read once by the library too)
-GROUPED_WS_KERNELS = (f"gemm_bf16_wsg{_WS8}_kernel<64>", f"gemm_bf16_wsg{_WS8}_kernel<96>")
-GROUPED_WSQ_KERNELS = (f"gemm_bf16_wsgq{_WS8}_kernel<64>", f"gemm_bf16_wsgq{_WS8}_kernel<96>")
+GROUPED_WS_KERNELS = ("gemm_bf16_wsg_kernel<64>", "gemm_bf16_wsg_kernel<96>")
+GROUPED_WSQ_KERNELS = ("gemm_bf16_wsgq_kernel<64>", "gemm_bf16_wsgq_kernel<96>")
 GROUPED_WSQA_KERNELS = ("gemm_bf16_wsgqa_kernel<64>", None)   # AdamW fused (beta 0 only)
+# g4 (gemm_wg.hip, round 5): 256x256 tiles, 4-stage ring of 32-deep stages; <EPI, stages, two row-sum blocks>
+# (2112 = E_ADAM | E_F32: AdamW fused)
+GROUPED_G4_KERNELS = {(False, False): ("gemm_bf16_g4q_kernel<64, 4, false>", "gemm_bf16_g4q_kernel<96, 4, false>"),
+                      (False, True): ("gemm_bf16_g4q_kernel<64, 4, true>", "gemm_bf16_g4q_kernel<96, 4, true>"),
+                      (True, False): ("gemm_bf16_g4q_kernel<2112, 4, false>", None),
+                      (True, True): ("gemm_bf16_g4q_kernel<2112, 4, true>", None)}
+GROUPED_FUSED_KERNELS = {GROUPED_WSQA_KERNELS[0], GROUPED_G4_KERNELS[(True, False)][0],
+                         GROUPED_G4_KERNELS[(True, True)][0]}
 
 
 def wgrad_groupable(dy, x, wgrad):
@@ -243,7 +249,7 @@ WGRAD_KIND = os.environ.get("ASRX_WGRAD_KIND", "ws")
 
 def _grouped_p3_ok(items, beta):
     """Can the LDS-DMA ring kernel take these weight gradients (fp32 C rows 16-byte aligned, beta 0 or 1)?"""
-    return WGRAD_KIND in ("p3", "p4", "ws") and beta in (0.0, 1.0) and all(
+    return WGRAD_KIND in ("p3", "p4", "ws", "g4") and beta in (0.0, 1.0) and all(
         x.shape[1] % 4 == 0 and wgrad.stride(0) % 4 == 0 and wgrad.data_ptr() % 16 == 0
         for (_, x, wgrad, _) in items)
 
@@ -320,7 +326,8 @@ def xcd_plan(shapes, tile=256, nxcd=8, pack=None):
     return plan
 
 
-_TILE_CODE = {"p3": ((256, 128), 3), "p4": ((256, 256), 4), "ws": ((256, 128), 5), "reg": ((128, 128), 128)}
+_TILE_CODE = {"p3": ((256, 128), 3), "p4": ((256, 256), 4), "ws": ((256, 128), 5), "g4": ((256, 256), 6),
+              "reg": ((128, 128), 128)}
 
 
 def upload(dst, host_bytes):
@@ -366,7 +373,14 @@ def _grouped_xcd(items, common, kind="p3", adam=None):
     # ws tiles: 8 per-XCD queue counters (+ 8 spare) and one counter per bias-carrying row panel after the block map,
     # zeroed by this upload, i.e. on every launch / replay; the row panels' [tiles][256] fp32 row-sum slabs beside
     o3 = (o2 + block_tile.nbytes + 63) // 64 * 64
-    queue = code == 5 and WGRAD_QUEUE and len(block_tile) % 8 == 0
+    g4 = code == 6   # (g4: always the queue launch; its row sums need no slabs or panel counters)
+    queue = (code == 5 and WGRAD_QUEUE or g4) and len(block_tile) % 8 == 0
+    if g4 and not queue:
+        raise RuntimeError("asrx: the g4 grouped launch needs a block map of whole 8-XCD rounds")
+    if g4:
+        panels = 0
+        # two row-sum blocks per wave where a bias-carrying group has a single column tile (n <= 256)
+        common.kernel = int(any(it[3] is not None and it[1].shape[1] <= tile[1] for it in items))
     n_all = o3 + 4 * (16 + panels) if queue else (o2 + block_tile.nbytes + 3) // 4 * 4
     host = np.zeros(n_all, dtype=np.uint8)
     host[:o1] = ents.view(np.uint8).reshape(-1)
@@ -378,10 +392,13 @@ def _grouped_xcd(items, common, kind="p3", adam=None):
     part = None
     if queue:
         common.workspace, common.workspace_elems = base + o3, 16 + panels
-        part = torch.empty(start * tile[0], dtype=torch.float32, device=dev.device)
-        common.rowsum_ws = part.data_ptr()
+        if not g4:
+            part = torch.empty(start * tile[0], dtype=torch.float32, device=dev.device)
+            common.rowsum_ws = part.data_ptr()
 
     fused = adam is not None and queue and common.beta == 0.0
+    if fused and g4 and getattr(adam, "nbytes", 2 ** 31) > 2 ** 31 - 16:
+        fused = False   # (g4's fused epilogue addresses the flat state with 32-bit byte offsets)
 
     def launch():
         if fused:   # (the AdamDesc is held by this closure until the call)
@@ -410,7 +427,7 @@ def linear_wgrad_grouped(items, *, beta=1.0, kind=None, adam=None):
     as ONE grouped launch (longest reductions first, tiles of a group on one XCD).  adam (AdamDesc, optional): the
     AdamW step of every written element fused into the launch (asrx_gemm_grouped_xcd_adam) where the launch can take
     it (ws queue launch, beta 0).  Returns the name of the kernel instantiation launched (the one rocprofv3 lists);
-    it is a GROUPED_WSQA_KERNELS name exactly when the optimizer step was fused."""
+    it is in GROUPED_FUSED_KERNELS exactly when the optimizer step was fused."""
     if not items:
         return None
     items = sorted(items, key=lambda it: -it[0].shape[0])
@@ -421,11 +438,12 @@ def linear_wgrad_grouped(items, *, beta=1.0, kind=None, adam=None):
     kind = kind or WGRAD_KIND
     # the table upload is issued first, so a timed bracket holds the grouped GEMM alone
     flops, launch, _, (queued, fused) = _grouped_xcd(items, common, kind if p3 else "reg",
-                                                     adam if p3 and (kind or WGRAD_KIND) == "ws" else None)
+                                                     adam if p3 and kind in ("ws", "g4") else None)
     # the kernel that actually runs: the ws tiles go to the persistent queue kernel only when _grouped_xcd took it
     # (its block map must hold whole 8-XCD rounds), else one workgroup per tile
     wsk = GROUPED_WSQA_KERNELS if fused else GROUPED_WSQ_KERNELS if queued else GROUPED_WS_KERNELS
-    kname = ({"p4": GROUPED_P4_KERNELS, "ws": wsk}.get(kind, GROUPED_P3_KERNELS)[beta == 1.0] if p3
+    g4k = GROUPED_G4_KERNELS[(bool(fused), bool(common.kernel & 1))]
+    kname = ({"p4": GROUPED_P4_KERNELS, "ws": wsk, "g4": g4k}.get(kind, GROUPED_P3_KERNELS)[beta == 1.0] if p3
              else GROUPED_TABLE_KERNEL)
     probe = PROBE
     if probe is not None and probe.active and probe.log is not None:
@@ -860,6 +878,7 @@ def adam_desc(p, m, v, p_bf16, g, lr, beta1, beta2, eps, weight_decay, step, gra
     d.lr, d.beta1, d.beta2, d.eps, d.weight_decay = lr, beta1, beta2, eps, weight_decay
     d.bias_corr1, d.bias_corr2 = 1.0 - beta1 ** step, 1.0 - beta2 ** step
     d.grad_scale, d.decoupled = grad_scale, int(decoupled)
+    d.nbytes = 4 * max(p.numel(), g.numel())   # (extent of the flat state: the g4 fused epilogue's 32-bit offsets)
     return d
 
 

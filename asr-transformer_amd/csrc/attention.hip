@@ -1253,17 +1253,12 @@ void attn_fwd_stream_kernel(AttnArgs a, const uint32_t* qmaj) {
 // the next chunk are prefetched into registers during the current one (double-buffered LDS images).  Masks:
 // key validity / padding is a per-lane score bias, query validity is folded into lse (+inf), causality is a
 // compare only in blocks that reach above the diagonal.
-// OPT (round 4, ASRX_ATTN_BWD_OPT; NKT = 8, one key block): bit 0 — waves 4-7 at issue priority 1 for the whole
-// loop (the arbitration loser of a 512-thread workgroup, MI355X_MICROARCH.md "Two waves per SIMD" item 4);
-// bit 1 — the dQ stores as buffer stores whose out-of-range lanes the descriptor drops (every chunk issues exactly
-// TPW store instructions), so the next chunk's publish waits for its prefetch only (counted vmcnt(TPW)) instead of
-// also for the write acknowledgements of the previous chunk's dQ (vmcnt(0)); bit 2 — stagger: waves 4-7 run each
-// chunk's dV/dK MFMAs one chunk late (at the head of the next chunk, beside the other half's softmax-gradient VALU;
-// their keep-scaled P and dS stay in registers across the barrier, the Q/dO images triple-buffered).
-template <int MODE, int NKT, int OPT = 0>
+// (Round 4 measured issue priority for waves 4-7, counted dQ-store waits and a half-chunk stagger of waves 4-7:
+// all within +-1 %, removed in round 5.)
+template <int MODE, int NKT>
 __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
   a.seed = seed_eff(a.seed);
-  constexpr int NQB = (OPT & 4) ? 3 : 2;                         // Q / dO image buffers
+  constexpr int NQB = 2;                                          // Q / dO image buffers
   // NKT 32-key blocks (= waves); keys past Lk are zero rows with a -inf score bias
   constexpr int NK = NKT * 32, NTHR = NKT * 64;
   constexpr int RDT = 32 + 8;                                     // dS^T image [key][32 queries] row stride
@@ -1373,12 +1368,9 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
     }
     praw = __uint_as_float(ld32_asm(lseb + min(q0 + (tid & 31), a.Lq - 1)));
   };
-  // cstore: (OPT bit 1) the previous chunk's TPW dQ store instructions are the only younger vector-memory operations
-  const bool cstore = (OPT & 2) && nkb == 1 && !a.dbg;
-  auto publish = [&](int buf, int qbuf, int ch, bool after_dq) {
+  auto publish = [&](int buf, int qbuf, int ch) {
     const int q0 = ch * 32;
-    if (cstore && after_dq) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(TPW) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
     for (int i = 0; i < PRE; ++i) {
       pin(pq[i]);
@@ -1426,8 +1418,6 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
   // dQ^T[d][q] = sum_key K^T[d][key] dS^T[key][q] for chunk cc: its 8 (sub-tile, 16-column) tiles, TPW per wave,
   // every operand read before the MFMA chain (compile-time trip counts, no branches)
   bf16_t* const dqh = a.dq + b * a.dqb + h * 64;
-  asrxg::v4i_t dqsrd = {0, 0, 0, 0};
-  if constexpr ((OPT & 2) != 0) dqsrd = asrxg::make_srd(dqh, ((int64_t)(a.Lq - 1) * a.dqr + 64) * 2);
   auto dq_chunk = [&](int cc) {
     const int bq = cc & 1, q0 = cc * 32;
 #pragma unroll
@@ -1459,15 +1449,7 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
         uint2 x;
         x.x = pack2bf(acc[0] * a.scale, acc[1] * a.scale);
         x.y = pack2bf(acc[2] * a.scale, acc[3] * a.scale);
-        if (cstore) {   // every lane issues; rows past Lq take an offset past the descriptor's range (dropped)
-          const uint32_t off = q0 + 16 * qs + li < a.Lq ? (uint32_t)(__mul24(q, (int)a.dqr) + 16 * u + 4 * g) * 2u
-                                                       : 0x80000000u;
-          asrxg::v4i_t d;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) d[e] = __builtin_amdgcn_readfirstlane(dqsrd[e]);
-          asm volatile("buffer_store_dwordx2 %0, %1, %2, 0 offen" ::"v"(__builtin_bit_cast(u2_t, x)), "v"(off), "s"(d)
-                       : "memory");
-        } else if (q0 + 16 * qs + li < a.Lq) {
+        if (q0 + 16 * qs + li < a.Lq) {
           *(uint2*)(dqh + __mul24(q, (int)a.dqr) + 16 * u + 4 * g) = x;
         }
       }
@@ -1476,16 +1458,9 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
 
   ATTN_TS(0);
   fetch(0);
-  publish(0, 0, 0, false);
+  publish(0, 0, 0);
   __syncthreads();
   ATTN_TS(1);
-  // stagger (OPT bit 2): waves 4-7 defer each chunk's dV/dK MFMAs to the head of the next chunk
-  const bool defer = (OPT & 4) && __builtin_amdgcn_readfirstlane(w) >= 4;
-  if constexpr ((OPT & 1) != 0) {
-    if (__builtin_amdgcn_readfirstlane(w) >= 4) __builtin_amdgcn_s_setprio(1);
-  }
-  bool pend = false;   // (defer) the dV/dK of the chunk in Q/dO buffer pqb is pending, its Pd / dS in pdb / dsb
-  int pqb = 0;
   s4_t pdb[2][2], dsb[2][2];
   // dV^T += dO^T Pd ; dK^T += Q^T dS   (k-slots: queries 4g+j of sub-tile 0, then of sub-tile 1)
   auto dvdk = [&](int qbuf) {
@@ -1508,7 +1483,7 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
   // straight-line block (the dQ MFMAs and LDS reads fill the gaps of the softmax-gradient VALU work); one
   // barrier per chunk publishes dS(ch) and the next chunk's Q/dO.
   for (int ch = 0; ch < nch; ++ch) {
-    const int buf = ch & 1, q0 = ch * 32, qb = NQB == 2 ? buf : ch % NQB;
+    const int buf = ch & 1, q0 = ch * 32, qb = buf;
     // 4-bit keep masks of this lane's queries (16qs + 4g + r) for its two keys
     uint32_t nib[2][2];
     if (!a.thr) {
@@ -1536,10 +1511,6 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
     ATTN_TS(2 + 4 * ch);
     const bf16_t* cq = sq + qb * 32 * R_CS;
     const bf16_t* cdo = sdo + qb * 32 * R_CS;
-    if (defer && pend) {
-      dvdk(pqb);
-      pend = false;
-    }
     if (causal && kw0 > q0 + 31) {
       // every key of this wave lies above every query of the chunk: dS = 0 (keeps the dQ sweep branch-free)
 #pragma unroll
@@ -1593,23 +1564,16 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
           *(s4_t*)(sds + (buf * NK + kwl + 16 * t + li) * RDT + 16 * qs + 4 * g) = dsb[qs][t];
         }
       }
-      if (defer) {
-        pend = true;
-        pqb = qb;
-      } else {
-        dvdk(qb);
-      }
+      dvdk(qb);
     }
     ATTN_TS(3 + 4 * ch);
-    if (ch + 1 < nch) publish(buf ^ 1, NQB == 2 ? buf ^ 1 : (ch + 1) % NQB, ch + 1, ch > 0);
+    if (ch + 1 < nch) publish(buf ^ 1, buf ^ 1, ch + 1);
     ATTN_TS(5 + 4 * ch);
     __syncthreads();
     ATTN_TS(4 + 4 * ch);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the unused last prefetch
   dq_chunk(nch - 1);
-  if (defer && pend) dvdk(pqb);
-  if constexpr ((OPT & 1) != 0) __builtin_amdgcn_s_setprio(0);
 
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -1632,13 +1596,9 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
 
 int bwd_res_nkt(int lk) { return lk <= 64 ? 2 : (lk <= 128 ? 4 : 8); }
 
-size_t bwd_res_smem(int nkt, int opt = 0) {
-  const int nk = nkt * 32, nqb = (opt & 4) ? 3 : 2;
+size_t bwd_res_smem(int nkt) {
+  const int nk = nkt * 32, nqb = 2;
   return (size_t)(nk * R_VS + 2 * nqb * 32 * R_CS + 2 * nk * (32 + 8)) * 2 + 128 * 4 + 16 * 16;
-}
-int bwd_res_opt() {   // ASRX_ATTN_BWD_OPT: bits of attn_bwd_res_kernel's OPT (A/B; default 0)
-  static const int o = [] { const char* e = getenv("ASRX_ATTN_BWD_OPT"); return e ? (atoi(e) & 7) : 0; }();
-  return o;
 }
 
 // dq (bf16, strided) = scale * sum of the nparts fp32 partials dq_acc[p] ([nparts][B][Lq][H][DH], added in order)
@@ -1880,34 +1840,18 @@ extern "C" int asrx_attention_bwd(const asrx_attn_desc* d, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const bool longk = stream_ok(d, a) && (!a.thr || a.dropmask);
   if ((resident_ok(d, a) || longk) && a.dqr % 4 == 0 && a.dqb % 4 == 0 && (uintptr_t)a.dq % 8 == 0) {   // forms delta itself
-    // ASRX_ATTN_XSPLIT=1 (A/B): short query blocks over 129..256 keys (the decoder's cross-attention, 64 x 249) as
-    // two 128-key blocks of 4 waves (1024 workgroups, two per CU) with per-block dQ partials, instead of one
-    // 256-key block of 8 waves per head
-    static const bool xsplit_on = [] { const char* e = getenv("ASRX_ATTN_XSPLIT"); return e && e[0] == '1'; }();
-    const bool xsplit = xsplit_on && a.Lq <= 64 && a.Lk > 128 && a.Lk <= R_MAXK && a.dq_acc;
-    const int nkt = xsplit ? 4 : bwd_res_nkt(a.Lk);
+    // (round 4's ASRX_ATTN_XSPLIT — short query blocks as two 128-key blocks of 4 waves — measured 30.8 -> 48.5 us:
+    //  removed in round 5)
+    const int nkt = bwd_res_nkt(a.Lk);
     const int nkb = (a.Lk + 32 * nkt - 1) / (32 * nkt);
-    const int opt = (nkt == 8 && nkb == 1) ? bwd_res_opt() : 0;
-    const size_t sm = bwd_res_smem(nkt, opt);
+    const size_t sm = bwd_res_smem(nkt);
     if (nkb > 1 && !a.dq_acc) return ASRX_ERR_ARG;   // key blocks store their dQ partials into dq_acc[blockIdx.y]
     const dim3 grid(a.B * a.H, nkb), blk(64 * nkt);
 #define ASRX_BWD_RES(M, N) hipLaunchKernelGGL((attn_bwd_res_kernel<M, N>), grid, blk, sm, st, a)
-#define ASRX_BWD_RES8(M)                                                                                           \
-  switch (opt) {                                                                                                   \
-    case 1: hipLaunchKernelGGL((attn_bwd_res_kernel<M, 8, 1>), grid, blk, sm, st, a); break;                       \
-    case 2: hipLaunchKernelGGL((attn_bwd_res_kernel<M, 8, 2>), grid, blk, sm, st, a); break;                       \
-    case 3: hipLaunchKernelGGL((attn_bwd_res_kernel<M, 8, 3>), grid, blk, sm, st, a); break;                       \
-    case 4: hipLaunchKernelGGL((attn_bwd_res_kernel<M, 8, 4>), grid, blk, sm, st, a); break;                       \
-    case 5: hipLaunchKernelGGL((attn_bwd_res_kernel<M, 8, 5>), grid, blk, sm, st, a); break;                       \
-    case 6: hipLaunchKernelGGL((attn_bwd_res_kernel<M, 8, 6>), grid, blk, sm, st, a); break;                       \
-    case 7: hipLaunchKernelGGL((attn_bwd_res_kernel<M, 8, 7>), grid, blk, sm, st, a); break;                       \
-    default: ASRX_BWD_RES(M, 8);                                                                                   \
-  }
-    if (a.mode == 0) { if (nkt == 2) ASRX_BWD_RES(0, 2); else if (nkt == 4) ASRX_BWD_RES(0, 4); else { ASRX_BWD_RES8(0) } }
-    else if (a.mode == 1) { if (nkt == 2) ASRX_BWD_RES(1, 2); else if (nkt == 4) ASRX_BWD_RES(1, 4); else { ASRX_BWD_RES8(1) } }
+    if (a.mode == 0) { if (nkt == 2) ASRX_BWD_RES(0, 2); else if (nkt == 4) ASRX_BWD_RES(0, 4); else ASRX_BWD_RES(0, 8); }
+    else if (a.mode == 1) { if (nkt == 2) ASRX_BWD_RES(1, 2); else if (nkt == 4) ASRX_BWD_RES(1, 4); else ASRX_BWD_RES(1, 8); }
     else { if (nkt == 2) ASRX_BWD_RES(2, 2); else if (nkt == 4) ASRX_BWD_RES(2, 4); else ASRX_BWD_RES(2, 8); }
 #undef ASRX_BWD_RES
-#undef ASRX_BWD_RES8
     ASRX_CHECK_LAUNCH();
     if (nkb > 1) {
       const int64_t total = (int64_t)a.B * a.Lq * a.H * d->dh;

@@ -791,8 +791,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_p3_kernel(GemmArgs g, int ntile
   __shared__ __attribute__((aligned(1024))) unsigned char lds[PGeo<128>::LDS];
   const int G = gridDim.x, b0 = blockIdx.x;
   if (b0 >= ntiles) return;
-  if (g.dbg & 16) p4_body<AT, BT, EPI, 128>(g, TileSeq::persistent(ntiles, xcd, b0, G), blockIdx.y, blockIdx.z, lds);
-  else p3_body<AT, BT, EPI, 128>(g, TileSeq::persistent(ntiles, xcd, b0, G), blockIdx.y, blockIdx.z, lds);
+  p3_body<AT, BT, EPI, 128>(g, TileSeq::persistent(ntiles, xcd, b0, G), blockIdx.y, blockIdx.z, lds);
 }
 
 template <bool AT, bool BT, int EPI>
@@ -825,8 +824,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_p3g_kernel(float alpha, float b
   g.splitk = 1; g.k_per_split = e.k; g.cvec = 1;
   g.rowsum = e.rowsum;
   g.dbg = dbg & 9;
-  if (dbg & 16) p4_body<true, true, EPI, 128>(g, TileSeq::single(tid - e.tile_start), 0, 0, lds);
-  else p3_body<true, true, EPI, 128>(g, TileSeq::single(tid - e.tile_start), 0, 0, lds);
+  p3_body<true, true, EPI, 128>(g, TileSeq::single(tid - e.tile_start), 0, 0, lds);
 }
 template <int EPI>
 __global__ __launch_bounds__(512) void gemm_bf16_p4g_kernel(float alpha, float beta, int c_dtype,
@@ -1441,7 +1439,7 @@ void dispatch_bf16(const GemmArgs& g, bool at, bool bt, bool vec, int batch, hip
 struct GemmPlan {
   int use;     // 1 = p3 (256x128 LDS-DMA ring), 2 = p4 (256x256), 3 = register path 128, 4 = register path 64,
                // 5 = ring 64x64, 6 = ring 128x64 (4-stage LDS-DMA, small grids), 9 = tall-K (conv2 dW),
-               // 11 = ws (warp-specialised 256x128, one-round N = 512 outputs), 12 = wsp (ws roles, persistent tiles)
+               // 11 = ws (warp-specialised 256x128, one-round N = 512 outputs), 13 = ws on 64x128 tiles
   bool vec;    // 16-byte aligned operands
   int epi;     // instantiated epilogue flags (E_GENERIC when the fast-path set has no match)
   int ntiles;  // output tiles of the chosen kernel
@@ -1459,30 +1457,6 @@ bool epi_instantiated(bool at, bool bt, int epi) {
 // ASRX_WS=0 keeps the N = 512 encoder GEMMs on p3 (A/B switch; default on)
 bool ws_auto() {
   static const bool on = [] { const char* e = getenv("ASRX_WS"); return !(e && e[0] == '0'); }();
-  return on;
-}
-// ASRX_WSP=0 keeps the wide projections off the persistent ws kernel (A/B switch; default on)
-// ASRX_WSP: 1 = plan the persistent ws kernel for the wide GEMMs below, 2 = the bias / plain forwards only, 3 = the
-// gated data gradients only, 0 (default) = off.  Each is faster alone (tools/blas_ref.py) and under rocprofv3
-// (12.37 vs 12.47 ms), but the graph-mode bench step measured 12.86-13.05 (1), 12.70-12.74 (2) and 12.98-13.01 (3)
-// against 12.67-12.71 ms (0), alternating on one box: off.
-int wsp_auto_mode() {
-  static const int m = [] { const char* e = getenv("ASRX_WSP"); return e ? atoi(e) : 0; }();
-  return m;
-}
-bool wsp_auto(int epi) {
-  const int m = wsp_auto_mode();
-  return m == 1 || (m == 2 && !(epi & E_GBITS)) || (m == 3 && (epi & E_GBITS));
-}
-int wsp_min_rows() {
-  static const int m = [] { const char* e = getenv("ASRX_WSP_M"); return e ? atoi(e) : 4096; }();
-  return m;
-}
-// ASRX_WSE=1 puts the wide projections on wse (A/B switch; default off: in the c3 step (profiles/r04_*) the FFN1
-// forward 61.9 -> 64.6 us and the gated FFN2 data gradient 50.3 -> 70.4 us against p4, the Q/K/V forward 40 us
-// either way against the multi-round ws kernel — 256x128 tiles ingest 1.5x the operand bytes of p4's 256x256)
-bool wse_auto() {
-  static const bool on = [] { const char* e = getenv("ASRX_WSE"); return e && e[0] == '1'; }();
   return on;
 }
 // ASRX_WS64=0 keeps the decoder's 4096-row N = 512 GEMMs on the ring kernels (A/B switch; default on): ws with
@@ -1520,8 +1494,7 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
     tile = t128 >= 400 ? 128 : 64;
   }
   const int kvar = d->kernel == 1 ? 1 : d->kernel == 3 ? 3 : d->kernel == 4 ? 4 : d->kernel == 5 ? 5 :
-                   d->kernel == 6 ? 6 : d->kernel == 8 ? 8 : d->kernel == 9 ? 9 : d->kernel == 10 ? 10 :
-                   d->kernel == 11 ? 11 : 0;
+                   d->kernel == 6 ? 6 : d->kernel == 8 ? 8 : d->kernel == 10 ? 10 : 0;
   const bool dma_ok = pl.vec && d->k % BK == 0 && (!d->a_trans || d->m % 8 == 0) && (!d->b_trans || d->n % 8 == 0) &&
                       d->m >= 8 && d->n >= 8;
   const int nt_p3 = ((d->m + P_BM - 1) / P_BM) * ((d->n + P_BN - 1) / P_BN);
@@ -1537,7 +1510,7 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
     // whose grid fills the chip; smaller grids (the decoder's 4096-row GEMMs) take the 4-stage ring kernel; the
     // register path wins the weight-gradient (A^T, reduction over B*T rows) and very long-K GEMMs.
     // (with the inline-asm LDS-DMA, p3 also wins the long-K cross-attention K/V data gradient, K = 12 288)
-    // (a forced ws-family code, 8 .. 11, on a GEMM that family cannot take plans as auto)
+    // (a forced ws-family code, 8 or 10, on a GEMM that family cannot take plans as auto)
     else if ((kvar == 0 || kvar >= 8) && !d->a_trans) {
       // wide outputs whose 256x256 tiles still fill the chip (>= 1.25 tiles per CU; the c3 FFN1 forward, the gated
       // FFN2 data gradient, the Q/K/V and cross K/V projections) take p4: half the operand ingest per FLOP
@@ -1605,32 +1578,6 @@ GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
     pl.epi = epi;
     pl.ntiles = ((d->m + 63) / 64) * (d->n / WS_BN);
   }
-  // wsp (use 12): the same roles over a persistent tile walk (multi-round grids: the wide projections); kernel
-  // code 9 forces it.  Candidates (tools/blas_ref.py): the Q/K/V projections with bias and the FFN2 data gradients
-  // gated by the FFN1 mask bits, N 1024 .. 4096, >= 4096 rows (encoder Q/K/V 39.3 -> 35.8 us, gated dX 53.8 ->
-  // 48.7-52.6; decoder 15.7 -> 13.4, 19.6 -> 17.0); the FFN1 forward's ReLU / dropout / mask epilogue stays on
-  // p4 / p3 (50.3 vs 59.1 us) and the 12 288-wide cross K/V on p4 (246 vs 313).  Auto only with ASRX_WSP (above).
-  const bool wsp_ok = dma_ok && !d->a_trans && batch == 1 && splitk == 1 && d->n % WS_BN == 0 && d->k >= BK &&
-                      !d->rowsum_a && !d->sc_outer && !d->sc_inner && epi != E_GENERIC &&
-                      wsp_instantiated(d->b_trans, epi);
-  if (wsp_ok && (kvar == 9 || (kvar == 0 && wsp_auto(epi) && d->n >= 1024 && d->n <= 4096 && d->m >= wsp_min_rows() &&
-                                !(epi & E_RELU)))) {
-    pl.use = 12;
-    pl.epi = epi;
-    pl.ntiles = ((d->m + WS_BM - 1) / WS_BM) * (d->n / WS_BN);
-  }
-  // wse (use 14, round 4): the persistent ws walk with the epilogue on the loader waves (gemm_ws.hip) — every wide
-  // projection of >= 2 rounds of 256x128 tiles: the encoder Q/K/V and all-layer cross K/V forwards, the FFN1 forward
-  // (ReLU / dropout / mask bits) and the gated FFN2 data gradient; kernel code 11 forces it (K >= 128)
-  const bool wse_ok = dma_ok && !d->a_trans && batch == 1 && splitk == 1 && d->n % WS_BN == 0 && d->k >= 2 * BK &&
-                      !d->rowsum_a && !d->sc_outer && !d->sc_inner && epi != E_GENERIC && d->c_dtype == ASRX_BF16 &&
-                      wse_instantiated(d->b_trans, epi);
-  const long nt_ws = (long)((d->m + WS_BM - 1) / WS_BM) * (d->n / WS_BN);
-  if (wse_ok && (kvar == 11 || (kvar == 0 && wse_auto() && nt_ws >= 512))) {
-    pl.use = 14;
-    pl.epi = epi;
-    pl.ntiles = (int)nt_ws;
-  }
   return pl;
 }
 
@@ -1654,13 +1601,7 @@ extern "C" int asrx_gemm_kernel_name(const asrx_gemm_desc* d, char* buf, int len
   }
   const GemmPlan pl = plan_bf16(d, batch, splitk);
   if (pl.use == 11 || pl.use == 13)
-    snprintf(buf, len, "gemm_bf16_ws%s_kernel<%s, %d, %d>",
-             ((pl.epi & E_F32) == 0 && wsr_on()) ? "r" : (ws8_mode() & (pl.use == 13 ? 2 : 1)) ? "8" : "",
-             tf[!!d->b_trans], pl.epi, pl.use == 13 ? 64 : 256);
-  else if (pl.use == 12)
-    snprintf(buf, len, "gemm_bf16_wsp_kernel<%s, %d>", tf[!!d->b_trans], pl.epi);
-  else if (pl.use == 14)
-    snprintf(buf, len, "gemm_bf16_wse_kernel<%s, %d>", tf[!!d->b_trans], pl.epi);
+    snprintf(buf, len, "gemm_bf16_ws_kernel<%s, %d, %d>", tf[!!d->b_trans], pl.epi, pl.use == 13 ? 64 : 256);
   else if (pl.use == 9)
     snprintf(buf, len, "gemm_bf16_tallk_kernel");
   else if (pl.use == 1 || pl.use == 2)
@@ -1706,10 +1647,6 @@ int gemm_bf16_run(const asrx_gemm_desc* d, const GemmArgs& g, const GemmPlan& pl
     }
   } else if (pl.use == 11 || pl.use == 13) {
     launch_ws(g, d->b_trans, epi, pl.ntiles, pl.use == 13 ? 64 : 256, st);
-  } else if (pl.use == 12) {
-    launch_wsp(g, d->b_trans, epi, pl.ntiles, st);
-  } else if (pl.use == 14) {
-    launch_wse(g, d->b_trans, epi, pl.ntiles, st);
   } else if (pl.use == 9) {
     hipLaunchKernelGGL(gemm_bf16_tallk_kernel, dim3(splitk), dim3(512), 0, st, g, TallkConv{0, 0, 0, 0, 0, 0});
   } else if (pl.use == 2) {
@@ -1831,15 +1768,24 @@ extern "C" int asrx_gemm_grouped_xcd_adam(const asrx_gemm_desc* common, const as
       (uintptr_t)adam->v | (uintptr_t)adam->g_base) % 16) || (adam->p_bf16 && (uintptr_t)adam->p_bf16 % 8))
     return ASRX_ERR_ARG;
   if (tiles == 0 || blocks == 0) return ASRX_OK;
-  if (common->in_dtype != ASRX_BF16 || !common->a_trans || !common->b_trans || common->tile != 5 ||
+  const bool g4 = common->tile == 6;
+  if (common->in_dtype != ASRX_BF16 || !common->a_trans || !common->b_trans || (common->tile != 5 && !g4) ||
       common->c_dtype != ASRX_F32 || common->alpha != 1.f || common->beta != 0.f || !common->workspace ||
-      common->workspace_elems < 16 || !common->rowsum_ws)
+      common->workspace_elems < (g4 ? 8 : 16) || (!g4 && !common->rowsum_ws))
     return ASRX_ERR_UNSUPPORTED;
   AdamFused ad;
   ad.p = adam->p; ad.m = adam->m; ad.v = adam->v; ad.pb = (bf16_t*)adam->p_bf16; ad.g0 = adam->g_base;
   ad.hyp = adam->hyp; ad.lr = adam->lr; ad.b1 = adam->beta1; ad.b2 = adam->beta2; ad.eps = adam->eps;
   ad.wd = adam->weight_decay; ad.bc1 = adam->bias_corr1; ad.rbc2 = 1.f / sqrtf(adam->bias_corr2);
   ad.gs = adam->grad_scale; ad.decoupled = adam->decoupled;
+  if (g4) {
+    // (the buffer descriptors of the fused epilogue address the flat state with 32-bit byte offsets)
+    if (launch_g4_grouped((const GroupEnt*)groups, tile_group, block_tile, tiles, blocks, 0.f, gemm_dbg(),
+                          (int*)common->workspace, &ad, (common->kernel & 1) != 0, (hipStream_t)stream) != 0)
+      return ASRX_ERR_UNSUPPORTED;
+    ASRX_CHECK_LAUNCH();
+    return ASRX_OK;
+  }
   if (launch_ws_grouped_adam((const GroupEnt*)groups, tile_group, block_tile, tiles, blocks, gemm_dbg(),
                              (int*)common->workspace, common->rowsum_ws, ad, (hipStream_t)stream) != 0)
     return ASRX_ERR_UNSUPPORTED;
@@ -1862,6 +1808,12 @@ extern "C" int asrx_gemm_grouped_xcd(const asrx_gemm_desc* common, const asrx_ge
                           common->workspace && common->workspace_elems >= 16 ? (int*)common->workspace : nullptr,
                           common->workspace && common->workspace_elems >= 16 ? common->rowsum_ws : nullptr,
                           (hipStream_t)stream) != 0)
+      return ASRX_ERR_UNSUPPORTED;
+  } else if (common->tile == 6) {   // g4: 256x256 tiles, 4-stage ring of 32-deep stages, queue launch (fp32 C, 16-B
+                                    // rows, n % 4 == 0, alpha 1, beta 0|1; workspace = 8 queue counters, zero on entry)
+    if (common->c_dtype != ASRX_F32 || common->alpha != 1.f || !common->workspace || common->workspace_elems < 8 ||
+        launch_g4_grouped((const GroupEnt*)groups, tile_group, block_tile, tiles, blocks, common->beta, gemm_dbg(),
+                          (int*)common->workspace, nullptr, (common->kernel & 1) != 0, (hipStream_t)stream) != 0)
       return ASRX_ERR_UNSUPPORTED;
   } else if (common->tile == 3 || common->tile == 4) {   // p3 / p4 LDS-DMA ring tiles, 256x128 / 256x256 (fp32 C, 16-B
                                                   // rows, n % 4 == 0, alpha 1, beta 0|1)

@@ -200,9 +200,7 @@ ASRX_DEV f4_t epi_vals(const GemmArgs& g, int m, int n, f4_t v, f4_t b4, uint2 p
   }
   if constexpr ((EPI & E_DROP) != 0) {   // n % 4 == 0 and N even: two pair hashes cover the 4 elements
     const uint32_t pb = (uint32_t)((int64_t)m * g.N + n) >> 1;
-    // (ASRX_GEMM_DBG & 512, diagnostics only: the index itself instead of its hash — wrong masks, hash cost A/B)
-    const bool nohash = (g.dbg & 512) != 0;
-    const uint32_t h0 = nohash ? pb * 0x10001u : rng_hash(g.seed, pb), h1 = nohash ? (pb + 1) * 0x10001u : rng_hash(g.seed, pb + 1);
+    const uint32_t h0 = rng_hash(g.seed, pb), h1 = rng_hash(g.seed, pb + 1);
     v[0] = rng_half(h0, 0) >= g.drop_thr ? v[0] * g.drop_scale : 0.f;
     v[1] = rng_half(h0, 1) >= g.drop_thr ? v[1] * g.drop_scale : 0.f;
     v[2] = rng_half(h1, 0) >= g.drop_thr ? v[2] * g.drop_scale : 0.f;
@@ -546,15 +544,11 @@ ASRX_DEV s8_t p4_frag(const unsigned char* img, int i0, int ks, uint32_t S) {
 // ws kernel (gemm_ws.hip): instantiated epilogues and the launch
 constexpr int WS_BM = 256, WS_BN = 128;
 bool ws_instantiated(bool bt, int epi);
-int ws8_mode();   // ASRX_WS8 bits: 1 the 256-row ws tiles, 2 the 64-row ones, on 8 compute waves (gemm_bf16_ws8_kernel)
-bool wsr_on();    // ASRX_WSR: bf16-output ws tiles stored from registers (gemm_bf16_wsr_kernel)
 void launch_ws(const GemmArgs& g, bool bt, int epi, int ntiles, int bm, hipStream_t st);
-bool wsp_instantiated(bool bt, int epi);
-void launch_wsp(const GemmArgs& g, bool bt, int epi, int ntiles, hipStream_t st);
-bool wse_instantiated(bool bt, int epi);
-void launch_wse(const GemmArgs& g, bool bt, int epi, int ntiles, hipStream_t st);
 int launch_ws_grouped(const GroupEnt* ents, const uint16_t* tile_group, const uint16_t* block_tile, int ntiles,
                       int blocks, float beta, int dbg, int* queue, float* part, hipStream_t st);
+int launch_g4_grouped(const GroupEnt* ents, const uint16_t* tile_group, const uint16_t* block_tile, int ntiles,
+                      int blocks, float beta, int dbg, int* queue, const AdamFused* ad, bool rs2, hipStream_t st);
 int launch_ws_grouped_adam(const GroupEnt* ents, const uint16_t* tile_group, const uint16_t* block_tile, int ntiles,
                            int blocks, int dbg, int* queue, float* part, const AdamFused& ad, hipStream_t st);
 

@@ -573,7 +573,7 @@ def main():
         if not same:
             roof["pmc_note"] = "traffic / pmc_mfma omitted: no committed PMC profile of a launch of this size"
         cover = getattr(trainer, "_cover", None)
-        if probe.target in K.GROUPED_WSQA_KERNELS and cover:
+        if probe.target in K.GROUPED_FUSED_KERNELS and cover:
             n_opt = sum(k for _, k in cover)
             roof["fused_optimizer"] = {
                 "op": "AdamW", "params": n_opt, "bytes_per_launch": 26 * n_opt,

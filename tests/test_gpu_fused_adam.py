@@ -28,10 +28,13 @@ def build(name, dropout):
     return m.to(dev).train(), cfg
 
 
-def run(name, fused, graph, steps, batch, dropout=0.0, wd=0.0, decoupled=True):
+def run(name, fused, graph, steps, batch, dropout=0.0, wd=0.0, decoupled=True, wkind=None):
+    import asrx.kernels as KK
     import asrx.train as T
-    old = T.FUSED_ADAM
+    old, oldk = T.FUSED_ADAM, KK.WGRAD_KIND
     T.FUSED_ADAM = fused
+    if wkind:
+        KK.WGRAD_KIND = wkind
     try:
         m, cfg = build(name, dropout)
         spec = CONFIGS[name]
@@ -45,14 +48,17 @@ def run(name, fused, graph, steps, batch, dropout=0.0, wd=0.0, decoupled=True):
         return tr, losses
     finally:
         T.FUSED_ADAM = old
+        KK.WGRAD_KIND = oldk
 
 
+@pytest.mark.parametrize("wkind", ["ws", "g4"])
 @pytest.mark.parametrize("wd,decoupled", [(0.0, True), (0.01, True), (0.01, False)])
-def test_fused_adam_equals_separate_adam_eager(wd, decoupled):
-    """c3 dimensions at B = 2 (the bench's GEMM shapes per row, the ws queue launch): 4 eager AdamW steps; from the
-    second (FreshGrads) on the fused path runs, covering every nn.Linear weight and bias gradient."""
-    ref, l0 = run("c3", False, False, 4, 2, wd=wd, decoupled=decoupled)
-    tr, l1 = run("c3", True, False, 4, 2, wd=wd, decoupled=decoupled)
+def test_fused_adam_equals_separate_adam_eager(wd, decoupled, wkind):
+    """c3 dimensions at B = 2 (the bench's GEMM shapes per row; the ws queue launch and the g4 256x256 one): 4 eager
+    AdamW steps; from the second (FreshGrads) on the fused path runs, covering every nn.Linear weight and bias
+    gradient."""
+    ref, l0 = run("c3", False, False, 4, 2, wd=wd, decoupled=decoupled, wkind=wkind)
+    tr, l1 = run("c3", True, False, 4, 2, wd=wd, decoupled=decoupled, wkind=wkind)
     assert tr._cover, "the fused launch did not run"
     assert ref._cover is None
     covered = sum(k for _, k in tr._cover)
@@ -62,11 +68,12 @@ def test_fused_adam_equals_separate_adam_eager(wd, decoupled):
         assert torch.equal(a, b)
 
 
-def test_fused_adam_graph_equals_eager():
+@pytest.mark.parametrize("wkind", ["ws", "g4"])
+def test_fused_adam_graph_equals_eager(wkind):
     """The captured step (fused launch + residual span-table AdamW, per-step hyper-parameters from the device) equals
     the eager fused step bit for bit over 5 steps (2 eager warm-up steps, capture, replays)."""
-    e, l0 = run("c3", True, False, 5, 2)
-    g, l1 = run("c3", True, True, 5, 2)
+    e, l0 = run("c3", True, False, 5, 2, wkind=wkind)
+    g, l1 = run("c3", True, True, 5, 2, wkind=wkind)
     assert g._cap is not None and g._cover
     assert l0 == l1
     assert torch.equal(e.store.flat, g.store.flat)

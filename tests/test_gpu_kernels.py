@@ -35,7 +35,7 @@ def bf(x):
 
 # ------------------------------------------------------------------------------------------------ GEMM
 
-VARIANTS = ["auto", "p3", "p4", "reg", "ring", "ring128", "wse"]   # kernel families the auto plan can select (gemm.hip plan_bf16)
+VARIANTS = ["auto", "p3", "p4", "reg", "ring", "ring128"]   # kernel families the auto plan can select (gemm.hip plan_bf16)
 
 
 @pytest.fixture
@@ -84,7 +84,7 @@ def test_gemm_epilogue(tile, kernel_variant):
     assert relerr(out.cpu(), ref) < 2e-3
 
 
-@pytest.mark.parametrize("kernel_variant", ["auto", "p3", "p4", "ring", "ring128", "wse"], indirect=True)
+@pytest.mark.parametrize("kernel_variant", ["auto", "p3", "p4", "ring", "ring128"], indirect=True)
 @pytest.mark.parametrize("m,n,p", [(300, 512, 0.1), (1000, 4160, 0.0), (4096, 2048, 0.1)])
 def test_gemm_relu_mask_bits(m, n, p, kernel_variant):
     """FFN hidden layer: the ReLU/dropout epilogue also writes the 1-bit mask C > 0 (mask_out), and the data
@@ -169,7 +169,8 @@ def test_gemm_fused_rowsum(tile, splitk, kernel_variant):
 
 
 @pytest.mark.parametrize("wkind,xcd", [("reg", False), ("reg", True), ("p3", False), ("p3", True), ("p4", False),
-                                       ("p4", True), ("ws", False), ("ws", True), ("wsq", False), ("wsq", True)])
+                                       ("p4", True), ("ws", False), ("ws", True), ("wsq", False), ("wsq", True),
+                                       ("g4", False), ("g4", True)])
 @pytest.mark.parametrize("ngroups", [1, 7, 60])
 def test_gemm_grouped_wgrad(ngroups, wkind, xcd, monkeypatch):
     """Grouped weight gradients (asrx_gemm_grouped_xcd): ragged shapes, K not a multiple of 64, fused bias-grad
@@ -193,12 +194,14 @@ def test_gemm_grouped_wgrad(ngroups, wkind, xcd, monkeypatch):
         items.append((dy, x, wg, bg))
     kname = K().linear_wgrad_grouped(items)
     torch.cuda.synchronize()
+    if wkind == "g4":
+        assert kname.startswith("gemm_bf16_g4q_kernel<96, 4, "), kname   # beta 1; two row-sum blocks for n <= 256
+        assert kname.endswith("true>") == any(bg is not None and x.shape[1] <= 256 for (_, x, _, bg) in items), kname
     if wkind == "wsq" and xcd:
-        assert kname.startswith(("gemm_bf16_wsgq_kernel", "gemm_bf16_wsgq8_kernel")), kname   # the queue kernel ran
+        assert kname.startswith("gemm_bf16_wsgq_kernel"), kname   # the queue kernel ran
     elif wkind in ("ws", "wsq"):
-        assert kname.startswith(("gemm_bf16_wsg_kernel", "gemm_bf16_wsgq_kernel", "gemm_bf16_wsg8_kernel",
-                                  "gemm_bf16_wsgq8_kernel")), kname
-        assert wkind == "wsq" or kname.startswith(("gemm_bf16_wsg_kernel", "gemm_bf16_wsg8_kernel")), kname
+        assert kname.startswith(("gemm_bf16_wsg_kernel", "gemm_bf16_wsgq_kernel")), kname
+        assert wkind == "wsq" or kname.startswith("gemm_bf16_wsg_kernel"), kname
     odd = bf(torch.randn(10, 250, device=dev))      # rows not 16-byte aligned: not groupable (C.wgrad runs it alone)
     assert not K().wgrad_groupable(odd, bf(torch.randn(10, 64, device=dev)), torch.zeros(250, 64, device=dev))
     for (dy, x, wg, bg), (rw, rb) in zip(items, refs):
@@ -284,7 +287,7 @@ def test_gemm_ws_plain(M, N, Kd, bt, wk):
     c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     ref = a.double() @ (b.double() if bt else b.double().t())
     kn = plan_name(M, N, Kd, bt=bt, kernel=wk)
-    assert kn.startswith(("gemm_bf16_ws_kernel", "gemm_bf16_ws8_kernel", "gemm_bf16_wsr_kernel")) and kn.endswith("64>" if wk == "ws64" else "256>"), kn
+    assert kn.startswith("gemm_bf16_ws_kernel") and kn.endswith("64>" if wk == "ws64" else "256>"), kn
     K().gemm(a.to(dev), b.to(dev), c, M, N, Kd, lda=Kd, ldb=b.shape[1], ldc=N, b_trans=bool(bt), kernel=wk)
     assert relerr(c.float().cpu(), ref) < 1e-2
     auto_ws = N == 512 and (M >= 8192 if wk == "ws" else 2048 <= M < 8192)
@@ -319,7 +322,7 @@ def test_gemm_ws_bias_resid(M, N, Kd, f32, resid, drop, wk):
         K().linear(x.to(dev), w.to(dev), c, bias=bias.to(dev), kernel=wk if kern == "ws" else kern, **kw)
         outs[kern] = c.float().cpu()
     kn = plan_name(M, N, Kd, bias=True, c_f32=bool(f32), resid=bool(resid), dropout=bool(drop), kernel=wk)
-    assert kn.startswith(("gemm_bf16_ws_kernel", "gemm_bf16_ws8_kernel", "gemm_bf16_wsr_kernel")) and kn.endswith("64>" if wk == "ws64" else "256>"), kn
+    assert kn.startswith("gemm_bf16_ws_kernel") and kn.endswith("64>" if wk == "ws64" else "256>"), kn
     if drop:   # same keep bits in both kernels; the reference is p3's kept pattern
         keep = (outs["p3"] - (r[:, :N] if resid else 0)) != 0
         ref = torch.where(keep, ref / 0.9, torch.zeros_like(ref))
@@ -328,74 +331,6 @@ def test_gemm_ws_bias_resid(M, N, Kd, f32, resid, drop, wk):
     for kern, o in outs.items():
         assert relerr(o, ref) < (1e-5 if f32 else 1e-2), kern
     assert (outs["ws"] - outs["p3"]).abs().max() <= (1e-4 if f32 else 1e-2) * ref.abs().max()
-
-
-@pytest.mark.parametrize("M,N,Kd", [(15936, 1536, 512), (15936, 2048, 512), (4096, 2048, 512), (1000, 384, 192)])
-def test_gemm_wsp_epilogues(M, N, Kd):
-    """The persistent warp-specialised kernel (kernel code 9, wsp) on the wide projections: bias (Q/K/V), bias + ReLU
-    + dropout + 1-bit mask out (FFN1 forward) and the data gradient gated by those bits with alpha (FFN2 dX) —
-    element for element equal to the p4 kernel (same MFMA accumulation order, same epilogue code) and the plain
-    product against fp64."""
-    g = torch.Generator(device=dev).manual_seed(M + N)
-    x = bf(torch.randn(M, Kd, device=dev, generator=g))
-    w = bf(torch.randn(N, Kd, device=dev, generator=g))
-    bias = torch.randn(N, device=dev, generator=g)
-    assert plan_name(M, N, Kd, bias=True, kernel="wsp").startswith("gemm_bf16_wsp_kernel")
-    outs = {}
-    for kern in ("wsp", "p4"):
-        y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-        K().linear(x, w, y, bias=bias, kernel=kern)
-        yr = torch.empty_like(y)
-        bits = torch.zeros(M, N // 32, device=dev, dtype=torch.int32)
-        K().linear(x, w, yr, bias=bias, relu=True, dropout_p=0.1, seed=9, mask_out=bits, ld_mask=N // 32, kernel=kern)
-        dy = bf(torch.randn(M, Kd, device=dev, generator=torch.Generator(device=dev).manual_seed(5)))
-        wt = bf(torch.randn(Kd, N, device=dev, generator=torch.Generator(device=dev).manual_seed(6)))
-        dx = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-        K().linear_dgrad(dy, wt, dx, alpha=1 / 0.9, gate=bits, ld_gate=N // 32, gate_bits=True, kernel=kern)
-        outs[kern] = (y, yr, bits, dx)
-    torch.cuda.synchronize()
-    for a, b in zip(outs["wsp"], outs["p4"]):
-        assert torch.equal(a, b)
-    ref = x.double() @ w.double().t() + bias.double()
-    assert relerr(outs["wsp"][0].float(), ref) < 1e-2
-
-
-@pytest.mark.parametrize("M,N,Kd", [(15936, 1536, 512), (15936, 2048, 512), (4096, 2048, 512), (1000, 384, 192),
-                                    (700, 256, 128), (15936, 1024, 128), (2500, 4096, 512)])
-def test_gemm_wse_epilogues(M, N, Kd):
-    """The persistent warp-specialised kernel with the epilogue on the loader waves (kernel code 11, wse): bias
-    (Q/K/V, cross K/V), bias + ReLU + dropout + 1-bit mask out (FFN1 forward), bias + ReLU + mask without dropout,
-    and the data gradient gated by the bits with alpha (FFN2 dX) — bit for bit equal to the p4 kernel's fused
-    epilogue (same MFMA accumulation order; the hand-off rounds once, zeroing commutes with it), incl. ragged M,
-    the shortest reduction (K = 128: two K-steps per tile, the whole hand-off in one interval), one tile per
-    workgroup (the drain only) and many; the plain product against fp64."""
-    g = torch.Generator(device=dev).manual_seed(M + N + Kd)
-    x = bf(torch.randn(M, Kd, device=dev, generator=g))
-    w = bf(torch.randn(N, Kd, device=dev, generator=g))
-    bias = torch.randn(N, device=dev, generator=g)
-    assert plan_name(M, N, Kd, bias=True, kernel="wse").startswith("gemm_bf16_wse_kernel")
-    outs = {}
-    for kern in ("wse", "p4"):
-        y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-        K().linear(x, w, y, bias=bias, kernel=kern)
-        yr = torch.empty_like(y)
-        bits = torch.full((M, N // 32 + 1), -1, device=dev, dtype=torch.int32)   # odd row stride, pad must survive
-        K().linear(x, w, yr, bias=bias, relu=True, dropout_p=0.1, seed=9, mask_out=bits, ld_mask=N // 32 + 1,
-                   kernel=kern)
-        y0 = torch.empty_like(y)
-        bits0 = torch.zeros(M, N // 32, device=dev, dtype=torch.int32)
-        K().linear(x, w, y0, bias=bias, relu=True, mask_out=bits0, ld_mask=N // 32, kernel=kern)
-        dy = bf(torch.randn(M, Kd, device=dev, generator=torch.Generator(device=dev).manual_seed(5)))
-        wt = bf(torch.randn(Kd, N, device=dev, generator=torch.Generator(device=dev).manual_seed(6)))
-        dx = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-        K().linear_dgrad(dy, wt, dx, alpha=1 / 0.9, gate=bits, ld_gate=N // 32 + 1, gate_bits=True, kernel=kern)
-        outs[kern] = (y, yr, bits, y0, bits0, dx)
-    torch.cuda.synchronize()
-    for name, a, b in zip(("bias", "relu+drop", "bits", "relu", "bits0", "gated dX"), outs["wse"], outs["p4"]):
-        assert torch.equal(a, b), name
-    assert bool((outs["wse"][2][:, N // 32:] == -1).all())
-    ref = x.double() @ w.double().t() + bias.double()
-    assert relerr(outs["wse"][0].float(), ref) < 1e-2
 
 
 def test_gemm_ws_rowadd():

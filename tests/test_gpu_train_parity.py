@@ -196,21 +196,17 @@ def _plan_log(fn):
 def _assert_bench_plan(log, rows):
     """The GEMM kernels of a c3 step at B = 64 (bench.py's workload): the wide encoder projections (FFN1 forward,
     the gated FFN2 data gradient, the Q/K/V projection forward, the all-layer cross K/V) on the warp-specialised
-    kernel family p4 (FFN) / ws (Q/K/V; with ASRX_WSE=1 both on wse, the epilogue on the loader waves), every 512-wide encoder output on
-    the ws kernel, the weight gradients in one grouped ws launch."""
+    kernel family p4 (FFN) / ws (Q/K/V), every 512-wide encoder output on the ws kernel, the weight gradients in one
+    grouped launch (g4: 256x256 tiles; ws with ASRX_WGRAD_KIND=ws)."""
     by_shape = {}
     for name, m, n, k, *_ in log:
         by_shape.setdefault((m, n, k), set()).add(name.split("<")[0])
     fam = {nm for names in by_shape.values() for nm in names}
-    wse = os.environ.get("ASRX_WSE", "0") == "1"
-    wsn = "gemm_bf16_ws8_kernel" if int(os.environ.get("ASRX_WS8", "0") or 0) & 1 else "gemm_bf16_ws_kernel"
-    wsb = "gemm_bf16_wsr_kernel" if os.environ.get("ASRX_WSR", "0") not in ("", "0") else wsn   # (bf16 outputs)
-    want_ffn, want_qkv = ({"gemm_bf16_wse_kernel"},) * 2 if wse else ({"gemm_bf16_p4_kernel"}, {wsb})
-    assert by_shape[(rows, 2048, 512)] == want_ffn, by_shape[(rows, 2048, 512)]   # FFN1 fwd + FFN2 dX
-    assert by_shape[(rows, 1536, 512)] == want_qkv, by_shape[(rows, 1536, 512)]   # Q/K/V fwd
+    assert by_shape[(rows, 2048, 512)] == {"gemm_bf16_p4_kernel"}, by_shape[(rows, 2048, 512)]   # FFN1 fwd + FFN2 dX
+    assert by_shape[(rows, 1536, 512)] == {"gemm_bf16_ws_kernel"}, by_shape[(rows, 1536, 512)]   # Q/K/V fwd
     for kk in (512, 1216, 1536, 2048):                                                          # N = 512 outputs
-        assert by_shape[(rows, 512, kk)] <= {wsn, wsb}, (kk, by_shape[(rows, 512, kk)])
-    assert fam & {"gemm_bf16_wsg_kernel", "gemm_bf16_wsgq_kernel", "gemm_bf16_wsg8_kernel", "gemm_bf16_wsgq8_kernel"}, fam
+        assert by_shape[(rows, 512, kk)] <= {"gemm_bf16_ws_kernel"}, (kk, by_shape[(rows, 512, kk)])
+    assert fam & {"gemm_bf16_wsg_kernel", "gemm_bf16_wsgq_kernel", "gemm_bf16_g4q_kernel"}, fam
 
 
 def test_trainer_grads_vs_oracle_bench_batch():
@@ -229,9 +225,7 @@ def test_trainer_grads_vs_oracle_bench_batch():
     m.eval()
     with torch.no_grad():
         logits, flog = _plan_log(lambda: m(s.to(dev), t[:, :-1].to(dev), k[:, :-1].to(dev)).cpu())
-    assert {nm.split("<")[0] for nm, mm, n, kk, *_ in flog if (mm, n) == (rows, 512)} <= {"gemm_bf16_ws_kernel",
-                                                                                         "gemm_bf16_ws8_kernel",
-                                                                                         "gemm_bf16_wsr_kernel"}
+    assert {nm.split("<")[0] for nm, mm, n, kk, *_ in flog if (mm, n) == (rows, 512)} <= {"gemm_bf16_ws_kernel"}
     torch.set_num_threads(max(1, min(32, len(os.sched_getaffinity(0)))))
     P = {kk: v.clone().requires_grad_(True) for kk, v in det_params(cfg, 0).items()}
     ref_loss, ref = train_step_grads(P, s, t, k, cfg, training=False)

@@ -184,24 +184,20 @@ def test_gemm_kernel_plan_names_without_gpu():
         return d
 
     # wide outputs (>= 400 256x256 tiles) take p4; the Q/K/V projection forward (bias) the ws kernel, encoder and
-    # decoder; the persistent ws kernels (wsp; wse, the epilogue on the loader waves) only when forced or with
-    # ASRX_WSP / ASRX_WSE=1 (round 4: wse measured no faster in the step)
+    # decoder (round 4's persistent ws variants, codes 9 and 11, were removed in round 5: they plan as auto)
     assert kernel_name(desc(15936, 1536, 512, bias=True)) == "gemm_bf16_ws_kernel<false, 1, 256>"
     assert kernel_name(desc(4096, 1536, 512, bias=True)) == "gemm_bf16_ws_kernel<false, 1, 256>"
     assert kernel_name(desc(15936, 1536, 512)) == "gemm_bf16_p3_kernel<false, false, 0>"
     forced = desc(15936, 1536, 512, bias=True)
-    forced.kernel = 9
-    assert kernel_name(forced) == "gemm_bf16_wsp_kernel<false, 1>"
-    forced.kernel = 11
-    assert kernel_name(forced) == "gemm_bf16_wse_kernel<false, 1>"
+    for code in (9, 11):
+        forced.kernel = code
+        assert kernel_name(forced) == "gemm_bf16_ws_kernel<false, 1, 256>"
     assert kernel_name(desc(15936, 2048, 512, bt=1)) == "gemm_bf16_p4_kernel<false, true, 0>"
     ffn1 = desc(15936, 2048, 512, bias=True)
     ffn1.relu = 1
     assert kernel_name(ffn1) == "gemm_bf16_p4_kernel<false, false, 3>"
-    ffn1.kernel = 11
-    assert kernel_name(ffn1) == "gemm_bf16_wse_kernel<false, 3>"
     ragged = desc(1000, 4160, 256, bias=True)   # N % 128 != 0: a forced ws-family code plans as auto
-    ragged.kernel = 11
+    ragged.kernel = 8
     assert kernel_name(ragged) == kernel_name(desc(1000, 4160, 256, bias=True))
     assert kernel_name(desc(15936, 12288, 512, bias=True)) == "gemm_bf16_p4_kernel<false, false, 1>"
     forced.kernel = 6                 # p4 forced: the 256x256 ring
