@@ -62,6 +62,7 @@ class KernelProbe:
         self.target = target
         self.events = {}            # name -> [(start, end)]
         self.flops = {}             # name -> algorithmic FLOPs
+        self.alg_bytes = {}         # name -> algorithmic HBM bytes of one launch (where the launch site states them)
         self.active = False
         self.log = log              # optional list: (kernel name, m, n, k, batch, splitk) of every GEMM launch
 
@@ -221,14 +222,7 @@ GROUPED_P4_KERNELS = ("gemm_bf16_p4g_kernel<64>", "gemm_bf16_p4g_kernel<96>")
 GROUPED_WS_KERNELS = ("gemm_bf16_wsg_kernel<64>", "gemm_bf16_wsg_kernel<96>")
 GROUPED_WSQ_KERNELS = ("gemm_bf16_wsgq_kernel<64>", "gemm_bf16_wsgq_kernel<96>")
 GROUPED_WSQA_KERNELS = ("gemm_bf16_wsgqa_kernel<64>", None)   # AdamW fused (beta 0 only)
-# g4 (gemm_wg.hip, round 5): 256x256 tiles, 4-stage ring of 32-deep stages; <EPI, stages, two row-sum blocks>
-# (2112 = E_ADAM | E_F32: AdamW fused)
-GROUPED_G4_KERNELS = {(False, False): ("gemm_bf16_g4q_kernel<64, 4, false>", "gemm_bf16_g4q_kernel<96, 4, false>"),
-                      (False, True): ("gemm_bf16_g4q_kernel<64, 4, true>", "gemm_bf16_g4q_kernel<96, 4, true>"),
-                      (True, False): ("gemm_bf16_g4q_kernel<2112, 4, false>", None),
-                      (True, True): ("gemm_bf16_g4q_kernel<2112, 4, true>", None)}
-GROUPED_FUSED_KERNELS = {GROUPED_WSQA_KERNELS[0], GROUPED_G4_KERNELS[(True, False)][0],
-                         GROUPED_G4_KERNELS[(True, True)][0]}
+GROUPED_FUSED_KERNELS = {GROUPED_WSQA_KERNELS[0]}
 
 
 def wgrad_groupable(dy, x, wgrad):
@@ -249,7 +243,7 @@ WGRAD_KIND = os.environ.get("ASRX_WGRAD_KIND", "ws")
 
 def _grouped_p3_ok(items, beta):
     """Can the LDS-DMA ring kernel take these weight gradients (fp32 C rows 16-byte aligned, beta 0 or 1)?"""
-    return WGRAD_KIND in ("p3", "p4", "ws", "g4") and beta in (0.0, 1.0) and all(
+    return WGRAD_KIND in ("p3", "p4", "ws") and beta in (0.0, 1.0) and all(
         x.shape[1] % 4 == 0 and wgrad.stride(0) % 4 == 0 and wgrad.data_ptr() % 16 == 0
         for (_, x, wgrad, _) in items)
 
@@ -326,8 +320,7 @@ def xcd_plan(shapes, tile=256, nxcd=8, pack=None):
     return plan
 
 
-_TILE_CODE = {"p3": ((256, 128), 3), "p4": ((256, 256), 4), "ws": ((256, 128), 5), "g4": ((256, 256), 6),
-              "reg": ((128, 128), 128)}
+_TILE_CODE = {"p3": ((256, 128), 3), "p4": ((256, 256), 4), "ws": ((256, 128), 5), "reg": ((128, 128), 128)}
 
 
 def upload(dst, host_bytes):
@@ -373,14 +366,7 @@ def _grouped_xcd(items, common, kind="p3", adam=None):
     # ws tiles: 8 per-XCD queue counters (+ 8 spare) and one counter per bias-carrying row panel after the block map,
     # zeroed by this upload, i.e. on every launch / replay; the row panels' [tiles][256] fp32 row-sum slabs beside
     o3 = (o2 + block_tile.nbytes + 63) // 64 * 64
-    g4 = code == 6   # (g4: always the queue launch; its row sums need no slabs or panel counters)
-    queue = (code == 5 and WGRAD_QUEUE or g4) and len(block_tile) % 8 == 0
-    if g4 and not queue:
-        raise RuntimeError("asrx: the g4 grouped launch needs a block map of whole 8-XCD rounds")
-    if g4:
-        panels = 0
-        # two row-sum blocks per wave where a bias-carrying group has a single column tile (n <= 256)
-        common.kernel = int(any(it[3] is not None and it[1].shape[1] <= tile[1] for it in items))
+    queue = code == 5 and WGRAD_QUEUE and len(block_tile) % 8 == 0
     n_all = o3 + 4 * (16 + panels) if queue else (o2 + block_tile.nbytes + 3) // 4 * 4
     host = np.zeros(n_all, dtype=np.uint8)
     host[:o1] = ents.view(np.uint8).reshape(-1)
@@ -392,13 +378,10 @@ def _grouped_xcd(items, common, kind="p3", adam=None):
     part = None
     if queue:
         common.workspace, common.workspace_elems = base + o3, 16 + panels
-        if not g4:
-            part = torch.empty(start * tile[0], dtype=torch.float32, device=dev.device)
-            common.rowsum_ws = part.data_ptr()
+        part = torch.empty(start * tile[0], dtype=torch.float32, device=dev.device)
+        common.rowsum_ws = part.data_ptr()
 
     fused = adam is not None and queue and common.beta == 0.0
-    if fused and g4 and getattr(adam, "nbytes", 2 ** 31) > 2 ** 31 - 16:
-        fused = False   # (g4's fused epilogue addresses the flat state with 32-bit byte offsets)
 
     def launch():
         if fused:   # (the AdamDesc is held by this closure until the call)
@@ -438,14 +421,27 @@ def linear_wgrad_grouped(items, *, beta=1.0, kind=None, adam=None):
     kind = kind or WGRAD_KIND
     # the table upload is issued first, so a timed bracket holds the grouped GEMM alone
     flops, launch, _, (queued, fused) = _grouped_xcd(items, common, kind if p3 else "reg",
-                                                     adam if p3 and kind in ("ws", "g4") else None)
+                                                     adam if p3 and kind == "ws" else None)
     # the kernel that actually runs: the ws tiles go to the persistent queue kernel only when _grouped_xcd took it
     # (its block map must hold whole 8-XCD rounds), else one workgroup per tile
     wsk = GROUPED_WSQA_KERNELS if fused else GROUPED_WSQ_KERNELS if queued else GROUPED_WS_KERNELS
-    g4k = GROUPED_G4_KERNELS[(bool(fused), bool(common.kernel & 1))]
-    kname = ({"p4": GROUPED_P4_KERNELS, "ws": wsk, "g4": g4k}.get(kind, GROUPED_P3_KERNELS)[beta == 1.0] if p3
+    kname = ({"p4": GROUPED_P4_KERNELS, "ws": wsk}.get(kind, GROUPED_P3_KERNELS)[beta == 1.0] if p3
              else GROUPED_TABLE_KERNEL)
     probe = PROBE
+    if probe is not None:
+        # algorithmic bytes: every operand panel once (bf16 dY and X, each distinct tensor counted once), the fp32 dW /
+        # db stores (+ their reads for beta 1), and with the optimizer fused 26 B more per parameter (fp32 master and
+        # both moments read and written, the bf16 shadow written)
+        seen, nb = set(), 0
+        for dy, x, gw, gb in items:
+            for t in (dy, x):
+                if t.data_ptr() not in seen:
+                    seen.add(t.data_ptr())
+                    nb += t.shape[0] * t.shape[1] * t.element_size()
+            for t in (gw, gb):
+                if t is not None:
+                    nb += t.numel() * 4 * (2 if beta == 1.0 else 1) + (26 * t.numel() if fused else 0)
+        probe.alg_bytes[kname] = nb
     if probe is not None and probe.active and probe.log is not None:
         probe.log.append((kname, len(items), 0,
                           sum(it[0].shape[0] * it[0].shape[1] * it[1].shape[1] for it in items), 1, 1))
@@ -878,7 +874,6 @@ def adam_desc(p, m, v, p_bf16, g, lr, beta1, beta2, eps, weight_decay, step, gra
     d.lr, d.beta1, d.beta2, d.eps, d.weight_decay = lr, beta1, beta2, eps, weight_decay
     d.bias_corr1, d.bias_corr2 = 1.0 - beta1 ** step, 1.0 - beta2 ** step
     d.grad_scale, d.decoupled = grad_scale, int(decoupled)
-    d.nbytes = 4 * max(p.numel(), g.numel())   # (extent of the flat state: the g4 fused epilogue's 32-bit offsets)
     return d
 
 

@@ -465,6 +465,19 @@ ASRX_DEV uint2 ld64_asm(const void* p) {
   asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(r) : "v"(p));
   return __builtin_bit_cast(uint2, r);
 }
+// buffer loads through a wave-uniform descriptor with a per-lane voffset and a wave-uniform soffset (SGPR); inline
+// asm like ld64_asm (the kernels count these loads in their own vmcnt waits)
+// (srd: from make_srd, already wave-uniform — SGPRs)
+ASRX_DEV uint2 bld64(asrxg::v4i_t srd, uint32_t voff, uint32_t soff) {
+  u2_t r;
+  asm volatile("buffer_load_dwordx2 %0, %1, %2, %3 offen" : "=v"(r) : "v"(voff), "s"(srd), "s"(soff));
+  return __builtin_bit_cast(uint2, r);
+}
+ASRX_DEV uint32_t bld32(asrxg::v4i_t srd, uint32_t voff, uint32_t soff) {
+  uint32_t r;
+  asm volatile("buffer_load_dword %0, %1, %2, %3 offen" : "=v"(r) : "v"(voff), "s"(srd), "s"(soff));
+  return r;
+}
 ASRX_DEV uint32_t ld32_asm(const void* p) {
   uint32_t r;
   asm volatile("global_load_dword %0, %1, off" : "=v"(r) : "v"(p));
@@ -1335,7 +1348,6 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
   const bool usebits = a.thr && a.dropmask;
   const uint32_t* dmb = usebits ? a.dropmask + (int64_t)bh * nch * a.Lk : nullptr;
   uint32_t dwn[2] = {0u, 0u};
-  const int keyc[2] = {min(kw0 + li, a.Lk - 1), min(kw0 + 16 + li, a.Lk - 1)};
   // delta = rowsum(dO * O) is formed here too: the threads that stage a dO piece also load the matching O
   // piece, dot the 8 elements and reduce over the row's 8 pieces (adjacent lanes) — no separate delta pass.
   const bf16_t* Ob = a.o + b * a.ob + h * 64;
@@ -1348,25 +1360,41 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
   // phi, which the compiler may realise as a register copy issued before the wait — a copy of an in-flight load.
   // Each thread stages PRE 8-B pieces of Q AND the same pieces of dO, O and O_lo (piece c: row c / 16, elements
   // 4 (c % 16) ..): every wave does the same loads and its share of delta (the 16 lanes of a row reduce by DPP).
-  const bf16_t* const Olv = Olb ? Olb : Ob;
-  auto fetch = [&](int ch) {
-    const int q0 = ch * 32;
+  // Buffer descriptors of this head's Q / dO / O / O_lo rows, its lse and keep words (round 5): rows and words past
+  // the end read as zero through the descriptor's range check, each lane's voffset is fixed for the kernel and the
+  // chunk's start rides in the SGPR soffset — the prefetch's per-chunk addressing is SALU only (it was a 64-bit
+  // pointer sum per load, ~40 VALU per chunk of a VALU-issue-bound loop).
+  const asrxg::v4i_t srq = asrxg::make_srd(Qb, ((int64_t)(a.Lq - 1) * a.qr + 64) * 2);
+  const asrxg::v4i_t srd = asrxg::make_srd(Db, ((int64_t)(a.Lq - 1) * a.dor + 64) * 2);
+  const asrxg::v4i_t sro = asrxg::make_srd(Ob, ((int64_t)(a.Lq - 1) * a.orr + 64) * 2);
+  const asrxg::v4i_t srol = asrxg::make_srd(Olb ? Olb : Ob, ((int64_t)(a.Lq - 1) * a.orr + 64) * 2);
+  const asrxg::v4i_t srl = asrxg::make_srd(lseb, (int64_t)a.Lq * 4);
+  const asrxg::v4i_t srm = usebits ? asrxg::make_srd(dmb, (int64_t)nch * a.Lk * 4) : srl;
+  uint32_t vq[PRE], vdo[PRE], vo[PRE];
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
-      dwn[t] = ld32_asm(usebits ? dmb + (int64_t)ch * a.Lk + keyc[t] : (const uint32_t*)lseb);
+  for (int i = 0; i < PRE; ++i) {
+    const int c = tid + NTHR * i;
+    const int row = c >> 4, dc = (c & 15) * 4;
+    vq[i] = (uint32_t)(row * (int)a.qr + dc) * 2u;
+    vdo[i] = (uint32_t)(row * (int)a.dor + dc) * 2u;
+    vo[i] = (uint32_t)(row * (int)a.orr + dc) * 2u;
+  }
+  const uint32_t vl = (uint32_t)(tid & 31) * 4u;
+  const uint32_t vk0 = usebits ? (uint32_t)(kw0 + li) * 4u : 0u, vk1 = usebits ? (uint32_t)(kw0 + 16 + li) * 4u : 0u;
+  auto fetch = [&](int ch) {
+    const uint32_t q0 = (uint32_t)ch * 32u;
+    const uint32_t sw = usebits ? (uint32_t)ch * (uint32_t)a.Lk * 4u : 0u;
+    dwn[0] = bld32(srm, vk0, sw);
+    dwn[1] = bld32(srm, vk1, sw);
+    const uint32_t sq_ = q0 * (uint32_t)a.qr * 2u, sd_ = q0 * (uint32_t)a.dor * 2u, so_ = q0 * (uint32_t)a.orr * 2u;
 #pragma unroll
     for (int i = 0; i < PRE; ++i) {
-      const int c = tid + NTHR * i;
-      const int row = c >> 4, dc = (c & 15) * 4;
-      const int q = min(q0 + row, a.Lq - 1);
-      // 24-bit row offsets (resident_ok: strides < 2^23): full-rate v_mul_i32_i24, not 64-bit multiplies
-      pq[i] = ld64_asm(Qb + __mul24(q, (int)a.qr) + dc);
-      pdo[i] = ld64_asm(Db + __mul24(q, (int)a.dor) + dc);
-      const int oq = __mul24(q, (int)a.orr) + dc;
-      po[i] = ld64_asm(Ob + oq);
-      pol[i] = ld64_asm(Olv + oq);
+      pq[i] = bld64(srq, vq[i], sq_);
+      pdo[i] = bld64(srd, vdo[i], sd_);
+      po[i] = bld64(sro, vo[i], so_);
+      pol[i] = bld64(srol, vo[i], so_);
     }
-    praw = __uint_as_float(ld32_asm(lseb + min(q0 + (tid & 31), a.Lq - 1)));
+    praw = __uint_as_float(bld32(srl, vl, q0 * 4u));
   };
   auto publish = [&](int buf, int qbuf, int ch) {
     const int q0 = ch * 32;
@@ -1388,17 +1416,17 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
       const bool qv = q0 + row < a.Lq;
       *(uint2*)(sq + (qbuf * 32 + row) * R_CS + dc) = qv ? pq[i] : make_uint2(0, 0);
       *(uint2*)(sdo + (qbuf * 32 + row) * R_CS + dc) = qv ? pdo[i] : make_uint2(0, 0);
+      // dO . (O + O_lo) over the lane's 4 elements: v_dot2_f32_bf16 on the packed pairs (bf16 products are exact in
+      // fp32; 4 instructions instead of unpacking 12 values)
+      typedef __bf16 b2_t __attribute__((ext_vector_type(2)));
       const uint32_t dd[2] = {pdo[i].x, pdo[i].y}, oo[2] = {po[i].x, po[i].y}, ol[2] = {pol[i].x, pol[i].y};
       float dot = 0.f;
-      if (Olb) {
 #pragma unroll
-        for (int e = 0; e < 2; ++e)
-          dot += bf2f(dd[e] & 0xffff) * (bf2f(oo[e] & 0xffff) + bf2f(ol[e] & 0xffff)) +
-                 bf2f(dd[e] >> 16) * (bf2f(oo[e] >> 16) + bf2f(ol[e] >> 16));
-      } else {
-#pragma unroll
-        for (int e = 0; e < 2; ++e)
-          dot += bf2f(dd[e] & 0xffff) * bf2f(oo[e] & 0xffff) + bf2f(dd[e] >> 16) * bf2f(oo[e] >> 16);
+      for (int e = 0; e < 2; ++e) {
+        dot = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(b2_t, dd[e]), __builtin_bit_cast(b2_t, oo[e]), dot, false);
+        if (Olb)
+          dot = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(b2_t, dd[e]), __builtin_bit_cast(b2_t, ol[e]), dot,
+                                                false);
       }
       // sum over the row's 16 adjacent lanes by DPP (quad swaps, half-row and row mirrors): no LDS round trips
       dot += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(dot), 0xB1, 0xF, 0xF, true));
@@ -1549,7 +1577,11 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
           for (int r = 0; r < 4; ++r) {
             float x;
             if (MODE == 2) x = masked(a, b, qb + r, key) ? -INFINITY : fmaf(s[qs][t][r], a.scale2, nlse4[r]);
-            else {
+            else if (MODE == 0) {
+              // (no key mask in mode 0: a padded key (>= Lk) gets a nonzero P here, but it reaches only its own dK / dV,
+              //  which are never stored, and dQ through its K row, which is zero in the LDS image)
+              x = fmaf(s[qs][t][r], a.scale2, nlse4[r]);
+            } else {
               x = fmaf(s[qs][t][r], a.scale2, nlse4[r]) + kbias[t];
               if (diag && key > qb + r) x = -INFINITY;
             }

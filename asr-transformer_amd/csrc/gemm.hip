@@ -1768,24 +1768,15 @@ extern "C" int asrx_gemm_grouped_xcd_adam(const asrx_gemm_desc* common, const as
       (uintptr_t)adam->v | (uintptr_t)adam->g_base) % 16) || (adam->p_bf16 && (uintptr_t)adam->p_bf16 % 8))
     return ASRX_ERR_ARG;
   if (tiles == 0 || blocks == 0) return ASRX_OK;
-  const bool g4 = common->tile == 6;
-  if (common->in_dtype != ASRX_BF16 || !common->a_trans || !common->b_trans || (common->tile != 5 && !g4) ||
+  if (common->in_dtype != ASRX_BF16 || !common->a_trans || !common->b_trans || common->tile != 5 ||
       common->c_dtype != ASRX_F32 || common->alpha != 1.f || common->beta != 0.f || !common->workspace ||
-      common->workspace_elems < (g4 ? 8 : 16) || (!g4 && !common->rowsum_ws))
+      common->workspace_elems < 16 || !common->rowsum_ws)
     return ASRX_ERR_UNSUPPORTED;
   AdamFused ad;
   ad.p = adam->p; ad.m = adam->m; ad.v = adam->v; ad.pb = (bf16_t*)adam->p_bf16; ad.g0 = adam->g_base;
   ad.hyp = adam->hyp; ad.lr = adam->lr; ad.b1 = adam->beta1; ad.b2 = adam->beta2; ad.eps = adam->eps;
   ad.wd = adam->weight_decay; ad.bc1 = adam->bias_corr1; ad.rbc2 = 1.f / sqrtf(adam->bias_corr2);
   ad.gs = adam->grad_scale; ad.decoupled = adam->decoupled;
-  if (g4) {
-    // (the buffer descriptors of the fused epilogue address the flat state with 32-bit byte offsets)
-    if (launch_g4_grouped((const GroupEnt*)groups, tile_group, block_tile, tiles, blocks, 0.f, gemm_dbg(),
-                          (int*)common->workspace, &ad, (common->kernel & 1) != 0, (hipStream_t)stream) != 0)
-      return ASRX_ERR_UNSUPPORTED;
-    ASRX_CHECK_LAUNCH();
-    return ASRX_OK;
-  }
   if (launch_ws_grouped_adam((const GroupEnt*)groups, tile_group, block_tile, tiles, blocks, gemm_dbg(),
                              (int*)common->workspace, common->rowsum_ws, ad, (hipStream_t)stream) != 0)
     return ASRX_ERR_UNSUPPORTED;
@@ -1808,12 +1799,6 @@ extern "C" int asrx_gemm_grouped_xcd(const asrx_gemm_desc* common, const asrx_ge
                           common->workspace && common->workspace_elems >= 16 ? (int*)common->workspace : nullptr,
                           common->workspace && common->workspace_elems >= 16 ? common->rowsum_ws : nullptr,
                           (hipStream_t)stream) != 0)
-      return ASRX_ERR_UNSUPPORTED;
-  } else if (common->tile == 6) {   // g4: 256x256 tiles, 4-stage ring of 32-deep stages, queue launch (fp32 C, 16-B
-                                    // rows, n % 4 == 0, alpha 1, beta 0|1; workspace = 8 queue counters, zero on entry)
-    if (common->c_dtype != ASRX_F32 || common->alpha != 1.f || !common->workspace || common->workspace_elems < 8 ||
-        launch_g4_grouped((const GroupEnt*)groups, tile_group, block_tile, tiles, blocks, common->beta, gemm_dbg(),
-                          (int*)common->workspace, nullptr, (common->kernel & 1) != 0, (hipStream_t)stream) != 0)
       return ASRX_ERR_UNSUPPORTED;
   } else if (common->tile == 3 || common->tile == 4) {   // p3 / p4 LDS-DMA ring tiles, 256x128 / 256x256 (fp32 C, 16-B
                                                   // rows, n % 4 == 0, alpha 1, beta 0|1)

@@ -547,8 +547,6 @@ bool ws_instantiated(bool bt, int epi);
 void launch_ws(const GemmArgs& g, bool bt, int epi, int ntiles, int bm, hipStream_t st);
 int launch_ws_grouped(const GroupEnt* ents, const uint16_t* tile_group, const uint16_t* block_tile, int ntiles,
                       int blocks, float beta, int dbg, int* queue, float* part, hipStream_t st);
-int launch_g4_grouped(const GroupEnt* ents, const uint16_t* tile_group, const uint16_t* block_tile, int ntiles,
-                      int blocks, float beta, int dbg, int* queue, const AdamFused* ad, bool rs2, hipStream_t st);
 int launch_ws_grouped_adam(const GroupEnt* ents, const uint16_t* tile_group, const uint16_t* block_tile, int ntiles,
                            int blocks, int dbg, int* queue, float* part, const AdamFused& ad, hipStream_t st);
 

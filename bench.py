@@ -572,6 +572,15 @@ def main():
                 "pmc_mfma": pm if same else None}
         if not same:
             roof["pmc_note"] = "traffic / pmc_mfma omitted: no committed PMC profile of a launch of this size"
+        ab = probe.alg_bytes.get(probe.target)
+        if ab:
+            # the launch is on both roofs at once (GEMM FLOPs on the matrix unit, operand panels + dW + fused optimizer
+            # state through HBM): its floor is the larger of the two times, frac = floor / measured time
+            t_mfma, t_hbm = flop_launch / (PEAK_BF16_TFLOPS * 1e12), ab / (PEAK_HBM_GBS * 1e9)
+            roof["combined"] = {"alg_bytes_per_launch": ab, "mfma_floor_us": round(t_mfma * 1e6, 1),
+                                "hbm_floor_us": round(t_hbm * 1e6, 1),
+                                "frac": round(max(t_mfma, t_hbm) / (avg_ms * 1e-3), 4),
+                                "note": "max(FLOP / dense bf16 peak, algorithmic bytes / HBM peak) / launch time"}
         cover = getattr(trainer, "_cover", None)
         if probe.target in K.GROUPED_FUSED_KERNELS and cover:
             n_opt = sum(k for _, k in cover)

@@ -115,11 +115,7 @@ typedef struct asrx_gemm_group_dev {
  * common->rowsum_ws as [tiles][256] fp32 scratch: the launch runs min(blocks, 256) persistent workgroups that take
  * the slots x, x + 8, x + 16, ... of block_tile from per-XCD queues (x = b % 8; blocks % 8 == 0; an empty queue
  * takes the others' last slots), and each panel's column tiles share its row sums (the last to finish adds them in
- * column order); the counters are left non-zero: zero them before the next launch), 6 = "g4": 256x256 tiles of
- * 8 waves, a 4-stage ring of 32-deep stages, persistent workgroups on the same per-XCD queues (workspace: >= 8 int32
- * counters, zero on entry) and the bias gradients (rowsum_a) summed by the matrix unit, each 16-row block by one of
- * its row panel's column tiles (no rowsum_ws); common->kernel bit 0 must be set when a group with a rowsum_a has
- * n <= 256 (fp32 C with 16-byte aligned rows, n % 4 == 0, alpha 1, beta 0 or 1), 128 = register-staged
+ * column order); the counters are left non-zero: zero them before the next launch), 128 = register-staged
  * 128x128 tiles (any alignment-checked table; common->relu carries its "every C row 16-byte aligned" flag).
  * Replaces the weight/bias-gradient mm + sum of autograd for every nn.Linear (layers.py:10-12,36,48,51). */
 int asrx_gemm_grouped_xcd(const asrx_gemm_desc* common, const asrx_gemm_group_dev* groups,
@@ -136,8 +132,7 @@ typedef struct asrx_adam_desc {
 } asrx_adam_desc;
 
 /* asrx_gemm_grouped_xcd (tile 5, the persistent queue launch: fp32 C, beta 0, workspace counters and rowsum_ws
- * slabs; or tile 6, g4: workspace counters only, the flat state within 2 GiB of g_base) with the optimizer step
- * fused into the epilogue: each dW element and each group's bias gradient (rowsum_a)
+ * slabs) with the optimizer step fused into the epilogue: each dW element and each group's bias gradient (rowsum_a)
  * is stored and the AdamW update of its parameter applied at once, the parameter / moment / shadow bytes moving
  * while the other tiles compute (single-GPU training: the gradients need no exchange first).  Replaces the
  * optimizer.step() (train.py:35) of every nn.Linear parameter together with its gradient mm + sum. */

@@ -197,7 +197,7 @@ def _assert_bench_plan(log, rows):
     """The GEMM kernels of a c3 step at B = 64 (bench.py's workload): the wide encoder projections (FFN1 forward,
     the gated FFN2 data gradient, the Q/K/V projection forward, the all-layer cross K/V) on the warp-specialised
     kernel family p4 (FFN) / ws (Q/K/V), every 512-wide encoder output on the ws kernel, the weight gradients in one
-    grouped launch (g4: 256x256 tiles; ws with ASRX_WGRAD_KIND=ws)."""
+    grouped ws launch."""
     by_shape = {}
     for name, m, n, k, *_ in log:
         by_shape.setdefault((m, n, k), set()).add(name.split("<")[0])
@@ -206,7 +206,7 @@ def _assert_bench_plan(log, rows):
     assert by_shape[(rows, 1536, 512)] == {"gemm_bf16_ws_kernel"}, by_shape[(rows, 1536, 512)]   # Q/K/V fwd
     for kk in (512, 1216, 1536, 2048):                                                          # N = 512 outputs
         assert by_shape[(rows, 512, kk)] <= {"gemm_bf16_ws_kernel"}, (kk, by_shape[(rows, 512, kk)])
-    assert fam & {"gemm_bf16_wsg_kernel", "gemm_bf16_wsgq_kernel", "gemm_bf16_g4q_kernel"}, fam
+    assert fam & {"gemm_bf16_wsg_kernel", "gemm_bf16_wsgq_kernel", "gemm_bf16_wsgqa_kernel"}, fam
 
 
 def test_trainer_grads_vs_oracle_bench_batch():
