@@ -10,7 +10,6 @@ FeedForward layers.py:53-58; front-end model.py:168-171 + 41-47; decoder embeddi
 """
 import bisect
 import math
-import os
 
 import torch
 
@@ -93,12 +92,6 @@ class Ctx:
     def seed(self):
         return self.seeds.next() if self.p > 0 else 0
 
-    def side_stream(self, device):
-        st = getattr(self, "_side", None)
-        if st is None:
-            st = self._side = _side_stream(device)
-        return st
-
     def wgrad(self, dy, x, gw, gb=None):
         """dW (+)= dy^T x, db (+)= colsum(dy).  Weight gradients feed nothing but the optimizer, so while a
         queue is open they are deferred and later issued as grouped launches (no split-K)."""
@@ -168,27 +161,6 @@ class Ctx:
         lq, self.lnq = self.lnq, None
         self._issue_wgrads(q or [])
         K.reduce_rows_grouped(lq or [])
-        side = getattr(self, "_wside", None)
-        if side is not None:          # weight gradients issued on the side stream are final only after it
-            torch.cuda.current_stream(side.device).wait_stream(side)
-            self._wside = None
-
-    def flush_wgrad_side(self):
-        """Issue the weight gradients queued so far on the side stream, so they overlap the rest of the backward
-        chain (they feed only the optimizer / all-reduce, which wait for them in flush_wgrad)."""
-        if not WGRAD_OVERLAP or not self.wq:
-            return
-        q, self.wq = self.wq, []
-        dev = q[0][0].device
-        main = torch.cuda.current_stream(dev)
-        side = self.side_stream(dev)
-        side.wait_stream(main)
-        for dy, x, _, _ in q:           # keep the operands' memory from being reused on the main stream
-            dy.record_stream(side)
-            x.record_stream(side)
-        with torch.cuda.stream(side):
-            self._issue_wgrads(q)
-        self._wside = side
 
 
 class Seeds:
@@ -202,27 +174,15 @@ class Seeds:
         return x ^ (x >> 31)
 
 
-_SIDE = {}
-# weight gradients of each finished layer issued on the side stream, overlapping the backward chain
-WGRAD_OVERLAP = os.environ.get("ASRX_WGRAD_OVERLAP", "0") == "1"
-# FFN hidden-layer ReLU/dropout mask kept as bits for the data gradient (ASRX_GATE_BITS=0: read the bf16 f)
-GATE_BITS = os.environ.get("ASRX_GATE_BITS", "1") == "1"
-# generating the keep bits on a side stream (overlapping the LN + Q/K/V GEMM) measured SLOWER than generating
-# them in line (18.2 vs 17.75 ms/step: the VALU-heavy generator steals the GEMM's CUs): off by default
-_SIDE_DROPGEN = os.environ.get("ASRX_DROPGEN_SIDE", "0") == "1"
-# the attention keep bits generated inside the preceding LayerNorm's launch (ASRX_LN_DROPGEN=0: by the attention
-# forward's own launch)
-LN_DROPGEN = os.environ.get("ASRX_LN_DROPGEN", "1") == "1"
-# ... also for the decoder's cross-attention (round 4; ASRX_LN_DROPGEN_CROSS=0: its own keep-bit launch, A/B)
-LN_DROPGEN_CROSS = os.environ.get("ASRX_LN_DROPGEN_CROSS", "1") == "1"
-
-
-def _side_stream(device):
-    """One auxiliary HIP stream per device for work that only depends on RNG seeds (dropout keep bits)."""
-    key = torch.device(device).index or 0
-    if key not in _SIDE:
-        _SIDE[key] = torch.cuda.Stream(device=device)
-    return _SIDE[key]
+# Fixed choices whose A/B switches were removed in round 5 (measurements in DESIGN §4):
+# * the FFN hidden layer's ReLU/dropout mask is kept as bits for the data gradient (not re-read from the bf16 f);
+# * the attention keep bits are generated inside the preceding LayerNorm's launch, for the decoder's
+#   cross-attention too (round 4);
+# * weight gradients are not issued per layer on a side stream (no gain: they compete with the backward chain
+#   for the same CUs), nor the keep bits (18.2 vs 17.75 ms/step: the VALU-heavy generator stole the GEMM's CUs).
+GATE_BITS = True
+LN_DROPGEN = True
+LN_DROPGEN_CROSS = True
 
 
 def _empty(shape, dtype, like):
@@ -260,23 +220,9 @@ def ln_bwd(C, x, dy, ln, mean, rstd, dres=None, drop_out=None, drop_seed=0, drop
 # ------------------------------------------------------------------------------------------------ attention
 
 def attn_prepare(C, B, H, Lq, Lk, dh, device):
-    """Draw the attention-dropout seed and, where the resident kernels will consume them, start generating the
-    keep bits on the side stream now — they depend only on (seed, shapes), so they overlap the LayerNorm and
-    Q/K/V projection that precede the attention on the main stream."""
-    prep = {"seed": C.seed(), "dropmask": None, "event": None}
-    if C.cd == torch.bfloat16 and C.attn_impl == "fused" and C.p > 0 and _SIDE_DROPGEN:
-        dm = K.dropmask_buffer(B, H, Lq, Lk, dh, C.p, device)
-        if dm is not None:
-            main = torch.cuda.current_stream(device)
-            side = C.side_stream(device)
-            side.wait_stream(main)             # the buffer's allocation is ordered on the main stream
-            with torch.cuda.stream(side):
-                K.attention_dropgen(B, H, Lq, Lk, dh, C.p, prep["seed"], dm)
-                ev = torch.cuda.Event()
-                ev.record(side)
-            dm.record_stream(side)
-            prep["dropmask"], prep["event"] = dm, ev
-    return prep
+    """Draw the attention-dropout seed (the keep bits themselves come from the preceding LayerNorm's launch where
+    ln_fwd_attn applies, else from the attention forward's own launch)."""
+    return {"seed": C.seed(), "dropmask": None, "event": None}
 
 
 def attn_fwd(C, q, k, v, o, B, H, Lq, Lk, dh, strides, scale, spec, prep=None):

@@ -229,7 +229,6 @@ def encoder_bwd(C, enc, S, dy, gate_feats, ready=None, release_every=None, carry
         nxt = torch.empty(x.shape, dtype=C.cd, device=x.device)
         dx = Bk.enc_layer_bwd(C, layer_S, dx, dx_c, nxt)
         dx_c = nxt
-        C.flush_wgrad_side()
         if by_rounds and i > 0 and C.wq is not None and hi == n:
             per = _queued_tiles(C, q0) // (n - i)
             if i * per + tail <= cus:
@@ -350,7 +349,6 @@ def model_backward(C, model, S, dlogits_c, ready=None):
     # their all-reduce then starts five encoder layers later, still overlapping the rest of the backward
     carry = ready is not None and own and RELEASE_LAYERS == 0
     if own:
-        C.flush_wgrad_side()
         if not carry:
             _release(C, ready, list(model.decoder.parameters()))
     dfeats = encoder_bwd(C, model.encoder, S["e"], denc, gate_feats=True, ready=ready if own else None,

@@ -255,7 +255,7 @@ def xcd_plan(shapes, tile=256, nxcd=8, pack=None):
     """Lay grouped weight-gradient tiles out over the 8 XCDs (workgroup b runs on XCD b % 8): whole groups
     (longest reductions, then largest groups first) go to the least-loaded XCD, so the tiles of a group run on
     one XCD at the same time and share its L2, and every XCD gets about the same work.
-    pack (default ASRX_WGRAD_PACK): additionally pack the groups into rounds of 32 tiles — one workgroup per CU,
+    pack (default WGRAD_PACK): additionally pack the groups into rounds of 32 tiles — one workgroup per CU,
     32 CUs per XCD — so that a group never straddles two rounds (the tiles of a straddling group run a whole
     reduction apart and fetch their shared operand panels twice).
     shapes: (m, n, k) per group (C[m,n], reduction k).  Returns (group order, tiles per group, block -> tile map)."""
@@ -393,16 +393,17 @@ def _grouped_xcd(items, common, kind="p3", adam=None):
     return flops, launch, (dev, part), (queue, fused)
 
 
-# lay each group's tiles on one XCD (ASRX_WGRAD_XCD=0: one table order over all XCDs, A/B)
-WGRAD_XCD = os.environ.get("ASRX_WGRAD_XCD", "1") != "0"
-# pack the groups into 32-tile rounds per XCD (xcd_plan; ASRX_WGRAD_PACK=0: whole groups per XCD).  Neutral for
+# lay each group's tiles on one XCD (False: one table order over all XCDs; module constants the tests patch — their
+# environment switches were removed in round 5)
+WGRAD_XCD = True
+# pack the groups into 32-tile rounds per XCD (xcd_plan; False: whole groups per XCD).  Neutral for
 # the single-GPU step's one grouped launch (13.37-13.40 ms either way), but a multi-GPU backward's decoder release
 # launch is the cross K/V group (96 long tiles) plus short decoder tiles: whole groups put all 96 on one XCD's 32 CUs
 # (three rounds, modelled makespan 747 K-steps) where packed 32-tile chunks spread them (313)
-WGRAD_PACK = os.environ.get("ASRX_WGRAD_PACK", "1") == "1"
-# ws grouped launch from persistent workgroups on per-XCD tile queues (ASRX_WGRAD_QUEUE=0: one workgroup per tile,
-# started by the in-order dispatcher)
-WGRAD_QUEUE = os.environ.get("ASRX_WGRAD_QUEUE", "1") == "1"
+WGRAD_PACK = True
+# ws grouped launch from persistent workgroups on per-XCD tile queues (False: one workgroup per tile, started by the
+# in-order dispatcher)
+WGRAD_QUEUE = True
 
 
 def linear_wgrad_grouped(items, *, beta=1.0, kind=None, adam=None):
@@ -488,7 +489,7 @@ def reduce_rows_grouped(items):
         call("asrx_reduce_rows_grouped", arr, len(chunk), stream())
 
 
-LN_BWD_BLOCKS = int(os.environ.get("ASRX_LN_BWD_BLOCKS", "512"))   # (tools/ln_bench.py: 26.1-26.6 us cold vs 26.7 at 1024)
+LN_BWD_BLOCKS = 512   # (tools/ln_bench.py: 26.1-26.6 us cold vs 26.7 at 1024; 256 measured equal in the step)
 
 
 def layernorm_bwd(x, dy, gamma, mean, rstd, dgb, *, dres=None, dx_drop=None, dropout_p=0.0, seed=0, defer=None):

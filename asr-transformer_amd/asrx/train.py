@@ -326,9 +326,7 @@ class Trainer:
     def _fused_adam_ok(self):
         """AdamW fused into the grouped weight-gradient launch: single GPU (no gradient exchange before the step),
         bf16, FreshGrads, one end-of-backward flush (ASRX_FUSED_ADAM=0: the separate optimizer launch)."""
-        from .blocks import WGRAD_OVERLAP
-        return (FUSED_ADAM and not self.reducer.active and self.model.precision == "bf16" and bool(self._wonly)
-                and not WGRAD_OVERLAP)
+        return FUSED_ADAM and not self.reducer.active and self.model.precision == "bf16" and bool(self._wonly)
 
     def _residual_spans(self, cover):
         """Device [n, 2] table of the flat ranges NOT covered by the fused launch, cut into pieces of at most

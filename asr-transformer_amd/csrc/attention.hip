@@ -1786,11 +1786,10 @@ extern "C" int asrx_attention_fwd(const asrx_attn_desc* d, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   // 128 < Lk <= 256 with more than 64 queries (the c3 encoder self-attention) on the streamed forward too: its K/V
   // arrive in two 128-key chunks, the first computed on while the second lands — in the c3 step 28.7 vs 30.3 us on
-  // the resident kernel, alone 40.4 vs 41.2 (round 4, same box; ASRX_ATTN_STREAM_FWD=0 keeps the resident kernel)
+  // the resident kernel, alone 40.4 vs 41.2 (round 4, same box)
   // (ASRX_ATTN_KERNEL=resident, read per call like =tiled: the resident kernel, for tests of both paths)
-  static const bool sfwd = [] { const char* e = getenv("ASRX_ATTN_STREAM_FWD"); return !(e && e[0] == '0'); }();
   const char* ak = getenv("ASRX_ATTN_KERNEL");
-  const bool take_stream = sfwd && !(ak && !strcmp(ak, "resident")) && a.Lk > 128 && a.Lk <= R_MAXK && a.Lq > 64 &&
+  const bool take_stream = !(ak && !strcmp(ak, "resident")) && a.Lk > 128 && a.Lk <= R_MAXK && a.Lq > 64 &&
                            stream_ok(d, a, true);
   if (!take_stream && resident_ok(d, a) && (!a.thr || a.dropmask)) {
     // dropout: keep bits (key-major for the backward, query-major for this kernel), generated here unless the
@@ -1805,11 +1804,9 @@ extern "C" int asrx_attention_fwd(const asrx_attn_desc* d, void* stream) {
     }
     // 8 waves always: idle query waves still help stage K/V, then leave
     dim3 grid((a.Lq + 255) / 256, a.B * a.H);
-    static const bool w8ok = [] { const char* e = getenv("ASRX_ATTN_W8"); return !(e && e[0] == '0'); }();
-    const bool w8 = w8ok && qmaj && ((a.Lk + 31) >> 5) == 8 && ((uintptr_t)qmaj % 16) == 0;
+    const bool w8 = qmaj && ((a.Lk + 31) >> 5) == 8 && ((uintptr_t)qmaj % 16) == 0;
     // short query blocks (the decoder's cross-attention): 2 query groups x 4 key quarters per head
-    static const bool kq_ok = [] { const char* e = getenv("ASRX_ATTN_KQ"); return !(e && e[0] == '0'); }();
-    if (kq_ok && a.mode == 0 && a.Lq <= 64 && (!qmaj || (((a.Lk + 31) >> 5) == 8 && (uintptr_t)qmaj % 8 == 0))) {
+    if (a.mode == 0 && a.Lq <= 64 && (!qmaj || (((a.Lk + 31) >> 5) == 8 && (uintptr_t)qmaj % 8 == 0))) {
       if (qmaj) hipLaunchKernelGGL((attn_fwd_kq_kernel<true>), grid, dim3(512), 0, st, a, qmaj);
       else hipLaunchKernelGGL((attn_fwd_kq_kernel<false>), grid, dim3(512), 0, st, a, qmaj);
       ASRX_CHECK_LAUNCH();

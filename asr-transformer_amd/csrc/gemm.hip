@@ -868,8 +868,8 @@ template <bool AT, bool BT, int EPI, bool P4>
 void launch_p3(const GemmArgs& g, int ntiles, int splitk, int batch, hipStream_t st) {
   const int per = splitk * batch;
   const int gx = std::max(1, std::min(ntiles, std::max(1, 256 / per)));
-  // XCD-contiguous tile order: measured 1-7% faster on the c3 shapes (ASRX_P3_XCD=0: round-robin, A/B)
-  static const int xcd = [] { const char* e = getenv("ASRX_P3_XCD"); return e ? atoi(e) : 1; }();
+  // XCD-contiguous tile order: measured 1-7% faster on the c3 shapes than round-robin (round 3 A/B)
+  constexpr int xcd = 1;
   if constexpr (P4)
     hipLaunchKernelGGL((gemm_bf16_p4_kernel<AT, BT, EPI>), dim3(gx, splitk, batch), dim3(P_THREADS), 0, st, g, ntiles,
                        xcd);
@@ -1074,7 +1074,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_ring_kernel(GemmArgs g, int nti
 template <int BM, int BN, bool AT, bool BT>
 void dispatch_ring(const GemmArgs& g, int epi, int splitk, int batch, hipStream_t st) {
   const int ntiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
-  static const int xcd = [] { const char* e = getenv("ASRX_RING_XCD"); return e ? atoi(e) : 1; }();
+  constexpr int xcd = 1;   // XCD-contiguous tile order (as p3)
   dim3 grid(xcd ? 8 * ((ntiles + 7) / 8) : ntiles, splitk, batch);
 #define ASRX_CASE(E) \
   case (E): hipLaunchKernelGGL((gemm_bf16_ring_kernel<BM, BN, AT, BT, (E)>), grid, dim3(R_THREADS), 0, st, g, ntiles, xcd); return;
@@ -1454,35 +1454,20 @@ bool epi_instantiated(bool at, bool bt, int epi) {
   return false;
 }
 
-// ASRX_WS=0 keeps the N = 512 encoder GEMMs on p3 (A/B switch; default on)
-bool ws_auto() {
-  static const bool on = [] { const char* e = getenv("ASRX_WS"); return !(e && e[0] == '0'); }();
-  return on;
-}
-// ASRX_WS64=0 keeps the decoder's 4096-row N = 512 GEMMs on the ring kernels (A/B switch; default on): ws with
-// 64 x 128 tiles (64 x 4 = 256 tiles = one per CU) for 2048 <= M < 8192
-bool ws64_auto() {
-  static const bool on = [] { const char* e = getenv("ASRX_WS64"); return !(e && e[0] == '0'); }();
-  return on;
-}
-// ASRX_WS_QKV=0 keeps the 1536-wide Q/K/V projection forwards (bias epilogue) on p3 (A/B switch; default on):
-// tools/blas_ref.py, same box: encoder 42.3 (p3) / 40.8 (p4) -> 37.1 us on ws, decoder (4096 rows) 15.7 -> 12.7 us
-bool ws_qkv_auto() {
-  static const bool on = [] { const char* e = getenv("ASRX_WS_QKV"); return !(e && e[0] == '0'); }();
-  return on;
-}
-// ASRX_WS_MIN_K: shortest reduction planned on ws (A/B; every K from 512 up measured faster than p3 at c3)
-int ws_min_k() {
-  static const int k = [] { const char* e = getenv("ASRX_WS_MIN_K"); return e ? atoi(e) : 64; }();
-  return k;
-}
-
-// ASRX_P4_MIN_TILES: fewest 256x256 tiles for the automatic p4 plan (A/B of the wave quantisation: the c3 Q/K/V
-// projection has 378 such tiles = 1.48 rounds over 256 CUs, 756 p3 tiles = 2.95 rounds)
-int p4_min_tiles() {
-  static const int t = [] { const char* e = getenv("ASRX_P4_MIN_TILES"); return e ? atoi(e) : 400; }();
-  return t;
-}
+// Planner constants (round 5: their A/B environment switches were removed; measurements in DESIGN §4):
+// * ws for the N = 512 encoder GEMMs (faster than p3 at every c3 shape);
+// * ws with 64 x 128 tiles (64 x 4 = 256 tiles = one per CU) for the decoder's 2048 <= M < 8192, N = 512 GEMMs
+//   (faster than the ring kernels);
+// * ws for the 1536-wide Q/K/V projection forwards (bias epilogue): tools/blas_ref.py, same box: encoder 42.3 (p3) /
+//   40.8 (p4) -> 37.1 us on ws, decoder (4096 rows) 15.7 -> 12.7 us;
+// * ws from the shortest reduction up (every K from 512 up measured faster than p3 at c3);
+// * p4 only from 400 256x256 tiles up (wave quantisation: the c3 Q/K/V projection has 378 such tiles = 1.48 rounds
+//   over 256 CUs, 756 p3 tiles = 2.95 rounds).
+constexpr bool ws_auto() { return true; }
+constexpr bool ws64_auto() { return true; }
+constexpr bool ws_qkv_auto() { return true; }
+constexpr int ws_min_k() { return 64; }
+constexpr int p4_min_tiles() { return 400; }
 
 GemmPlan plan_bf16(const asrx_gemm_desc* d, int batch, int splitk) {
   GemmPlan pl;
@@ -1606,7 +1591,8 @@ extern "C" int asrx_gemm_kernel_name(const asrx_gemm_desc* d, char* buf, int len
     snprintf(buf, len, "gemm_bf16_tallk_kernel");
   else if (pl.use == 1 || pl.use == 2)
     snprintf(buf, len, "gemm_bf16_p%d_kernel<%s, %s, %d>", pl.use == 2 ? 4 : 3, tf[!!d->a_trans], tf[!!d->b_trans],
-             pl.epi);
+             pl.use == 2 && (pl.epi == (E_BIAS | E_RELU) || pl.epi == (E_BIAS | E_RELU | E_MASKOUT)) ? pl.epi | E_DROP
+                                                                                                  : pl.epi);
   else if (pl.use >= 5)
     snprintf(buf, len, "gemm_bf16_ring_kernel<%d, 64, %s, %s, %d>", pl.use == 6 ? 128 : 64, tf[!!d->a_trans],
              tf[!!d->b_trans], pl.epi);
@@ -1617,9 +1603,18 @@ extern "C" int asrx_gemm_kernel_name(const asrx_gemm_desc* d, char* buf, int len
 }
 
 // Enqueue the bf16 plan `pl` (asrx_gemm after argument checks).
-int gemm_bf16_run(const asrx_gemm_desc* d, const GemmArgs& g, const GemmPlan& pl, int batch, int splitk,
+int gemm_bf16_run(const asrx_gemm_desc* d, const GemmArgs& g0, const GemmPlan& pl, int batch, int splitk,
                   hipStream_t st) {
-  const int epi = pl.epi;
+  int epi = pl.epi;
+  GemmArgs g = g0;
+  // p4's bias + ReLU (+ mask bits) instantiations without dropout spill registers into the K-loop (the allocator's
+  // margin at ~240 VGPRs; the dropout ones do not): run them as the dropout epilogue with threshold 0 and scale 1 —
+  // every element kept, v * 1.0 = v exactly (eval FFN1 forward 69.9 -> ~57 us alone, round 5)
+  if (pl.use == 2 && (epi == (E_BIAS | E_RELU) || epi == (E_BIAS | E_RELU | E_MASKOUT))) {
+    epi |= E_DROP;
+    g.drop_thr = 0u;
+    g.drop_scale = 1.f;
+  }
   // the bit-mask output is written only by the paired bf16 store path of the fast epilogues
   if (d->mask_out && (!(epi != E_GENERIC && (epi & E_MASKOUT)) || !d->relu || d->c_dtype != ASRX_BF16 || d->n % 32 != 0 ||
                       d->ldc % 8 != 0 || (uintptr_t)d->c % 16 != 0 || (uintptr_t)d->mask_out % 4 != 0 ||
@@ -1627,8 +1622,9 @@ int gemm_bf16_run(const asrx_gemm_desc* d, const GemmArgs& g, const GemmPlan& pl
     return ASRX_ERR_UNSUPPORTED;
   if ((pl.use == 1 || pl.use == 2) && (epi & E_BIAS) && epi != E_GENERIC && d->n > P_BIAS_BYTES / 4) {
     // the p3 bias epilogue stages the whole bias vector in LDS (16 KiB): wider outputs run as column chunks
-    // (fast-path epilogues without dropout only: their element math does not depend on N)
-    if ((epi & E_DROP) || d->a_trans || d->b_trans || batch != 1 || splitk != 1) return ASRX_ERR_UNSUPPORTED;
+    // (fast-path epilogues without dropout only: their element math does not depend on N — the threshold-0 dropout
+    // above keeps every element whatever its hash index)
+    if (((epi & E_DROP) && g.drop_thr != 0u) || d->a_trans || d->b_trans || batch != 1 || splitk != 1) return ASRX_ERR_UNSUPPORTED;
     for (int c0 = 0; c0 < d->n; c0 += P_BIAS_BYTES / 4) {
       GemmArgs gc = g;
       gc.N = std::min(P_BIAS_BYTES / 4, d->n - c0);

@@ -1,6 +1,8 @@
 // Shared pieces of the bf16/f32 GEMM kernels (gemm.hip): kernel arguments, the fused
 // epilogues, LDS image helpers and counted-vmcnt waits.
 #pragma once
+#include <type_traits>
+
 #include "common.h"
 
 namespace asrxg {
@@ -184,10 +186,11 @@ ASRX_DEV void epi_prefetch(EpiPre<EPI, TN, TM>& p, const GemmArgs& g, int m0, in
     }
 }
 
-// pre_gt / pre_rr: the prefetched gate / residual-or-row-add values (PRE), else read here
-template <int EPI, bool PRE = false>
+// pre_gt / pre_rr: the prefetched gate / residual-or-row-add values (PRE), else read here.  IDX: eidx is the
+// element index (uint32) m N + n of the dropout hash, computed incrementally by the caller (else from m, n here)
+template <int EPI, bool PRE = false, bool IDX = false>
 ASRX_DEV f4_t epi_vals(const GemmArgs& g, int m, int n, f4_t v, f4_t b4, uint2 pre_gt = uint2{0u, 0u},
-                       f4_t pre_rr = f4_t{0.f, 0.f, 0.f, 0.f}) {
+                       f4_t pre_rr = f4_t{0.f, 0.f, 0.f, 0.f}, uint32_t eidx = 0u) {
   if constexpr ((EPI & E_ALPHA) != 0) v *= g.alpha;
   if constexpr ((EPI & E_BIAS) != 0) v += b4;
   if constexpr ((EPI & E_ROWADD) != 0) {
@@ -199,7 +202,7 @@ ASRX_DEV f4_t epi_vals(const GemmArgs& g, int m, int n, f4_t v, f4_t b4, uint2 p
     for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
   }
   if constexpr ((EPI & E_DROP) != 0) {   // n % 4 == 0 and N even: two pair hashes cover the 4 elements
-    const uint32_t pb = (uint32_t)((int64_t)m * g.N + n) >> 1;
+    const uint32_t pb = (IDX ? eidx : (uint32_t)((int64_t)m * g.N + n)) >> 1;
     const uint32_t h0 = rng_hash(g.seed, pb), h1 = rng_hash(g.seed, pb + 1);
     v[0] = rng_half(h0, 0) >= g.drop_thr ? v[0] * g.drop_scale : 0.f;
     v[1] = rng_half(h0, 1) >= g.drop_thr ? v[1] * g.drop_scale : 0.f;
@@ -277,15 +280,31 @@ ASRX_DEV int epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int
       // before the first store — a load issued between the stores waits (in-order vmcnt) for all of them, which
       // serialised one load latency per fragment row (FFN2 data gradient 57 -> see DESIGN §4)
       constexpr bool GPL = !PRE && (EPI & E_GBITS) != 0 && (EPI & (E_RESID | E_ROWADD | E_GATE)) == 0;
+      // Per-lane bases of row block 0, each row block j adding a wave-uniform step (round 5): the 64-bit address
+      // and hash-index products the unrolled loop recomputed per fragment (v_mad_u64_u32 and quarter-rate
+      // v_mul_lo_u32, the largest VALU item of the FFN1 forward's epilogue) become one add each.  The dropout hash's
+      // element index (uint32) m N + n wraps exactly as the 64-bit product truncated to 32 bits did.
+      int mr = m0 + wm + (l & 15);
+      // (opaque: keeps the compiler from hoisting the per-lane base products out of a persistent kernel's K-loop,
+      //  where they held registers beside the accumulators for the whole loop)
+      asm volatile("" : "+v"(mr));
+      const int nl = n0 + wn;   // (multiple of 64)
+      bf16_t* const cbase = (bf16_t*)g.c + (int64_t)mr * g.ldc + nl + 16 * (gq & 1) + 8 * (gq >> 1);
+      const int64_t cstep = (int64_t)16 * g.ldc;
+      const uint32_t ibase = (uint32_t)mr * (uint32_t)g.N + (uint32_t)(nl + 4 * gq), istep = 16u * (uint32_t)g.N;
+      uint32_t* const mbase = (EPI & E_MASKOUT) ? (uint32_t*)g.mask_out + (int64_t)mr * g.ld_mask + (nl >> 5) : nullptr;
+      const int64_t mstep = (int64_t)16 * g.ld_mask;
       uint32_t gwl[GPL ? TN / 2 : 1][GPL ? TM : 1];
 
       if constexpr (GPL) {
+        const uint32_t* gbase = (const uint32_t*)g.gate + (int64_t)mr * g.ld_gate + (nl >> 5);
+        const int64_t gstep = (int64_t)16 * g.ld_gate;
 #pragma unroll
         for (int i = 0; i < TN; i += 2)
 #pragma unroll
           for (int j = 0; j < TM; ++j) {
-            const int m = m0 + wm + 16 * j + (l & 15), na = n0 + wn + 16 * i + 4 * gq;
-            gwl[i / 2][j] = (m < g.M && na < g.N) ? ((const uint32_t*)g.gate)[(int64_t)m * g.ld_gate + (na >> 5)] : 0u;
+            const int na = nl + 16 * i + 4 * gq;
+            gwl[i / 2][j] = (mr + 16 * j < g.M && na < g.N) ? gbase[j * gstep + i / 2] : 0u;
           }
       }
       // row-major store order (round 4): per row block j, both fragment pairs i — the two 64-byte halves of each
@@ -294,7 +313,7 @@ ASRX_DEV int epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int
       f4_t bav[TN / 2], bbv[TN / 2];
 #pragma unroll
       for (int i = 0; i < TN; i += 2) {
-        const int na = n0 + wn + 16 * i + 4 * gq, nb = na + 16;
+        const int na = nl + 16 * i + 4 * gq, nb = na + 16;
         f4_t ba = f4_t{0.f, 0.f, 0.f, 0.f}, bb = ba;
         if constexpr ((EPI & E_BIAS) != 0) {
           if constexpr (LB) {
@@ -308,56 +327,70 @@ ASRX_DEV int epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int
         bav[i / 2] = ba;
         bbv[i / 2] = bb;
       }
+      // the tile body, with bounds checks (CHK: a ragged edge tile) or without (a full tile — no exec-mask branch per
+      // fragment)
+      auto tile_body = [&](auto chk_tag) {
+        constexpr bool CHK = decltype(chk_tag)::value;
+        bf16_t* cj = cbase;
+        uint32_t* mj = mbase;
+        uint32_t ij = ibase;
 #pragma unroll
-      for (int j = 0; j < TM; ++j) {
-#pragma unroll
-        for (int i = 0; i < TN; i += 2) {
-          const int na = n0 + wn + 16 * i + 4 * gq, nb = na + 16;
-          const f4_t ba = bav[i / 2], bb = bbv[i / 2];
-          const int ncol = n0 + wn + 16 * (i + (gq & 1)) + 8 * (gq >> 1);
-          const int m = m0 + wm + 16 * j + (l & 15);
-          f4_t va = acc[i][j], vb = acc[i + 1][j];
-          if (m < g.M) {
-            if constexpr (PRE) {
-              if (na < g.N) va = epi_vals<EPI, true>(g, m, na, va, ba, ASRX_PGT(i, j), ASRX_PRR(i, j));
-              if (nb < g.N) vb = epi_vals<EPI, true>(g, m, nb, vb, bb, ASRX_PGT(i + 1, j), ASRX_PRR(i + 1, j));
-            } else if constexpr (GPL) {   // (the gate is the only memory operand of these epilogues)
-              if (na < g.N) va = epi_vals<EPI, true>(g, m, na, va, ba, uint2{gwl[i / 2][j], 0u});
-              if (nb < g.N) vb = epi_vals<EPI, true>(g, m, nb, vb, bb, uint2{gwl[i / 2][j], 0u});
-            } else {
-              if (na < g.N) va = epi_vals<EPI>(g, m, na, va, ba);
-              if (nb < g.N) vb = epi_vals<EPI>(g, m, nb, vb, bb);
+        for (int j = 0; j < TM; ++j, cj += cstep, mj += mstep, ij += istep) {
+          // (opaque: one uniform step register pair, not TM - 1 precomputed multiples of it in scalar registers)
+          asm volatile("" : "+v"(cj));
+          if constexpr ((EPI & E_MASKOUT) != 0) asm volatile("" : "+v"(mj));
+          const int m = mr + 16 * j;
+  #pragma unroll
+          for (int i = 0; i < TN; i += 2) {
+            const int na = nl + 16 * i + 4 * gq, nb = na + 16;
+            const f4_t ba = bav[i / 2], bb = bbv[i / 2];
+            const int ncol = nl + 16 * (i + (gq & 1)) + 8 * (gq >> 1);
+            f4_t va = acc[i][j], vb = acc[i + 1][j];
+            const uint32_t ia = ij + 16u * i, ibb = ia + 16u;
+            if (!CHK || m < g.M) {
+              if constexpr (PRE) {
+                if (!CHK || na < g.N) va = epi_vals<EPI, true, true>(g, m, na, va, ba, ASRX_PGT(i, j), ASRX_PRR(i, j), ia);
+                if (!CHK || nb < g.N) vb = epi_vals<EPI, true, true>(g, m, nb, vb, bb, ASRX_PGT(i + 1, j), ASRX_PRR(i + 1, j), ibb);
+              } else if constexpr (GPL) {   // (the gate is the only memory operand of these epilogues)
+                if (!CHK || na < g.N) va = epi_vals<EPI, true, true>(g, m, na, va, ba, uint2{gwl[i / 2][j], 0u}, f4_t{0.f, 0.f, 0.f, 0.f}, ia);
+                if (!CHK || nb < g.N) vb = epi_vals<EPI, true, true>(g, m, nb, vb, bb, uint2{gwl[i / 2][j], 0u}, f4_t{0.f, 0.f, 0.f, 0.f}, ibb);
+              } else {
+                if (!CHK || na < g.N) va = epi_vals<EPI, false, true>(g, m, na, va, ba, uint2{0u, 0u}, f4_t{0.f, 0.f, 0.f, 0.f}, ia);
+                if (!CHK || nb < g.N) vb = epi_vals<EPI, false, true>(g, m, nb, vb, bb, uint2{0u, 0u}, f4_t{0.f, 0.f, 0.f, 0.f}, ibb);
+              }
+            }
+            const uint32_t ax = pack2bf(va[0], va[1]), ay = pack2bf(va[2], va[3]);
+            const uint32_t bx = pack2bf(vb[0], vb[1]), by = pack2bf(vb[2], vb[3]);
+            const auto sx = __builtin_amdgcn_permlane16_swap(ax, bx, false, false);
+            const auto sy = __builtin_amdgcn_permlane16_swap(ay, by, false, false);
+            if (!CHK || (m < g.M && ncol < g.N)) {
+              v4u_t u = {sx[0], sy[0], sx[1], sy[1]};
+              epi_store(g, (v4u_t*)(cj + 16 * i), u);
+            }
+            if constexpr ((EPI & E_MASKOUT) != 0) {
+              // ReLU outputs are >= 0, so "> 0" is "low 15 bits nonzero": adding 0x7fff to each 15-bit half sets
+              // its bit 15 exactly then (no carry across halves).  The lane's 8 bits (va cols 0-3, vb cols 0-3)
+              // form byte gq of the row's word for the 32 columns [na - 4 gq, +32): mask_bit_pos() below.
+              const uint32_t hi = 0x80008000u, lo = 0x7fff7fffu;
+              const uint32_t ma = ((ax & lo) + lo) & hi, mb = ((ay & lo) + lo) & hi;
+              const uint32_t mc = ((bx & lo) + lo) & hi, md = ((by & lo) + lo) & hi;
+              const uint32_t r = (ma >> 15) | (mb >> 13) | (mc >> 11) | (md >> 9);
+              const uint32_t byte = (r | (r >> 15)) & 0xffu;
+              // the 4 lanes l, l ^ 16, l ^ 32, l ^ 48 hold the 4 bytes of the row's 32-column word: OR-ed together by two
+              // permlane swaps (no register held across the loop), stored as one dword by lane group 0 (16 lanes, one
+              // dword store per fragment pair and row block instead of a byte store per lane)
+              uint32_t wv = byte << (8 * gq);
+              const auto x16 = __builtin_amdgcn_permlane16_swap(wv, wv, false, false);
+              wv = x16[0] | x16[1];
+              const auto x32 = __builtin_amdgcn_permlane32_swap(wv, wv, false, false);
+              wv = x32[0] | x32[1];
+              if (gq == 0 && (!CHK || (m < g.M && na < g.N))) epi_store(g, mj + i / 2, wv);
             }
           }
-          const uint32_t ax = pack2bf(va[0], va[1]), ay = pack2bf(va[2], va[3]);
-          const uint32_t bx = pack2bf(vb[0], vb[1]), by = pack2bf(vb[2], vb[3]);
-          const auto sx = __builtin_amdgcn_permlane16_swap(ax, bx, false, false);
-          const auto sy = __builtin_amdgcn_permlane16_swap(ay, by, false, false);
-          if (m < g.M && ncol < g.N) {
-            v4u_t u = {sx[0], sy[0], sx[1], sy[1]};
-            epi_store(g, (v4u_t*)((bf16_t*)g.c + (int64_t)m * g.ldc + ncol), u);
-          }
-          if constexpr ((EPI & E_MASKOUT) != 0) {
-            // ReLU outputs are >= 0, so "> 0" is "low 15 bits nonzero": adding 0x7fff to each 15-bit half sets
-            // its bit 15 exactly then (no carry across halves).  The lane's 8 bits (va cols 0-3, vb cols 0-3)
-            // form byte gq of the row's word for the 32 columns [na - 4 gq, +32): mask_bit_pos() below.
-            const uint32_t hi = 0x80008000u, lo = 0x7fff7fffu;
-            const uint32_t ma = ((ax & lo) + lo) & hi, mb = ((ay & lo) + lo) & hi;
-            const uint32_t mc = ((bx & lo) + lo) & hi, md = ((by & lo) + lo) & hi;
-            const uint32_t r = (ma >> 15) | (mb >> 13) | (mc >> 11) | (md >> 9);
-            const uint32_t byte = (r | (r >> 15)) & 0xffu;
-            // the 4 lanes l, l ^ 16, l ^ 32, l ^ 48 hold the 4 bytes of the row's 32-column word: OR-ed together by two
-            // permlane swaps (no register held across the loop), stored as one dword by lane group 0 (16 lanes, one
-            // dword store per fragment pair and row block instead of a byte store per lane)
-            uint32_t wv = byte << (8 * gq);
-            const auto x16 = __builtin_amdgcn_permlane16_swap(wv, wv, false, false);
-            wv = x16[0] | x16[1];
-            const auto x32 = __builtin_amdgcn_permlane32_swap(wv, wv, false, false);
-            wv = x32[0] | x32[1];
-            if (gq == 0 && m < g.M && na < g.N) epi_store(g, (uint32_t*)g.mask_out + (int64_t)m * g.ld_mask + (na >> 5), wv);
-          }
         }
-      }
+      };
+      if (EPI != 0 && full) tile_body(std::false_type{});   // (E 0: the fast-path copy spilled)
+      else tile_body(std::true_type{});
       return full ? ((EPI & E_MASKOUT) != 0 ? TN * TM : TN * TM / 2) : 0;
     }
   }

@@ -261,18 +261,11 @@ __global__ __launch_bounds__(256) void ln_bwd512_kernel(const float* __restrict_
     part[(int64_t)blockIdx.x * 2 * D + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
 }
 
-// LN variant selection (asrx_set_tuning ASRX_TUNE_LN_PF / ASRX_LN_PF: rows in flight per wave of the d = 512
-// kernels, default 2 (round 4, c3 step: ln_fwd512 7.49 -> 7.13 us, ln_dropgen 11.27 -> 11.08, ln_bwd512 equal
-// against 1), 8 (ASRX_LN_PF=0) = the general CH x NJ kernels; ASRX_TUNE_LN_BPC / ASRX_LN_BPC: blocks of 4 waves per
-// CU of the forward)
-int ln_pf() {
-  static const int env = [] { const char* e = getenv("ASRX_LN_PF"); return e ? atoi(e) : 2; }();
-  return g_tune_ln_pf == 8 ? 0 : g_tune_ln_pf > 0 ? g_tune_ln_pf : env;
-}
-int ln_bpc() {
-  static const int env = [] { const char* e = getenv("ASRX_LN_BPC"); return e ? atoi(e) : 4; }();
-  return g_tune_ln_bpc > 0 ? g_tune_ln_bpc : env;
-}
+// LN variant selection (asrx_set_tuning ASRX_TUNE_LN_PF: rows in flight per wave of the d = 512 kernels, default 2
+// (round 4, c3 step: ln_fwd512 7.49 -> 7.13 us, ln_dropgen 11.27 -> 11.08, ln_bwd512 equal against 1), 8 = the
+// general CH x NJ kernels; ASRX_TUNE_LN_BPC: blocks of 4 waves per CU of the forward, default 4)
+int ln_pf() { return g_tune_ln_pf == 8 ? 0 : g_tune_ln_pf > 0 ? g_tune_ln_pf : 2; }
+int ln_bpc() { return g_tune_ln_bpc > 0 ? g_tune_ln_bpc : 4; }
 
 // Column sums: stage 1 (per block partial over a row range), stage 2 (sum of partials in block order).
 __global__ __launch_bounds__(256) void colsum_stage1(int dtype, const void* in, int64_t rows, int cols, int64_t ld,
@@ -353,12 +346,8 @@ template <int CH, int NJ>
 bool ln_fwd_launch(int x_dtype, const void* x, int y_dtype, void* y, const float* gamma, const float* beta,
                    float* mean, float* rstd, int64_t rows, int d, float eps, hipStream_t st) {
   if (d != CH * NJ * 64) return false;
-  static const int rw_env = [] {   // rows per wave (ASRX_LN_RW = 1, 2 or 4; default 2: 9.4 -> 8.6 us at 15936 x 512)
-    const char* e = getenv("ASRX_LN_RW");
-    const int v = e ? atoi(e) : 2;
-    return (v == 1 || v == 4) ? v : 2;
-  }();
-  const int rw = g_tune_ln_rw ? g_tune_ln_rw : rw_env;
+  // rows per wave (ASRX_TUNE_LN_RW = 1, 2 or 4; default 2: 9.4 -> 8.6 us at 15936 x 512)
+  const int rw = (g_tune_ln_rw == 1 || g_tune_ln_rw == 4) ? g_tune_ln_rw : 2;
   const unsigned blocks = (unsigned)((rows + 4 * rw - 1) / (4 * rw));
   if (rw == 4)
     hipLaunchKernelGGL((ln_fwd_kernel<CH, NJ, 4>), dim3(blocks), dim3(256), 0, st, x_dtype, x, y_dtype, y, gamma, beta,

@@ -336,36 +336,22 @@ __global__ __launch_bounds__(256) void softmax_bwd_kernel(SmArgs a, void* ds) {
   }
 }
 
-// ASRX_SOFTMAX_NT (A/B switch): bit 0 = non-temporal forward loads, bit 2 = forward stores, bit 1 = backward
-// loads and stores.  Default 4: the forward's probabilities are streamed out non-temporally (cold 30.7 -> 28.7 us
-// at 512 x 249^2 bf16, warm unchanged); non-temporal loads cost the warm case (24.7 -> 26-28 us: the scores a
-// preceding GEMM just wrote sit in the Infinity Cache).  ASRX_SOFTMAX_LPR16 (default 1; 0 = off): rows of
-// 129..256 elements on 16 lanes x 2 vectors (4 rows per wave, two 16-B loads per lane in flight).
-int softmax_nt() {
-  const char* e = getenv("ASRX_SOFTMAX_NT");
-  return e ? atoi(e) : 4;
-}
-
+// The forward's probabilities are streamed out non-temporally (cold 30.7 -> 28.7 us at 512 x 249^2 bf16, warm
+// unchanged); non-temporal loads (forward or backward) cost the warm case (24.7 -> 26-28 us: the scores a
+// preceding GEMM just wrote sit in the Infinity Cache), so loads stay temporal.  (Round 5: the A/B switches of these
+// choices were removed; the measurements stand in DESIGN §4.)
 template <int V, int LPR, int NJ, int U>
 bool try_launch(const SmArgs& a, bool bwd, void* ds, hipStream_t st) {
   if ((int64_t)a.lk > (int64_t)NJ * LPR * V) return false;
   constexpr int RPW = 64 / LPR;
   const int64_t waves = (a.rows + RPW * U - 1) / (RPW * U);
   const unsigned blocks = (unsigned)((waves + 3) / 4);
-  const int nt = softmax_nt();
-  if (bwd) {
-    if (nt & 2) hipLaunchKernelGGL((softmax_bwd_kernel<V, LPR, NJ, U, 3>), dim3(blocks), dim3(256), 0, st, a, ds);
-    else hipLaunchKernelGGL((softmax_bwd_kernel<V, LPR, NJ, U, 0>), dim3(blocks), dim3(256), 0, st, a, ds);
-  } else {
-    const int m = ((nt & 1) ? 1 : 0) | ((nt & 4) ? 2 : 0);
-#define ASRX_SMF(M) hipLaunchKernelGGL((softmax_fwd_kernel<V, LPR, NJ, U, M>), dim3(blocks), dim3(256), 0, st, a)
-    if (m == 0) ASRX_SMF(0); else if (m == 1) ASRX_SMF(1); else if (m == 2) ASRX_SMF(2); else ASRX_SMF(3);
-#undef ASRX_SMF
-  }
+  if (bwd) hipLaunchKernelGGL((softmax_bwd_kernel<V, LPR, NJ, U, 0>), dim3(blocks), dim3(256), 0, st, a, ds);
+  else hipLaunchKernelGGL((softmax_fwd_kernel<V, LPR, NJ, U, 2>), dim3(blocks), dim3(256), 0, st, a);   // NT stores
   return true;
 }
 
-// Short rows (one step per lane) may batch U rows per lane group (ASRX_SOFTMAX_U = 1, 2 or 4; default 1);
+// Short rows (one step per lane) may batch U rows per lane group (asrx_tune softmax_u = 1, 2 or 4; default 1);
 // long rows already keep NJ loads in flight.
 template <int V, int U>
 bool dispatch_u(const SmArgs& a, bool bwd, void* ds, hipStream_t st) {
@@ -374,20 +360,14 @@ bool dispatch_u(const SmArgs& a, bool bwd, void* ds, hipStream_t st) {
 }
 
 int softmax_u() {
-  static const int env = [] {
-    const char* e = getenv("ASRX_SOFTMAX_U");
-    const int v = e ? atoi(e) : 1;
-    return (v == 2 || v == 4) ? v : 1;
-  }();
-  return g_tune_softmax_u ? g_tune_softmax_u : env;
+  return (g_tune_softmax_u == 2 || g_tune_softmax_u == 4) ? g_tune_softmax_u : 1;
 }
 
-// ASRX_SOFTMAX_STREAM (default 1; 0 = off): the persistent streaming forward for bf16, no mask, no dropout output,
-// 128 < Lk <= 256 (ASRX_SOFTMAX_BPC blocks of 4 waves per CU, default 4)
+// The persistent streaming forward for bf16, no mask, no dropout output, 128 < Lk <= 256 (4 blocks of 4 waves
+// per CU)
 bool try_stream(const SmArgs& a, hipStream_t st) {
-  static const bool on = [] { const char* e = getenv("ASRX_SOFTMAX_STREAM"); return !(e && e[0] == '0'); }();
-  static const int bpc = [] { const char* e = getenv("ASRX_SOFTMAX_BPC"); const int v = e ? atoi(e) : 4; return v > 0 ? v : 4; }();
-  if (!on || a.dtype != ASRX_BF16 || a.mode != 0 || a.pd || a.lk <= 128 || a.lk > 256 || a.ld % 8) return false;
+  constexpr int bpc = 4;
+  if (a.dtype != ASRX_BF16 || a.mode != 0 || a.pd || a.lk <= 128 || a.lk > 256 || a.ld % 8) return false;
   const int64_t groups = (a.rows + 3) / 4;
   const unsigned blocks = (unsigned)std::min<int64_t>((groups + 3) / 4, (int64_t)256 * bpc);
   hipLaunchKernelGGL((softmax_fwd_stream_kernel<2>), dim3(blocks), dim3(256), 0, st, a);
@@ -398,8 +378,8 @@ template <int V>
 bool dispatch(const SmArgs& a, bool bwd, void* ds, hipStream_t st) {
   if (V == 8 && !bwd && try_stream(a, st)) return true;
   const int u = softmax_u();
-  static const bool lpr16 = [] { const char* e = getenv("ASRX_SOFTMAX_LPR16"); return !(e && e[0] == '0'); }();
-  if (lpr16 && !bwd && V == 8 && a.lk > 128 && try_launch<V, 16, 2, 1>(a, bwd, ds, st)) return true;
+  // rows of 129..256 elements on 16 lanes x 2 vectors (4 rows per wave, two 16-B loads per lane in flight)
+  if (!bwd && V == 8 && a.lk > 128 && try_launch<V, 16, 2, 1>(a, bwd, ds, st)) return true;
   const bool shortrow = u == 4 ? dispatch_u<V, 4>(a, bwd, ds, st)
                       : u == 2 ? dispatch_u<V, 2>(a, bwd, ds, st) : dispatch_u<V, 1>(a, bwd, ds, st);
   return shortrow || try_launch<V, 64, 2, 1>(a, bwd, ds, st) ||

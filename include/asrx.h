@@ -150,14 +150,14 @@ int asrx_gemm_kernel_name(const asrx_gemm_desc* d, char* buf, int32_t len);
  * operand loads (compute on stale LDS); 0 = normal.  Results are garbage while any flag is set. */
 int asrx_gemm_set_debug(int32_t flags);
 
-/* Process-wide kernel-variant switches (override the environment variables named; value 0 = back to the
- * environment / default).  key ASRX_TUNE_SOFTMAX_U: rows per lane group of the short-row softmax kernels (1, 2, 4;
- * ASRX_SOFTMAX_U); key ASRX_TUNE_LN_RW: rows per wave of the LayerNorm forward (1, 2, 4; ASRX_LN_RW).  Every
- * variant computes the same values; the switch exists so tests and tools can run each one in one process. */
+/* Process-wide kernel-variant switches (value 0 = back to the default; there is no environment fallback since
+ * round 5).  key ASRX_TUNE_SOFTMAX_U: rows per lane group of the short-row softmax kernels (1, 2, 4; default 1);
+ * key ASRX_TUNE_LN_RW: rows per wave of the LayerNorm forward (1, 2, 4; default 2).  Every variant computes the same
+ * values; the switch exists so tests and tools can run each one in one process. */
 #define ASRX_TUNE_SOFTMAX_U 1
 #define ASRX_TUNE_LN_RW 2
 #define ASRX_TUNE_LN_PF 3    /* rows in flight per wave of the d = 512 LayerNorm kernels (1, 2, 4; 8 = the general kernels) */
-#define ASRX_TUNE_LN_BPC 4   /* blocks per CU of the d = 512 LayerNorm forward (1..16; 0 = ASRX_LN_BPC) */
+#define ASRX_TUNE_LN_BPC 4   /* blocks per CU of the d = 512 LayerNorm forward (1..16; 0 = default 4) */
 int asrx_set_tuning(int32_t key, int32_t value);
 
 /* ---------------------------------------------------------------------------------------------------

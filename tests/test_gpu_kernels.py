@@ -391,7 +391,7 @@ def tuning():
 @pytest.mark.parametrize("rw,pf", [(0, 0), (1, 8), (4, 8), (2, 8), (0, 1), (0, 4)])
 @pytest.mark.parametrize("rows", [333, 15936])
 def test_layernorm(d, ydt, rw, pf, rows, tuning):
-    """rw: rows per wave of the general forward (0 = default 2; 1 and 4 are the ASRX_LN_RW variants); pf: rows in
+    """rw: rows per wave of the general forward (0 = default 2; 1 and 4 the other variants); pf: rows in
     flight per wave of the d = 512 streaming kernels (0 = default 2; 8 = the general kernels)."""
     tuning("ln_rw", rw)
     tuning("ln_pf", pf)
@@ -674,7 +674,7 @@ def test_attention_dense_mask_and_dropout_consistency(L, attn_variant, bits):
 @pytest.mark.parametrize("Lk", [24, 64, 127, 249, 999])
 @pytest.mark.parametrize("u", [0, 2, 4])
 def test_softmax_masked(dtype, Lk, u, tuning):
-    """u: rows per lane group of the short-row kernels (0 = default 1; 2 and 4 are the ASRX_SOFTMAX_U variants)."""
+    """u: rows per lane group of the short-row kernels (0 = default 1; 2 and 4 the other variants)."""
     from asrx.kernels import MaskSpec
     tuning("softmax_u", u)
     B, H, Lq = 2, 3, min(Lk, 70)
