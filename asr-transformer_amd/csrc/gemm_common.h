@@ -70,10 +70,9 @@ ASRX_DEV void epilogue4(const GemmArgs& g, int z, int m, int n0, const float* ac
 #pragma unroll
     for (int i = 0; i < 4; ++i) r[i] = rng_keep(g.seed, base + i, g.drop_thr) ? r[i] * g.drop_scale : 0.f;
   }
-  if (g.gate) {
-    const int64_t o = (int64_t)m * g.ld_gate + n0;
+  if (g.gate) {   // (gate_at: bf16 / fp32 values or ASRX_BITS words)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) if (i < nv && !(ld_any(g.gate, g.gate_dtype, o + i) > 0.f)) r[i] = 0.f;
+    for (int i = 0; i < 4; ++i) if (i < nv && !(gate_at(g, m, n0 + i) > 0.f)) r[i] = 0.f;
   }
   if (g.resid) {
     const int64_t o = (int64_t)m * g.ld_resid + n0;
@@ -240,7 +239,8 @@ ASRX_DEV f4_t epi_vals(const GemmArgs& g, int m, int n, f4_t v, f4_t b4, uint2 p
 typedef uint32_t epi_u2_t __attribute__((ext_vector_type(2)));
 template <typename T>
 ASRX_DEV void epi_store(const GemmArgs& g, T* p, T v) {
-  if (g.dbg & 1024) *p = v;
+  if (g.dbg & 2048) asm volatile("" :: "v"(v), "v"(p));   // (diagnostic: the epilogue without its stores)
+  else if (g.dbg & 1024) *p = v;
   else __builtin_nontemporal_store(v, p);
 }
 
@@ -315,14 +315,9 @@ ASRX_DEV int epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int
       for (int i = 0; i < TN; i += 2) {
         const int na = nl + 16 * i + 4 * gq, nb = na + 16;
         f4_t ba = f4_t{0.f, 0.f, 0.f, 0.f}, bb = ba;
-        if constexpr ((EPI & E_BIAS) != 0) {
-          if constexpr (LB) {
-            ba = *(const __attribute__((address_space(3))) f4_t*)(lbias + (na - n0));
-            bb = *(const __attribute__((address_space(3))) f4_t*)(lbias + (nb - n0));
-          } else {
-            if (na < g.N) ba = *(const f4_t*)(g.bias + na);
-            if (nb < g.N) bb = *(const f4_t*)(g.bias + nb);
-          }
+        if constexpr ((EPI & E_BIAS) != 0 && !LB) {
+          if (na < g.N) ba = *(const f4_t*)(g.bias + na);
+          if (nb < g.N) bb = *(const f4_t*)(g.bias + nb);
         }
         bav[i / 2] = ba;
         bbv[i / 2] = bb;
@@ -343,7 +338,12 @@ ASRX_DEV int epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int
   #pragma unroll
           for (int i = 0; i < TN; i += 2) {
             const int na = nl + 16 * i + 4 * gq, nb = na + 16;
-            const f4_t ba = bav[i / 2], bb = bbv[i / 2];
+            // (LDS bias: read at its use — 16 VGPRs fewer held across the row loop than the hoisted copies)
+            f4_t ba = bav[i / 2], bb = bbv[i / 2];
+            if constexpr ((EPI & E_BIAS) != 0 && LB) {
+              ba = *(const __attribute__((address_space(3))) f4_t*)(lbias + (na - n0));
+              bb = *(const __attribute__((address_space(3))) f4_t*)(lbias + (nb - n0));
+            }
             const int ncol = nl + 16 * (i + (gq & 1)) + 8 * (gq >> 1);
             f4_t va = acc[i][j], vb = acc[i + 1][j];
             const uint32_t ia = ij + 16u * i, ibb = ia + 16u;

@@ -14,6 +14,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--step", type=int, default=-1, help="which adam-to-adam interval (default: the last)")
+    ap.add_argument("--by-grid", action="store_true", help="one row per (kernel, grid size): separates the shapes")
     args = ap.parse_args()
     rows = sorted(csv.DictReader(open(args.trace)), key=lambda r: int(r["Start_Timestamp"]))
     adam = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"] or "adam_spans_kernel" in r["Kernel_Name"]]
@@ -26,7 +27,9 @@ def main():
     agg = collections.defaultdict(list)
     for r in seg:
         n = re.sub(r"\(.*", "", r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", ""))
-        agg[n[:70]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+        if args.by_grid:
+            n = n[:60] + " g" + "x".join(r.get(k, "?") for k in ("Grid_Size_X", "Grid_Size_Y", "Grid_Size_Z"))
+        agg[n[:80]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     busy = sum(sum(v) for v in agg.values())
     print(f"one step: {len(seg)} launches, {wall / 1e3:.3f} ms adam-to-adam, {busy / 1e3:.3f} ms of kernel time "
           f"(trace timestamps include each launch's boundary)")
