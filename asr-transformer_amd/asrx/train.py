@@ -36,6 +36,7 @@ EARLY_ADAM = os.environ.get("ASRX_DP_EARLY_ADAM", "0") == "1"
 # one span-table launch (ASRX_FUSED_ADAM=0: the separate optimizer launch over the flat buffers)
 FUSED_ADAM = os.environ.get("ASRX_FUSED_ADAM", "1") == "1"
 ADAM_SPAN = 8192   # elements per workgroup of the residual span-table launch
+ZERO_SPAN = 16384  # elements per workgroup of the per-step gradient zeroing (asrx_zero_spans)
 
 
 def _aligned_spans(spans, n, q=4):
@@ -321,6 +322,9 @@ class Trainer:
                 pos = max(pos, o + k)
             if pos < n:
                 spans.append((pos, n))
+            # (one workgroup per row of the table: long spans — the embedding, the front-end, the positional tables —
+            #  cut into ZERO_SPAN pieces, round 5; a 512 KiB span on one workgroup took most of the launch's 21 us)
+            spans = [(c, min(c + ZERO_SPAN, b)) for a, b in spans for c in range(a, b, ZERO_SPAN)]
             self._zero_spans = torch.tensor(spans, dtype=torch.int64).reshape(-1, 2).to(self.store.grad.device)
 
     def _fused_adam_ok(self):

@@ -15,9 +15,15 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--step", type=int, default=-1, help="which adam-to-adam interval (default: the last)")
     ap.add_argument("--by-grid", action="store_true", help="one row per (kernel, grid size): separates the shapes")
+    ap.add_argument("--marker", default="", help="kernel-name substring that starts a step (default: the optimizer "
+                    "launches; the data-parallel step runs several)")
     args = ap.parse_args()
     rows = sorted(csv.DictReader(open(args.trace)), key=lambda r: int(r["Start_Timestamp"]))
-    adam = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"] or "adam_spans_kernel" in r["Kernel_Name"]]
+    if args.marker:
+        adam = [i - 1 for i, r in enumerate(rows) if args.marker in r["Kernel_Name"] and i > 0]
+    else:
+        adam = [i for i, r in enumerate(rows)
+                if "adam_kernel" in r["Kernel_Name"] or "adam_spans_kernel" in r["Kernel_Name"]]
     if len(adam) < 2:
         raise SystemExit("need two optimizer launches (adam_kernel / adam_spans_kernel) in the trace")
     pairs = list(zip(adam[:-1], adam[1:]))
