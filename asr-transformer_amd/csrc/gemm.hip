@@ -1241,6 +1241,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g) {
 constexpr int TK_ROWS = 32;
 constexpr int TK_MAXN = 576;
 constexpr int TK_STAGE = TK_ROWS * (64 + TK_MAXN) * 2;   // 40 KiB
+// ring depth (round 5: 4 stages = the whole 160 KiB LDS, three in flight during a step; the gathered im2col rows of
+// conv2 are latency-bound — 3 stages, two in flight, ran at 1.6 TB/s)
+constexpr int TK_NST = 4;
 
 // conv2 gather mode (cv.on): B rows are the conv2 im2col rows gathered straight from the channels-last conv1
 // output y1 (g.b): chunk c of row (b, t2, f2) = tap c / 8 (kh, kw), channels 8 (c % 8) .. +7.
@@ -1250,7 +1253,7 @@ struct TallkConv {
 };
 
 __global__ __launch_bounds__(512) void gemm_bf16_tallk_kernel(GemmArgs g, TallkConv cv) {
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[3 * TK_STAGE];
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[TK_NST * TK_STAGE];
   const int z = blockIdx.x, w = threadIdx.x >> 6, l = threadIdx.x & 63, g4 = l >> 4, li = l & 15;
   const int N = g.N, ntt = N >> 4;
   const int k0 = z * g.k_per_split, k1 = min(g.K, k0 + g.k_per_split);
@@ -1264,7 +1267,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tallk_kernel(GemmArgs g, TallkC
   const int opw = (ninst - w + 7) / 8;                   // this wave's pieces per stage
   const int cpr = N / 8;                                 // 16-B chunks per B row
   auto issue = [&](int s) {
-    unsigned char* img = lds + (s % 3) * TK_STAGE;
+    unsigned char* img = lds + (s % TK_NST) * TK_STAGE;
     const int r0 = s * TK_ROWS;
     // gather mode: (b, t2, f2) of the stage's first row once; a lane's row (first + dr, dr < 32) by carries
     int f20 = 0, t20 = 0, b0 = 0;
@@ -1275,6 +1278,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tallk_kernel(GemmArgs g, TallkC
       t20 = q % cv.T2;
       b0 = q / cv.T2;
     }
+    if (g.dbg & 8) return;   // (diagnostic: no operand loads)
     for (int j = w; j < ninst; j += 8) {
       const int slot = j * 64 + l;   // 16-B slot of the stage image
       if (slot < a_bytes / 16) {
@@ -1315,14 +1319,17 @@ __global__ __launch_bounds__(512) void gemm_bf16_tallk_kernel(GemmArgs g, TallkC
   // fragment addressing: lane reads rows 4 g4 + (li >> 2) (+16) at 8-B column 4 (li & 3) of a 16-column tile;
   // (row & 6) is the same for both rows
   const int frow = 4 * g4 + (li >> 2), fsw = frow & 6, fsub = (li >> 1) & 1, fhalf = 4 * (li & 1);
-  if (nsteps > 0) issue(0);
-  if (nsteps > 1) issue(1);
+#pragma unroll
+  for (int i = 0; i < TK_NST - 1; ++i)
+    if (i < nsteps) issue(i);
   for (int s = 0; s < nsteps; ++s) {
-    wait_vmcnt_bs<0, 15>(s + 1 < nsteps ? opw : 0);
+    // stage s landed: this wave's pieces of the younger stages in flight (at most TK_NST - 2 of them) may stay
+    if (g.dbg & 8) wait_vmcnt<0>();
+    else wait_vmcnt_bs<0, 15>(min(TK_NST - 2, nsteps - 1 - s) * opw);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (s + 2 < nsteps) issue(s + 2);
-    const bf16_t* ia = (const bf16_t*)(lds + (s % 3) * TK_STAGE);
+    if (s + TK_NST - 1 < nsteps) issue(s + TK_NST - 1);   // into the buffer step s - 1 released
+    const bf16_t* ia = (const bf16_t*)(lds + (s % TK_NST) * TK_STAGE);
     const bf16_t* ib = ia + TK_ROWS * 64;
     s8_t fa[2];
 #pragma unroll
@@ -1333,6 +1340,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tallk_kernel(GemmArgs g, TallkC
       const s4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4_t*)(p + 16 * 64));
       fa[i] = s8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     }
+    if (g.dbg & 16) continue;   // (diagnostic: no fragment reads / MFMAs)
 #pragma unroll
     for (int j = 0; j < 9; ++j) {
       const int nt = 9 * nq + j;
@@ -1829,6 +1837,7 @@ extern "C" int asrx_conv2_wgrad(const void* dy2, const void* y1, int32_t B, int3
   g.splitk = splitk;
   g.k_per_split = (int)(((rows + BK - 1) / BK + splitk - 1) / splitk) * BK;
   g.ws = ws; g.rowsum = db; g.rowsum_ws = rws;
+  g.dbg = gemm_dbg();
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(gemm_bf16_tallk_kernel, dim3(splitk), dim3(512), 0, st, g,
                      TallkConv{1, F1, T1, F2, T2, y1_bytes});
