@@ -142,6 +142,8 @@ SIGNATURES = {
     "asrx_set_seed_offset": [c_u64, c_vp],
     "asrx_dropout_mask": [c_vp, c_i64, c_f32, c_u64, c_vp],
     "asrx_zero_spans": [c_vp, c_vp, c_i32, c_vp],
+    "asrx_clip_grad_norm": [c_vp, c_i32, c_f32, c_vp, c_i32, c_vp, c_vp],
+    "asrx_remove_after_eos": [c_vp, c_i32, c_i32, c_vp, c_i32, c_i32, c_vp, c_i64, c_vp],
     "asrx_rowwise": [c_i32, c_vp, c_vp, c_vp, c_i64, c_i32, c_i64, c_vp],
     "asrx_transpose_last2": [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp],
     "asrx_step_tokens": [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp],

@@ -1420,6 +1420,104 @@ __global__ __launch_bounds__(256) void zero_spans_kernel(float* __restrict__ bas
   for (int64_t i = a4 + 4 * (int64_t)threadIdx.x; i < b4; i += 1024) *(f4_t*)(base + i) = f4_t{0.f, 0.f, 0.f, 0.f};
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// torch.nn.utils.clip_grad_norm_(parameters, max_norm) (new/train.py:31) over a device table of fp32 gradient
+// tensors {address, numel}: stage 1 — workgroup b sums the squares of its fixed share (chunks c = b mod nparts of
+// every tensor) into part[b] (fixed tree, deterministic); stage 2 — every workgroup adds the nparts partials in
+// order, total = sqrt, coef = min(max_norm / (total + 1e-6), 1), and scales the same share of elements by coef
+// (always, as torch does: x 1.0 is exact).  out[0] = total norm, out[1] = the coefficient (written by block 0).
+namespace {
+constexpr int CLIP_CHUNK = 4096;   // elements per chunk (1024 threads' worth of float4 per 256-thread block x 4)
+
+ASRX_DEV float block_sum256(float v, float* red) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const float t = (red[0] + red[1]) + (red[2] + red[3]);
+  __syncthreads();
+  return t;
+}
+
+template <bool SCALE>
+__global__ __launch_bounds__(256) void clip_spans_kernel(const int64_t* __restrict__ spans, int count, float max_norm,
+                                                         float* __restrict__ part, int nparts, float* __restrict__ out) {
+  __shared__ float red[4];
+  float coef = 1.f;
+  if constexpr (SCALE) {
+    float t = 0.f;
+    for (int i = threadIdx.x; i < nparts; i += 256) t += part[i];   // (fixed order per thread, then a fixed tree)
+    const float total = sqrtf(block_sum256(t, red));
+    coef = fminf(max_norm / (total + 1e-6f), 1.f);
+    if (blockIdx.x == 0 && threadIdx.x == 0) { out[0] = total; out[1] = coef; }
+  }
+  float acc = 0.f;
+  for (int s = 0; s < count; ++s) {
+    float* g = (float*)(uintptr_t)spans[2 * s];
+    const int64_t n = spans[2 * s + 1];
+    const bool vec = ((uintptr_t)g & 15) == 0;
+    for (int64_t c0 = (int64_t)blockIdx.x * CLIP_CHUNK; c0 < n; c0 += (int64_t)nparts * CLIP_CHUNK) {
+      const int64_t c1 = min(n, c0 + CLIP_CHUNK);
+      if (vec && c1 - c0 == CLIP_CHUNK) {
+        for (int64_t i = c0 + 4 * threadIdx.x; i < c1; i += 1024) {
+          f4_t v = *(f4_t*)(g + i);
+          if constexpr (SCALE) *(f4_t*)(g + i) = v * coef;
+          else acc += (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]);
+        }
+      } else {
+        for (int64_t i = c0 + threadIdx.x; i < c1; i += 256) {
+          if constexpr (SCALE) g[i] *= coef;
+          else acc += g[i] * g[i];
+        }
+      }
+    }
+  }
+  if constexpr (!SCALE) {
+    const float t = block_sum256(acc, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = t;
+  }
+}
+
+// new/train.py:122-128 remove_after_eos: per sample i, pred[i, e:] = eos_token and logits[i, e:] = the one-hot row
+// of index e (the reference's quirk: the EOS position, not the EOS token), e = eoses[i].
+__global__ __launch_bounds__(256) void after_eos_kernel(int64_t* __restrict__ pred, int lp, float* __restrict__ logits,
+                                                        int ll, int v, const int64_t* __restrict__ eoses, int64_t eos) {
+  const int i = blockIdx.y;
+  const int64_t e = eoses[i];
+  for (int t = (int)blockIdx.x; t < max(lp, ll); t += (int)gridDim.x) {
+    if (t < e) continue;
+    if (t < lp && threadIdx.x == 0) pred[(int64_t)i * lp + t] = eos;
+    if (t < ll) {
+      float* row = logits + ((int64_t)i * ll + t) * v;
+      for (int k = threadIdx.x; k < v; k += 256) row[k] = (k == e) ? 1.f : 0.f;
+    }
+  }
+}
+}  // namespace
+
+extern "C" int asrx_clip_grad_norm(const int64_t* spans, int32_t count, float max_norm, float* part, int32_t nparts,
+                                   float* out, void* stream) {
+  if (count < 0 || (count > 0 && !spans) || !part || !out || nparts <= 0 || nparts > 4096) return ASRX_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(clip_spans_kernel<false>, dim3(nparts), dim3(256), 0, st, spans, count, max_norm, part, nparts,
+                     out);
+  ASRX_CHECK_LAUNCH();
+  hipLaunchKernelGGL(clip_spans_kernel<true>, dim3(nparts), dim3(256), 0, st, spans, count, max_norm, part, nparts,
+                     out);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
+extern "C" int asrx_remove_after_eos(int64_t* pred, int32_t batch, int32_t pred_len, float* logits, int32_t logit_len,
+                                     int32_t vocab, const int64_t* eoses, int64_t eos_token, void* stream) {
+  if (!pred || !logits || !eoses || batch <= 0 || pred_len <= 0 || logit_len <= 0 || vocab <= 0 || batch > 65535)
+    return ASRX_ERR_ARG;
+  const int rows = std::max(pred_len, logit_len);
+  hipLaunchKernelGGL(after_eos_kernel, dim3((unsigned)std::min(rows, 1024), (unsigned)batch), dim3(256), 0,
+                     (hipStream_t)stream, pred, pred_len, logits, logit_len, vocab, eoses, eos_token);
+  ASRX_CHECK_LAUNCH();
+  return ASRX_OK;
+}
+
 extern "C" int asrx_zero_spans(float* base, const int64_t* spans, int32_t nspans, void* stream) {
   if (nspans < 0 || (nspans > 0 && (!base || !spans))) return ASRX_ERR_ARG;
   if (((uintptr_t)base & 15) != 0) return ASRX_ERR_ARG;

@@ -393,6 +393,19 @@ int asrx_adam_spans(float* p, const float* g, float* m, float* v, void* p_bf16, 
  * (16-B aligned base), one workgroup per span.  The training step zeroes the accumulating gradient regions with it
  * (optimizer.zero_grad, train.py:27, for everything a weight-gradient GEMM does not overwrite). */
 int asrx_zero_spans(float* base, const int64_t* spans, int32_t nspans, void* stream);
+
+/* torch.nn.utils.clip_grad_norm_(parameters, max_norm) (new/train.py:31, round 5): spans = device int64 table
+ * [count][2] of {address of an fp32 gradient tensor, numel}; the total 2-norm over all of them, then every element
+ * times min(max_norm / (norm + 1e-6), 1) (always applied, as torch does).  Deterministic: part = device workspace of
+ * nparts floats (1..4096; one workgroup each, a fixed share of every tensor), out = device float[2] {norm, coef}.
+ * Two launches, no host synchronisation. */
+int asrx_clip_grad_norm(const int64_t* spans, int32_t count, float max_norm, float* part, int32_t nparts, float* out,
+                        void* stream);
+/* new/train.py:122-128 remove_after_eos on the device: for each sample i, pred[i][t] = eos_token for t >= eoses[i]
+ * (pred int64 [batch][pred_len]) and logits[i][t][:] = the one-hot row of index eoses[i] for t >= eoses[i] (fp32
+ * [batch][logit_len][vocab]; the reference writes the EOS *position* as the hot index, kept here). */
+int asrx_remove_after_eos(int64_t* pred, int32_t batch, int32_t pred_len, float* logits, int32_t logit_len,
+                          int32_t vocab, const int64_t* eoses, int64_t eos_token, void* stream);
 /* Teacher-forced step inputs (train.py:22-24,32 without the index_put quirk; model.py:108-115): from the (B, L+1)
  * token rows `text` (targets) and `inp` (decoder input; = text unless shifted), row strides in elements, and the
  * float pad mask (B, L+1): dec_in[b*L+t] = inp[b][t], tgt[b*L+t] = text[b][t+1], valid[b*L+t] = mask[b][t] >= 1. */
