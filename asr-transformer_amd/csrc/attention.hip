@@ -527,14 +527,33 @@ ASRX_DEV float xsum4(float v) {
 //   query-major qmaj[(bh * Lq + q) * qmaj_stride + kw],  bit j = keep(q, key 32 kw + j)           (forward)
 // qmaj_stride = ceil(Lk / 32) for Lk <= 256 (the resident kernels), rounded up to a multiple of 4 past that (the
 // streamed forward moves a 128-key chunk's 4 words per query by one LDS-DMA dword each).
-// grid (nqc, B*H, ceil(Lk / 256)), 256 threads: thread = key (32 queries -> 16 pair hashes), LDS transpose for qmaj.
+// grid (nqc, B*H, ceil(Lk / 256)), 256 threads: thread = key (32 queries -> 16 pair hashes); the query-major words are
+// the key-major ones transposed as a 32 x 32 bit matrix per half-wave, in registers (round 5: five lane-swap stages,
+// ~40 VALU, replacing an LDS staging round and a 32-step bit gather per thread).
 __host__ __device__ inline int qmaj_stride(int lk) {
   const int nkw = (lk + 31) >> 5;
   return lk <= R_MAXK ? nkw : (nkw + 3) & ~3;
 }
 
-ASRX_DEV void dropgen_block(const AttnArgs& a, int qc, int bh, int kblk, int nqc, uint32_t* kmaj, uint32_t* qmaj,
-                            uint32_t* sw) {
+// lane l of each 32-lane half holds row l of a 32 x 32 bit matrix (bit i = column i); returns column l, i.e. bit j
+// of the result = bit l of lane j's word (recursive 2 x 2 block swaps of 16, 8, 4, 2, 1 bits)
+ASRX_DEV uint32_t transpose32(uint32_t x) {
+  const int l = threadIdx.x & 31;
+#define ASRX_TSTAGE(S, M)                                                            \
+  {                                                                                  \
+    const uint32_t p = (uint32_t)__shfl_xor((int)x, S, 32);                          \
+    x = (l & S) ? ((x & ~(M)) | ((p >> S) & (M))) : ((x & (M)) | ((p & (M)) << S)); \
+  }
+  ASRX_TSTAGE(16, 0x0000FFFFu)
+  ASRX_TSTAGE(8, 0x00FF00FFu)
+  ASRX_TSTAGE(4, 0x0F0F0F0Fu)
+  ASRX_TSTAGE(2, 0x33333333u)
+  ASRX_TSTAGE(1, 0x55555555u)
+#undef ASRX_TSTAGE
+  return x;
+}
+
+ASRX_DEV void dropgen_block(const AttnArgs& a, int qc, int bh, int kblk, int nqc, uint32_t* kmaj, uint32_t* qmaj) {
   const int tid = threadIdx.x;
   const int q0 = qc * 32;
   const int key = kblk * R_MAXK + tid;
@@ -549,22 +568,17 @@ ASRX_DEV void dropgen_block(const AttnArgs& a, int qc, int bh, int kblk, int nqc
     }
     kmaj[((int64_t)bh * nqc + qc) * a.Lk + key] = word;
   }
-  sw[tid] = key < a.Lk ? word : 0u;
-  __syncthreads();
+  // (keys past Lk: zero rows of the matrix, the padding bits of the last query-major word)
+  const uint32_t qw = transpose32(word);
   const int ql = tid & 31, kw = kblk * (R_MAXK / 32) + (tid >> 5);
   const int qst = qmaj_stride(a.Lk);
-  if (kw < qst && q0 + ql < a.Lq) {   // (words past ceil(Lk / 32): the padding, zero)
-    uint32_t qw = 0;
-#pragma unroll 8
-    for (int j = 0; j < 32; ++j) qw |= ((sw[32 * (tid >> 5) + j] >> ql) & 1u) << j;
+  if (kw < qst && q0 + ql < a.Lq)   // (words past ceil(Lk / 32): the padding, zero)
     qmaj[((int64_t)bh * a.Lq + q0 + ql) * qst + kw] = qw;
-  }
 }
 
 __global__ __launch_bounds__(256) void attn_dropgen_kernel(AttnArgs a, uint32_t* kmaj, uint32_t* qmaj) {
   a.seed = seed_eff(a.seed);
-  __shared__ uint32_t sw[R_MAXK];
-  dropgen_block(a, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, kmaj, qmaj, sw);
+  dropgen_block(a, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, kmaj, qmaj);
 }
 
 // Horizontal fusion of the attention's LayerNorm (d = 512) and its keep bits: blocks [0, nln) run the LayerNorm
@@ -576,7 +590,6 @@ struct LnJob {
 };
 __global__ __launch_bounds__(256) void ln_dropgen_kernel(AttnArgs a, uint32_t* kmaj, uint32_t* qmaj, LnJob ln,
                                                         int nln) {
-  __shared__ uint32_t sw[R_MAXK];
   if ((int)blockIdx.x < nln) {
     asrxln::ln_fwd512_rows<1>(ln.x, ln.y, ln.gamma, ln.beta, ln.mean, ln.rstd, ln.rows, ln.eps,
                               (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), (int64_t)nln * 4);
@@ -584,7 +597,7 @@ __global__ __launch_bounds__(256) void ln_dropgen_kernel(AttnArgs a, uint32_t* k
   }
   a.seed = seed_eff(a.seed);
   const int nqc = (a.Lq + 31) / 32, nkb = (a.Lk + R_MAXK - 1) / R_MAXK, j = (int)blockIdx.x - nln;
-  dropgen_block(a, (j / nkb) % nqc, j / (nkb * nqc), j % nkb, nqc, kmaj, qmaj, sw);
+  dropgen_block(a, (j / nkb) % nqc, j / (nkb * nqc), j % nkb, nqc, kmaj, qmaj);
 }
 
 // MODE: 0 = no mask, 1 = causal / key-valid / query-valid vectors (folded into per-key biases and lse),
