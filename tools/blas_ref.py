@@ -74,7 +74,7 @@ def main():
     ap.add_argument("--dbg", default="0", help="comma list of asrx_gemm_set_debug flags to time (diagnostics)")
     ap.add_argument("--only", default="", help="comma list of shape names")
     ap.add_argument("--nobias", action="store_true")
-    ap.add_argument("--wgrad", default="p3,p4,p5", help="grouped weight-gradient kinds to time")
+    ap.add_argument("--wgrad", default="ws,p4,p3", help="grouped weight-gradient kinds to time")
     ap.add_argument("--nogrouped", action="store_true")
     ap.add_argument("--noblas", action="store_true")
     args = ap.parse_args()
