@@ -401,3 +401,30 @@ def test_new_over_length_inputs_raise():
     L = m.decoder.pe.pe.shape[1] + 1
     with pytest.raises(ValueError):
         m.decoder(torch.zeros(1, L, dtype=torch.int64), torch.zeros(1, 4, c.n_mels), torch.tensor([4]))
+
+
+def test_device_code_has_no_sgpr_hazard_before_vector_memory():
+    """No VALU write of an SGPR within 5 wait states of a buffer / global instruction reading it and no VALU
+    overwrite of a 16-B store's data right after it, in any built kernel (tools/asm_hazards.py: the compiler pads
+    neither around inline asm; round 5's loader-wave AdamW experiment faulted on the one, corrupted moments by the
+    other)."""
+    import glob
+    import shutil
+    import sys
+    objs = sorted(glob.glob(os.path.join(REPO, "asr-transformer_amd", "asrx", "lib", "*.o")))
+    if not objs or not shutil.which("objcopy") or not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-objdump"):
+        pytest.skip("built objects / ROCm binutils not present")
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    try:
+        import asm_hazards
+    finally:
+        sys.path.pop(0)
+    bad = [(os.path.basename(o), h) for o in objs for h in asm_hazards.scan_text(asm_hazards.disassemble(o))]
+    assert not bad, bad[:5]
+    # the scanner itself sees the faulting pattern
+    assert asm_hazards.scan_text("v_readlane_b32 s83, v253, 57\nbuffer_store_dwordx2 v[2:3], v6, s[80:83], 0 offen")
+    assert not asm_hazards.scan_text(
+        "v_readlane_b32 s83, v253, 57\ns_nop 4\nbuffer_store_dwordx2 v[2:3], v6, s[80:83], 0 offen")
+    assert asm_hazards.scan_text("buffer_store_dwordx4 v[22:25], v39, s[76:79], 0 offen\nv_cndmask_b32_e64 v22, 0, 1, s[80:81]")
+    assert not asm_hazards.scan_text(
+        "buffer_store_dwordx4 v[22:25], v39, s[76:79], 0 offen\ns_nop 1\nv_cndmask_b32_e64 v22, 0, 1, s[80:81]")

@@ -1,0 +1,113 @@
+"""Scan the built device code for two gfx9 hazards the compiler pads for its own instructions but not around an
+inline-asm block (round 5's loader-wave AdamW experiment, DESIGN.md §4, hit both):
+  - a VALU write of an SGPR followed within 5 wait states by a vector-memory instruction reading it (a descriptor
+    restored from a spill by v_readlane right before an asm buffer store: stale descriptor words, a GPU fault);
+  - a vector-memory store of more than 8 bytes followed, with no wait state between, by a VALU write of one of its
+    data VGPRs (the store may send the new value: silently corrupted data).
+
+usage: python tools/asm_hazards.py [objects...]   (default: asr-transformer_amd/asrx/lib/*.o; exit 1 on a hit)
+"""
+import glob
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+TARGET = "hipv4-amdgcn-amd-amdhsa--gfx950"
+_REG = re.compile(r"s\[(\d+):(\d+)\]|\bs(\d+)\b")
+
+
+def _sregs(text):
+    out = set()
+    for m in _REG.finditer(text):
+        if m.group(1):
+            out |= set(range(int(m.group(1)), int(m.group(2)) + 1))
+        else:
+            out.add(int(m.group(3)))
+    return out
+
+
+def _sgpr_defs(inst):
+    """SGPRs a VALU instruction writes (lane reads, VOP3 compares, carry / scale outputs)."""
+    op, _, args = inst.partition(" ")
+    ops = [a.strip() for a in args.split(",")]
+    if op.startswith(("v_readlane", "v_readfirstlane")) or (op.startswith("v_cmp") and op.endswith("_e64")):
+        return _sregs(ops[0])
+    if ("_co_" in op or op.startswith("v_div_scale")) and op.endswith("_e64") and len(ops) > 1:
+        return _sregs(ops[1])
+    return set()
+
+
+_VREG = re.compile(r"v\[(\d+):(\d+)\]|\bv(\d+)\b")
+
+
+def _vregs(text):
+    out = set()
+    for m in _VREG.finditer(text):
+        if m.group(1):
+            out |= set(range(int(m.group(1)), int(m.group(2)) + 1))
+        else:
+            out.add(int(m.group(3)))
+    return out
+
+
+def scan_text(dis):
+    """(line, vmem instruction, writer) for every hit in llvm-objdump / -S output."""
+    insts = []
+    for ln, raw in enumerate(dis.split("\n"), 1):
+        t = raw.split("//")[0].split(";")[0].strip()
+        if not t or t.startswith(".") or t.endswith(":") or t.startswith("<"):
+            continue
+        insts.append((ln, t))
+    hits = []
+    for k, (ln, t) in enumerate(insts):
+        if not t.startswith(("buffer_", "global_", "tbuffer_")):
+            continue
+        op = t.split()[0]
+        if "store" in op and op.endswith(("x3", "x4")) and k + 1 < len(insts):
+            nxt = insts[k + 1][1]
+            data = _vregs(t.partition(" ")[2].split(",")[0] if not op.startswith("global_")
+                          else t.partition(" ")[2].split(",")[1])
+            if nxt.startswith("v_") and _vregs(nxt.partition(" ")[2].split(",")[0]) & data:
+                hits.append((ln, t, nxt))
+        reads = _sregs(t.partition(" ")[2])
+        ws, j = 0, k - 1
+        while j >= 0 and ws < 5:
+            lt = insts[j][1]
+            if lt.startswith("s_nop"):
+                ws += int(lt.split()[1], 0) + 1
+            else:
+                if lt.startswith("v_") and _sgpr_defs(lt) & reads:
+                    hits.append((ln, t, lt))
+                ws += 1
+            j -= 1
+    return hits
+
+
+def disassemble(obj):
+    with tempfile.TemporaryDirectory() as d:
+        fb, co = os.path.join(d, "fb"), os.path.join(d, "co")
+        subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", obj, fb], check=True)
+        subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fb}",
+                        f"--targets={TARGET}", f"--output={co}"], check=True)
+        return subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn", co], check=True,
+                              capture_output=True, text=True).stdout
+
+
+def main(argv):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    objs = argv or sorted(glob.glob(os.path.join(root, "asr-transformer_amd", "asrx", "lib", "*.o")))
+    bad = 0
+    for o in objs:
+        hits = scan_text(disassemble(o))
+        for ln, t, w in hits:
+            print(f"{os.path.basename(o)}:{ln}: {t}  <-  {w}")
+        bad += len(hits)
+    print(f"{len(objs)} objects, {bad} hazards")
+    return 1 if bad else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main(sys.argv[1:]))
