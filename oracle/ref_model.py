@@ -70,8 +70,21 @@ def _ln(P, key, x):
     return F.layer_norm(x, (x.shape[-1],), P[key + ".weight"], P[key + ".bias"], 1e-5)
 
 
-def _drop(x, p, training):
-    return F.dropout(x, p, training) if (training and p > 0) else x
+# Tests only: a callable (site, shape) -> keep mask (bool, broadcastable to shape) that replaces torch's dropout
+# draws, so a training-mode forward / backward can be compared with the HIP path's own masks (the counter hash of
+# csrc/common.h, restated in tests/rng_ref.py).  site: ("attn", head key) for the attention probabilities,
+# ("out", MHA key) for the MHA output, ("ffn", FeedForward key) for the hidden layer, ("emb", "decoder") for the
+# decoder input.  None = nn.Dropout's own masks (the reference).
+DROP_MASKS = None
+
+
+def _drop(x, p, training, site=None):
+    """nn.Dropout (layers.py:27,40,56; model.py:117): x * keep / (1 - p) in training mode."""
+    if not (training and p > 0):
+        return x
+    if DROP_MASKS is not None:
+        return x * DROP_MASKS(site, tuple(x.shape)).to(x.dtype) / (1.0 - p)
+    return F.dropout(x, p, training)
 
 
 def attention_head(P, key, x, kv, mask, d_model, p, training):
@@ -84,7 +97,7 @@ def attention_head(P, key, x, kv, mask, d_model, p, training):
     if mask is not None:
         s = s.masked_fill(mask.gt(0), float("-inf"))
     a = torch.nan_to_num(torch.softmax(s, dim=-1))
-    a = _drop(a, p, training)
+    a = _drop(a, p, training, ("attn", key))
     return torch.bmm(a, v)
 
 
@@ -94,13 +107,13 @@ def multi_head(P, key, x, kv, mask, cfg: OracleConfig, training):
     outs = [attention_head(P, f"{key}._heads.{i}", x, kv, mask, cfg.d_model, cfg.dropout, training)
             for i in range(cfg.n_heads)]
     y = _lin(P, key + "._out_linear", torch.cat(outs, dim=-1))
-    return _drop(y, cfg.dropout, training)
+    return _drop(y, cfg.dropout, training, ("out", key))
 
 
 def feed_forward(P, key, x, cfg: OracleConfig, training):
     """`FeedForward.forward` (layers.py:53-58): squeeze -> ReLU -> dropout -> unsqueeze."""
     h = torch.relu(_lin(P, key + ".squeeze", x))
-    h = _drop(h, cfg.dropout, training)
+    h = _drop(h, cfg.dropout, training, ("ffn", key))
     return _lin(P, key + ".unsqueeze", h)
 
 
@@ -145,7 +158,7 @@ def decoder(P, text, mask, enc, cfg: OracleConfig, training=False):
     pe = pe_table(cfg.dec_len, cfg.d_model)
     m = decoder_mask(mask)
     x = F.embedding(text, P["decoder._embedding.weight"], padding_idx=cfg.pad_id) + pe[: text.shape[1]].unsqueeze(0)
-    x = _drop(x, cfg.dropout, training)
+    x = _drop(x, cfg.dropout, training, ("emb", "decoder"))
     for l in range(cfg.n_dec):
         x = decoder_layer(P, f"decoder._layers.{l}", x, m, enc, cfg, training)
     x = _ln(P, "decoder._norm_layer", x)
