@@ -1040,7 +1040,7 @@ ASRX_DEV void dma4_asm(const void* lds_dst, asrxg::v4i_t srd, uint32_t voff) {
   asrxg::v4i_t d;
 #pragma unroll
   for (int i = 0; i < 4; ++i) d[i] = __builtin_amdgcn_readfirstlane(srd[i]);
-  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, 0 offen lds" ::"s"(m0), "v"(voff), "s"(d)
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds" ::"s"(m0), "v"(voff), "s"(d)
                : "memory", "m0");
 }
 

@@ -470,7 +470,9 @@ ASRX_DEV void wait_vmcnt_rt(int n) { wait_vmcnt_bs<0, 63>(n < 63 ? n : 63); }
 // compiler does not see an LDS write in flight: it then inserts no conservative vmcnt(0) in front of the
 // kernel's LDS fragment reads (it did in some epilogue instantiations), and the kernel's own counted vmcnt
 // waits + barriers order the DMA against its readers.  dst: LDS byte address (wave-uniform, M0); the
-// descriptor words are wave-uniform (SGPRs); voff: per-lane byte offset.
+// descriptor words are wave-uniform (SGPRs); voff: per-lane byte offset.  An SALU write of M0 needs one wait state
+// before an LDS-DMA reads it (the hip guide's LDS-DMA recipe; the compiler pads nothing inside an asm string):
+// the s_nop 0 (tools/asm_hazards.py checks every built DMA).
 typedef int v4i_t __attribute__((ext_vector_type(4)));
 ASRX_DEV v4i_t make_srd(const void* base, int64_t num_bytes) {
   const uint64_t a = (uint64_t)base;
@@ -488,7 +490,7 @@ ASRX_DEV void dma16_asm(const void* lds_dst, v4i_t srd, uint32_t voff) {
   v4i_t d;   // (re-)assert uniformity: a descriptor merged across branches may otherwise sit in VGPRs
 #pragma unroll
   for (int i = 0; i < 4; ++i) d[i] = __builtin_amdgcn_readfirstlane(srd[i]);
-  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0), "v"(voff), "s"(d)
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0), "v"(voff), "s"(d)
                : "memory", "m0");
 }
 

@@ -116,7 +116,7 @@ def run_hip(name, precision, batch=None, frames=None):
     with torch.no_grad():
         for p1, p2 in zip(m.parameters(), twin.parameters()):
             p2.copy_(p1.grad.cpu() if p1.grad is not None else torch.zeros_like(p2))
-    return logits.detach().cpu(), float(loss), twin.state_dict(), drawn, (s, t, k), cfg
+    return logits.detach().cpu(), float(loss.detach()), twin.state_dict(), drawn, (s, t, k), cfg
 
 
 def run_oracle(cfg, batch, masks, autocast=False):

@@ -404,8 +404,8 @@ def test_new_over_length_inputs_raise():
 
 
 def test_device_code_has_no_sgpr_hazard_before_vector_memory():
-    """No VALU write of an SGPR within 5 wait states of a buffer / global instruction reading it and no VALU
-    overwrite of a 16-B store's data right after it, in any built kernel (tools/asm_hazards.py: the compiler pads
+    """No VALU write of an SGPR within 5 wait states of a buffer / global instruction reading it, no VALU
+    overwrite of a 16-B store's data right after it and no LDS-DMA right after an M0 write, in any built kernel (tools/asm_hazards.py: the compiler pads
     neither around inline asm; round 5's loader-wave AdamW experiment faulted on the one, corrupted moments by the
     other)."""
     import glob
@@ -428,3 +428,5 @@ def test_device_code_has_no_sgpr_hazard_before_vector_memory():
     assert asm_hazards.scan_text("buffer_store_dwordx4 v[22:25], v39, s[76:79], 0 offen\nv_cndmask_b32_e64 v22, 0, 1, s[80:81]")
     assert not asm_hazards.scan_text(
         "buffer_store_dwordx4 v[22:25], v39, s[76:79], 0 offen\ns_nop 1\nv_cndmask_b32_e64 v22, 0, 1, s[80:81]")
+    assert asm_hazards.scan_text("s_mov_b32 m0, s4\nbuffer_load_dwordx4 v2, s[28:31], 0 offen lds")
+    assert not asm_hazards.scan_text("s_mov_b32 m0, s4\ns_nop 0\nbuffer_load_dwordx4 v2, s[28:31], 0 offen lds")

@@ -3,7 +3,9 @@ inline-asm block (round 5's loader-wave AdamW experiment, DESIGN.md §4, hit bot
   - a VALU write of an SGPR followed within 5 wait states by a vector-memory instruction reading it (a descriptor
     restored from a spill by v_readlane right before an asm buffer store: stale descriptor words, a GPU fault);
   - a vector-memory store of more than 8 bytes followed, with no wait state between, by a VALU write of one of its
-    data VGPRs (the store may send the new value: silently corrupted data).
+    data VGPRs (the store may send the new value: silently corrupted data);
+  - an SALU write of M0 directly followed by an LDS-DMA (`... lds`) that takes its LDS address from M0 (one wait
+    state needed: the hip guide's LDS-DMA recipe pads it; the DMA statements had not until round 5).
 
 usage: python tools/asm_hazards.py [objects...]   (default: asr-transformer_amd/asrx/lib/*.o; exit 1 on a hit)
 """
@@ -66,6 +68,10 @@ def scan_text(dis):
         if not t.startswith(("buffer_", "global_", "tbuffer_")):
             continue
         op = t.split()[0]
+        if t.rstrip().endswith(" lds") and k > 0:
+            prev = insts[k - 1][1]
+            if prev.startswith("s_") and not prev.startswith("s_nop") and prev.partition(" ")[2].split(",")[0].strip() == "m0":
+                hits.append((ln, t, prev))
         if "store" in op and op.endswith(("x3", "x4")) and k + 1 < len(insts):
             nxt = insts[k + 1][1]
             data = _vregs(t.partition(" ")[2].split(",")[0] if not op.startswith("global_")
