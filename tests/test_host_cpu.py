@@ -405,7 +405,8 @@ def test_new_over_length_inputs_raise():
 
 def test_device_code_has_no_sgpr_hazard_before_vector_memory():
     """No VALU write of an SGPR within 5 wait states of a buffer / global instruction reading it, no VALU
-    overwrite of a 16-B store's data right after it and no LDS-DMA right after an M0 write, in any built kernel (tools/asm_hazards.py: the compiler pads
+    overwrite of a 16-B store's data right after it, no LDS-DMA right after an M0 write and no load's destination
+    touched before a wait that proves it landed, in any built kernel (tools/asm_hazards.py: the compiler pads
     neither around inline asm; round 5's loader-wave AdamW experiment faulted on the one, corrupted moments by the
     other)."""
     import glob
@@ -419,7 +420,10 @@ def test_device_code_has_no_sgpr_hazard_before_vector_memory():
         import asm_hazards
     finally:
         sys.path.pop(0)
-    bad = [(os.path.basename(o), h) for o in objs for h in asm_hazards.scan_text(asm_hazards.disassemble(o))]
+    bad = []
+    for o in objs:
+        dis = asm_hazards.disassemble(o)
+        bad += [(os.path.basename(o), h) for h in asm_hazards.scan_text(dis) + asm_hazards.scan_loads(dis)]
     assert not bad, bad[:5]
     # the scanner itself sees the faulting pattern
     assert asm_hazards.scan_text("v_readlane_b32 s83, v253, 57\nbuffer_store_dwordx2 v[2:3], v6, s[80:83], 0 offen")
@@ -430,3 +434,7 @@ def test_device_code_has_no_sgpr_hazard_before_vector_memory():
         "buffer_store_dwordx4 v[22:25], v39, s[76:79], 0 offen\ns_nop 1\nv_cndmask_b32_e64 v22, 0, 1, s[80:81]")
     assert asm_hazards.scan_text("s_mov_b32 m0, s4\nbuffer_load_dwordx4 v2, s[28:31], 0 offen lds")
     assert not asm_hazards.scan_text("s_mov_b32 m0, s4\ns_nop 0\nbuffer_load_dwordx4 v2, s[28:31], 0 offen lds")
+    # a load's destination read before a wait that proves it landed (an inline-asm load hipcc does not count)
+    two = "global_load_dwordx4 v[2:5], v[0:1], off\nglobal_load_dwordx4 v[6:9], v[0:1], off\ns_waitcnt vmcnt(1)\n"
+    assert not asm_hazards.scan_loads(two + "v_mov_b32 v10, v2")
+    assert asm_hazards.scan_loads(two + "v_mov_b32 v10, v6")

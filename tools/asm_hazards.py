@@ -6,6 +6,11 @@ inline-asm block (round 5's loader-wave AdamW experiment, DESIGN.md §4, hit bot
     data VGPRs (the store may send the new value: silently corrupted data);
   - an SALU write of M0 directly followed by an LDS-DMA (`... lds`) that takes its LDS address from M0 (one wait
     state needed: the hip guide's LDS-DMA recipe pads it; the DMA statements had not until round 5).
+Plus, with --loads, an audit of every vector-memory load into VGPRs: along the fall-through path (up to the next
+branch) no instruction may read or write its destination before an s_waitcnt whose vmcnt proves the load complete
+(in-order completion: vmcnt(N) with fewer than N+1 operations issued after it).  hipcc's own loads pass by
+construction; an inline-asm load (which hipcc does not count) fails it when the compiler copies or reuses the
+destination before the kernel's own wait — garbage values, or a fault where the register held an address.
 
 usage: python tools/asm_hazards.py [objects...]   (default: asr-transformer_amd/asrx/lib/*.o; exit 1 on a hit)
 """
@@ -92,6 +97,51 @@ def scan_text(dis):
     return hits
 
 
+_VMEM = ("buffer_", "global_", "tbuffer_", "flat_", "scratch_")
+_VMCNT = re.compile(r"vmcnt\((\d+)\)")
+
+
+def scan_loads(dis, horizon=4000):
+    """(line, load, first toucher) for every VGPR load used before a wait that proves it complete."""
+    insts = []
+    for ln, raw in enumerate(dis.split("\n"), 1):
+        t = raw.split("//")[0].split(";")[0].strip()
+        if not t or t.startswith(".") or t.endswith(":") or t.startswith("<"):
+            continue
+        insts.append((ln, t))
+    hits = []
+    for k, (ln, t) in enumerate(insts):
+        op, _, args = t.partition(" ")
+        if not op.startswith(_VMEM) or "load" not in op or t.rstrip().endswith(" lds"):
+            continue
+        dst = _vregs(args.split(",")[0])
+        if not dst:
+            continue
+        after = 0
+        for j in range(k + 1, min(len(insts), k + 1 + horizon)):
+            lt = insts[j][1]
+            lop, _, largs = lt.partition(" ")
+            if lop == "s_waitcnt":
+                m = _VMCNT.search(largs)
+                if m and int(m.group(1)) < after + 1 and int(m.group(1)) <= after - 0:
+                    break
+                if m and int(m.group(1)) == 0:
+                    break
+                continue
+            if lop.startswith(("s_branch", "s_cbranch", "s_setpc", "s_endpgm")):
+                break
+            if lop.startswith(_VMEM):
+                if _vregs(largs) & dst:
+                    hits.append((ln, t, lt))
+                    break
+                after += 1
+                continue
+            if _vregs(largs) & dst:
+                hits.append((ln, t, lt))
+                break
+    return hits
+
+
 def disassemble(obj):
     with tempfile.TemporaryDirectory() as d:
         fb, co = os.path.join(d, "fb"), os.path.join(d, "co")
@@ -104,10 +154,13 @@ def disassemble(obj):
 
 def main(argv):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    loads = "--loads" in argv
+    argv = [a for a in argv if a != "--loads"]
     objs = argv or sorted(glob.glob(os.path.join(root, "asr-transformer_amd", "asrx", "lib", "*.o")))
     bad = 0
     for o in objs:
-        hits = scan_text(disassemble(o))
+        dis = disassemble(o)
+        hits = scan_text(dis) + (scan_loads(dis) if loads else [])
         for ln, t, w in hits:
             print(f"{os.path.basename(o)}:{ln}: {t}  <-  {w}")
         bad += len(hits)
