@@ -286,6 +286,53 @@ FWD_MFLOP_PER_FRAME = {"c2": 4.21, "c5": 36.44}
 PEAK_F32_TFLOPS = 157.3   # MI355X fp32 matrix (= vector) peak (MI355X_MICROARCH.md)
 
 
+def new_train_step(name="new_small", batch=32, reps=20):
+    """The `new/` family's training step as new/train.py:17-34 runs it (forward, CrossEntropyLoss on the shifted
+    targets, backward, global-norm clip at 1.0 — asrx.new.clip_grad_norm_, one native reduction — and the caller's
+    torch AdamW), eager, fp32 (the variant's own precision), dropout 0.1, at `name`'s dims: utterances/s and
+    spectrogram frames/s over `reps` steps after 3 warm-up ones (HIP events)."""
+    import asrx.new
+    from oracle import ref_model_new as N
+    c = N.NEW_CONFIGS[name]
+    torch.manual_seed(0)
+    m = asrx.new.Transformer(c.vocab_size, c.n_mels, c.enc_seq_len, c.dec_seq_len, c.hidden_dim, c.n_enc, c.n_dec,
+                             c.n_heads, c.ff_dim, "cuda", dropout=0.1, sr=c.sr, n_fft=c.n_fft, padding_idx=c.pad_id,
+                             eos_token=c.eos_id, bos_token=c.bos_id).cuda().train()
+    spectre, lens, text = N.synthetic_batch(c, batch, seed=99)
+    true = torch.full_like(text, c.eos_id)
+    true[:, :-1] = text[:, 1:]
+    b = {"spectre": spectre.cuda(), "spectrogram_len": lens.cuda(), "encoded_text": text.cuda(),
+         "text_len": lens.cuda(), "true_text": true.cuda()}
+    params = list(m.parameters())
+    opt = torch.optim.AdamW(params, lr=1e-4)
+    ce = torch.nn.CrossEntropyLoss()
+
+    def step():
+        opt.zero_grad()
+        loss = ce(m(b).transpose(1, 2), b["true_text"])
+        loss.backward()
+        asrx.new.clip_grad_norm_(params, 1.0)
+        opt.step()
+        return loss
+
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        loss = step()
+    e1.record()
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    return {"metric": "utterances/s (train step: fwd + CE + bwd + clip 1.0 + AdamW, eager)",
+            "value": round(batch / (ms * 1e-3), 1), "ms_per_step": round(ms, 3),
+            "frames_per_s": round(batch * c.enc_len / (ms * 1e-3), 1), "dtype": "f32", "batch": batch,
+            "frames": c.enc_len, "text_len": c.dec_seq_len, "d_model": c.n_mels, "layers": f"{c.n_enc}+{c.n_dec}",
+            "loss": round(float(loss.detach()), 4),
+            "note": "tiny model (d 80): launch-bound; the variant's own training-script dims (oracle/ref_model_new.py)"}
+
+
 def other_configs(names=("c2", "c5"), reps=5):
     """The BASELINE.json forward configs beside the headline step, timed after it: c2 (configs[1]: fp32 forward,
     B=32, T=512, 6+6 layers d256) against the fp32 matrix peak and c5 (configs[4]: bf16 forward, B=16, T=4000 ->
@@ -611,6 +658,10 @@ def main():
                                              cfg.dropout)
     if rank == 0 and world == 1 and not args.no_other:
         out["other_configs"] = other_configs()
+        try:   # (a supplementary line: an error here must not cost the headline its JSON line)
+            out["other_configs"]["new_small"] = new_train_step()
+        except Exception as ex:   # noqa: BLE001
+            out["other_configs"]["new_small"] = {"error": f"{type(ex).__name__}: {ex}"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, T, L, args.cpu_batch, args.cpu_steps)
     if rank == 0:
