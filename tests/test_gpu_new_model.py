@@ -177,3 +177,54 @@ def test_new_training_steps_reduce_loss():
         opt.step()
         losses.append(float(loss))
     assert losses[-1] < 0.8 * losses[0], losses
+
+
+def test_new_wide_fp32_forward_and_grads_vs_oracle():
+    """The variant beyond the fixtures' toy widths: d_model 256 (4 full-width heads of 256, ff 1024), 4+4 layers,
+    125 encoder frames, 32 text positions — fp32 logits (<= 1e-4) and every parameter gradient of the dropout-0
+    training loss (<= 1e-3, the key-bias rule) against the oracle (oracle/ref_model_new.py, pinned to the
+    reference's fixtures at the toy sizes) run in fp64."""
+    import asrx.new
+    c = N.NewConfig(vocab_size=250, n_mels=256, enc_seq_len=4, dec_seq_len=32, hidden_dim=8, n_enc=4, n_dec=4,
+                    n_heads=4, ff_dim=1024)
+    m = asrx.new.Transformer(c.vocab_size, c.n_mels, c.enc_seq_len, c.dec_seq_len, c.hidden_dim, c.n_enc, c.n_dec,
+                             c.n_heads, c.ff_dim, dev, dropout=0.0, sr=c.sr, n_fft=c.n_fft, padding_idx=c.pad_id,
+                             eos_token=c.eos_id, bos_token=c.bos_id)
+    sd = m.state_dict()
+    sd.update(N.det_params(c, 0))
+    m.load_state_dict(sd)
+    m = m.to(dev).train()
+    s, lens, text = N.synthetic_batch(c, 4, seed=21)
+    batch = {"spectre": s.to(dev), "spectrogram_len": lens.to(dev), "encoded_text": text.to(dev)}
+    logits = m(batch)
+    tgt = targets(text, c.eos_id)
+    loss = torch.nn.functional.cross_entropy(logits.transpose(1, 2), tgt.to(dev))
+    loss.backward()
+    torch.set_num_threads(max(1, min(32, len(os.sched_getaffinity(0)))))
+    P = {k: v.double().requires_grad_(True) for k, v in N.det_params(c, 0).items()}
+    ref = N.forward(P, s.double(), lens, text, c, True)
+    ref_loss = torch.nn.functional.cross_entropy(ref.transpose(1, 2), tgt)
+    ref_loss.backward()
+    e = relerr(logits.detach(), ref.detach())
+    ref_loss = ref_loss.detach()
+    print(f"\nnew d256 4+4 fp32: logits rel err {e:.2e}, loss {float(loss.detach()):.6f} vs {float(ref_loss):.6f}")
+    assert e < 1e-4, e
+    assert abs(float(loss.detach()) - float(ref_loss)) < 1e-5 * abs(float(ref_loss))
+    twin = asrx.new.Transformer(c.vocab_size, c.n_mels, c.enc_seq_len, c.dec_seq_len, c.hidden_dim, c.n_enc, c.n_dec,
+                                c.n_heads, c.ff_dim, dev, dropout=0.0, sr=c.sr, n_fft=c.n_fft, padding_idx=c.pad_id,
+                                eos_token=c.eos_id, bos_token=c.bos_id).to(dev)
+    with torch.no_grad():
+        for (k1, p1), (k2, p2) in zip(m.named_parameters(), twin.named_parameters()):
+            assert k1 == k2
+            p2.copy_(p1.grad if p1.grad is not None else torch.zeros_like(p2))
+    gsd = twin.state_dict()
+    names = [k for k, v in P.items() if v.grad is not None]
+    gmax = max(float(P[k].grad.abs().max()) for k in names)
+    worst = 0.0
+    for k in names:
+        want = P[k].grad
+        den = max(float(want.abs().max()), 1e-4 * gmax)
+        err = float((gsd[k].double().cpu() - want).abs().max()) / den
+        worst = max(worst, err)
+        assert err < 1e-3, (k, err)
+    print(f"{len(names)} gradients, worst {worst:.2e}")
