@@ -62,8 +62,18 @@ def _ln(P, key, x):
     return F.layer_norm(x, (x.shape[-1],), P[key + ".weight"], P[key + ".bias"], 1e-5)
 
 
-def _drop(x, p, training):
-    return F.dropout(x, p, training) if (training and p > 0) else x
+# Tests only (as oracle/ref_model.py): a callable (site, shape) -> keep mask replacing nn.Dropout's draws; site
+# ("attn", head key), ("out", MHA key), ("ffn", FeedForward key) or ("emb", "decoder").  None = torch's dropout.
+DROP_MASKS = None
+
+
+def _drop(x, p, training, site=None):
+    """nn.Dropout (new/layers.py:29,46,63; new/model.py:121): x * keep / (1 - p) in training mode."""
+    if not (training and p > 0):
+        return x
+    if DROP_MASKS is not None:
+        return x * DROP_MASKS(site, tuple(x.shape)).to(x.dtype) / (1.0 - p)
+    return F.dropout(x, p, training)
 
 
 def head(P, key, x, kv, mask, d, p, training):
@@ -75,7 +85,7 @@ def head(P, key, x, kv, mask, d, p, training):
     s = q.bmm(k.transpose(1, 2)) * (d ** -0.5)
     if mask is not None:
         s = s.masked_fill(mask.gt(0), float("-inf"))
-    a = _drop(torch.softmax(s, dim=-1), p, training)
+    a = _drop(torch.softmax(s, dim=-1), p, training, ("attn", key))
     return a.bmm(v)
 
 
@@ -84,12 +94,12 @@ def mha(P, key, x, kv, mask, cfg: NewConfig, training):
     kv = x if kv is None else kv
     hs = torch.cat([head(P, f"{key}.heads.{i}", x, kv, mask, cfg.n_mels, cfg.dropout, training)
                     for i in range(cfg.n_heads)], dim=-1)
-    return _drop(_lin(P, key + ".out", hs), cfg.dropout, training) + x
+    return _drop(_lin(P, key + ".out", hs), cfg.dropout, training, ("out", key)) + x
 
 
 def ffn(P, key, x, cfg: NewConfig, training):
     """new/layers.py:59-64: x + unsqueeze(dropout(relu(squeeze(x))))."""
-    h = _drop(torch.relu(_lin(P, key + ".squeeze", x)), cfg.dropout, training)
+    h = _drop(torch.relu(_lin(P, key + ".squeeze", x)), cfg.dropout, training, ("ffn", key))
     return x + _lin(P, key + ".unsqueeze", h)
 
 
@@ -132,7 +142,7 @@ def decoder(P, text, enc, enc_lens, cfg: NewConfig, training=False):
     amask = (causal + text.eq(cfg.eos_id).unsqueeze(1).expand(-1, L, -1)).gt(0)
     emask = valid_rows(enc_lens, enc.shape[1]).lt(1).unsqueeze(1).expand(-1, cfg.dec_seq_len, -1)
     x = F.embedding(text, P["decoder.emb.weight"], padding_idx=cfg.pad_id) + pe_interleaved(cfg.dec_seq_len, cfg.n_mels)[:L]
-    x = _drop(x, cfg.dropout, training)
+    x = _drop(x, cfg.dropout, training, ("emb", "decoder"))
     for l in range(cfg.n_dec):
         x = decoder_layer(P, f"decoder.layers.{l}", x, amask, enc, emask, npm, cfg, training)
     return F.linear(x, P["decoder.classifier.weight"])

@@ -10,7 +10,9 @@ backward.  Tolerances as tests/test_gpu_model.py / test_gpu_train_parity.py: fp3
 <= 1e-3 (relative, both norms); bf16 (the bench's fused attention + LayerNorm keep-bit path, d_head 64): logits
 within 1.5x the reference's own bf16-autocast error, gradients <= 5e-2 Frobenius / 1.5e-1 max norm or within 1.5x
 that path's own error."""
+import dataclasses
 import os
+import re
 
 import numpy as np
 import pytest
@@ -66,7 +68,7 @@ def mask_provider(seeds, cfg, batch, swap=None):
     def masks(site, shape):
         kind, key = site
         if kind == "attn":
-            mha, head = key.rsplit("._heads.", 1)
+            mha, head = re.match(r"(.*)\._?heads\.(\d+)$", key).groups()   # main `._heads.i`, new/ `.heads.i`
             seed = seeds[("attn", mha)] ^ (1 if ("attn", mha) == swap else 0)
             b, lq, lk = shape
             keep = attn_keep(seed, b * H, lq, lk, P_DROP).reshape(b, H, lq, lk)[:, int(head)]
@@ -204,3 +206,79 @@ def test_dropout_training_step_bf16_matches_oracle_with_same_masks(name, batch, 
     assert e <= 1.5 * e16, (e, e16)
     assert abs(loss - ref_loss) < 1e-2 * abs(ref_loss)
     check_grads(gsd, ref_grads, 5e-2, 1.5e-1, ref16=grads16)
+
+
+def test_new_family_dropout_training_step_matches_oracle_with_same_masks():
+    """The new/ family (post-LN, full-width heads, asrx.new) at new_small dims, fp32, dropout 0.1: logits, loss and
+    every gradient against oracle/ref_model_new.py (fp64) with the HIP path's masks — the same draw order as the
+    main family (per encoder layer: attention probabilities, output, FFN; the decoder embedding; per decoder layer:
+    masked self-attention, cross-attention, FFN)."""
+    import asrx.blocks as Bk
+    import asrx.kernels as K
+    import asrx.new
+    import oracle.ref_model_new as N
+    torch.set_num_threads(max(1, min(32, len(os.sched_getaffinity(0)))))
+    c = N.NEW_CONFIGS["new_small"]
+    m = asrx.new.Transformer(c.vocab_size, c.n_mels, c.enc_seq_len, c.dec_seq_len, c.hidden_dim, c.n_enc, c.n_dec,
+                             c.n_heads, c.ff_dim, dev, dropout=P_DROP, sr=c.sr, n_fft=c.n_fft, padding_idx=c.pad_id,
+                             eos_token=c.eos_id, bos_token=c.bos_id)
+    sd = m.state_dict()
+    sd.update(N.det_params(c, 0))
+    m.load_state_dict(sd)
+    m = m.to(dev).train()
+    s, lens, text = N.synthetic_batch(c, 4, seed=31)
+    tgt = torch.full_like(text, c.eos_id)
+    tgt[:, :-1] = text[:, 1:]
+    batch = {"spectre": s.to(dev), "spectrogram_len": lens.to(dev), "encoded_text": text.to(dev)}
+    K.set_seed_offset(0)
+    torch.cuda.manual_seed(4321)
+    drawn, nxt = [], Bk.Seeds.next
+
+    def record(self):
+        v = nxt(self)
+        drawn.append(v)
+        return v
+
+    Bk.Seeds.next = record
+    try:
+        logits = m(batch)
+    finally:
+        Bk.Seeds.next = nxt
+    loss = torch.nn.functional.cross_entropy(logits.transpose(1, 2), tgt.to(dev))
+    loss.backward()
+    it = iter(drawn)
+    seeds = {}
+    for l in range(c.n_enc):
+        k = f"encoder.layers.{l}"
+        seeds[("attn", k + ".attention")], seeds[("out", k + ".attention")] = next(it), next(it)
+        seeds[("ffn", k + ".ff")] = next(it)
+    seeds[("emb", "decoder")] = next(it)
+    for l in range(c.n_dec):
+        k = f"decoder.layers.{l}"
+        for mha in (".mask_attention", ".attention"):
+            seeds[("attn", k + mha)], seeds[("out", k + mha)] = next(it), next(it)
+        seeds[("ffn", k + ".ff")] = next(it)
+    assert next(it, None) is None
+    cfg_like = type("C", (), {"n_heads": c.n_heads})
+    masks = mask_provider(seeds, cfg_like, None)
+    P = {k: v.double().requires_grad_(True) for k, v in N.det_params(c, 0).items()}
+    old = N.DROP_MASKS
+    N.DROP_MASKS = masks
+    try:   # (the oracle's dropout rate comes from its config: new_small's is the reference constructor's 0.0)
+        ref = N.forward(P, s.double(), lens, text, dataclasses.replace(c, dropout=P_DROP), True)
+    finally:
+        N.DROP_MASKS = old
+    ref_loss = torch.nn.functional.cross_entropy(ref.transpose(1, 2), tgt)
+    ref_loss.backward()
+    e = relerr(logits.detach(), ref.detach())
+    print(f"\nnew_small fp32 dropout {P_DROP}: logits rel err {e:.2e}, loss {float(loss.detach()):.6f} vs "
+          f"{float(ref_loss.detach()):.6f}")
+    assert e < 1e-4, e
+    twin = asrx.new.Transformer(c.vocab_size, c.n_mels, c.enc_seq_len, c.dec_seq_len, c.hidden_dim, c.n_enc, c.n_dec,
+                                c.n_heads, c.ff_dim, dev, dropout=0.0, sr=c.sr, n_fft=c.n_fft, padding_idx=c.pad_id,
+                                eos_token=c.eos_id, bos_token=c.bos_id).to(dev)
+    with torch.no_grad():
+        for p1, p2 in zip(m.parameters(), twin.parameters()):
+            p2.copy_(p1.grad if p1.grad is not None else torch.zeros_like(p2))
+    gsd = {k: v.cpu() for k, v in twin.state_dict().items()}
+    check_grads(gsd, {k: v.grad for k, v in P.items() if v.grad is not None}, 1e-3, 1e-3)
