@@ -135,7 +135,7 @@ def run_oracle(cfg, batch, masks, autocast=False):
             logits = R.forward(P, s.double(), t[:, :-1], k[:, :-1], cfg, True)
         loss = torch.nn.functional.cross_entropy(logits.transpose(1, 2), t[:, 1:])
         loss.backward()
-        return logits.detach(), float(loss), {k_: v.grad for k_, v in P.items()}
+        return logits.detach(), float(loss.detach()), {k_: v.grad for k_, v in P.items()}
     finally:
         R.DROP_MASKS = old
 
