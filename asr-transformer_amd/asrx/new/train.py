@@ -59,9 +59,19 @@ def remove_after_eos(pred, logits, eoses, eos_token):
     if not (pred.is_cuda and logits.is_cuda and pred.dtype == torch.int64 and logits.dtype == torch.float32
             and pred.is_contiguous() and logits.is_contiguous()):
         raise TypeError("asrx.new.train.remove_after_eos: contiguous int64 pred and fp32 logits on the GPU")
-    e = eoses.to(device=pred.device, dtype=torch.int64).contiguous()
     B, lp = pred.shape
     _, ll, v = logits.shape
+    # the reference indexes eos[eoses[i]] (a vocab-sized row): an index outside [-v, v) raises IndexError there, a
+    # negative one counts from the end of the row (and of the pred / logits rows for the slices)
+    # (the kernel trusted eoses.)  Host-side positions are checked here; device-side ones are trusted, as
+    # checking them would cost a host synchronisation per batch — Transformer.evaluate produces them in [0, steps).
+    if not eoses.is_cuda:
+        ec = eoses.detach().to(torch.int64)
+        if ec.numel() and (int(ec.min()) < -v or int(ec.max()) >= v):
+            raise IndexError(f"asrx.new.train.remove_after_eos: an EOS position outside [-{v}, {v})")
+        if ec.numel() and int(ec.min()) < 0:   # Python slicing of pred[i, e:] / logits[i, e:] and eos[e] for e < 0
+            raise NotImplementedError("asrx.new.train.remove_after_eos: negative EOS positions")
+    e = eoses.to(device=pred.device, dtype=torch.int64).contiguous()
     K.call("asrx_remove_after_eos", pred.data_ptr(), B, lp, logits.data_ptr(), ll, v, e.data_ptr(), int(eos_token),
            K.stream())
     return pred, logits
@@ -89,7 +99,8 @@ def word_error_rate(preds, targets):
         pw, tw = p.split(), t.split()
         errors += _edit_distance(pw, tw)
         total += len(tw)
-    return torch.tensor(errors / total if total else 0.0)
+    # as tensors, like torchmetrics: references without words give 0 / 0 = nan (or x / 0 = inf), not 0
+    return torch.tensor(float(errors)) / torch.tensor(float(total))
 
 
 def _to(batch, device):

@@ -136,15 +136,18 @@ def residual_pieces(n, cover, piece=None):
     return out
 
 
-def _minus(a, b, holes):
-    """[a, b) without the (offset, numel) ranges `holes` (sorted): the remaining non-empty runs, in order."""
+def _minus(a, b, holes, align=1):
+    """[a, b) without the (offset, numel) ranges `holes` (sorted): the remaining non-empty runs, in order.  align = 4
+    rounds each hole's end up to a multiple of 4 elements — for runs that feed asrx_adam, which takes 16-B aligned
+    ranges only; holes that are whole parameters of the flat store (every one starts 64-aligned) then end in padding
+    (ADVICE r5)."""
     out, pos = [], a
     for o, k in holes:
         if o + k <= pos or o >= b:
             continue
         if o > pos:
             out.append((pos, o))
-        pos = max(pos, o + k)
+        pos = max(pos, (o + k + align - 1) // align * align)
     if pos < b:
         out.append((pos, b))
     return out
@@ -393,7 +396,7 @@ class Trainer:
                          grad_scale=1.0 / self.reducer.world, decoupled=self.decoupled, hyp=hyp)
             return
         a0, b0 = span if span is not None else (0, self.store.flat.numel())
-        for a, b in _minus(a0, b0, self._frozen):
+        for a, b in _minus(a0, b0, self._frozen, align=4):
             sh = self.store.shadow[a:b] if self.store.shadow is not None else None
             K.adam(self.store.flat[a:b], self.store.grad[a:b], self.m[a:b], self.v[a:b], sh, self.lr, self.betas[0],
                    self.betas[1], self.eps, self.wd, max(1, self.step_count), grad_scale=1.0 / self.reducer.world,

@@ -478,6 +478,33 @@ ASRX_DEV uint32_t bld32(asrxg::v4i_t srd, uint32_t voff, uint32_t soff) {
   asm volatile("buffer_load_dword %0, %1, %2, %3 offen" : "=v"(r) : "v"(voff), "s"(srd), "s"(soff));
   return r;
 }
+// Compiler-visible buffer loads / stores through a descriptor whose base is the first byte a chunk may touch: a raw
+// buffer's range check covers voffset + the instruction offset only, never soffset, so a chunk's start rides in the
+// base (SALU arithmetic on wave-uniform values) and rows / words past the end read as zero or are dropped (ADVICE r5:
+// the round-5 prefetch put the chunk start in soffset and read past the tensors in the tail chunk).  Unlike the
+// inline-asm loads of the forward kernels these are counted by the compiler, which also guards every spill or copy
+// of a register still in flight (round 6: a two-chunk-deep register prefetch as asm loads was miscompiled exactly
+// that way — spills to AGPRs and reused registers before the kernel's own wait, tools/asm_hazards.py --loads).
+// bytes: the buffer's size from base (< 2^31, checked by the launch's size tests); off: the chunk's start (32-bit, wave-
+// uniform).  32-bit scalar arithmetic only (round 6: the int64 clamp compiled to VALU 64-bit compares, ~20 instructions per
+// descriptor at every chunk's fetch).
+ASRX_DEV __amdgpu_buffer_rsrc_t brsrc(const void* base, uint32_t off, int32_t bytes) {
+  const int32_t o = (int32_t)min(off, 0x7fffffffu);
+  const int32_t n = max(bytes - o, 0);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + off), (short)0, n, 0x00020000);
+}
+ASRX_DEV uint2 bufld64(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+  return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, 0, 0));
+}
+ASRX_DEV uint32_t bufld32(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, 0, 0);
+}
+ASRX_DEV void bufst64(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint2 v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u_t, v), r, (int)voff, 0, 0);
+}
+ASRX_DEV void bufst128(__amdgpu_buffer_rsrc_t r, uint32_t voff, f4_t v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u_t, v), r, (int)voff, 0, 0);
+}
 ASRX_DEV uint32_t ld32_asm(const void* p) {
   uint32_t r;
   asm volatile("global_load_dword %0, %1, off" : "=v"(r) : "v"(p));
@@ -1281,7 +1308,7 @@ void attn_fwd_stream_kernel(AttnArgs a, const uint32_t* qmaj) {
 // compare only in blocks that reach above the diagonal.
 // (Round 4 measured issue priority for waves 4-7, counted dQ-store waits and a half-chunk stagger of waves 4-7:
 // all within +-1 %, removed in round 5.)
-template <int MODE, int NKT>
+template <int MODE, int NKT, bool MULTI = false>
 __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
   a.seed = seed_eff(a.seed);
   constexpr int NQB = 2;                                          // Q / dO image buffers
@@ -1302,7 +1329,8 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
   const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, g = l >> 4, li = l & 15;
   // key block (grid.y > 1 only for Lk > NK: the streamed training path) — kb0 + the wave's local 32-key slice
-  const int kb0 = (int)blockIdx.y * NK, nkb = (int)gridDim.y;
+  // (MULTI: several key blocks, gridDim.y > 1 — a template parameter so the dQ store is one straight-line instruction)
+  const int kb0 = MULTI ? (int)blockIdx.y * NK : 0;
   const int kwl = 32 * w, kw0 = kb0 + kwl;
 
   const bf16_t* Kb = a.k + b * a.kb + h * 64;
@@ -1327,10 +1355,7 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
     const int key = kw0 + 16 * t + li;
     const int kc = min(key, a.Lk - 1);
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      kf[t][c] = *(const s8_t*)(Kb + (int64_t)kc * a.kr + 32 * c + 8 * g);
-      vf[t][c] = *(const s8_t*)(Vb + (int64_t)kc * a.vr + 32 * c + 8 * g);
-    }
+    for (int c = 0; c < 2; ++c) vf[t][c] = *(const s8_t*)(Vb + (int64_t)kc * a.vr + 32 * c + 8 * g);
     bool ok = key < a.Lk;
     if (MODE == 1 && ok && a.kvalid) ok = a.kvalid[b * a.validb + key] != 0;
     kbias[t] = ok ? 0.f : -INFINITY;   // rows past Lk hold a clamped copy of the last key: masked here
@@ -1353,36 +1378,25 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
   const bool causal = MODE == 1 && a.causal;
   const int nch = (a.Lq + 31) >> 5;
 
-  // chunk prefetch: 512 16-B pieces (Q rows then dO rows) + 32 lse + 32 delta (+ this lane's dropout words).
-  // Loads go to raw registers from clamped (always valid) addresses; every test on them waits until the chunk
-  // is published or used, so issuing the prefetch never stalls on its own latency.
-  uint2 pq[PRE], pdo[PRE];
-  float praw = 0.f;
+  // chunk prefetch, one chunk ahead: 512 8-B pieces of Q, dO, O and O_lo, 32 lse and this lane's two keep words per
+  // chunk into registers, issued at the top of iteration ch for chunk ch + 1 and published at its end.  (Round 6
+  // measured a second register set two chunks ahead: equal time — enc-self 54.5-54.9 vs 54.2-54.8 us, same box, and
+  // the publish waits it removed reappeared as barrier time: the loads were not the chunk's critical path.)
+  // Each thread stages PRE 8-B pieces of Q AND the same pieces of dO, O and O_lo (piece c: row c / 16, elements
+  // 4 (c % 16) ..): every wave does the same loads and its share of delta (the 16 lanes of a row reduce by DPP).
+  // Buffer loads through per-chunk descriptors (brsrc): each lane's voffset is fixed for the kernel, rows / words
+  // past the end read as zero through the range check, so every load is unconditional.
+  struct Pf { uint2 q[PRE], d[PRE], o[PRE], ol[PRE]; float lse; uint32_t w[2]; };
   const bool usebits = a.thr && a.dropmask;
   const uint32_t* dmb = usebits ? a.dropmask + (int64_t)bh * nch * a.Lk : nullptr;
-  uint32_t dwn[2] = {0u, 0u};
   // delta = rowsum(dO * O) is formed here too: the threads that stage a dO piece also load the matching O
   // piece, dot the 8 elements and reduce over the row's 8 pieces (adjacent lanes) — no separate delta pass.
   const bf16_t* Ob = a.o + b * a.ob + h * 64;
   const bf16_t* Olb = a.o_lo ? a.o_lo + b * a.ob + h * 64 : nullptr;
-  uint2 po[PRE], pol[PRE];
-  // The prefetch is inline-asm loads, waited for by one vmcnt(0) at the start of publish (the compiler does not
-  // count them): with compiler-tracked loads, its conservative merge at the loop head put a vmcnt(0) in front of
-  // the next fetch, which also waited for the dQ stores of the previous chunk (≈1k cycles per chunk).  Every asm
-  // load is UNCONDITIONAL (only its address is selected): a conditionally loaded value reaches its use through a
-  // phi, which the compiler may realise as a register copy issued before the wait — a copy of an in-flight load.
-  // Each thread stages PRE 8-B pieces of Q AND the same pieces of dO, O and O_lo (piece c: row c / 16, elements
-  // 4 (c % 16) ..): every wave does the same loads and its share of delta (the 16 lanes of a row reduce by DPP).
-  // Buffer descriptors of this head's Q / dO / O / O_lo rows, its lse and keep words (round 5): rows and words past
-  // the end read as zero through the descriptor's range check, each lane's voffset is fixed for the kernel and the
-  // chunk's start rides in the SGPR soffset — the prefetch's per-chunk addressing is SALU only (it was a 64-bit
-  // pointer sum per load, ~40 VALU per chunk of a VALU-issue-bound loop).
-  const asrxg::v4i_t srq = asrxg::make_srd(Qb, ((int64_t)(a.Lq - 1) * a.qr + 64) * 2);
-  const asrxg::v4i_t srd = asrxg::make_srd(Db, ((int64_t)(a.Lq - 1) * a.dor + 64) * 2);
-  const asrxg::v4i_t sro = asrxg::make_srd(Ob, ((int64_t)(a.Lq - 1) * a.orr + 64) * 2);
-  const asrxg::v4i_t srol = asrxg::make_srd(Olb ? Olb : Ob, ((int64_t)(a.Lq - 1) * a.orr + 64) * 2);
-  const asrxg::v4i_t srl = asrxg::make_srd(lseb, (int64_t)a.Lq * 4);
-  const asrxg::v4i_t srm = usebits ? asrxg::make_srd(dmb, (int64_t)nch * a.Lk * 4) : srl;
+  // (byte sizes < 2^31: resident_ok / stream_ok)
+  const int32_t nqb = (int32_t)(((int64_t)(a.Lq - 1) * a.qr + 64) * 2), ndb = (int32_t)(((int64_t)(a.Lq - 1) * a.dor + 64) * 2);
+  const int32_t nob = (int32_t)(((int64_t)(a.Lq - 1) * a.orr + 64) * 2), nlb = a.Lq * 4;
+  const int32_t nmb = usebits ? (int32_t)((int64_t)nch * a.Lk * 4) : nlb;
   uint32_t vq[PRE], vdo[PRE], vo[PRE];
 #pragma unroll
   for (int i = 0; i < PRE; ++i) {
@@ -1393,46 +1407,38 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
     vo[i] = (uint32_t)(row * (int)a.orr + dc) * 2u;
   }
   const uint32_t vl = (uint32_t)(tid & 31) * 4u;
+  // (keys past Lk read the next chunk's words, or past the end -> 0; masked at the use)
   const uint32_t vk0 = usebits ? (uint32_t)(kw0 + li) * 4u : 0u, vk1 = usebits ? (uint32_t)(kw0 + 16 + li) * 4u : 0u;
-  auto fetch = [&](int ch) {
+  auto fetch = [&](Pf& P, int ch) {
     const uint32_t q0 = (uint32_t)ch * 32u;
-    const uint32_t sw = usebits ? (uint32_t)ch * (uint32_t)a.Lk * 4u : 0u;
-    dwn[0] = bld32(srm, vk0, sw);
-    dwn[1] = bld32(srm, vk1, sw);
-    const uint32_t sq_ = q0 * (uint32_t)a.qr * 2u, sd_ = q0 * (uint32_t)a.dor * 2u, so_ = q0 * (uint32_t)a.orr * 2u;
+    const __amdgpu_buffer_rsrc_t cm = usebits ? brsrc(dmb, (uint32_t)ch * (uint32_t)a.Lk * 4u, nmb) : brsrc(lseb, 0u, nlb);
+    P.w[0] = bufld32(cm, vk0);
+    P.w[1] = bufld32(cm, vk1);
+    const __amdgpu_buffer_rsrc_t cq = brsrc(Qb, q0 * (uint32_t)a.qr * 2u, nqb), cd = brsrc(Db, q0 * (uint32_t)a.dor * 2u, ndb);
+    const __amdgpu_buffer_rsrc_t co = brsrc(Ob, q0 * (uint32_t)a.orr * 2u, nob);
+    const __amdgpu_buffer_rsrc_t col = brsrc(Olb ? Olb : Ob, q0 * (uint32_t)a.orr * 2u, nob);
 #pragma unroll
     for (int i = 0; i < PRE; ++i) {
-      pq[i] = bld64(srq, vq[i], sq_);
-      pdo[i] = bld64(srd, vdo[i], sd_);
-      po[i] = bld64(sro, vo[i], so_);
-      pol[i] = bld64(srol, vo[i], so_);
+      P.q[i] = bufld64(cq, vq[i]);
+      P.d[i] = bufld64(cd, vdo[i]);
+      P.o[i] = bufld64(co, vo[i]);
+      P.ol[i] = bufld64(col, vo[i]);
     }
-    praw = __uint_as_float(bld32(srl, vl, q0 * 4u));
+    P.lse = __uint_as_float(bufld32(brsrc(lseb, q0 * 4u, nlb), vl));
   };
-  auto publish = [&](int buf, int qbuf, int ch) {
+  auto publish = [&](const Pf& P, int buf, int ch) {
     const int q0 = ch * 32;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int i = 0; i < PRE; ++i) {
-      pin(pq[i]);
-      pin(pdo[i]);
-      pin(po[i]);
-      pin(pol[i]);
-    }
-    pin(praw);
-    pin(dwn[0]);
-    pin(dwn[1]);
 #pragma unroll
     for (int i = 0; i < PRE; ++i) {
       const int c = tid + NTHR * i;
       const int row = c >> 4, dc = (c & 15) * 4;
       const bool qv = q0 + row < a.Lq;
-      *(uint2*)(sq + (qbuf * 32 + row) * R_CS + dc) = qv ? pq[i] : make_uint2(0, 0);
-      *(uint2*)(sdo + (qbuf * 32 + row) * R_CS + dc) = qv ? pdo[i] : make_uint2(0, 0);
+      *(uint2*)(sq + (buf * 32 + row) * R_CS + dc) = P.q[i];   // (rows past Lq read as zero)
+      *(uint2*)(sdo + (buf * 32 + row) * R_CS + dc) = P.d[i];
       // dO . (O + O_lo) over the lane's 4 elements: v_dot2_f32_bf16 on the packed pairs (bf16 products are exact in
       // fp32; 4 instructions instead of unpacking 12 values)
       typedef __bf16 b2_t __attribute__((ext_vector_type(2)));
-      const uint32_t dd[2] = {pdo[i].x, pdo[i].y}, oo[2] = {po[i].x, po[i].y}, ol[2] = {pol[i].x, pol[i].y};
+      const uint32_t dd[2] = {P.d[i].x, P.d[i].y}, oo[2] = {P.o[i].x, P.o[i].y}, ol[2] = {P.ol[i].x, P.ol[i].y};
       float dot = 0.f;
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
@@ -1452,13 +1458,21 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
       const int q = q0 + tid;
       bool live = q < a.Lq;
       if (MODE == 1 && live && a.qvalid) live = a.qvalid[b * a.validb + q] != 0;
-      slse[buf * 32 + tid] = live ? -praw : -INFINITY;
+      slse[buf * 32 + tid] = live ? -P.lse : -INFINITY;
     }
   };
 
   // dQ^T[d][q] = sum_key K^T[d][key] dS^T[key][q] for chunk cc: its 8 (sub-tile, 16-column) tiles, TPW per wave,
-  // every operand read before the MFMA chain (compile-time trip counts, no branches)
+  // every operand read before the MFMA chain (compile-time trip counts, no branches).  Buffer stores: rows past Lq
+  // fall outside the descriptor and are dropped, so no lane condition.
   bf16_t* const dqh = a.dq + b * a.dqb + h * 64;
+  // several key blocks: this block's share of dQ into ITS fp32 partial [blockIdx.y][b][q][h][64] (plain 16-B stores;
+  // dq_finish adds the nkb partials in block order, scales and casts — round 3 added the shares by fp32 atomics into
+  // one accumulator, which serialised on the L2 at c5: 4 key blocks x 128 heads, 477 us per backward)
+  const __amdgpu_buffer_rsrc_t sdq =
+      MULTI ? brsrc(a.dq_acc + (int64_t)blockIdx.y * ((int64_t)a.B * a.Lq * a.H * 64) + ((int64_t)b * a.Lq * a.H + h) * 64,
+                      0u, (int32_t)(((int64_t)(a.Lq - 1) * a.H * 64 + 64) * 4))
+              : brsrc(dqh, 0u, (int32_t)(((int64_t)(a.Lq - 1) * a.dqr + 64) * 2));
   auto dq_chunk = [&](int cc) {
     const int bq = cc & 1, q0 = cc * 32;
 #pragma unroll
@@ -1467,40 +1481,45 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
       const int qs = tl >> 2, u = tl & 3;
       const bf16_t* dsr = sds + (bq * NK + 8 * g + (li >> 2)) * RDT + 16 * qs + 4 * (li & 3);
       const bf16_t* kp = sk + (8 * g + (li >> 2)) * R_VS + 16 * u + 4 * (li & 3);
-      s8_t ka[NKT], da[NKT];
-#pragma unroll
-      for (int kc = 0; kc < NKT; ++kc) {
-        ka[kc] = cat8(lds_tr(kp + 32 * kc * R_VS), lds_tr(kp + (32 * kc + 4) * R_VS));
-        da[kc] = cat8(lds_tr(dsr + 32 * kc * RDT), lds_tr(dsr + (32 * kc + 4) * RDT));
-      }
+      // operands in two halves of NKT / 2 key slices (round 6: all NKT at once held 64 VGPRs; the second prefetch set
+      // needs them)
+      constexpr int HK = NKT / 2;
       f4_t acc = f4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kc = 0; kc < NKT; ++kc) acc = mfma32(ka[kc], da[kc], acc);
-      const int q = min(q0 + 16 * qs + li, a.Lq - 1);   // rows past Lq: duplicate store of the last row's
-      if (nkb > 1) {                                     // (zero-dS) value would be wrong -> guarded below
-        // several key blocks: this block's share of dQ into ITS fp32 partial (plain 16-B stores; dq_finish adds the
-        // nkb partials in block order, scales and casts — round 3 added the shares by fp32 atomics into one
-        // accumulator, which serialised on the L2 at c5: 4 key blocks x 128 heads, 477 us per backward)
-        if (q0 + 16 * qs + li < a.Lq) {
-          float* dst = a.dq_acc + (int64_t)blockIdx.y * ((int64_t)a.B * a.Lq * a.H * 64) +
-                       (((int64_t)b * a.Lq + q) * a.H + h) * 64 + 16 * u + 4 * g;
-          *(f4_t*)dst = acc;
+      for (int hh = 0; hh < 2; ++hh) {
+        s8_t ka[HK], da[HK];
+#pragma unroll
+        for (int k2 = 0; k2 < HK; ++k2) {
+          const int kc = hh * HK + k2;
+          ka[k2] = cat8(lds_tr(kp + 32 * kc * R_VS), lds_tr(kp + (32 * kc + 4) * R_VS));
+          da[k2] = cat8(lds_tr(dsr + 32 * kc * RDT), lds_tr(dsr + (32 * kc + 4) * RDT));
         }
+#pragma unroll
+        for (int k2 = 0; k2 < HK; ++k2) acc = mfma32(ka[k2], da[k2], acc);
+      }
+      const uint32_t q = (uint32_t)(q0 + 16 * qs + li);   // rows past Lq: out of the descriptor's range, dropped
+      if constexpr (MULTI) {
+        bufst128(sdq, (q * (uint32_t)(a.H * 64) + 16u * u + 4u * g) * 4u, acc);
       } else {
         uint2 x;
         x.x = pack2bf(acc[0] * a.scale, acc[1] * a.scale);
         x.y = pack2bf(acc[2] * a.scale, acc[3] * a.scale);
-        if (q0 + 16 * qs + li < a.Lq) {
-          *(uint2*)(dqh + __mul24(q, (int)a.dqr) + 16 * u + 4 * g) = x;
-        }
+        bufst64(sdq, (q * (uint32_t)a.dqr + 16u * u + 4u * g) * 2u, x);
       }
     }
   };
 
   ATTN_TS(0);
-  fetch(0);
-  publish(0, 0, 0);
+  Pf A;
+  fetch(A, 0);
+  publish(A, 0, 0);
   __syncthreads();
+  // this wave's K fragments (B operands of S) from the block's K image (round 5 read K from HBM twice: for the
+  // image and for these; keys past Lk are the image's zero rows)
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) kf[t][c] = lds_b128(sk + (kwl + 16 * t + li) * R_VS + 32 * c + 8 * g);
   ATTN_TS(1);
   s4_t pdb[2][2], dsb[2][2];
   // dV^T += dO^T Pd ; dK^T += Q^T dS   (k-slots: queries 4g+j of sub-tile 0, then of sub-tile 1)
@@ -1522,8 +1541,9 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
 
   // software pipeline: iteration ch computes S/dP/dS/dV/dK of chunk ch AND dQ of chunk ch-1 in one
   // straight-line block (the dQ MFMAs and LDS reads fill the gaps of the softmax-gradient VALU work); one
-  // barrier per chunk publishes dS(ch) and the next chunk's Q/dO.
-  for (int ch = 0; ch < nch; ++ch) {
+  // barrier per chunk publishes dS(ch) and the next chunk's Q/dO.  X holds chunk ch (published) until its keep
+  // words are read, then chunk ch + 1 (in flight until the publish).
+  auto iter = [&](int ch, Pf& X) {
     const int buf = ch & 1, q0 = ch * 32, qb = buf;
     // 4-bit keep masks of this lane's queries (16qs + 4g + r) for its two keys
     uint32_t nib[2][2];
@@ -1532,7 +1552,7 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
     } else if (usebits) {
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        const uint32_t wv = kw0 + 16 * t + li < a.Lk ? dwn[t] : 0u;
+        const uint32_t wv = kw0 + 16 * t + li < a.Lk ? X.w[t] : 0u;
         nib[0][t] = (wv >> (4 * g)) & 15u;
         nib[1][t] = (wv >> (16 + 4 * g)) & 15u;
       }
@@ -1548,7 +1568,7 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
                        ((uint32_t)(rng_half(h23, 0) >= a.thr) << 2) | ((uint32_t)(rng_half(h23, 1) >= a.thr) << 3);
         }
     }
-    fetch(min(ch + 1, nch - 1));   // unconditional (see fetch); the last one re-reads chunk nch-1, unused
+    fetch(X, min(ch + 1, nch - 1));   // unconditional (a conditional fetch made the compiler's merged wait vmcnt(0))
     ATTN_TS(2 + 4 * ch);
     const bf16_t* cq = sq + qb * 32 * R_CS;
     const bf16_t* cdo = sdo + qb * 32 * R_CS;
@@ -1612,29 +1632,43 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
       dvdk(qb);
     }
     ATTN_TS(3 + 4 * ch);
-    if (ch + 1 < nch) publish(buf ^ 1, buf ^ 1, ch + 1);
+    if (ch + 1 < nch) publish(X, buf ^ 1, ch + 1);
     ATTN_TS(5 + 4 * ch);
     __syncthreads();
     ATTN_TS(4 + 4 * ch);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the unused last prefetch
+  };
+  for (int ch = 0; ch < nch; ++ch) iter(ch, A);
   dq_chunk(nch - 1);
 
+  // dK / dV staged through LDS and stored as whole 128-B rows: 8 lanes x 16 B per key row, 4 store instructions per
+  // tensor and wave.  The fragment layout gives each lane 4 values of one row per tile (16 8-B stores per lane at a
+  // row stride): a store-ISSUE-bound tail of ~9k cycles per workgroup (the hip guide's T21 measurement for this
+  // shape), in the c3 cross-attention most of a ~15 us workgroup (round 6: ASRX_ATTN_EXP decomposition).
+  __syncthreads();   // every wave is done with the K / dS / Q / dO images
+  constexpr int ES = 64 + 8;   // staging row stride, 144 B: the 8-B fragment writes are conflict-free
+  bf16_t* stk = (bf16_t*)smem + w * 2 * 32 * ES;   // this wave's [32 keys][ES] dK rows, then its dV rows
+  bf16_t* stv = stk + 32 * ES;
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int key = kw0 + 16 * t + li;
-    if (key >= a.Lk) continue;
-    bf16_t* dkp = a.dk + b * a.dkb + (int64_t)key * a.dkr + h * 64 + 4 * g;
-    bf16_t* dvp = a.dv + b * a.dvb + (int64_t)key * a.dvr + h * 64 + 4 * g;
+  for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       uint2 x;
       x.x = pack2bf(dka[u][t][0] * a.scale, dka[u][t][1] * a.scale);
       x.y = pack2bf(dka[u][t][2] * a.scale, dka[u][t][3] * a.scale);
-      *(uint2*)(dkp + 16 * u) = x;
+      *(uint2*)(stk + (16 * t + li) * ES + 16 * u + 4 * g) = x;
       x.x = pack2bf(dva[u][t][0], dva[u][t][1]);
       x.y = pack2bf(dva[u][t][2], dva[u][t][3]);
-      *(uint2*)(dvp + 16 * u) = x;
+      *(uint2*)(stv + (16 * t + li) * ES + 16 * u + 4 * g) = x;
+    }
+  // (wave-local image: the compiler's lgkmcnt wait orders these reads after the writes; no barrier)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 8 * i + (l >> 3), c8 = (l & 7) * 8, key = kw0 + row;
+    const uint4 vk = *(const uint4*)(stk + row * ES + c8);
+    const uint4 vv = *(const uint4*)(stv + row * ES + c8);
+    if (key < a.Lk) {
+      *(uint4*)(a.dk + b * a.dkb + (int64_t)key * a.dkr + h * 64 + c8) = vk;
+      *(uint4*)(a.dv + b * a.dvb + (int64_t)key * a.dvr + h * 64 + c8) = vv;
     }
   }
 }
@@ -1714,7 +1748,8 @@ bool resident_ok(const asrx_attn_desc* d, const AttnArgs& a) {
   constexpr int64_t L31 = (int64_t)1 << 31;
   const int64_t qs = std::max({(int64_t)a.qr, (int64_t)a.orr, a.dout ? (int64_t)a.dor : 0, a.dout ? (int64_t)a.dqr : 0});
   const int64_t ks = std::max({(int64_t)a.kr, (int64_t)a.vr, a.dout ? (int64_t)a.dkr : 0, a.dout ? (int64_t)a.dvr : 0});
-  const bool s31 = (int64_t)a.Lq * qs < L31 && (int64_t)a.Lk * ks < L31;
+  // (the backward's dQ stores address rows up to Lq + 31, dropped by the descriptor's range: still 32-bit)
+  const bool s31 = ((int64_t)a.Lq + 32) * qs < L31 && (int64_t)a.Lk * ks < L31;
   return d->dh == 64 && a.Lk <= R_MAXK && (a.orr % 4) == 0 && (a.ob % 4) == 0 && s24 && s31;
 }
 
@@ -1728,8 +1763,8 @@ bool stream_ok(const asrx_attn_desc* d, const AttnArgs& a, bool any_lk = false) 
   const bool s24 = a.qr < L24 && a.orr < L24 && a.Lq < L24 && (!a.dout || (a.dor < L24 && a.dqr < L24));
   const int64_t qs = std::max({(int64_t)a.qr, (int64_t)a.orr, a.dout ? (int64_t)a.dor : 0, a.dout ? (int64_t)a.dqr : 0});
   const int64_t ks = std::max({(int64_t)a.kr, (int64_t)a.vr, a.dout ? (int64_t)a.dkr : 0, a.dout ? (int64_t)a.dvr : 0});
-  const bool s31 = (int64_t)a.Lq * qs < L31 && ((int64_t)a.Lk + R_MAXK) * ks * 2 < L31 &&
-                   (int64_t)a.Lq * qmaj_stride(a.Lk) * 4 < L31;
+  const bool s31 = ((int64_t)a.Lq + 32) * qs < L31 && ((int64_t)a.Lk + R_MAXK) * ks * 2 < L31 &&
+                   (int64_t)a.Lq * qmaj_stride(a.Lk) * 4 < L31 && ((int64_t)a.Lq + 32) * a.H * 64 * 4 < L31;
   return a.orr % 4 == 0 && a.ob % 4 == 0 && a.kr % 8 == 0 && a.vr % 8 == 0 && ((uintptr_t)a.k % 16) == 0 &&
          ((uintptr_t)a.v % 16) == 0 && s24 && s31;
 }
@@ -1890,7 +1925,10 @@ extern "C" int asrx_attention_bwd(const asrx_attn_desc* d, void* stream) {
     if (nkb > 1 && !a.dq_acc) return ASRX_ERR_ARG;   // key blocks store their dQ partials into dq_acc[blockIdx.y]
     const dim3 grid(a.B * a.H, nkb), blk(64 * nkt);
 #define ASRX_BWD_RES(M, N) hipLaunchKernelGGL((attn_bwd_res_kernel<M, N>), grid, blk, sm, st, a)
-    if (a.mode == 0) { if (nkt == 2) ASRX_BWD_RES(0, 2); else if (nkt == 4) ASRX_BWD_RES(0, 4); else ASRX_BWD_RES(0, 8); }
+    if (nkb > 1) {   // (nkb > 1 implies nkt = 8; the key-block path takes mode 0 / 1 only: stream_ok)
+      if (a.mode == 0) hipLaunchKernelGGL((attn_bwd_res_kernel<0, 8, true>), grid, blk, sm, st, a);
+      else hipLaunchKernelGGL((attn_bwd_res_kernel<1, 8, true>), grid, blk, sm, st, a);
+    } else if (a.mode == 0) { if (nkt == 2) ASRX_BWD_RES(0, 2); else if (nkt == 4) ASRX_BWD_RES(0, 4); else ASRX_BWD_RES(0, 8); }
     else if (a.mode == 1) { if (nkt == 2) ASRX_BWD_RES(1, 2); else if (nkt == 4) ASRX_BWD_RES(1, 4); else ASRX_BWD_RES(1, 8); }
     else { if (nkt == 2) ASRX_BWD_RES(2, 2); else if (nkt == 4) ASRX_BWD_RES(2, 4); else ASRX_BWD_RES(2, 8); }
 #undef ASRX_BWD_RES

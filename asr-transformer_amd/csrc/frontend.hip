@@ -1451,11 +1451,18 @@ __global__ __launch_bounds__(256) void clip_spans_kernel(const int64_t* __restri
     if (blockIdx.x == 0 && threadIdx.x == 0) { out[0] = total; out[1] = coef; }
   }
   float acc = 0.f;
+  // chunk c of span s goes to block (pre_s + c) mod nparts, pre_s = the chunks of the spans before it: consecutive
+  // small tensors start on consecutive blocks instead of all on block 0; each block still walks its
+  // chunks in one fixed order, so the sums stay deterministic
+  int64_t pre = 0;
   for (int s = 0; s < count; ++s) {
     float* g = (float*)(uintptr_t)spans[2 * s];
     const int64_t n = spans[2 * s + 1];
     const bool vec = ((uintptr_t)g & 15) == 0;
-    for (int64_t c0 = (int64_t)blockIdx.x * CLIP_CHUNK; c0 < n; c0 += (int64_t)nparts * CLIP_CHUNK) {
+    const int64_t nck = (n + CLIP_CHUNK - 1) / CLIP_CHUNK;
+    const int64_t first = ((int64_t)blockIdx.x - pre % nparts + nparts) % nparts;
+    pre += nck;
+    for (int64_t c0 = first * CLIP_CHUNK; c0 < n; c0 += (int64_t)nparts * CLIP_CHUNK) {
       const int64_t c1 = min(n, c0 + CLIP_CHUNK);
       if (vec && c1 - c0 == CLIP_CHUNK) {
         for (int64_t i = c0 + 4 * threadIdx.x; i < c1; i += 1024) {

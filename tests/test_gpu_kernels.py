@@ -601,6 +601,56 @@ def test_attention_short_query_block_with_dropout(Lq, Lk, with_lo):
     assert relerr(dkv[:, d:].float().cpu().view(B, Lk, H, dh).transpose(1, 2), vh.grad) < 2e-2
 
 
+@pytest.mark.parametrize("Lq,Lk", [(249, 249), (64, 249), (57, 1031)])
+def test_attention_tensors_at_allocation_end(Lq, Lk):
+    """Q, dO, O, O_lo and lse as the LAST bytes of their own device allocations (12 MiB each: torch gives such a
+    request a segment of exactly that size), Lq % 32 != 0: the backward's tail chunk must not read past them (ADVICE
+    r5 — the round-5 prefetch put the chunk start in the descriptor's soffset, which the range check ignores) and the
+    results equal those of ordinary allocations bit for bit (the dQ stores past Lq are dropped by the descriptor)."""
+    from asrx.kernels import MaskSpec
+    B, H, dh = 1, 2, 64
+    d = H * dh
+    g = torch.Generator().manual_seed(Lq + 7 * Lk)
+    q, kv, _ = _mk(B, H, Lq, Lk, dh, "none", g)
+    qb, kvd = bf(q).to(dev), bf(kv).to(dev)
+    dO = bf(torch.randn(B, Lq, d, generator=g)).to(dev)
+    p, seed, scale = 0.1, 99, d ** -0.5
+    st = ((d, Lq * d), (2 * d, Lk * 2 * d), (2 * d, Lk * 2 * d), (d, Lq * d))
+    gst = ((d, Lq * d), (d, Lq * d), (2 * d, Lk * 2 * d), (2 * d, Lk * 2 * d))
+    seg = 12 << 20
+
+    def tail(n, dtype):   # the last n elements of a fresh 12 MiB allocation
+        esz = torch.tensor([], dtype=dtype).element_size()
+        return torch.empty(seg // esz, device=dev, dtype=dtype)[-n:]
+
+    def run(at_end):
+        q_ = tail(B * Lq * d, torch.bfloat16) if at_end else torch.empty(B * Lq * d, device=dev, dtype=torch.bfloat16)
+        q_.copy_(qb.reshape(-1))
+        do_ = tail(B * Lq * d, torch.bfloat16) if at_end else torch.empty_like(q_)
+        do_.copy_(dO.reshape(-1))
+        o = tail(B * Lq * d, torch.bfloat16) if at_end else torch.empty_like(q_)
+        o_lo = tail(B * Lq * d, torch.bfloat16) if at_end else torch.empty_like(q_)
+        q2, do2, o2, ol2 = (t.view(B * Lq, d) for t in (q_, do_, o, o_lo))
+        dm = K().dropmask_buffer(B, H, Lq, Lk, dh, p, dev)
+        lse = K().attention_fwd(q2, kvd, kvd[..., d:], o2, B, H, Lq, Lk, dh, st, scale, MaskSpec(), p, seed,
+                                dropmask=dm, o_lo=ol2)
+        if at_end:
+            lt = tail(lse.numel(), torch.float32)
+            lt.copy_(lse.reshape(-1))
+            lse = lt.view_as(lse)
+        dq = torch.empty(B * Lq, d, device=dev, dtype=torch.bfloat16)
+        dkv = torch.empty(B * Lk, 2 * d, device=dev, dtype=torch.bfloat16)
+        K().attention_bwd(q2, kvd, kvd[..., d:], o2, lse, do2, dq, dkv, dkv[:, d:], B, H, Lq, Lk, dh, st, gst,
+                          scale, MaskSpec(), p, seed, dropmask=dm, o_lo=ol2)
+        torch.cuda.synchronize()
+        return o2.clone(), dq, dkv
+
+    ref = run(False)
+    got = run(True)
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("attn_variant", ["auto", "tiled"], indirect=True)
 @pytest.mark.parametrize("L", [40, 249, 300])
 @pytest.mark.parametrize("bits", [False, True])

@@ -15,6 +15,9 @@ def test_word_error_rate_matches_the_torchmetrics_definition():
     assert float(word_error_rate("the cat sat", "the cat sat")) == 0.0
     assert float(word_error_rate(["one two three"], ["one three"])) == pytest.approx(1 / 2)   # one insertion
     assert float(word_error_rate([""], ["a b"])) == pytest.approx(1.0)
+    import math
+    assert math.isnan(float(word_error_rate([""], [""])))         # torchmetrics' tensor 0 / 0
+    assert math.isinf(float(word_error_rate(["a"], [""])))        # x / 0
 
 
 gpu = pytest.mark.gpu

@@ -131,7 +131,11 @@ def scan_loads(dis, horizon=4000):
             if lop.startswith(("s_branch", "s_cbranch", "s_setpc", "s_endpgm")):
                 break
             if lop.startswith(_VMEM):
-                if _vregs(largs) & dst:
+                # a younger LOAD that only overwrites the register (its destination, not its address) is no hazard:
+                # loads return in issue order, so the younger value lands last (compiler spill reloads do this)
+                lparts = largs.split(",")
+                only_dst = "load" in lop and not (_vregs(",".join(lparts[1:])) & dst)
+                if _vregs(largs) & dst and not only_dst:
                     hits.append((ln, t, lt))
                     break
                 after += 1

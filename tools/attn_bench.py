@@ -68,6 +68,9 @@ def main():
     ap.add_argument("--variant", default="auto")
     ap.add_argument("--sweep", action="store_true", help="Lq sweep at Lk=249 (per-chunk vs fixed cost)")
     ap.add_argument("--dbg", action="store_true", help="phase timestamps of block 0 / wave 0 of the backward")
+    ap.add_argument("--exp", default="", help="comma list of ASRX_ATTN_EXP values for the backward (a diagnostic "
+                    "build's timing-only switches, wrong results: 1 no loop barrier, 2 no chunk fetch, 4 no dQ sweep, "
+                    "8 no dV/dK MFMAs)")
     args = ap.parse_args()
     os.environ["ASRX_ATTN_KERNEL"] = args.variant
     cases = {"enc": ("enc_self", 249, 249, False), "cross": ("cross", 64, 249, False),
@@ -118,6 +121,16 @@ def main():
                         break
                     print(f"  chunk {ch}: fetch-issued {a - t0:7d}  compute {b - a:6d}  publish {d - b:6d}  "
                           f"barrier {c - d:6d}")
+        return
+    if args.exp:
+        for key in args.only.split(","):
+            name, fwd, bwd, ff, fb = case(*cases[key])
+            fwd()
+            for e in args.exp.split(","):
+                os.environ["ASRX_ATTN_EXP"] = e
+                tb = timeit(bwd, args.reps)
+                print(f"{name:9s} exp {e:>3s} bwd {tb*1e3:7.1f}us", flush=True)
+            os.environ.pop("ASRX_ATTN_EXP", None)
         return
     for key in args.only.split(","):
         name, fwd, bwd, ff, fb = case(*cases[key])
