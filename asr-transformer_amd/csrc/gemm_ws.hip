@@ -554,13 +554,16 @@ ASRX_DEV void wsgq_body(const GroupEnt* __restrict__ ents, const uint16_t* __res
     __syncthreads();
     const int i = s_slot;
     __syncthreads();   // every wave has read s_slot before the next grab overwrites it
-    if (i >= depth) {
+    // (unsigned compares: a counter that was not zeroed before the launch — e.g. a negative one — reads as an empty
+    //  queue instead of indexing block_tile out of range; the round-5 graph-table experiment that faulted is
+    //  analysed in DESIGN.md §4 round 6)
+    if ((unsigned)i >= (unsigned)depth) {
       if (++q == 8) break;
       continue;
     }
     const int slot = xq + 8 * i;
     const int t_all = (int)block_tile[slot];
-    if (t_all >= ntiles) continue;
+    if ((unsigned)t_all >= (unsigned)ntiles) continue;
     wsg_tile<EPI>(ents, tile_group, t_all, slot, dbg, lds, cnt + 16, part, &s_last, ad);
     __syncthreads();   // the epilogue's staging image is dead before the next tile's LDS-DMA
   }
