@@ -1308,18 +1308,31 @@ void attn_fwd_stream_kernel(AttnArgs a, const uint32_t* qmaj) {
 // compare only in blocks that reach above the diagonal.
 // (Round 4 measured issue priority for waves 4-7, counted dQ-store waits and a half-chunk stagger of waves 4-7:
 // all within +-1 %, removed in round 5.)
+// backward LDS image offsets (elements): K image rows of 64, dS^T image rows of 32, 16-B chunks XOR-swizzled by row
+ASRX_DEV int bk_kswz(int r) { return 2 * (((r >> 1) + 2 * (r >> 3)) & 3); }
+ASRX_DEV int bk_dswz(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) << 1); }
+ASRX_DEV int bk_koff(int r, int e) { return r * 64 + 8 * ((e >> 3) ^ bk_kswz(r)) + (e & 7); }
+ASRX_DEV int bk_doff(int r, int e) { return r * 32 + 8 * ((e >> 3) ^ bk_dswz(r)) + (e & 7); }
+
 template <int MODE, int NKT, bool MULTI = false>
 __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
   a.seed = seed_eff(a.seed);
   constexpr int NQB = 2;                                          // Q / dO image buffers
   // NKT 32-key blocks (= waves); keys past Lk are zero rows with a -inf score bias
   constexpr int NK = NKT * 32, NTHR = NKT * 64;
-  constexpr int RDT = 32 + 8;                                     // dS^T image [key][32 queries] row stride
+  // LDS images with swizzled 16-B chunks instead of padded rows (round 6: SQ_LDS_BANK_CONFLICT was 31 % of the
+  // kernel's LDS cycles, the dQ sweep's transposed reads 2-way on every K^T read — rows r and r + 8 of a 32-lane half
+  // met in one bank window at the 160-B stride):
+  //   K image [NK][64]: chunk c of key row r at slot c ^ bk_kswz(r)
+  //   dS^T image [2][NK][32]: chunk c of key row r at slot c ^ bk_dswz(r)
+  // conflict-free for the dQ sweep's ds_read_b64_tr_b16 halves (rows {0..3, 8..11} + 4 k + 32 m); the dS^T writes
+  // stay 2-way, as with the padded rows.
+  constexpr int RDT = 32;                                         // dS^T image [key][32 queries] row stride
   constexpr int PRE = 512 / NTHR;                                 // 8-B Q (and dO, O, O_lo) pieces per thread
   constexpr int TPW = 8 / NKT;                                    // dQ tiles per wave per chunk
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  bf16_t* sk = (bf16_t*)smem;                                // [NK][R_VS]
-  bf16_t* sq = sk + NK * R_VS;                               // [NQB][32][R_CS]
+  bf16_t* sk = (bf16_t*)smem;                                // [NK][64] (bk_koff)
+  bf16_t* sq = sk + NK * 64;                                 // [NQB][32][R_CS]
   bf16_t* sdo = sq + NQB * 32 * R_CS;                        // [NQB][32][R_CS]
   bf16_t* sds = sdo + NQB * 32 * R_CS;                       // [2][NK][RDT]  dS^T (bf16)
   float* slse = (float*)(sds + 2 * NK * RDT);                // [2][32]  (-lse, -inf for dead queries)
@@ -1345,7 +1358,7 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
 #pragma unroll
     for (int i = 0; i < NK * 8 / NTHR; ++i) {
       const int c = tid + i * NTHR, row = c >> 3, dc = (c & 7) * 8;
-      *(uint4*)(sk + row * R_VS + dc) = kb0 + row < a.Lk ? kv[i] : make_uint4(0, 0, 0, 0);
+      *(uint4*)(sk + bk_koff(row, dc)) = kb0 + row < a.Lk ? kv[i] : make_uint4(0, 0, 0, 0);
     }
   }
   s8_t kf[2][2], vf[2][2];
@@ -1479,8 +1492,9 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
     for (int j = 0; j < TPW; ++j) {
       const int tl = w + NKT * j;
       const int qs = tl >> 2, u = tl & 3;
-      const bf16_t* dsr = sds + (bq * NK + 8 * g + (li >> 2)) * RDT + 16 * qs + 4 * (li & 3);
-      const bf16_t* kp = sk + (8 * g + (li >> 2)) * R_VS + 16 * u + 4 * (li & 3);
+      const int rr = 8 * g + (li >> 2);   // (row + 32 kc and row + 4 keep the swizzle: bk_kswz / bk_dswz are periodic)
+      const bf16_t* dsr = sds + bq * NK * RDT + bk_doff(rr, 16 * qs + 4 * (li & 3));
+      const bf16_t* kp = sk + bk_koff(rr, 16 * u + 4 * (li & 3));
       // operands in two halves of NKT / 2 key slices (round 6: all NKT at once held 64 VGPRs; the second prefetch set
       // needs them)
       constexpr int HK = NKT / 2;
@@ -1491,8 +1505,10 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
 #pragma unroll
         for (int k2 = 0; k2 < HK; ++k2) {
           const int kc = hh * HK + k2;
-          ka[k2] = cat8(lds_tr(kp + 32 * kc * R_VS), lds_tr(kp + (32 * kc + 4) * R_VS));
-          da[k2] = cat8(lds_tr(dsr + 32 * kc * RDT), lds_tr(dsr + (32 * kc + 4) * RDT));
+          ka[k2] = cat8(lds_tr(kp + 32 * kc * 64), lds_tr(kp + bk_koff(rr + 4, 16 * u + 4 * (li & 3)) -
+                                                            bk_koff(rr, 16 * u + 4 * (li & 3)) + 32 * kc * 64));
+          da[k2] = cat8(lds_tr(dsr + 32 * kc * RDT), lds_tr(dsr + bk_doff(rr + 4, 16 * qs + 4 * (li & 3)) -
+                                                              bk_doff(rr, 16 * qs + 4 * (li & 3)) + 32 * kc * RDT));
         }
 #pragma unroll
         for (int k2 = 0; k2 < HK; ++k2) acc = mfma32(ka[k2], da[k2], acc);
@@ -1519,7 +1535,7 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int c = 0; c < 2; ++c) kf[t][c] = lds_b128(sk + (kwl + 16 * t + li) * R_VS + 32 * c + 8 * g);
+    for (int c = 0; c < 2; ++c) kf[t][c] = lds_b128(sk + bk_koff(kwl + 16 * t + li, 32 * c + 8 * g));
   ATTN_TS(1);
   s4_t pdb[2][2], dsb[2][2];
   // dV^T += dO^T Pd ; dK^T += Q^T dS   (k-slots: queries 4g+j of sub-tile 0, then of sub-tile 1)
@@ -1578,7 +1594,7 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
       for (int qs = 0; qs < 2; ++qs)
 #pragma unroll
         for (int t = 0; t < 2; ++t)
-          *(uint2*)(sds + (buf * NK + kwl + 16 * t + li) * RDT + 16 * qs + 4 * g) = make_uint2(0, 0);
+          *(uint2*)(sds + buf * NK * RDT + bk_doff(kwl + 16 * t + li, 16 * qs + 4 * g)) = make_uint2(0, 0);
       if (ch > 0) dq_chunk(ch - 1);
     } else {
       f4_t s[2][2], dp[2][2];   // [qs][t]
@@ -1626,7 +1642,7 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
           pdb[qs][t] = to_bf4(pd);
           dsb[qs][t] = to_bf4(dsv);
           // dS^T image: this lane's 4 consecutive queries of one key -> one 8-byte write
-          *(s4_t*)(sds + (buf * NK + kwl + 16 * t + li) * RDT + 16 * qs + 4 * g) = dsb[qs][t];
+          *(s4_t*)(sds + buf * NK * RDT + bk_doff(kwl + 16 * t + li, 16 * qs + 4 * g)) = dsb[qs][t];
         }
       }
       dvdk(qb);
@@ -1677,7 +1693,7 @@ int bwd_res_nkt(int lk) { return lk <= 64 ? 2 : (lk <= 128 ? 4 : 8); }
 
 size_t bwd_res_smem(int nkt) {
   const int nk = nkt * 32, nqb = 2;
-  return (size_t)(nk * R_VS + 2 * nqb * 32 * R_CS + 2 * nk * (32 + 8)) * 2 + 128 * 4 + 16 * 16;
+  return (size_t)(nk * 64 + 2 * nqb * 32 * R_CS + 2 * nk * 32) * 2 + 128 * 4 + 16 * 16;
 }
 
 // dq (bf16, strided) = scale * sum of the nparts fp32 partials dq_acc[p] ([nparts][B][Lq][H][DH], added in order)

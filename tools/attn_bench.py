@@ -71,6 +71,8 @@ def main():
     ap.add_argument("--exp", default="", help="comma list of ASRX_ATTN_EXP values for the backward (a diagnostic "
                     "build's timing-only switches, wrong results: 1 no loop barrier, 2 no chunk fetch, 4 no dQ sweep, "
                     "8 no dV/dK MFMAs)")
+    ap.add_argument("--exp-fwd", action="store_true", help="--exp sweeps the forward instead (1 no K/V wait, 2 no "
+                    "output stores, 4 no v_exp, 8 no PV MFMAs, 16 no QK MFMAs)")
     args = ap.parse_args()
     os.environ["ASRX_ATTN_KERNEL"] = args.variant
     cases = {"enc": ("enc_self", 249, 249, False), "cross": ("cross", 64, 249, False),
@@ -128,8 +130,8 @@ def main():
             fwd()
             for e in args.exp.split(","):
                 os.environ["ASRX_ATTN_EXP"] = e
-                tb = timeit(bwd, args.reps)
-                print(f"{name:9s} exp {e:>3s} bwd {tb*1e3:7.1f}us", flush=True)
+                tb = timeit(fwd if args.exp_fwd else bwd, args.reps)
+                print(f"{name:9s} exp {e:>3s} {'fwd' if args.exp_fwd else 'bwd'} {tb*1e3:7.1f}us", flush=True)
             os.environ.pop("ASRX_ATTN_EXP", None)
         return
     for key in args.only.split(","):

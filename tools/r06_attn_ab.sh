@@ -9,7 +9,7 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 tail -2 gpurun_out/t_attn.log
 only=${ATTN_ONLY:-enc,cross,dec,c5}
 for v in old new new old; do
-  if [ $v = old ]; then lib=$PWD/ab/lib_base.so; else lib=$PWD/asr-transformer_amd/asrx/lib/libasrx.so; fi
+  if [ $v = old ]; then lib=$PWD/${ATTN_BASE:-ab/lib_base.so}; else lib=$PWD/asr-transformer_amd/asrx/lib/libasrx.so; fi
   ASRX_LIB=$lib timeout -k 10 300 python tools/attn_bench.py --only $only > gpurun_out/attn_$v.log 2>&1 || exit 1
   echo "== $v"; cat gpurun_out/attn_$v.log
 done
