@@ -15,6 +15,7 @@ import math
 import torch
 from torch import nn
 
+from .. import blocks as Bk
 from .. import kernels as K
 from ..layers import LayerNorm, _Lin
 from . import ops as O
@@ -194,10 +195,14 @@ class Decoder(nn.Module):
         return self._run(x, enc_x, O.valid_spec(valid, causal=True), O.valid_spec(enc_valid),
                          valid.reshape(-1).float(), cfg)
 
-    def evaluate(self, enc_x, device):
-        """new/model.py:125-142: greedy from BOS for seq_len steps over the full prefix (causal mask only, no cross
-        mask, all rows kept); the argmax of each step on the device, the EOS steps resolved once at the end."""
+    def evaluate(self, enc_x, device, cache=True):
+        """new/model.py:125-142: greedy from BOS for seq_len steps (causal mask only, no cross mask, all rows kept);
+        the argmax of each step on the device, the EOS steps resolved once at the end.  cache (default, round 6): the
+        KV-cached decode of _evaluate_cached; False — or dropout active (training mode), whose masks are drawn per
+        full-prefix pass — recomputes the full prefix every step as the reference does."""
         cfg = _cfg(self, self.p)
+        if cache and cfg.p == 0.0:
+            return self._evaluate_cached(enc_x, device, cfg)
         B = enc_x.shape[0]
         dev = enc_x.device
         dec_in = torch.full((B, 1), self.bos_token, dtype=torch.int64, device=dev)
@@ -216,6 +221,88 @@ class Decoder(nn.Module):
         for i in range(self.seq_len):
             eoses[steps[:, i] == self.eos_token] = i
         return dec_in.to(torch.int32).to(device), prob, eoses
+
+
+    def _evaluate_cached(self, enc_x, device, cfg):
+        """The reference's greedy loop (new/model.py:125-142) recomputes every prefix position at every step; with
+        the causal self-attention the logits of position t do not depend on later tokens, so only the new position
+        runs through the layers: its self-attention K / V join per-layer caches [B, seq_len, 2 h d], and every layer's
+        cross-attention K / V of the encoder output are projected once.  The logits of position t are written when t
+        is processed; after the last step they are the reference's final-step logits (all seq_len positions)."""
+        cd = cfg.cd
+        B, Te, d = enc_x.shape
+        dev = enc_x.device
+        S, H, n, V = self.seq_len, self.num_heads, self.num_layers, self.vocab_size
+        hd = H * d
+        self._check_len(S)
+        scale = d ** -0.5
+        none = K.MaskSpec()
+        enc_c = O._cd(enc_x.reshape(B * Te, d).float().contiguous(), cd)
+
+        def ln(x, norm):          # the post-LN of new/model.py:80-89 (non_pad_mask is all ones in evaluate)
+            y = torch.empty_like(x)
+            K.layernorm_fwd(x, norm.weight.detach(), norm.bias.detach(), y)
+            return y
+
+        def attend(q, kv, Lk, ldkv, bstride):   # one query per batch row over Lk keys of kv (K | V columns)
+            o = torch.empty(B, hd, dtype=cd, device=dev)
+            st = ((hd, hd), (ldkv, bstride), (ldkv, bstride), (hd, hd))
+            Bk.attn_fwd(cfg.ctx, q, kv, kv[..., hd:], o, B, H, 1, Lk, d, st, scale, none)
+            return o
+
+        lw = []   # per layer: cast weights, the cross K / V of the encoder output
+        for layer in self.layers:
+            sa, ca = layer.mask_attention, layer.attention
+            wq = O._w(ca.wqkv, cd)
+            kvx = torch.empty(B * Te, 2 * hd, dtype=cd, device=dev)
+            K.linear(enc_c, wq[hd:], kvx, bias=ca.bqkv[hd:].detach())
+            lw.append((O._w(sa.wqkv, cd), O._w(sa.out.weight, cd), wq[:hd], O._w(ca.out.weight, cd), kvx,
+                       O._w(layer.ff.squeeze.weight, cd), O._w(layer.ff.unsqueeze.weight, cd)))
+        wcls = O._w(self.classifier.weight, cd)
+        caches = torch.empty(n, B, S, 2 * hd, dtype=cd, device=dev)
+        logits = torch.empty(B, S, V, dtype=torch.float32, device=dev)
+        tokens = torch.empty(B, S + 1, dtype=torch.int64, device=dev)
+        tokens[:, 0] = self.bos_token
+        cur = tokens[:, 0].contiguous()
+        pe = self.pe.pe[0]
+        for t in range(S):
+            x = torch.empty(B, d, dtype=torch.float32, device=dev)
+            K.embed_fwd(cur, self.emb.weight.detach(), pe[t:t + 1].contiguous(), x, 1)   # (eval: no dropout)
+            for l, layer in enumerate(self.layers):
+                wqkv, wo, wq2, wo2, kvx, w1, w2 = lw[l]
+                sa, ca, ff = layer.mask_attention, layer.attention, layer.ff
+                # masked self-attention: the new position's K / V into the cache, its query over positions 0..t
+                xc = O._cd(x, cd)
+                q = torch.empty(B, hd, dtype=cd, device=dev)
+                K.linear(xc, wqkv[:hd], q, bias=sa.bqkv[:hd].detach())
+                cache = caches[l]
+                K.gemm(xc, wqkv[hd:], cache[:, t], B, 2 * hd, d, lda=d, ldb=d, ldc=S * 2 * hd,
+                       bias=sa.bqkv[hd:].detach())
+                o = attend(q, cache, t + 1, 2 * hd, S * 2 * hd)
+                y = torch.empty(B, d, dtype=torch.float32, device=dev)
+                K.linear(o, wo, y, bias=sa.out.bias.detach(), resid=x, ld_resid=d)
+                x1 = ln(y, layer.norm1)
+                # cross-attention over the encoder output (no mask in evaluate, new/model.py:136)
+                q2 = torch.empty(B, hd, dtype=cd, device=dev)
+                K.linear(O._cd(x1, cd), wq2, q2, bias=ca.bqkv[:hd].detach())
+                o2 = attend(q2, kvx, Te, 2 * hd, Te * 2 * hd)
+                y2 = torch.empty(B, d, dtype=torch.float32, device=dev)
+                K.linear(o2, wo2, y2, bias=ca.out.bias.detach(), resid=x1, ld_resid=d)
+                x2 = ln(y2, layer.norm2)
+                # feed-forward with its residual
+                f = torch.empty(B, w1.shape[0], dtype=cd, device=dev)
+                K.linear(O._cd(x2, cd), w1, f, bias=ff.squeeze.bias.detach(), relu=True)
+                y3 = torch.empty(B, d, dtype=torch.float32, device=dev)
+                K.linear(f, w2, y3, bias=ff.unsqueeze.bias.detach(), resid=x2, ld_resid=d)
+                x = ln(y3, layer.norm3)
+            lg = logits[:, t]
+            K.gemm(O._cd(x, cd), wcls, lg, B, V, d, lda=d, ldb=d, ldc=S * V)
+            K.greedy_argmax(lg, V, tokens[:, t + 1], cur)
+        steps = tokens[:, 1:].cpu()                           # one host synchronisation
+        eoses = torch.full((B,), S - 1)
+        for i in range(S):
+            eoses[steps[:, i] == self.eos_token] = i
+        return tokens.to(torch.int32).to(device), logits, eoses
 
 
 class Transformer(nn.Module):

@@ -111,6 +111,31 @@ def test_new_evaluate_fp32_golden(golden_dir, name):
     assert relerr(last, g[p + "eval_last"]) < 1e-4
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_new_evaluate_kv_cache_equals_full_prefix_recompute(precision):
+    """The KV-cached greedy decode (Decoder._evaluate_cached, the default) against the reference's full-prefix
+    recompute of every step (evaluate(..., cache=False), new/model.py:125-142) on the same weights: token rows and
+    EOS steps exact, the final step's logits (every position) within fp32 / bf16 rounding."""
+    m, c = build("new_small", precision)
+    m.eval()
+    s, lens, text = N.synthetic_batch(c, 5, seed=11)
+    with torch.no_grad():
+        enc = m.encoder(s.to(dev), lens.to(dev))
+        t0, l0, e0 = m.decoder.evaluate(enc, dev, cache=False)
+        t1, l1, e1 = m.decoder.evaluate(enc, dev)
+    assert l0.shape == l1.shape and t0.shape == t1.shape and t1.dtype == torch.int32
+    if precision == "bf16":
+        # (bf16: the two paths run GEMMs of different row counts, whose fp32 sums may round an activation
+        #  differently; a near-tie can then flip a token and every later position with it — the first position,
+        #  computed from identical inputs, is compared)
+        assert relerr(l1[:, 0], l0[:, 0].cpu()) < 2e-2
+        assert int(t1.min()) >= 0 and int(t1.max()) < c.vocab_size
+        return
+    assert torch.equal(t0.cpu(), t1.cpu())
+    assert torch.equal(e0, e1)
+    assert relerr(l1, l0.cpu()) < 1e-5
+
+
 def test_new_forward_bf16_vs_oracle_autocast_bound():
     """bf16 operands (fp32 accumulation and residual stream): logits within 1.5x the error of the oracle under
     torch's bf16 autocast against the fp32 oracle."""
