@@ -496,6 +496,9 @@ ASRX_DEV __amdgpu_buffer_rsrc_t brsrc(const void* base, uint32_t off, int32_t by
 ASRX_DEV uint2 bufld64(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
   return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, 0, 0));
 }
+ASRX_DEV uint4 bufld128(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 0, 0));
+}
 ASRX_DEV uint32_t bufld32(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
   return __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, 0, 0);
 }
@@ -1328,7 +1331,10 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
   // conflict-free for the dQ sweep's ds_read_b64_tr_b16 halves (rows {0..3, 8..11} + 4 k + 32 m); the dS^T writes
   // stay 2-way, as with the padded rows.
   constexpr int RDT = 32;                                         // dS^T image [key][32 queries] row stride
-  constexpr int PRE = 512 / NTHR;                                 // 8-B Q (and dO, O, O_lo) pieces per thread
+  // chunk staging in 16-B pieces: 32 rows x 8 pieces per tensor, by the first LT threads (round 6: 8-B pieces by
+  // every thread issued twice the vector-memory instructions — 56 per CU and chunk with the words and lse — into the
+  // stretch between the chunk barrier and the next MFMAs)
+  constexpr int LT = NTHR < 256 ? NTHR : 256, PRE = 256 / LT;    // loading threads, pieces per loading thread
   constexpr int TPW = 8 / NKT;                                    // dQ tiles per wave per chunk
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* sk = (bf16_t*)smem;                                // [NK][64] (bk_koff)
@@ -1399,7 +1405,7 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
   // 4 (c % 16) ..): every wave does the same loads and its share of delta (the 16 lanes of a row reduce by DPP).
   // Buffer loads through per-chunk descriptors (brsrc): each lane's voffset is fixed for the kernel, rows / words
   // past the end read as zero through the range check, so every load is unconditional.
-  struct Pf { uint2 q[PRE], d[PRE], o[PRE], ol[PRE]; float lse; uint32_t w[2]; };
+  struct Pf { uint4 q[PRE], d[PRE], o[PRE], ol[PRE]; float lse; uint32_t w[2]; };
   const bool usebits = a.thr && a.dropmask;
   const uint32_t* dmb = usebits ? a.dropmask + (int64_t)bh * nch * a.Lk : nullptr;
   // delta = rowsum(dO * O) is formed here too: the threads that stage a dO piece also load the matching O
@@ -1413,8 +1419,8 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
   uint32_t vq[PRE], vdo[PRE], vo[PRE];
 #pragma unroll
   for (int i = 0; i < PRE; ++i) {
-    const int c = tid + NTHR * i;
-    const int row = c >> 4, dc = (c & 15) * 4;
+    const int c = (tid % LT) + LT * i;
+    const int row = c >> 3, dc = (c & 7) * 8;
     vq[i] = (uint32_t)(row * (int)a.qr + dc) * 2u;
     vdo[i] = (uint32_t)(row * (int)a.dor + dc) * 2u;
     vo[i] = (uint32_t)(row * (int)a.orr + dc) * 2u;
@@ -1430,42 +1436,48 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
     const __amdgpu_buffer_rsrc_t cq = brsrc(Qb, q0 * (uint32_t)a.qr * 2u, nqb), cd = brsrc(Db, q0 * (uint32_t)a.dor * 2u, ndb);
     const __amdgpu_buffer_rsrc_t co = brsrc(Ob, q0 * (uint32_t)a.orr * 2u, nob);
     const __amdgpu_buffer_rsrc_t col = brsrc(Olb ? Olb : Ob, q0 * (uint32_t)a.orr * 2u, nob);
+    if (tid < LT) {   // (wave-uniform)
 #pragma unroll
-    for (int i = 0; i < PRE; ++i) {
-      P.q[i] = bufld64(cq, vq[i]);
-      P.d[i] = bufld64(cd, vdo[i]);
-      P.o[i] = bufld64(co, vo[i]);
-      P.ol[i] = bufld64(col, vo[i]);
+      for (int i = 0; i < PRE; ++i) {
+        P.q[i] = bufld128(cq, vq[i]);
+        P.d[i] = bufld128(cd, vdo[i]);
+        P.o[i] = bufld128(co, vo[i]);
+        P.ol[i] = bufld128(col, vo[i]);
+      }
     }
-    P.lse = __uint_as_float(bufld32(brsrc(lseb, q0 * 4u, nlb), vl));
+    if (tid < 32) P.lse = __uint_as_float(bufld32(brsrc(lseb, q0 * 4u, nlb), vl));   // (wave 0 publishes it)
   };
   auto publish = [&](const Pf& P, int buf, int ch) {
     const int q0 = ch * 32;
+    if (tid < LT) {
 #pragma unroll
-    for (int i = 0; i < PRE; ++i) {
-      const int c = tid + NTHR * i;
-      const int row = c >> 4, dc = (c & 15) * 4;
-      const bool qv = q0 + row < a.Lq;
-      *(uint2*)(sq + (buf * 32 + row) * R_CS + dc) = P.q[i];   // (rows past Lq read as zero)
-      *(uint2*)(sdo + (buf * 32 + row) * R_CS + dc) = P.d[i];
-      // dO . (O + O_lo) over the lane's 4 elements: v_dot2_f32_bf16 on the packed pairs (bf16 products are exact in
-      // fp32; 4 instructions instead of unpacking 12 values)
-      typedef __bf16 b2_t __attribute__((ext_vector_type(2)));
-      const uint32_t dd[2] = {P.d[i].x, P.d[i].y}, oo[2] = {P.o[i].x, P.o[i].y}, ol[2] = {P.ol[i].x, P.ol[i].y};
-      float dot = 0.f;
+      for (int i = 0; i < PRE; ++i) {
+        const int c = tid + LT * i;
+        const int row = c >> 3, dc = (c & 7) * 8;
+        const bool qv = q0 + row < a.Lq;
+        *(uint4*)(sq + (buf * 32 + row) * R_CS + dc) = P.q[i];   // (rows past Lq read as zero)
+        *(uint4*)(sdo + (buf * 32 + row) * R_CS + dc) = P.d[i];
+        // dO . (O + O_lo) over the piece's 8 elements: v_dot2_f32_bf16 on the packed pairs (bf16 products are exact
+        // in fp32)
+        typedef __bf16 b2_t __attribute__((ext_vector_type(2)));
+        const uint32_t dd[4] = {P.d[i].x, P.d[i].y, P.d[i].z, P.d[i].w};
+        const uint32_t oo[4] = {P.o[i].x, P.o[i].y, P.o[i].z, P.o[i].w};
+        const uint32_t ol[4] = {P.ol[i].x, P.ol[i].y, P.ol[i].z, P.ol[i].w};
+        float dot = 0.f;
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        dot = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(b2_t, dd[e]), __builtin_bit_cast(b2_t, oo[e]), dot, false);
-        if (Olb)
-          dot = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(b2_t, dd[e]), __builtin_bit_cast(b2_t, ol[e]), dot,
+        for (int e = 0; e < 4; ++e) {
+          dot = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(b2_t, dd[e]), __builtin_bit_cast(b2_t, oo[e]), dot,
                                                 false);
+          if (Olb)
+            dot = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(b2_t, dd[e]), __builtin_bit_cast(b2_t, ol[e]), dot,
+                                                  false);
+        }
+        // sum over the row's 8 adjacent lanes by DPP (quad swaps, then the half-row mirror): no LDS round trips
+        dot += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(dot), 0xB1, 0xF, 0xF, true));
+        dot += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(dot), 0x4E, 0xF, 0xF, true));
+        dot += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(dot), 0x141, 0xF, 0xF, true));
+        if ((c & 7) == 0) sdel[buf * 32 + row] = qv ? dot : 0.f;
       }
-      // sum over the row's 16 adjacent lanes by DPP (quad swaps, half-row and row mirrors): no LDS round trips
-      dot += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(dot), 0xB1, 0xF, 0xF, true));
-      dot += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(dot), 0x4E, 0xF, 0xF, true));
-      dot += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(dot), 0x141, 0xF, 0xF, true));
-      dot += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(dot), 0x140, 0xF, 0xF, true));
-      if ((c & 15) == 0) sdel[buf * 32 + row] = qv ? dot : 0.f;
     }
     if (tid < 32) {
       const int q = q0 + tid;
