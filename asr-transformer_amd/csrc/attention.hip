@@ -1428,24 +1428,27 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
   const uint32_t vl = (uint32_t)(tid & 31) * 4u;
   // (keys past Lk read the next chunk's words, or past the end -> 0; masked at the use)
   const uint32_t vk0 = usebits ? (uint32_t)(kw0 + li) * 4u : 0u, vk1 = usebits ? (uint32_t)(kw0 + 16 + li) * 4u : 0u;
+  // One descriptor per buffer for the kernel; a chunk's start is added to the per-lane voffset (one VALU add per
+  // load), which the raw-buffer range check covers — rows / words past the end read as zero (round 6; the first
+  // round-6 cut rebuilt five descriptors per chunk in SALU, whose SGPRs spilled: v_readlane restores in the loop)
+  const __amdgpu_buffer_rsrc_t rq = brsrc(Qb, 0u, nqb), rd = brsrc(Db, 0u, ndb), ro = brsrc(Ob, 0u, nob);
+  const __amdgpu_buffer_rsrc_t rol = brsrc(Olb ? Olb : Ob, 0u, nob), rl = brsrc(lseb, 0u, nlb);
+  const __amdgpu_buffer_rsrc_t rm = usebits ? brsrc(dmb, 0u, nmb) : rl;
   auto fetch = [&](Pf& P, int ch) {
-    const uint32_t q0 = (uint32_t)ch * 32u;
-    const __amdgpu_buffer_rsrc_t cm = usebits ? brsrc(dmb, (uint32_t)ch * (uint32_t)a.Lk * 4u, nmb) : brsrc(lseb, 0u, nlb);
-    P.w[0] = bufld32(cm, vk0);
-    P.w[1] = bufld32(cm, vk1);
-    const __amdgpu_buffer_rsrc_t cq = brsrc(Qb, q0 * (uint32_t)a.qr * 2u, nqb), cd = brsrc(Db, q0 * (uint32_t)a.dor * 2u, ndb);
-    const __amdgpu_buffer_rsrc_t co = brsrc(Ob, q0 * (uint32_t)a.orr * 2u, nob);
-    const __amdgpu_buffer_rsrc_t col = brsrc(Olb ? Olb : Ob, q0 * (uint32_t)a.orr * 2u, nob);
+    const uint32_t q0 = (uint32_t)ch * 32u, wo = usebits ? (uint32_t)ch * (uint32_t)a.Lk * 4u : 0u;
+    P.w[0] = bufld32(rm, vk0 + wo);
+    P.w[1] = bufld32(rm, vk1 + wo);
+    const uint32_t oq = q0 * (uint32_t)a.qr * 2u, od = q0 * (uint32_t)a.dor * 2u, oo = q0 * (uint32_t)a.orr * 2u;
     if (tid < LT) {   // (wave-uniform)
 #pragma unroll
       for (int i = 0; i < PRE; ++i) {
-        P.q[i] = bufld128(cq, vq[i]);
-        P.d[i] = bufld128(cd, vdo[i]);
-        P.o[i] = bufld128(co, vo[i]);
-        P.ol[i] = bufld128(col, vo[i]);
+        P.q[i] = bufld128(rq, vq[i] + oq);
+        P.d[i] = bufld128(rd, vdo[i] + od);
+        P.o[i] = bufld128(ro, vo[i] + oo);
+        P.ol[i] = bufld128(rol, vo[i] + oo);
       }
     }
-    if (tid < 32) P.lse = __uint_as_float(bufld32(brsrc(lseb, q0 * 4u, nlb), vl));   // (wave 0 publishes it)
+    if (tid < 32) P.lse = __uint_as_float(bufld32(rl, vl + q0 * 4u));   // (wave 0 publishes it)
   };
   auto publish = [&](const Pf& P, int buf, int ch) {
     const int q0 = ch * 32;
