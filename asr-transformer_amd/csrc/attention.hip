@@ -1578,26 +1578,16 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
     const int buf = ch & 1, q0 = ch * 32, qb = buf;
     // 4-bit keep masks of this lane's queries (16qs + 4g + r) for its two keys
     uint32_t nib[2][2];
-    if (!a.thr) {
+    // (dropout needs the keep words here: the launch sends calls without them to the tiled kernels, which hash)
+    if (!usebits) {
       nib[0][0] = nib[0][1] = nib[1][0] = nib[1][1] = 15u;
-    } else if (usebits) {
+    } else {
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         const uint32_t wv = kw0 + 16 * t + li < a.Lk ? X.w[t] : 0u;
         nib[0][t] = (wv >> (4 * g)) & 15u;
         nib[1][t] = (wv >> (16 + 4 * g)) & 15u;
       }
-    } else {
-#pragma unroll
-      for (int qs = 0; qs < 2; ++qs)
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const int key = kw0 + 16 * t + li, qb = q0 + 16 * qs + 4 * g;
-          const uint32_t h01 = rng_hash(a.seed, attn_pair(bh, a.Lq, a.Lk, qb, key));
-          const uint32_t h23 = rng_hash(a.seed, attn_pair(bh, a.Lq, a.Lk, qb + 2, key));
-          nib[qs][t] = (uint32_t)(rng_half(h01, 0) >= a.thr) | ((uint32_t)(rng_half(h01, 1) >= a.thr) << 1) |
-                       ((uint32_t)(rng_half(h23, 0) >= a.thr) << 2) | ((uint32_t)(rng_half(h23, 1) >= a.thr) << 3);
-        }
     }
     fetch(X, min(ch + 1, nch - 1));   // unconditional (a conditional fetch made the compiler's merged wait vmcnt(0))
     ATTN_TS(2 + 4 * ch);
@@ -1947,7 +1937,9 @@ extern "C" int asrx_attention_bwd(const asrx_attn_desc* d, void* stream) {
   for (int64_t s : ostr) if (s % 8) return ASRX_ERR_UNSUPPORTED;
   hipStream_t st = (hipStream_t)stream;
   const bool longk = stream_ok(d, a) && (!a.thr || a.dropmask);
-  if ((resident_ok(d, a) || longk) && a.dqr % 4 == 0 && a.dqb % 4 == 0 && (uintptr_t)a.dq % 8 == 0) {   // forms delta itself
+  // (dropout without the keep words — a forward that took the tiled kernel — goes to the tiled backward, which hashes
+  //  the same decisions in-kernel)
+  if ((resident_ok(d, a) || longk) && (!a.thr || a.dropmask) && a.dqr % 4 == 0 && a.dqb % 4 == 0 && (uintptr_t)a.dq % 8 == 0) {   // forms delta itself
     // (round 4's ASRX_ATTN_XSPLIT — short query blocks as two 128-key blocks of 4 waves — measured 30.8 -> 48.5 us:
     //  removed in round 5)
     const int nkt = bwd_res_nkt(a.Lk);
