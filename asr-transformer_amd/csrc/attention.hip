@@ -80,6 +80,10 @@ __device__ unsigned long long g_attn_dbg[128 + 4 * 1024];   // [128..]: per-bloc
 #define ATTN_TS(i) do { if (a.dbg && blockIdx.x == 0 && blockIdx.y == 0 && (threadIdx.x & 255) == 0 && (i) < 64) \
                           g_attn_dbg[(i) + (threadIdx.x >> 8) * 64] = __builtin_amdgcn_s_memtime(); } while (0)
 
+// IEEE-754 maximum (NaN-propagating, like torch.max): v_maximum3_f32 on gfx950.  fmaxf (maxnum) first
+// canonicalises every MFMA result with a v_max_f32 x, x — twice the instructions of the row-max reductions.
+ASRX_DEV float fmx(float a, float b) { return __builtin_elementwise_maximum(a, b); }
+
 ASRX_DEV bool masked(const AttnArgs& a, int b, int q, int key) {
   if (key >= a.Lk) return true;
   if (a.mode == 1) {
@@ -179,11 +183,11 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
         const int key = kt * 64 + 16 * t + 4 * g + r;
         const float x = (!qlive || masked(a, b, q, key)) ? -INFINITY : s[t][r] * a.scale2;
         s[t][r] = x;
-        mt = fmaxf(mt, x);
+        mt = fmx(mt, x);
       }
-    mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-    const float m_new = fmaxf(m_run, mt);
+    mt = fmx(mt, __shfl_xor(mt, 16, 64));
+    mt = fmx(mt, __shfl_xor(mt, 32, 64));
+    const float m_new = fmx(m_run, mt);
     const float m_use = m_new == -INFINITY ? 0.f : m_new;
     const float alpha = exp2f(m_run - m_use);
     float rs = 0.f;
@@ -540,9 +544,9 @@ ASRX_DEV uint32_t xchg1(uint32_t v) { return (uint32_t)__builtin_amdgcn_mov_dpp(
 // max / sum over the four lanes {l, l^16, l^32, l^48} (one query's 16-lane groups): VALU permlane swaps
 ASRX_DEV float xmax4(float v) {
   auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  v = fmx(__uint_as_float(r[0]), __uint_as_float(r[1]));
   r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  return fmx(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 ASRX_DEV float xsum4(float v) {
   auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
@@ -795,10 +799,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
             if (diag && key > q) x = -INFINITY;
           }
           s[t][qs][r] = x;
-          mt = fmaxf(mt, x);
+          mt = fmx(mt, x);
         }
       mt = xmax4(mt);
-      const float m_new = fmaxf(m_run[qs], mt);
+      const float m_new = fmx(m_run[qs], mt);
       const float m_use = m_new == -INFINITY ? 0.f : m_new;
       if (__ballot(m_new != m_run[qs])) {   // rescale only when some row's max grew (exact, wave-uniform)
         const float alpha = exp2_raw(m_run[qs] - m_use);
@@ -807,7 +811,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
         for (int u = 0; u < 4; ++u) o[u][qs] *= alpha;
         m_run[qs] = m_new;
       }
-      float rs = 0.f;
+      float rs = -0.f;   // (x + -0 = x exactly: the first add folds away)
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         const f4_t fk = slut[(dw[qs][kt] >> (16 * t + 4 * g)) & 15u];
@@ -961,10 +965,10 @@ void attn_fwd_kq_kernel(AttnArgs a, const uint32_t* qmaj) {
     s4_t pf[2][2];
 #pragma unroll
     for (int qs = 0; qs < 2; ++qs) {
-      float mt = fmaxf(fmaxf(fmaxf(sc[0][qs][0], sc[0][qs][1]), fmaxf(sc[0][qs][2], sc[0][qs][3])),
-                       fmaxf(fmaxf(sc[1][qs][0], sc[1][qs][1]), fmaxf(sc[1][qs][2], sc[1][qs][3])));
+      float mt = fmx(fmx(fmx(sc[0][qs][0], sc[0][qs][1]), fmx(sc[0][qs][2], sc[0][qs][3])),
+                       fmx(fmx(sc[1][qs][0], sc[1][qs][1]), fmx(sc[1][qs][2], sc[1][qs][3])));
       mt = xmax4(mt);
-      const float m_new = fmaxf(m_run[qs], mt);
+      const float m_new = fmx(m_run[qs], mt);
       const float m_use = m_new == -INFINITY ? 0.f : m_new;
       if (__ballot(m_new != m_run[qs])) {
         const float alpha = exp2_raw((m_run[qs] - m_use) * sc2);
@@ -974,7 +978,7 @@ void attn_fwd_kq_kernel(AttnArgs a, const uint32_t* qmaj) {
         m_run[qs] = m_new;
       }
       const float nm = -m_use * sc2;
-      float rs = 0.f;
+      float rs = -0.f;   // (x + -0 = x exactly: the first add folds away)
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         f4_t e;
@@ -1031,7 +1035,7 @@ void attn_fwd_kq_kernel(AttnArgs a, const uint32_t* qmaj) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       mj[j] = sml[w + j][0][qs][li];
-      M = fmaxf(M, mj[j]);
+      M = fmx(M, mj[j]);
     }
     const float Mu = M == -INFINITY ? 0.f : M;
     float L = 0.f, fj[4];
@@ -1133,6 +1137,8 @@ void attn_fwd_stream_kernel(AttnArgs a, const uint32_t* qmaj) {
   }
   const bool kvm = MODE == 1 && a.kvalid;
   if (kvm) msrd = asrxg::make_srd(a.kvalid + b * a.validb, a.Lk);
+  uint64_t t_start = 0, t_staged = 0;   // per-block real-time stamps (ASRX_ATTN_DBG=1, tools/attn_bench.py --dbg)
+  if (a.dbg) t_start = __builtin_amdgcn_s_memrealtime();
   constexpr int NC = 4 + (DROP ? 2 : 0) + (MODE == 1 ? 1 : 0);   // vector-memory ops per chunk and wave
   // chunk c -> buffer c & 1: two 64-key pieces, wave w moves key rows 64 i + 8 w .. + 7 of K and of V
   auto issue = [&](int c) {
@@ -1174,6 +1180,7 @@ void attn_fwd_stream_kernel(AttnArgs a, const uint32_t* qmaj) {
                           ((n & 4) ? 0xffffu : 0u) | ((n & 8) ? 0xffff0000u : 0u));
   }
   lds_barrier();
+  if (a.dbg) t_staged = __builtin_amdgcn_s_memrealtime();
   const bool act = qw0 < a.Lq;
   const int qlast = min(a.Lq, qw0 + 32) - 1;   // the wave's last query (causal: later key tiles are all masked)
   const float sc2 = a.scale2;
@@ -1226,10 +1233,10 @@ void attn_fwd_stream_kernel(AttnArgs a, const uint32_t* qmaj) {
         s4_t pf[2][2];
 #pragma unroll
         for (int qs = 0; qs < 2; ++qs) {
-          float mt = fmaxf(fmaxf(fmaxf(s[0][qs][0], s[0][qs][1]), fmaxf(s[0][qs][2], s[0][qs][3])),
-                           fmaxf(fmaxf(s[1][qs][0], s[1][qs][1]), fmaxf(s[1][qs][2], s[1][qs][3])));
+          float mt = fmx(fmx(fmx(s[0][qs][0], s[0][qs][1]), fmx(s[0][qs][2], s[0][qs][3])),
+                           fmx(fmx(s[1][qs][0], s[1][qs][1]), fmx(s[1][qs][2], s[1][qs][3])));
           mt = xmax4(mt);
-          const float m_new = fmaxf(m_run[qs], mt);
+          const float m_new = fmx(m_run[qs], mt);
           const float m_use = m_new == -INFINITY ? 0.f : m_new;
           if (__ballot(m_new != m_run[qs])) {   // rescale only when some row's max grew (exact, wave-uniform)
             const float alpha = exp2_raw((m_run[qs] - m_use) * sc2);
@@ -1240,7 +1247,7 @@ void attn_fwd_stream_kernel(AttnArgs a, const uint32_t* qmaj) {
           }
           const float nm = -m_use * sc2;
           const uint32_t dword = (&dwc[qs].x)[kt];
-          float rs = 0.f;
+          float rs = -0.f;   // (x + -0 = x exactly: the first add folds away)
 #pragma unroll
           for (int t = 0; t < 2; ++t) {
             f4_t e;
@@ -1281,6 +1288,12 @@ void attn_fwd_stream_kernel(AttnArgs a, const uint32_t* qmaj) {
       }
       lds_barrier();                 // ... and visible to every wave
     }
+  }
+  if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0 && bh < 1024) {
+    g_attn_dbg[128 + 4 * bh] = t_start;
+    g_attn_dbg[129 + 4 * bh] = t_staged;
+    g_attn_dbg[130 + 4 * bh] = __builtin_amdgcn_s_memrealtime();   // (compute done; the stores follow)
+    g_attn_dbg[131 + 4 * bh] = __smid();
   }
   if (!act) return;
   const float dsc = DROP ? a.dscale : 1.f;
