@@ -16,7 +16,9 @@ LIB = os.path.join(OUTDIR, "libasrx.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("ASRX_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=fast",
-         "-I" + os.path.join(REPO, "include"), "-Wno-unused-result"]
+         "-I" + os.path.join(REPO, "include"), "-Wno-unused-result"] + os.environ.get("ASRX_CFLAGS", "").split()
+# (ASRX_CFLAGS: diagnostic builds only, e.g. -DASRX_ATTN_STAMPS for tools/attn_bench.py --dbg; the objects are not
+#  tracked by flags, so build with force=True when switching)
 
 
 def sources():

@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "common.h"
 #include "gemm_common.h"
@@ -74,10 +75,18 @@ struct AttnArgs {
 };
 
 __device__ unsigned long long g_attn_dbg[128 + 4 * 1024];   // [128..]: per-block real-time (fwd)
-#define FWD_TS(i) do { if (a.dbg && threadIdx.x == 0) sdbg[(i)] = __builtin_amdgcn_s_memtime(); } while (0)
-#define FWD_RT(i) do { if (a.dbg && threadIdx.x == 0) sdbg[(i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+// The stamps are compiled in only for diagnostic builds (ASRX_CFLAGS=-DASRX_ATTN_STAMPS; the shipped library reads
+// ASRX_ATTN_DBG but records nothing): four stamp branches per backward chunk had cost ~25 scalar / exec-mask
+// instructions of the loop.
+#ifdef ASRX_ATTN_STAMPS
+constexpr bool kStamps = true;
+#else
+constexpr bool kStamps = false;
+#endif
+#define FWD_TS(i) do { if (kStamps && a.dbg && threadIdx.x == 0) sdbg[(i)] = __builtin_amdgcn_s_memtime(); } while (0)
+#define FWD_RT(i) do { if (kStamps && a.dbg && threadIdx.x == 0) sdbg[(i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 // backward: wave 0 -> [i], wave 4 -> [64 + i] (block 0)
-#define ATTN_TS(i) do { if (a.dbg && blockIdx.x == 0 && blockIdx.y == 0 && (threadIdx.x & 255) == 0 && (i) < 64) \
+#define ATTN_TS(i) do { if (kStamps && a.dbg && blockIdx.x == 0 && blockIdx.y == 0 && (threadIdx.x & 255) == 0 && (i) < 64) \
                           g_attn_dbg[(i) + (threadIdx.x >> 8) * 64] = __builtin_amdgcn_s_memtime(); } while (0)
 
 // IEEE-754 maximum (NaN-propagating, like torch.max): v_maximum3_f32 on gfx950.  fmaxf (maxnum) first
@@ -655,7 +664,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
   const bf16_t* Vb = a.v + b * a.vb + h * 64;
   // phase timestamps (ASRX_ATTN_DBG) go to LDS and are stored at the end: no store among the counted loads
   __shared__ uint64_t sdbg[16];
-  if (a.dbg && threadIdx.x < 16) sdbg[threadIdx.x] = 0;
+  if (kStamps && a.dbg && threadIdx.x < 16) sdbg[threadIdx.x] = 0;
   FWD_RT(12);
   FWD_TS(0);
   // Every global load of the prologue is issued up front, in this order per wave: [MODE 1: key / query
@@ -855,9 +864,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
     }
   }
   FWD_TS(11);
-  if (a.dbg && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+  if (kStamps && a.dbg && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
     for (int i = 0; i < 12; ++i) g_attn_dbg[44 + i] = sdbg[i];
-  if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0 && bh < 1024) {
+  if (kStamps && a.dbg && blockIdx.x == 0 && threadIdx.x == 0 && bh < 1024) {
     g_attn_dbg[128 + 4 * bh] = sdbg[12];
     g_attn_dbg[129 + 4 * bh] = sdbg[13];
     g_attn_dbg[130 + 4 * bh] = __builtin_amdgcn_s_memrealtime();
@@ -1138,7 +1147,7 @@ void attn_fwd_stream_kernel(AttnArgs a, const uint32_t* qmaj) {
   const bool kvm = MODE == 1 && a.kvalid;
   if (kvm) msrd = asrxg::make_srd(a.kvalid + b * a.validb, a.Lk);
   uint64_t t_start = 0, t_staged = 0;   // per-block real-time stamps (ASRX_ATTN_DBG=1, tools/attn_bench.py --dbg)
-  if (a.dbg) t_start = __builtin_amdgcn_s_memrealtime();
+  if (kStamps && a.dbg) t_start = __builtin_amdgcn_s_memrealtime();
   constexpr int NC = 4 + (DROP ? 2 : 0) + (MODE == 1 ? 1 : 0);   // vector-memory ops per chunk and wave
   // chunk c -> buffer c & 1: two 64-key pieces, wave w moves key rows 64 i + 8 w .. + 7 of K and of V
   auto issue = [&](int c) {
@@ -1180,7 +1189,7 @@ void attn_fwd_stream_kernel(AttnArgs a, const uint32_t* qmaj) {
                           ((n & 4) ? 0xffffu : 0u) | ((n & 8) ? 0xffff0000u : 0u));
   }
   lds_barrier();
-  if (a.dbg) t_staged = __builtin_amdgcn_s_memrealtime();
+  if (kStamps && a.dbg) t_staged = __builtin_amdgcn_s_memrealtime();
   const bool act = qw0 < a.Lq;
   const int qlast = min(a.Lq, qw0 + 32) - 1;   // the wave's last query (causal: later key tiles are all masked)
   const float sc2 = a.scale2;
@@ -1289,7 +1298,7 @@ void attn_fwd_stream_kernel(AttnArgs a, const uint32_t* qmaj) {
       lds_barrier();                 // ... and visible to every wave
     }
   }
-  if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0 && bh < 1024) {
+  if (kStamps && a.dbg && blockIdx.x == 0 && threadIdx.x == 0 && bh < 1024) {
     g_attn_dbg[128 + 4 * bh] = t_start;
     g_attn_dbg[129 + 4 * bh] = t_staged;
     g_attn_dbg[130 + 4 * bh] = __builtin_amdgcn_s_memrealtime();   // (compute done; the stores follow)
@@ -1331,7 +1340,8 @@ ASRX_DEV int bk_koff(int r, int e) { return r * 64 + 8 * ((e >> 3) ^ bk_kswz(r))
 ASRX_DEV int bk_doff(int r, int e) { return r * 32 + 8 * ((e >> 3) ^ bk_dswz(r)) + (e & 7); }
 
 template <int MODE, int NKT, bool MULTI = false>
-__global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
+__global__ __launch_bounds__(64 * NKT) __attribute__((amdgpu_waves_per_eu(NKT == 4 && MODE != 2 ? 2 : 1)))
+void attn_bwd_res_kernel(AttnArgs a) {   // (NKT 4: two workgroups per CU, the 256-register file without AGPRs)
   a.seed = seed_eff(a.seed);
   constexpr int NQB = 2;                                          // Q / dO image buffers
   // NKT 32-key blocks (= waves); keys past Lk are zero rows with a -inf score bias
@@ -1514,8 +1524,9 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
       MULTI ? brsrc(a.dq_acc + (int64_t)blockIdx.y * ((int64_t)a.B * a.Lq * a.H * 64) + ((int64_t)b * a.Lq * a.H + h) * 64,
                       0u, (int32_t)(((int64_t)(a.Lq - 1) * a.H * 64 + 64) * 4))
               : brsrc(dqh, 0u, (int32_t)(((int64_t)(a.Lq - 1) * a.dqr + 64) * 2));
-  auto dq_chunk = [&](int cc) {
-    const int bq = cc & 1, q0 = cc * 32;
+  auto dq_chunk = [&](int cc, auto bqc) {
+    const int bq = (int)bqc;   // (= cc & 1; a std::integral_constant in the unrolled loop: immediate LDS offsets)
+    const int q0 = cc * 32;
 #pragma unroll
     for (int j = 0; j < TPW; ++j) {
       const int tl = w + NKT * j;
@@ -1587,8 +1598,9 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
   // straight-line block (the dQ MFMAs and LDS reads fill the gaps of the softmax-gradient VALU work); one
   // barrier per chunk publishes dS(ch) and the next chunk's Q/dO.  X holds chunk ch (published) until its keep
   // words are read, then chunk ch + 1 (in flight until the publish).
-  auto iter = [&](int ch, Pf& X) {
-    const int buf = ch & 1, q0 = ch * 32, qb = buf;
+  auto iter = [&](int ch, Pf& X, auto bufc) {
+    const int buf = (int)bufc, qb = buf;   // (= ch & 1, compile-time in the unrolled loop)
+    const int q0 = ch * 32;
     // 4-bit keep masks of this lane's queries (16qs + 4g + r) for its two keys
     uint32_t nib[2][2];
     // (dropout needs the keep words here: the launch sends calls without them to the tiled kernels, which hash)
@@ -1613,7 +1625,7 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
 #pragma unroll
         for (int t = 0; t < 2; ++t)
           *(uint2*)(sds + buf * NK * RDT + bk_doff(kwl + 16 * t + li, 16 * qs + 4 * g)) = make_uint2(0, 0);
-      if (ch > 0) dq_chunk(ch - 1);
+      if (ch > 0) dq_chunk(ch - 1, buf ^ 1);
     } else {
       f4_t s[2][2], dp[2][2];   // [qs][t]
 #pragma unroll
@@ -1628,7 +1640,7 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
           dp[qs][t] = mfma32(d1f, vf[t][1], mfma32(d0f, vf[t][0], f4_t{0.f, 0.f, 0.f, 0.f}));
         }
       }
-      if (ch > 0) dq_chunk(ch - 1);
+      if (ch > 0) dq_chunk(ch - 1, buf ^ 1);
       const bool diag = causal && kw0 + 31 > q0;
 #pragma unroll
       for (int qs = 0; qs < 2; ++qs) {
@@ -1671,8 +1683,22 @@ __global__ __launch_bounds__(64 * NKT) void attn_bwd_res_kernel(AttnArgs a) {
     __syncthreads();
     ATTN_TS(4 + 4 * ch);
   };
-  for (int ch = 0; ch < nch; ++ch) iter(ch, A);
-  dq_chunk(nch - 1);
+  // unrolled by two: each copy's LDS buffers are compile-time (round 6: the ch & 1 buffer offsets had cost ~30 VALU
+  // address operations per chunk)
+  // (the dense-mask mode keeps the rolled loop: unrolled, its per-element mask loads spilled ~100 VGPRs)
+  using B0 = std::integral_constant<int, 0>;
+  using B1 = std::integral_constant<int, 1>;
+  if constexpr (MODE == 2) {
+    for (int ch = 0; ch < nch; ++ch) iter(ch, A, ch & 1);
+  } else {
+    int ch = 0;
+    for (; ch + 1 < nch; ch += 2) {
+      iter(ch, A, B0{});
+      iter(ch + 1, A, B1{});
+    }
+    if (ch < nch) iter(ch, A, B0{});
+  }
+  dq_chunk(nch - 1, (nch - 1) & 1);
 
   // dK / dV staged through LDS and stored as whole 128-B rows: 8 lanes x 16 B per key row, 4 store instructions per
   // tensor and wave.  The fragment layout gives each lane 4 values of one row per tile (16 8-B stores per lane at a
