@@ -74,7 +74,7 @@ struct AttnArgs {
   int dbg;   // phase timestamps of block 0 / wave 0 into g_attn_dbg (tools only; ASRX_ATTN_DBG=1)
 };
 
-__device__ unsigned long long g_attn_dbg[128 + 4 * 1024];   // [128..]: per-block real-time (fwd)
+__device__ unsigned long long g_attn_dbg[128 + 8 * 1024];   // [128..]: per-block real-time (fwd), [128 + 4096..] (bwd)
 // The stamps are compiled in only for diagnostic builds (ASRX_CFLAGS=-DASRX_ATTN_STAMPS; the shipped library reads
 // ASRX_ATTN_DBG but records nothing): four stamp branches per backward chunk had cost ~25 scalar / exec-mask
 // instructions of the loop.
@@ -1343,6 +1343,8 @@ template <int MODE, int NKT, bool MULTI = false>
 __global__ __launch_bounds__(64 * NKT) __attribute__((amdgpu_waves_per_eu(NKT == 4 && MODE != 2 ? 2 : 1)))
 void attn_bwd_res_kernel(AttnArgs a) {   // (NKT 4: two workgroups per CU, the 256-register file without AGPRs)
   a.seed = seed_eff(a.seed);
+  uint64_t t_blk0 = 0;   // per-block real-time stamps (diagnostic builds)
+  if (kStamps && a.dbg) t_blk0 = __builtin_amdgcn_s_memrealtime();
   constexpr int NQB = 2;                                          // Q / dO image buffers
   // NKT 32-key blocks (= waves); keys past Lk are zero rows with a -inf score bias
   constexpr int NK = NKT * 32, NTHR = NKT * 64;
@@ -1377,18 +1379,13 @@ void attn_bwd_res_kernel(AttnArgs a) {   // (NKT 4: two workgroups per CU, the 2
 
   const bf16_t* Kb = a.k + b * a.kb + h * 64;
   const bf16_t* Vb = a.v + b * a.vb + h * 64;
-  {
-    uint4 kv[NK * 8 / NTHR];
+  // K rows for the LDS image: loads issued here, the image written after chunk 0's loads are issued too (round 6:
+  // written first, the image's wait had put chunk 0's fetch a second HBM round trip behind the K rows)
+  uint4 kv[NK * 8 / NTHR];
 #pragma unroll
-    for (int i = 0; i < NK * 8 / NTHR; ++i) {
-      const int c = tid + i * NTHR, row = c >> 3, dc = (c & 7) * 8;
-      kv[i] = *(const uint4*)(Kb + (int64_t)min(kb0 + row, a.Lk - 1) * a.kr + dc);
-    }
-#pragma unroll
-    for (int i = 0; i < NK * 8 / NTHR; ++i) {
-      const int c = tid + i * NTHR, row = c >> 3, dc = (c & 7) * 8;
-      *(uint4*)(sk + bk_koff(row, dc)) = kb0 + row < a.Lk ? kv[i] : make_uint4(0, 0, 0, 0);
-    }
+  for (int i = 0; i < NK * 8 / NTHR; ++i) {
+    const int c = tid + i * NTHR, row = c >> 3, dc = (c & 7) * 8;
+    kv[i] = *(const uint4*)(Kb + (int64_t)min(kb0 + row, a.Lk - 1) * a.kr + dc);
   }
   s8_t kf[2][2], vf[2][2];
   float kbias[2];
@@ -1567,6 +1564,11 @@ void attn_bwd_res_kernel(AttnArgs a) {   // (NKT 4: two workgroups per CU, the 2
   ATTN_TS(0);
   Pf A;
   fetch(A, 0);
+#pragma unroll
+  for (int i = 0; i < NK * 8 / NTHR; ++i) {
+    const int c = tid + i * NTHR, row = c >> 3, dc = (c & 7) * 8;
+    *(uint4*)(sk + bk_koff(row, dc)) = kb0 + row < a.Lk ? kv[i] : make_uint4(0, 0, 0, 0);
+  }
   publish(A, 0, 0);
   __syncthreads();
   // this wave's K fragments (B operands of S) from the block's K image (round 5 read K from HBM twice: for the
@@ -1730,6 +1732,12 @@ void attn_bwd_res_kernel(AttnArgs a) {   // (NKT 4: two workgroups per CU, the 2
       *(uint4*)(a.dk + b * a.dkb + (int64_t)key * a.dkr + h * 64 + c8) = vk;
       *(uint4*)(a.dv + b * a.dvb + (int64_t)key * a.dvr + h * 64 + c8) = vv;
     }
+  }
+  if (kStamps && a.dbg && blockIdx.y == 0 && tid == 0 && bh < 1024) {
+    g_attn_dbg[128 + 4096 + 4 * bh] = t_blk0;
+    g_attn_dbg[129 + 4096 + 4 * bh] = 0;
+    g_attn_dbg[130 + 4096 + 4 * bh] = __builtin_amdgcn_s_memrealtime();   // (stores issued, not landed)
+    g_attn_dbg[131 + 4096 + 4 * bh] = __smid();
   }
 }
 
@@ -2029,7 +2037,7 @@ extern "C" int asrx_attention_bwd(const asrx_attn_desc* d, void* stream) {
 
 // tools only (not part of include/asrx.h): copy the phase timestamps of the last debug launch
 extern "C" int asrx_attn_debug_read(unsigned long long* host, int n) {
-  if (!host || n < 0 || n > 128 + 4 * 1024) return ASRX_ERR_ARG;
+  if (!host || n < 0 || n > 128 + 8 * 1024) return ASRX_ERR_ARG;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_attn_dbg), sizeof(unsigned long long) * n) == hipSuccess ? ASRX_OK
                                                                                                        : ASRX_ERR_LAUNCH;
 }

@@ -67,7 +67,7 @@ def main():
     ap.add_argument("--only", default="enc,cross,dec")
     ap.add_argument("--variant", default="auto")
     ap.add_argument("--sweep", action="store_true", help="Lq sweep at Lk=249 (per-chunk vs fixed cost)")
-    ap.add_argument("--dbg", action="store_true", help="phase timestamps of block 0 / wave 0 of the backward")
+    ap.add_argument("--dbg", action="store_true", help="phase timestamps (a diagnostic build: ASRX_CFLAGS=-DASRX_ATTN_STAMPS)")
     ap.add_argument("--exp", default="", help="comma list of ASRX_ATTN_EXP values for the backward (a diagnostic "
                     "build's timing-only switches, wrong results: 1 no loop barrier, 2 no chunk fetch, 4 no dQ sweep, "
                     "8 no dV/dK MFMAs)")
@@ -95,12 +95,20 @@ def main():
             bwd()
             torch.cuda.synchronize()
             nb = B * H
-            buf = (ctypes.c_ulonglong * (128 + 4 * nb))()
-            lib().asrx_attn_debug_read(buf, 128 + 4 * nb)
+            buf = (ctypes.c_ulonglong * (128 + 8 * 1024))()
+            lib().asrx_attn_debug_read(buf, 128 + 8 * 1024)
             ts = list(buf)
+            pc = lambda v: [int(sorted(v)[int(q * (len(v) - 1))]) for q in (0, .1, .5, .9, 1)]   # noqa: E731
+            bb = [ts[128 + 4096 + 4 * i:132 + 4096 + 4 * i] for i in range(nb)]
+            if bb[0][0]:
+                t0b = min(x[0] for x in bb)
+                print(name, "bwd per-block (10 ns ticks; pct 0/10/50/90/100): start", pc([x[0] - t0b for x in bb]),
+                      " total", pc([x[2] - x[0] for x in bb]), " end", pc([x[2] - t0b for x in bb]),
+                      " distinct CUs", len(set(x[3] for x in bb)))
+                srt = sorted(bb, key=lambda x: x[0])
+                print("   bwd start ticks of blocks 240..272 by start order:", [x[0] - t0b for x in srt[240:272]])
             blk = [ts[128 + 4 * i:132 + 4 * i] for i in range(nb)]
             t00 = min(x[0] for x in blk)
-            pc = lambda v: [int(sorted(v)[int(q * (len(v) - 1))]) for q in (0, .1, .5, .9, 1)]   # noqa: E731
             print(name, "fwd per-block (10 ns ticks; pct 0/10/50/90/100): start", pc([x[0] - t00 for x in blk]),
                   " staged", pc([x[1] - x[0] for x in blk]), " total", pc([x[2] - x[0] for x in blk]),
                   " end", pc([x[2] - t00 for x in blk]), " distinct CUs", len(set(x[3] for x in blk)))
