@@ -92,6 +92,8 @@ constexpr bool kStamps = false;
 // IEEE-754 maximum (NaN-propagating, like torch.max): v_maximum3_f32 on gfx950.  fmaxf (maxnum) first
 // canonicalises every MFMA result with a v_max_f32 x, x — twice the instructions of the row-max reductions.
 ASRX_DEV float fmx(float a, float b) { return __builtin_elementwise_maximum(a, b); }
+// lazy-rescale threshold of the forwards' online softmax (log2 units: probabilities up to 2^8 against a stale max)
+constexpr float kLazy = 8.f;
 
 ASRX_DEV bool masked(const AttnArgs& a, int b, int q, int key) {
   if (key >= a.Lk) return true;
@@ -812,14 +814,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
         }
       mt = xmax4(mt);
       const float m_new = fmx(m_run[qs], mt);
-      const float m_use = m_new == -INFINITY ? 0.f : m_new;
-      if (__ballot(m_new != m_run[qs])) {   // rescale only when some row's max grew (exact, wave-uniform)
-        const float alpha = exp2_raw(m_run[qs] - m_use);
+      // lazy rescale (wave-uniform): the rows' reference maxima move only when some row's max grew by more than
+      // 2^8; in between, probabilities up to 2^8 accumulate against the stale reference (exact algebra, fp32 sums;
+      // round 6: the exact rescale ran on almost every tile of random scores, ~40 of the tile's ~190 VALU)
+      if (__ballot(m_new - m_run[qs] > kLazy)) {
+        const float alpha = exp2_raw(m_run[qs] - (m_new == -INFINITY ? 0.f : m_new));
         l_run[qs] *= alpha;
 #pragma unroll
         for (int u = 0; u < 4; ++u) o[u][qs] *= alpha;
         m_run[qs] = m_new;
       }
+      const float m_use = m_run[qs] == -INFINITY ? 0.f : m_run[qs];
       float rs = -0.f;   // (x + -0 = x exactly: the first add folds away)
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
@@ -978,14 +983,14 @@ void attn_fwd_kq_kernel(AttnArgs a, const uint32_t* qmaj) {
                        fmx(fmx(sc[1][qs][0], sc[1][qs][1]), fmx(sc[1][qs][2], sc[1][qs][3])));
       mt = xmax4(mt);
       const float m_new = fmx(m_run[qs], mt);
-      const float m_use = m_new == -INFINITY ? 0.f : m_new;
-      if (__ballot(m_new != m_run[qs])) {
-        const float alpha = exp2_raw((m_run[qs] - m_use) * sc2);
+      if (__ballot((m_new - m_run[qs]) * sc2 > kLazy)) {   // lazy rescale (see attn_fwd_res_kernel)
+        const float alpha = exp2_raw((m_run[qs] - (m_new == -INFINITY ? 0.f : m_new)) * sc2);
         l_run[qs] *= alpha;
 #pragma unroll
         for (int u = 0; u < 4; ++u) o[u][qs] *= alpha;
         m_run[qs] = m_new;
       }
+      const float m_use = m_run[qs] == -INFINITY ? 0.f : m_run[qs];
       const float nm = -m_use * sc2;
       float rs = -0.f;   // (x + -0 = x exactly: the first add folds away)
 #pragma unroll
@@ -1198,14 +1203,16 @@ void attn_fwd_stream_kernel(AttnArgs a, const uint32_t* qmaj) {
 #pragma unroll
   for (int u = 0; u < 4; ++u) o[u][0] = o[u][1] = f4_t{0.f, 0.f, 0.f, 0.f};
   float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
+  // (round 6: unrolled by two with compile-time buffers this loop spilled 52 VGPRs at the 128-register bound)
   for (int c = 0; c < nch; ++c) {
-    const bf16_t* skc = sk + (c & 1) * S_CK * 64;
-    const bf16_t* svc = sv + (c & 1) * S_CK * 64;
+    const int cbuf = c & 1;
+    const bf16_t* skc = sk + cbuf * S_CK * 64;
+    const bf16_t* svc = sv + cbuf * S_CK * 64;
     if (act) {
       uint4 dwc[2] = {make_uint4(~0u, ~0u, ~0u, ~0u), make_uint4(~0u, ~0u, ~0u, ~0u)};
       if constexpr (DROP) {
 #pragma unroll
-        for (int qs = 0; qs < 2; ++qs) dwc[qs] = *(const uint4*)(skw + (c & 1) * 1024 + w * 128 + (16 * qs + li) * 4);
+        for (int qs = 0; qs < 2; ++qs) dwc[qs] = *(const uint4*)(skw + cbuf * 1024 + w * 128 + (16 * qs + li) * 4);
       }
 #pragma unroll
       for (int kt = 0; kt < S_CK / 32; ++kt) {
@@ -1225,7 +1232,7 @@ void attn_fwd_stream_kernel(AttnArgs a, const uint32_t* qmaj) {
         uint32_t kvw[2] = {~0u, ~0u};
         if (kvm) {
 #pragma unroll
-          for (int t = 0; t < 2; ++t) kvw[t] = *(const uint32_t*)(skv + (c & 1) * 256 + kt * 32 + 16 * t + 4 * g);
+          for (int t = 0; t < 2; ++t) kvw[t] = *(const uint32_t*)(skv + cbuf * 256 + kt * 32 + 16 * t + 4 * g);
         }
         if (tail || diag || kvm) {
 #pragma unroll
@@ -1246,13 +1253,27 @@ void attn_fwd_stream_kernel(AttnArgs a, const uint32_t* qmaj) {
                            fmx(fmx(s[1][qs][0], s[1][qs][1]), fmx(s[1][qs][2], s[1][qs][3])));
           mt = xmax4(mt);
           const float m_new = fmx(m_run[qs], mt);
-          const float m_use = m_new == -INFINITY ? 0.f : m_new;
-          if (__ballot(m_new != m_run[qs])) {   // rescale only when some row's max grew (exact, wave-uniform)
-            const float alpha = exp2_raw((m_run[qs] - m_use) * sc2);
-            l_run[qs] *= alpha;
+          float m_use;
+          if constexpr (MODE == 1 && DROP) {
+            // exact rescale in the masked dropout copy: the lazy form's longer live ranges spilled 5 VGPRs at the
+            // 128-register bound
+            m_use = m_new == -INFINITY ? 0.f : m_new;
+            if (__ballot(m_new != m_run[qs])) {
+              const float alpha = exp2_raw((m_run[qs] - m_use) * sc2);
+              l_run[qs] *= alpha;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) o[u][qs] *= alpha;
-            m_run[qs] = m_new;
+              for (int u = 0; u < 4; ++u) o[u][qs] *= alpha;
+              m_run[qs] = m_new;
+            }
+          } else {
+            if (__ballot((m_new - m_run[qs]) * sc2 > kLazy)) {   // lazy rescale (see attn_fwd_res_kernel)
+              const float alpha = exp2_raw((m_run[qs] - (m_new == -INFINITY ? 0.f : m_new)) * sc2);
+              l_run[qs] *= alpha;
+#pragma unroll
+              for (int u = 0; u < 4; ++u) o[u][qs] *= alpha;
+              m_run[qs] = m_new;
+            }
+            m_use = m_run[qs] == -INFINITY ? 0.f : m_run[qs];
           }
           const float nm = -m_use * sc2;
           const uint32_t dword = (&dwc[qs].x)[kt];

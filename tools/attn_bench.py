@@ -66,6 +66,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="enc,cross,dec")
     ap.add_argument("--variant", default="auto")
+    ap.add_argument("--batch", type=int, default=B, help="batch size of the c3 cases (default 64)")
     ap.add_argument("--sweep", action="store_true", help="Lq sweep at Lk=249 (per-chunk vs fixed cost)")
     ap.add_argument("--dbg", action="store_true", help="phase timestamps (a diagnostic build: ASRX_CFLAGS=-DASRX_ATTN_STAMPS)")
     ap.add_argument("--exp", default="", help="comma list of ASRX_ATTN_EXP values for the backward (a diagnostic "
@@ -75,8 +76,9 @@ def main():
                     "output stores, 4 no v_exp, 8 no PV MFMAs, 16 no QK MFMAs)")
     args = ap.parse_args()
     os.environ["ASRX_ATTN_KERNEL"] = args.variant
-    cases = {"enc": ("enc_self", 249, 249, False), "cross": ("cross", 64, 249, False),
-             "cross24k": ("cross24k", 64, 249, False, 12 * 2 * D), "dec": ("dec_self", 64, 64, True),
+    bb = args.batch
+    cases = {"enc": ("enc_self", 249, 249, False, 2 * D, bb), "cross": ("cross", 64, 249, False, 2 * D, bb),
+             "cross24k": ("cross24k", 64, 249, False, 12 * 2 * D, bb), "dec": ("dec_self", 64, 64, True, 2 * D, bb),
              "c5": ("c5_self", 999, 999, False, 2 * D, 16)}   # c5: B = 16, T' = 999 (the streamed kernels)
     if args.sweep:
         for lq in (32, 64, 128, 192, 249):
@@ -94,18 +96,18 @@ def main():
             fwd()
             bwd()
             torch.cuda.synchronize()
-            nb = B * H
+            nb = bb * H
             buf = (ctypes.c_ulonglong * (128 + 8 * 1024))()
             lib().asrx_attn_debug_read(buf, 128 + 8 * 1024)
             ts = list(buf)
             pc = lambda v: [int(sorted(v)[int(q * (len(v) - 1))]) for q in (0, .1, .5, .9, 1)]   # noqa: E731
-            bb = [ts[128 + 4096 + 4 * i:132 + 4096 + 4 * i] for i in range(nb)]
-            if bb[0][0]:
-                t0b = min(x[0] for x in bb)
-                print(name, "bwd per-block (10 ns ticks; pct 0/10/50/90/100): start", pc([x[0] - t0b for x in bb]),
-                      " total", pc([x[2] - x[0] for x in bb]), " end", pc([x[2] - t0b for x in bb]),
-                      " distinct CUs", len(set(x[3] for x in bb)))
-                srt = sorted(bb, key=lambda x: x[0])
+            bw = [ts[128 + 4096 + 4 * i:132 + 4096 + 4 * i] for i in range(nb)]
+            if bw[0][0]:
+                t0b = min(x[0] for x in bw)
+                print(name, "bwd per-block (10 ns ticks; pct 0/10/50/90/100): start", pc([x[0] - t0b for x in bw]),
+                      " total", pc([x[2] - x[0] for x in bw]), " end", pc([x[2] - t0b for x in bw]),
+                      " distinct CUs", len(set(x[3] for x in bw)))
+                srt = sorted(bw, key=lambda x: x[0])
                 print("   bwd start ticks of blocks 240..272 by start order:", [x[0] - t0b for x in srt[240:272]])
             blk = [ts[128 + 4 * i:132 + 4 * i] for i in range(nb)]
             t00 = min(x[0] for x in blk)

@@ -59,18 +59,30 @@ def report(trace):
     if len(gem) != len(log):
         print(f"warning: {len(gem)} GEMM dispatches in the last step vs {len(log)} logged launches")
     agg = collections.OrderedDict()
-    for (kn, us), (ln, m, n, k, batch, sk) in zip(gem, log):
-        if kn != ln:
-            print("mismatch", kn, ln)
-        key = (ln, m, n, k, batch, sk)
-        a = agg.setdefault(key, [0, 0.0])
-        a[0] += 1
+    j, prev = 0, None
+    for kn, us in gem:   # a launch split into several dispatches adds them to its logged entry
+        if j < len(log) and log[j][0] == kn:
+            key = tuple(log[j])
+            j += 1
+            a = agg.setdefault(key, [0, 0.0])
+            a[0] += 1
+        elif prev is not None and prev[0] == kn:
+            key = prev
+            a = agg[key]
+        else:
+            key = (kn, 0, 0, 0, 1, 1)   # not logged (e.g. the conv2 weight-gradient GEMM)
+            a = agg.setdefault(key, [0, 0.0])
+            a[0] += 1
         a[1] += us
+        prev = key
+    if j != len(log):
+        print(f"warning: {len(log) - j} logged launches unmatched")
     tot = sum(v[1] for v in agg.values())
     print(f"{'us/call':>8s} {'calls':>5s} {'ms':>7s} {'TF':>6s}  m x n x k (batch, splitk)  kernel")
     for (ln, m, n, k, batch, sk), (cnt, us) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
         fl = 2.0 * (m * n * k if n else k) * batch
         print(f"{us / cnt:8.1f} {cnt:5d} {us / 1e3:7.3f} {fl / (us / cnt) / 1e6:6.0f}  {m}x{n}x{k} ({batch},{sk})  {ln}")
+    print(f"GEMM dispatches {len(gem)}, logged launches {len(log)}")
     print(f"GEMM total {tot / 1e3:.3f} ms/step")
 
 
