@@ -1247,6 +1247,10 @@ constexpr int TK_NST = 4;
 
 // conv2 gather mode (cv.on): B rows are the conv2 im2col rows gathered straight from the channels-last conv1
 // output y1 (g.b): chunk c of row (b, t2, f2) = tap c / 8 (kh, kw), channels 8 (c % 8) .. +7.
+// Reduction order (round 6): the K sweep runs over (b, f2, t2) with t2 fastest, not over dy2's storage order
+// (b, t2, f2): consecutive rows then read y1 at t1 = 2 t2 + kw, 256 B apart, so a 32-row stage gathers three
+// contiguous ~8 KiB spans of y1 per tap row kh instead of 32 isolated 128-B lines 2 f1 rows (128 KiB) apart; the
+// dy2 rows become 2.4 KiB-strided whole lines.  (ASRX_GEMM_DBG & 4096: the storage order, for A/B.)
 struct TallkConv {
   int on, F1, T1, F2, T2;
   int64_t y1_bytes;
@@ -1260,7 +1264,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_tallk_kernel(GemmArgs g, TallkC
   const int nsteps = k1 > k0 ? (k1 - k0 + TK_ROWS - 1) / TK_ROWS : 0;
   const bf16_t* A = (const bf16_t*)g.a + (int64_t)k0 * g.lda;
   const bf16_t* B = (const bf16_t*)g.b + (int64_t)k0 * g.ldb;
-  const v4i_t srda = make_srd(A, (int64_t)max(0, k1 - k0) * g.lda * 2);
+  const bool tord = cv.on && !(g.dbg & 4096);   // K order (b, f2, t2), see TallkConv
+  const v4i_t srda = tord ? make_srd(g.a, (int64_t)g.K * g.lda * 2) : make_srd(A, (int64_t)max(0, k1 - k0) * g.lda * 2);
   const v4i_t srdb = cv.on ? make_srd(g.b, cv.y1_bytes) : make_srd(B, (int64_t)max(0, k1 - k0) * g.ldb * 2);
   const int a_bytes = TK_ROWS * 64 * 2;                  // A image [32][64]
   const int ninst = (a_bytes + TK_ROWS * N * 2) / 1024;  // 1-KiB DMA pieces per stage
@@ -1271,19 +1276,49 @@ __global__ __launch_bounds__(512) void gemm_bf16_tallk_kernel(GemmArgs g, TallkC
     const int r0 = s * TK_ROWS;
     // gather mode: (b, t2, f2) of the stage's first row once; a lane's row (first + dr, dr < 32) by carries
     int f20 = 0, t20 = 0, b0 = 0;
-    if (cv.on) {
+    if (tord) {
+      const int gr0 = k0 + r0;
+      t20 = gr0 % cv.T2;
+      const int q = gr0 / cv.T2;
+      f20 = q % cv.F2;
+      b0 = q / cv.F2;
+    } else if (cv.on) {
       const int gr0 = k0 + r0;
       f20 = gr0 % cv.F2;
       const int q = gr0 / cv.F2;
       t20 = q % cv.T2;
       b0 = q / cv.T2;
     }
+    // (b, t2, f2) of stage row `row` (row < 32) by carries from the stage's first row
+    auto rowpos = [&](int row, int& b, int& t2, int& f2) {
+      b = b0;
+      if (tord) {
+        t2 = t20 + row;
+        f2 = f20;
+        while (t2 >= cv.T2) { t2 -= cv.T2; if (++f2 == cv.F2) { f2 = 0; ++b; } }
+      } else {
+        f2 = f20 + row;
+        t2 = t20;
+        while (f2 >= cv.F2) { f2 -= cv.F2; ++t2; }
+        while (t2 >= cv.T2) { t2 -= cv.T2; ++b; }
+      }
+    };
     if (g.dbg & 8) return;   // (diagnostic: no operand loads)
     for (int j = w; j < ninst; j += 8) {
       const int slot = j * 64 + l;   // 16-B slot of the stage image
       if (slot < a_bytes / 16) {
         const int row = slot >> 3, c = (slot & 7) ^ (row & 6);
-        dma16_asm(img + j * 1024, srda, (uint32_t)(((r0 + row) * g.lda + c * 8) * 2));
+        uint32_t voff;
+        if (!tord) {
+          voff = (uint32_t)(((r0 + row) * g.lda + c * 8) * 2);
+        } else if (k0 + r0 + row >= k1) {
+          voff = 0x80000000u;   // past the split: reads as zeros
+        } else {
+          int b, t2, f2;
+          rowpos(row, b, t2, f2);
+          voff = (uint32_t)((((b * cv.T2 + t2) * cv.F2 + f2) * g.lda + c * 8) * 2);
+        }
+        dma16_asm(img + j * 1024, srda, voff);
       } else {
         const int sb = slot - a_bytes / 16, row = sb / cpr, c = (sb % cpr) ^ (row & 6);
         uint32_t voff;
@@ -1294,9 +1329,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_tallk_kernel(GemmArgs g, TallkC
           if (gr >= k1) {
             voff = 0x80000000u;   // past the split: reads as zeros
           } else {
-            int f2 = f20 + row, t2 = t20, b = b0;
-            while (f2 >= cv.F2) { f2 -= cv.F2; ++t2; }
-            while (t2 >= cv.T2) { t2 -= cv.T2; ++b; }
+            int b, t2, f2;
+            rowpos(row, b, t2, f2);
             const int tap = c >> 3, kh = (tap * 11) >> 5, kw = tap - 3 * kh;   // tap / 3 for tap <= 8
             voff = (uint32_t)(((((b * cv.F1 + 2 * f2 + kh) * cv.T1 + 2 * t2 + kw) * 64) + (c & 7) * 8) * 2);
           }
