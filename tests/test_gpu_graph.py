@@ -152,3 +152,48 @@ def test_graphed_forward_sees_weight_updates():
         out2 = fwd(s, t[:, :-1], k[:, :-1]).clone()
         ref2 = m(s, t[:, :-1], k[:, :-1])
     assert torch.equal(out2, ref2)
+
+
+def test_graph_pool_block_reuse_breaks_write_once_buffers():
+    """Cause of the round-5 graph fault: the reverted experiment allocated the grouped
+    weight-gradient table DURING the capture and wrote it once, outside the replayed work.  Torch's graph pool hands
+    a block freed earlier in the same capture to a later allocation of the capture, so on every replay the kernels
+    of the block's earlier tenant write into the "write-once" table before its reader runs — the first replay read
+    garbage group pointers (hipErrorIllegalAddress).  Per-replay uploads are immune (the upload is a captured launch
+    right before its reader, in stream order), and the shipped device-resident tile / block maps are allocated only
+    outside a capture (asrx.kernels._grouped_xcd).  This test reproduces the aliasing without a fault."""
+    n = 1 << 16
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        x = torch.empty(n, dtype=torch.int32, device=dev)
+        x.fill_(1)                     # the earlier tenant's captured kernel
+        px = x.data_ptr()
+        del x
+        table = torch.empty(n, dtype=torch.int32, device=dev)   # the pool reuses x's block
+        out = table + 0                # the table's captured reader
+    assert table.data_ptr() == px
+    table.fill_(7)                     # "written once", outside the graph
+    g.replay()
+    torch.cuda.synchronize()
+    assert bool((out == 1).all()), "the replay's earlier kernel overwrote the write-once buffer"
+    assert bool((table == 1).all())
+
+
+def test_grouped_const_maps_allocated_outside_capture():
+    """The shipped form of write-once graph data: the grouped launch's shape-only maps (asrx.kernels._CONST_MAPS)
+    are created only when no capture is underway, so they never come from a graph's private pool; a plan first met
+    inside a capture takes the per-call buffer with a captured upload instead."""
+    from asrx import kernels as K
+    from asrx.train import Trainer
+    m, cfg = build("c1", 0.0)
+    data = batches(cfg, CONFIGS["c1"], 4)
+    # (never cleared here: graphs captured earlier in the process point at these buffers)
+    tr = Trainer(m, lr=1e-3, graph=True)
+    for b in data:                     # eager warm-up steps, then the capture and replays
+        tr.step(*b)
+    torch.cuda.synchronize()
+    assert tr._cap is not None
+    assert K._CONST_MAPS, "no device-resident map was created outside the capture"
+    for cdev, _, _ in K._CONST_MAPS.values():
+        assert cdev.is_cuda and cdev.numel() > 0
