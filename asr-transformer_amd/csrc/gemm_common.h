@@ -237,10 +237,28 @@ ASRX_DEV f4_t epi_vals(const GemmArgs& g, int m, int n, f4_t v, f4_t b4, uint2 p
 // output otherwise sits dirty in L2 until the end-of-kernel write-back.  c3 step 12.13-12.14 -> 12.07-12.08 ms
 // (same box, both orders); ASRX_GEMM_DBG & 1024 restores ordinary stores (A/B)
 typedef uint32_t epi_u2_t __attribute__((ext_vector_type(2)));
+// The diagnostic store variants are compiled only into diagnostic builds (ASRX_CFLAGS=-DASRX_GEMM_DIAG; round 6):
+// tested per store at run time they had cost two branches and their SALU in every fragment store of the epilogues.
+#ifdef ASRX_GEMM_DIAG
+constexpr bool kGemmDiag = true;
+#else
+constexpr bool kGemmDiag = false;
+#endif
 template <typename T>
 ASRX_DEV void epi_store(const GemmArgs& g, T* p, T v) {
-  if (g.dbg & 2048) asm volatile("" :: "v"(v), "v"(p));   // (diagnostic: the epilogue without its stores)
-  else if (g.dbg & 1024) *p = v;
+  if (kGemmDiag && (g.dbg & 2048)) asm volatile("" :: "v"(v), "v"(p));   // (diagnostic: the epilogue without its stores)
+  else if (kGemmDiag && (g.dbg & 1024)) *p = v;
+  else __builtin_nontemporal_store(v, p);
+}
+// global-address-space form: pointers laundered through an opaque asm (the paired epilogue's row steps) lose their
+// address space, and a generic pointer compiles to FLAT stores, which the hardware counts on lgkmcnt too — every
+// later s_waitcnt lgkmcnt(0) for an LDS read (the bias) also waited for them
+typedef __attribute__((address_space(1))) v4u_t g_v4u_t;
+typedef __attribute__((address_space(1))) uint32_t g_u32_t;
+template <typename T>
+ASRX_DEV void epi_store_g(const GemmArgs& g, __attribute__((address_space(1))) T* p, T v) {
+  if (kGemmDiag && (g.dbg & 2048)) asm volatile("" :: "v"(v), "v"(p));
+  else if (kGemmDiag && (g.dbg & 1024)) *p = v;
   else __builtin_nontemporal_store(v, p);
 }
 
@@ -289,10 +307,11 @@ ASRX_DEV int epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int
       //  where they held registers beside the accumulators for the whole loop)
       asm volatile("" : "+v"(mr));
       const int nl = n0 + wn;   // (multiple of 64)
-      bf16_t* const cbase = (bf16_t*)g.c + (int64_t)mr * g.ldc + nl + 16 * (gq & 1) + 8 * (gq >> 1);
+      typedef __attribute__((address_space(1))) bf16_t g_bf16_t;
+      g_bf16_t* const cbase = (g_bf16_t*)g.c + (int64_t)mr * g.ldc + nl + 16 * (gq & 1) + 8 * (gq >> 1);
       const int64_t cstep = (int64_t)16 * g.ldc;
       const uint32_t ibase = (uint32_t)mr * (uint32_t)g.N + (uint32_t)(nl + 4 * gq), istep = 16u * (uint32_t)g.N;
-      uint32_t* const mbase = (EPI & E_MASKOUT) ? (uint32_t*)g.mask_out + (int64_t)mr * g.ld_mask + (nl >> 5) : nullptr;
+      g_u32_t* const mbase = (EPI & E_MASKOUT) ? (g_u32_t*)g.mask_out + (int64_t)mr * g.ld_mask + (nl >> 5) : nullptr;
       const int64_t mstep = (int64_t)16 * g.ld_mask;
       uint32_t gwl[GPL ? TN / 2 : 1][GPL ? TM : 1];
 
@@ -326,8 +345,8 @@ ASRX_DEV int epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int
       // fragment)
       auto tile_body = [&](auto chk_tag) {
         constexpr bool CHK = decltype(chk_tag)::value;
-        bf16_t* cj = cbase;
-        uint32_t* mj = mbase;
+        g_bf16_t* cj = cbase;
+        g_u32_t* mj = mbase;
         uint32_t ij = ibase;
 #pragma unroll
         for (int j = 0; j < TM; ++j, cj += cstep, mj += mstep, ij += istep) {
@@ -365,7 +384,7 @@ ASRX_DEV int epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int
             const auto sy = __builtin_amdgcn_permlane16_swap(ay, by, false, false);
             if (!CHK || (m < g.M && ncol < g.N)) {
               v4u_t u = {sx[0], sy[0], sx[1], sy[1]};
-              epi_store(g, (v4u_t*)(cj + 16 * i), u);
+              epi_store_g(g, (g_v4u_t*)(cj + 16 * i), u);
             }
             if constexpr ((EPI & E_MASKOUT) != 0) {
               // ReLU outputs are >= 0, so "> 0" is "low 15 bits nonzero": adding 0x7fff to each 15-bit half sets
@@ -384,7 +403,7 @@ ASRX_DEV int epilogue_tile(const GemmArgs& g, int z, int m0, int n0, int wm, int
               wv = x16[0] | x16[1];
               const auto x32 = __builtin_amdgcn_permlane32_swap(wv, wv, false, false);
               wv = x32[0] | x32[1];
-              if (gq == 0 && (!CHK || (m < g.M && na < g.N))) epi_store(g, mj + i / 2, wv);
+              if (gq == 0 && (!CHK || (m < g.M && na < g.N))) epi_store_g(g, mj + i / 2, wv);
             }
           }
         }
