@@ -250,16 +250,17 @@ ASRX_DEV void epi_store(const GemmArgs& g, T* p, T v) {
   else if (kGemmDiag && (g.dbg & 1024)) *p = v;
   else __builtin_nontemporal_store(v, p);
 }
-// global-address-space form: pointers laundered through an opaque asm (the paired epilogue's row steps) lose their
-// address space, and a generic pointer compiles to FLAT stores, which the hardware counts on lgkmcnt too — every
-// later s_waitcnt lgkmcnt(0) for an LDS read (the bias) also waited for them
+// global-address-space form for the paired bf16 epilogue of the p3 / p4 / ring tiles: their row pointers are laundered
+// through an opaque asm and had compiled to FLAT stores, which carry no non-temporal bit — these tiles' C and mask
+// stores were ordinary (temporal) stores all along.  Measured (round 6, tools/blas_ref.py): as global non-temporal
+// stores the FFN1 forward with its mask bits went 49 -> 65 us, so they stay temporal, now as global stores
+// (round 4 had found temporal stores faster for the p4 GEMMs alone, and kept non-temporal for the one-round ws tiles).
 typedef __attribute__((address_space(1))) v4u_t g_v4u_t;
 typedef __attribute__((address_space(1))) uint32_t g_u32_t;
 template <typename T>
 ASRX_DEV void epi_store_g(const GemmArgs& g, __attribute__((address_space(1))) T* p, T v) {
   if (kGemmDiag && (g.dbg & 2048)) asm volatile("" :: "v"(v), "v"(p));
-  else if (kGemmDiag && (g.dbg & 1024)) *p = v;
-  else __builtin_nontemporal_store(v, p);
+  else *p = v;
 }
 
 typedef __attribute__((address_space(3))) const float lds_cfloat_t;
