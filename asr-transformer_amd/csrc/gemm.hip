@@ -250,7 +250,9 @@ __global__ __launch_bounds__(256) void gemm_bf16_grouped_dev_kernel(float alpha,
 
 // diagnostics switch (ASRX_GEMM_DBG, or asrx_gemm_set_debug for interleaved A/B in one process): 1 = skip the
 // epilogue stores, 4 = issue each LDS-DMA stage in one block, 8 = no operand loads (compute on stale LDS), 256 =
-// the fused AdamW epilogue without its load look-ahead
+// the fused AdamW epilogue without its load look-ahead.  The kernels honour it only in diagnostic builds
+// (ASRX_CFLAGS=-DASRX_GEMM_DIAG, kGemmDiag; round 6): tested at run time, the bits had cost branches in every
+// K-step and epilogue store of the shipped kernels.
 int g_gemm_dbg = -1;
 int gemm_dbg() {
   if (g_gemm_dbg < 0) { const char* e = getenv("ASRX_GEMM_DBG"); g_gemm_dbg = e ? atoi(e) : 0; }
@@ -358,7 +360,7 @@ ASRX_DEV void p3_body(const GemmArgs& g, const TileSeq tl, int split, int z, uns
 
   PStage<P_BM, AT> sa;
   PStage<BN, BT> sb;
-  const bool noload = (g.dbg & 8) != 0;   // diagnostics (ASRX_GEMM_DBG & 8): no operand loads, compute on stale LDS
+  const bool noload = (kGemmDiag && (g.dbg & 8)) != 0;   // diagnostics (ASRX_GEMM_DBG & 8): no operand loads, compute on stale LDS
   // issue cursor (runs NST - 1 steps ahead of the compute cursor)
   int iv = 0, ik = 0, ib = 0;
   // (a macro rather than a lambda: hipcc/ROCm 7.2 dropped the host device-stubs of most instantiations of this
@@ -401,7 +403,7 @@ ASRX_DEV void p3_body(const GemmArgs& g, const TileSeq tl, int split, int z, uns
   // the tile's last K-step and issue that step's stage only AFTER the epilogue, so the epilogue's wait for its
   // loads (in-order vmcnt) covers only the stage already needed next, not a freshly issued one.
   constexpr bool PRE = EpiPre<EPI, TN, TM>::ANY;
-  const bool sp_iss = !(g.dbg & 4);   // ASRX_GEMM_DBG=4: issue each stage in one block (A/B)
+  const bool sp_iss = !(kGemmDiag && (g.dbg & 4));   // ASRX_GEMM_DBG=4: issue each stage in one block (A/B)
   // younger-operation ledger (lower bounds; an under-count only over-waits).  NST = 3: stage s was issued in step
   // s - 2; younger than it: the stores of step s - 2's epilogue if issued after that step's stage (ea2), stage
   // s + 1 (INST pieces), and the stores of step s - 1's epilogue (eb1 before / ea1 after its stage issue).
@@ -417,7 +419,7 @@ ASRX_DEV void p3_body(const GemmArgs& g, const TileSeq tl, int split, int z, uns
     ea1 = 0;
     eb1 = 0;
     const bool last = kk == nk - 1;
-    const bool defer = PRE && last && g.splitk == 1 && !(g.dbg & 1);
+    const bool defer = PRE && last && g.splitk == 1 && !(kGemmDiag && (g.dbg & 1));
     // This step's stage (s + NST - 1): issued in one block right after the barrier, or (split) in two halves,
     // each behind the fragment reads of one 32-deep k-slice, so the DMA issue overlaps the LDS read latency
     // instead of holding every wave's MFMAs after the barrier.
@@ -506,7 +508,7 @@ ASRX_DEV void p3_body(const GemmArgs& g, const TileSeq tl, int split, int z, uns
             store_partial4(g, split, m0 + wm + 16 * j + (l & 15), n0 + wn + 16 * i + 4 * gq, v);
           }
       } else {
-        if (g.dbg & 1) {
+        if (kGemmDiag && (g.dbg & 1)) {
           keep_live(acc);
         } else {
           const int full = m0 + P_BM <= g.M && n0 + BN <= g.N;
@@ -600,7 +602,7 @@ ASRX_DEV void p4_body(const GemmArgs& g, const TileSeq tl, int split, int z, uns
   const int wave = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int wm = BN == 256 ? (wave >> 2) * 128 : (wave >> 1) * 64;
   const int wn = BN == 256 ? (wave & 3) * 64 : (wave & 1) * 64;
-  const bool noload = (g.dbg & 8) != 0;
+  const bool noload = (kGemmDiag && (g.dbg & 8)) != 0;
 
   P4Stage<P_BM, AT> sa;
   P4Stage<BN, BT> sb;
@@ -705,7 +707,7 @@ ASRX_DEV void p4_body(const GemmArgs& g, const TileSeq tl, int split, int z, uns
     e1 = 0;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    const bool defer = PRE && last && g.splitk == 1 && !(g.dbg & 1);
+    const bool defer = PRE && last && g.splitk == 1 && !(kGemmDiag && (g.dbg & 1));
     EpiPre<EPI, TN, TM> pre;
     if constexpr (PRE) {
       if (defer) epi_prefetch<EPI, TN, TM>(pre, g, (t / ntn) * P_BM, (t % ntn) * BN, wm, wn);
@@ -760,7 +762,7 @@ ASRX_DEV void p4_body(const GemmArgs& g, const TileSeq tl, int split, int z, uns
             float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
             store_partial4(g, split, m0 + wm + 16 * j + (l & 15), n0 + wn + 16 * i + 4 * gq, v);
           }
-      } else if (g.dbg & 1) {
+      } else if (kGemmDiag && (g.dbg & 1)) {
         keep_live(acc);
       } else {
         const int full = m0 + P_BM <= g.M && n0 + BN <= g.N;
@@ -1264,7 +1266,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tallk_kernel(GemmArgs g, TallkC
   const int nsteps = k1 > k0 ? (k1 - k0 + TK_ROWS - 1) / TK_ROWS : 0;
   const bf16_t* A = (const bf16_t*)g.a + (int64_t)k0 * g.lda;
   const bf16_t* B = (const bf16_t*)g.b + (int64_t)k0 * g.ldb;
-  const bool tord = cv.on && !(g.dbg & 4096);   // K order (b, f2, t2), see TallkConv
+  const bool tord = cv.on && !(kGemmDiag && (g.dbg & 4096));   // K order (b, f2, t2), see TallkConv
   const v4i_t srda = tord ? make_srd(g.a, (int64_t)g.K * g.lda * 2) : make_srd(A, (int64_t)max(0, k1 - k0) * g.lda * 2);
   const v4i_t srdb = cv.on ? make_srd(g.b, cv.y1_bytes) : make_srd(B, (int64_t)max(0, k1 - k0) * g.ldb * 2);
   const int a_bytes = TK_ROWS * 64 * 2;                  // A image [32][64]
@@ -1303,7 +1305,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tallk_kernel(GemmArgs g, TallkC
         while (t2 >= cv.T2) { t2 -= cv.T2; ++b; }
       }
     };
-    if (g.dbg & 8) return;   // (diagnostic: no operand loads)
+    if (kGemmDiag && (g.dbg & 8)) return;   // (diagnostic: no operand loads)
     for (int j = w; j < ninst; j += 8) {
       const int slot = j * 64 + l;   // 16-B slot of the stage image
       if (slot < a_bytes / 16) {
@@ -1358,7 +1360,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tallk_kernel(GemmArgs g, TallkC
     if (i < nsteps) issue(i);
   for (int s = 0; s < nsteps; ++s) {
     // stage s landed: this wave's pieces of the younger stages in flight (at most TK_NST - 2 of them) may stay
-    if (g.dbg & 8) wait_vmcnt<0>();
+    if (kGemmDiag && (g.dbg & 8)) wait_vmcnt<0>();
     else wait_vmcnt_bs<0, 15>(min(TK_NST - 2, nsteps - 1 - s) * opw);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -1374,7 +1376,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_tallk_kernel(GemmArgs g, TallkC
       const s4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4_t*)(p + 16 * 64));
       fa[i] = s8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     }
-    if (g.dbg & 16) continue;   // (diagnostic: no fragment reads / MFMAs)
+    if (kGemmDiag && (g.dbg & 16)) continue;   // (diagnostic: no fragment reads / MFMAs)
 #pragma unroll
     for (int j = 0; j < 9; ++j) {
       const int nt = 9 * nq + j;

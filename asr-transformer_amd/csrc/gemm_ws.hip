@@ -131,7 +131,7 @@ do {                                                                            
   }                                                                                         \
 } while (0)
   // ASRX_GEMM_DBG & 64 (diagnostic, garbage results): no loads, no ring barriers — the compute waves' own stream
-  const bool nobar = (g.dbg & 64) != 0;
+  const bool nobar = (kGemmDiag && (g.dbg & 64)) != 0;
   if (!nobar) __builtin_amdgcn_s_barrier();
 #pragma unroll
   for (int j = 0; j < TM; ++j) fa0[j] = p4_frag<BM, AT>(lds, wm + 16 * j, 0, S);
@@ -201,7 +201,7 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
   const bool loader = wave >= 4;
   const int lw = wave & 3;   // loader index (loaders) / compute index
   const int wm = WsWave<BM>::wm(wave), wn = WsWave<BM>::wn(wave);
-  const bool noload = (g.dbg & 8) != 0;
+  const bool noload = (kGemmDiag && (g.dbg & 8)) != 0;
 
   float* stg = (float*)lds;
   // RES: a memory operand added by the epilogue, loaded into registers ahead of the store pass: the fp32 residual
@@ -235,7 +235,7 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
 
   // The two roles run separate loops with the same barrier count (1 + nk): a shared loop with role branches made
   // the compiler merge the accumulators through phi copies (and spill them).
-  if (loader && (g.dbg & 64)) {
+  if (loader && (kGemmDiag && (g.dbg & 64))) {
     // (diagnostic: the compute waves run their stream alone; see ws_compute)
   } else if (loader) {
     // ---------------- loader waves: 3-stage ring, stage s + 3 issued once step s has released its buffer
@@ -328,10 +328,10 @@ ASRX_DEV void ws_tile(const GemmArgs& g, int m0, int n0, bool rs_tile, unsigned 
   };
   constexpr bool apf = true;   // (round 4's A/B of the look-ahead, ASRX_GEMM_DBG & 256, removed in round 5)
   if constexpr ((EPI & E_ADAM) != 0) {
-    if (apf && !(g.dbg & 1)) adam_load(0, 0);
+    if (apf && !(kGemmDiag && (g.dbg & 1))) adam_load(0, 0);
   }
   __syncthreads();
-  if (g.dbg & 1) return;
+  if (kGemmDiag && (g.dbg & 1)) return;
   if (!loader) load_resid();
   if constexpr ((EPI & E_ADAM) != 0) {
     // E_ADAM (the grouped weight gradients of a single-GPU step, asrx_gemm_grouped_xcd_adam): each thread's rows in
@@ -433,7 +433,7 @@ ASRX_DEV void wsg_tile(const GroupEnt* __restrict__ ents, const uint16_t* __rest
                        int dbg, unsigned char* lds, int* __restrict__ pcnt = nullptr, float* __restrict__ part = nullptr,
                        int* s_last = nullptr, const AdamFused* ad = nullptr) {
   // tools only (ASRX_GEMM_DBG & 128): per-tile start / end real time, XCD, CU and tile into g_ws_trace
-  const bool trace = (dbg & 128) && threadIdx.x == 0 && slot < WS_TRACE_BLOCKS;
+  const bool trace = (kGemmDiag && (dbg & 128)) && threadIdx.x == 0 && slot < WS_TRACE_BLOCKS;
   const uint64_t t_start = trace ? __builtin_amdgcn_s_memrealtime() : 0;
   const int gi = __builtin_amdgcn_readfirstlane((int)tile_group[t_all]);
   const GroupEnt e = ents[gi];
