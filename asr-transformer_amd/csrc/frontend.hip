@@ -804,6 +804,127 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const int64_t* __restric
   }
 }
 
+// d % 8 == 0 (round 6): the same block per vocabulary row and token-order match list, but the 4 waves split the
+// row's matches (wave w sums its contiguous quarter of each chunk's list, in order) and a lane owns 8 consecutive
+// columns of each 512-column chunk — 16-B loads, one dropout hash per column PAIR (the kernel above hashes every
+// element, and its 2-column-per-thread layout kept all 4 waves on every match: ~30 us at c3, instruction-bound at
+// one wave per SIMD).  The 4 wave partials are added in wave order through LDS: deterministic.
+constexpr int EB8_MAXD = 2048;
+__global__ __launch_bounds__(256) void embed_bwd_v8_kernel(const int64_t* __restrict__ tok, int64_t ntok, int d,
+                                                           const float* __restrict__ dout, int pad_id, uint32_t thr,
+                                                           float sc, uint64_t seed, float* __restrict__ dtable) {
+  seed = seed_eff(seed);
+  const int v = blockIdx.x;
+  if (v == pad_id) return;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  constexpr int EB_WIN = 16, EB_CHUNK = 4 * 64 * EB_WIN, NJ = EB8_MAXD / 512;
+  __shared__ int rows_[EB_CHUNK];
+  __shared__ int wcnt[4 * EB_WIN];
+  __shared__ __attribute__((aligned(16))) float red[3][EB8_MAXD];
+  const int nj = (d + 511) / 512;
+  f4_t acc[NJ][2];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) acc[j][0] = acc[j][1] = f4_t{0.f, 0.f, 0.f, 0.f};
+  for (int64_t base = 0; base < ntok; base += EB_CHUNK) {
+    unsigned long long mk[EB_WIN];
+#pragma unroll
+    for (int q = 0; q < EB_WIN; ++q) {
+      const int64_t i = base + 64 * (EB_WIN * w + q) + lane;
+      mk[q] = __ballot(i < ntok && tok[i] == v);
+    }
+    if (lane < EB_WIN) {
+      int c = 0;
+#pragma unroll
+      for (int q = 0; q < EB_WIN; ++q) c = q == lane ? __popcll(mk[q]) : c;
+      wcnt[EB_WIN * w + lane] = c;
+    }
+    __syncthreads();
+    int off = 0, n = 0;
+    for (int u = 0; u < 4 * EB_WIN; ++u) {
+      const int c = wcnt[u];
+      if (u < EB_WIN * w) off += c;
+      n += c;
+    }
+#pragma unroll
+    for (int q = 0; q < EB_WIN; ++q) {
+      const unsigned long long m = mk[q];
+      if ((m >> lane) & 1ull) rows_[off + __popcll(m & ((1ull << lane) - 1ull))] = (int)(64 * (EB_WIN * w + q) + lane);
+      off += __popcll(m);
+    }
+    __syncthreads();
+    // this wave's quarter of the list, 4 matches' loads in flight
+    const int e0 = (n * w) >> 2, e1 = (n * (w + 1)) >> 2;
+    for (int e = e0; e < e1; e += 4) {
+      int64_t r[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) r[k] = base + rows_[min(e + k, e1 - 1)];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        if (j >= nj) break;   // (block-uniform)
+        const int c = 512 * j + 8 * lane;
+        f4_t g[4][2];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (c < d) {
+            g[k][0] = *(const f4_t*)(dout + r[k] * d + c);
+            g[k][1] = *(const f4_t*)(dout + r[k] * d + c + 4);
+          } else {
+            g[k][0] = g[k][1] = f4_t{0.f, 0.f, 0.f, 0.f};
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (e + k >= e1) break;
+          if (thr) {
+            // elements r d + c .. + 7: pairs (r d + c) / 2 + 0..3 (d and c even)
+            const uint32_t pb = (uint32_t)(r[k] * d + c) >> 1;
+#pragma unroll
+            for (int hq = 0; hq < 2; ++hq)
+#pragma unroll
+              for (int pp = 0; pp < 2; ++pp) {
+                const uint32_t h = rng_hash(seed, pb + 2 * hq + pp);
+                g[k][hq][2 * pp] = rng_half(h, 0) >= thr ? g[k][hq][2 * pp] * sc : 0.f;
+                g[k][hq][2 * pp + 1] = rng_half(h, 1) >= thr ? g[k][hq][2 * pp + 1] * sc : 0.f;
+              }
+          }
+          acc[j][0] += g[k][0];
+          acc[j][1] += g[k][1];
+        }
+      }
+    }
+    __syncthreads();   // rows_ / wcnt are rewritten by the next chunk
+  }
+  // wave partials in wave order: waves 1-3 publish, wave 0 adds them in order
+  if (w > 0) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = 512 * j + 8 * lane;
+      if (j < nj && c < d) {
+        *(f4_t*)(&red[w - 1][c]) = acc[j][0];
+        *(f4_t*)(&red[w - 1][c + 4]) = acc[j][1];
+      }
+    }
+  }
+  __syncthreads();
+  if (w == 0) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = 512 * j + 8 * lane;
+      if (j < nj && c < d) {
+        f4_t s0 = acc[j][0], s1 = acc[j][1];
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+          s0 += *(const f4_t*)(&red[u][c]);
+          s1 += *(const f4_t*)(&red[u][c + 4]);
+        }
+        float* o = dtable + (int64_t)v * d + c;
+        *(f4_t*)o += s0;
+        *(f4_t*)(o + 4) += s1;
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void ce_count_kernel(const int64_t* tgt, int64_t rows, int64_t ignore, float* ws) {
   __shared__ float red[256];
   float c = 0.f;
@@ -1128,8 +1249,12 @@ extern "C" int asrx_embed_bwd(const int64_t* tok, int64_t ntok, int32_t L, const
   if (!tok || !dout || !dtable || vocab <= 0 || d > 2048) return ASRX_ERR_ARG;
   const uint32_t thr = drop_threshold(dropout_p);
   const float sc = (dropout_p > 0.f && dropout_p < 1.f) ? 1.f / (1.f - dropout_p) : 1.f;
-  hipLaunchKernelGGL(embed_bwd_kernel, dim3(vocab), dim3(256), 0, (hipStream_t)stream, tok, ntok, d, dout, pad_id, thr,
-                     sc, seed, dtable);
+  if (d % 8 == 0 && (uintptr_t)dout % 16 == 0 && (uintptr_t)dtable % 16 == 0)
+    hipLaunchKernelGGL(embed_bwd_v8_kernel, dim3(vocab), dim3(256), 0, (hipStream_t)stream, tok, ntok, d, dout, pad_id,
+                       thr, sc, seed, dtable);
+  else
+    hipLaunchKernelGGL(embed_bwd_kernel, dim3(vocab), dim3(256), 0, (hipStream_t)stream, tok, ntok, d, dout, pad_id,
+                       thr, sc, seed, dtable);
   ASRX_CHECK_LAUNCH();
   return ASRX_OK;
 }

@@ -901,6 +901,27 @@ def test_conv_frontend(dtype, T):
 
 # ------------------------------------------------------------------------------------------------ misc
 
+@pytest.mark.parametrize("d,ntok", [(512, 4096), (80, 9000), (2048, 700), (12, 300)])
+def test_embed_bwd_dropout_repeats(d, ntok):
+    """Embedding gradient (nn.Embedding padding_idx backward of dropout(E[tok] + PE)) with dropout 0.1 and heavily
+    repeated tokens (a few ids take most of the rows, more than one 4096-token chunk): against index_add of the
+    masked, rescaled gradient rows, the keep mask from rng_ref (element index row * d + column)."""
+    from rng_ref import elem_keep
+    V, pad, p, seed = 250, 0, 0.1, 1234
+    g = torch.Generator().manual_seed(9)
+    tok = torch.randint(0, V, (ntok,), generator=g)
+    tok[torch.rand(ntok, generator=g) < 0.3] = 1      # a very frequent id (BOS / EOS-like)
+    tok[torch.rand(ntok, generator=g) < 0.2] = pad
+    dout = torch.randn(ntok, d, generator=g)
+    keep = torch.from_numpy(elem_keep(seed, ntok * d, p).reshape(ntok, d).astype(np.float32))
+    ref = torch.zeros(V, d, dtype=torch.float64)
+    ref.index_add_(0, tok, (dout * keep / (1 - p)).double())
+    ref[pad] = 0
+    dE = torch.zeros(V, d, device=dev)
+    K().embed_bwd(tok.to(dev), dout.to(dev), dE, 64, pad_id=pad, dropout_p=p, seed=seed)
+    assert relerr(dE.cpu().double(), ref) < 1e-6
+
+
 def test_embedding_and_ce_and_adam():
     V, d, B, L = 250, 128, 4, 16
     g = torch.Generator().manual_seed(6)
