@@ -501,8 +501,14 @@ __global__ __launch_bounds__(256) void conv1_bwd_fused_v8_kernel(const bf16_t* _
 // per lane), B = the staged weights.  A wave walks its (chunk, tap) items software-pipelined: the next item's
 // dy2 fragments are in flight while the current item's MFMAs (and, after a chunk's last tap, its epilogue)
 // run.  Epilogue: each lane holds 4 positions x 1 channel per 16-channel tile, gates them with conv1_fwd's
-// sign bits and accumulates channel x (9 x-taps + bias) in fp32 from the row's three input lines (LDS).
-// Per-workgroup partials [640] finish in conv1_bwd_finish.
+// sign bits, and the chunk's conv1 weight / bias gradient dW1[c][q] += sum_p dy1[p][c] x_q[p] (9 x-taps + a ones
+// column for the bias) is one 16x16x16 bf16 MFMA per channel tile (round 6): the gated accumulator IS the A operand
+// (lane (li, g) holds dy1[4 g + r][16 c + li]), the B operand the lane's tap q = li of the chunk's positions 4 g + r
+// from the row's three input lines (LDS).  bf16 operands with fp32 accumulation — the arithmetic of the reference's
+// autocast conv backward (bf16 grad_output and input); the fp32 FMA form it replaces (160 FMAs per chunk and lane)
+// took 113 -> 97 us (tools/fe_bench.py).  Round 6 also measured the items two ahead (101-102 us) and a chunk's
+// taps issued together (123 us): the one-item pipeline stays.  Per-workgroup partials [640] finish in
+// conv1_bwd_finish.
 constexpr int CB_MAXT1 = 1024;
 
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void conv_bwd_implicit_kernel(
@@ -529,11 +535,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
     }
     *(uint4*)(sW + (ts * 64 + ci) * 64 + 8 * (c8 ^ (ci & 7))) = make_uint4(u[0], u[1], u[2], u[3]);
   }
-  float aw[4][10];
+  f4_t aw[4];   // dW1 partial: lane (li, g) holds [channel 16 c + 4 g + r][tap li] (taps 9: bias, 10-15: zero)
 #pragma unroll
-  for (int c = 0; c < 4; ++c)
-#pragma unroll
-    for (int k = 0; k < 10; ++k) aw[c][k] = 0.f;
+  for (int c = 0; c < 4; ++c) aw[c] = f4_t{0.f, 0.f, 0.f, 0.f};
+  const int qkh = li / 3, qkw = li - 3 * (li / 3);   // this lane's x tap (li < 9)
   const int nF = par ? F1 / 2 : (F1 + 1) / 2;                  // rows of this parity per utterance
   const int R = B * nF;
   const int n0 = (T1 + 1) / 2, n1 = T1 / 2;                    // positions of even / odd t1
@@ -593,50 +598,45 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
       }
       if (nch_ != ch) {   // chunk done: lane holds dy1 of positions j0 + 4 g + r, channels 16 c + li
         const int j0 = 16 * (pt ? ch - c0 : ch), np = pt ? n1 : n0;
+        uint2 mw[4];       // sign-bit words of the lane's 4 positions (8 bytes = 64 channels each)
+        float xq[4];       // B operand: this lane's tap of the 4 positions (0 past the row: A is 0 there too)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int j = j0 + 4 * g + r;
-          if (j >= np) continue;
-          const int t1 = pt + 2 * j;
-          float xv[9];
-#pragma unroll
-          for (int kh = 0; kh < 3; ++kh)
-#pragma unroll
-            for (int kw = 0; kw < 3; ++kw) xv[kh * 3 + kw] = sX[kh * T + 2 * t1 + kw];
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const int ci = 16 * c + li;
-            const float gv = ((sM[t1 * 8 + (ci >> 3)] >> (ci & 7)) & 1) ? acc[c][r] : 0.f;
-#pragma unroll
-            for (int q = 0; q < 9; ++q) aw[c][q] = fmaf(gv, xv[q], aw[c][q]);
-            aw[c][9] += gv;
-          }
+          const bool ok = j < np;
+          const int t1 = pt + 2 * (ok ? j : 0);
+          mw[r] = ok ? *(const uint2*)(sM + t1 * 8) : make_uint2(0u, 0u);
+          xq[r] = !ok ? 0.f : li < 9 ? sX[qkh * T + 2 * t1 + qkw] : (li == 9 ? 1.f : 0.f);
         }
+        const s4_t bx = __builtin_bit_cast(s4_t, make_uint2(pack2bf(xq[0], xq[1]), pack2bf(xq[2], xq[3])));
 #pragma unroll
-        for (int c = 0; c < 4; ++c) acc[c] = f4_t{0.f, 0.f, 0.f, 0.f};
+        for (int c = 0; c < 4; ++c) {
+          const int ci = 16 * c + li;
+          float gv[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const uint32_t wb = (ci >> 5) ? mw[r].y : mw[r].x;
+            gv[r] = ((wb >> (ci & 31)) & 1u) ? acc[c][r] : 0.f;
+          }
+          const s4_t ga = __builtin_bit_cast(s4_t, make_uint2(pack2bf(gv[0], gv[1]), pack2bf(gv[2], gv[3])));
+          aw[c] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ga, bx, aw[c], 0, 0, 0);
+          acc[c] = f4_t{0.f, 0.f, 0.f, 0.f};
+        }
       }
       if (!more) break;
       ch = nch_; ih = nih; iw = niw;
       cur0 = nx0; cur1 = nx1; cok = nok;
     }
   }
-  // lanes with the same li hold the same channels: reduce over g, then over the waves (in the weight image)
+  // each wave holds its whole [64 channels][taps] partial (lane (li, g): channels 16 c + 4 g + r, tap li): the
+  // waves' partials meet in the dead weight image and are added in wave order
   __syncthreads();
   float (*red)[640] = (float (*)[640])smem;
-#pragma unroll
-  for (int c = 0; c < 4; ++c)
-#pragma unroll
-    for (int k = 0; k < 10; ++k) {
-      float v = aw[c][k];
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
-      aw[c][k] = v;
-    }
-  if (g == 0) {
+  if (li < 10) {
 #pragma unroll
     for (int c = 0; c < 4; ++c)
 #pragma unroll
-      for (int k = 0; k < 10; ++k) red[w][(16 * c + li) * 10 + k] = aw[c][k];
+      for (int r = 0; r < 4; ++r) red[w][(16 * c + 4 * g + r) * 10 + li] = aw[c][r];
   }
   __syncthreads();
   for (int i = tid; i < 640; i += 512) {

@@ -895,8 +895,16 @@ def test_conv_frontend(dtype, T):
         dw3 = torch.zeros(64, 9, device=dev)
         db3 = torch.zeros(64, device=dev)
         K().conv_bwd_implicit(dy2, w2p, y1m, x.to(dev), dw3, db3)
-        assert relerr(dw3.cpu(), w1r2.grad.reshape(64, 9)) < 1e-5
-        assert relerr(db3.cpu(), b1r2.grad) < 1e-5
+        # (round 6: the conv1 weight gradient on bf16 MFMAs — bf16 dy1 and x, fp32 accumulation, the reference's
+        #  autocast arithmetic: against the fp64 gradient of the bf16-rounded operands, and the exact one at bf16 level)
+        w1r3 = w1.double().requires_grad_(True)
+        b1r3 = b1.double().requires_grad_(True)
+        gy1 = (y1g2.grad * (y1r > 0)).to(torch.bfloat16).double()
+        torch.nn.functional.conv2d(xr.to(torch.bfloat16).double(), w1r3, b1r3, stride=2).backward(gy1)
+        assert relerr(dw3.cpu(), w1r3.grad.reshape(64, 9)) < 1e-3
+        assert relerr(db3.cpu(), b1r3.grad) < 1e-3
+        assert relerr(dw3.cpu(), w1r2.grad.reshape(64, 9)) < 1e-2
+        assert relerr(db3.cpu(), b1r2.grad) < 1e-2
 
 
 # ------------------------------------------------------------------------------------------------ misc
