@@ -516,6 +516,7 @@ def reduce_rows_grouped(items):
 
 
 LN_BWD_BLOCKS = 512   # (tools/ln_bench.py: 26.1-26.6 us cold vs 26.7 at 1024; 256 measured equal in the step)
+LN_BWD512_WAVES = 8   # waves per block of the d = 512 kernel (norm.hip LNB_W): half the blocks for the same waves
 
 
 def layernorm_bwd(x, dy, gamma, mean, rstd, dgb, *, dres=None, dx_drop=None, dropout_p=0.0, seed=0, defer=None):
@@ -525,7 +526,8 @@ def layernorm_bwd(x, dy, gamma, mean, rstd, dgb, *, dres=None, dx_drop=None, dro
     _cuda(x, dy, gamma, mean, rstd, dgb)
     rows, d = x.shape
     dx = torch.empty(rows, d, device=x.device, dtype=torch.float32)
-    nblocks = max(1, min(LN_BWD_BLOCKS, (rows + 7) // 8))   # >= 2 rows per wave: the kernel prefetches the next
+    wpb = LN_BWD512_WAVES if d == 512 else 4   # (the d = 512 kernel's blocks hold 8 waves)
+    nblocks = max(1, min(LN_BWD_BLOCKS * 4 // wpb, (rows + 2 * wpb - 1) // (2 * wpb)))   # >= 2 rows per wave
     part = torch.empty(nblocks * 2 * d, device=x.device, dtype=torch.float32)
     call("asrx_layernorm_bwd", code(x), x.data_ptr(), code(dy), dy.data_ptr(), gamma.data_ptr(), mean.data_ptr(),
          rstd.data_ptr(), _p(dres), dx.data_ptr(), _p(dx_drop), code(dx_drop) if dx_drop is not None else 0,

@@ -188,9 +188,12 @@ __global__ __launch_bounds__(256) void ln_fwd512_kernel(const float* __restrict_
 }
 
 // Backward, d = 512: as ln_bwd_kernel (dgamma | dbeta partials per block into part[block][2 D]), lanes own 8
-// columns, PF rows of x / dy / dres / stats in flight per wave.  dy bf16 (the compute dtype).
+// columns, PF rows of x / dy / dres / stats in flight per wave.  dy bf16 (the compute dtype).  Blocks of 8 waves
+// (round 6; were 4): the same waves per CU with half the blocks, so half the dgamma|dbeta partials written here and
+// read back by the step's grouped reduce (61 calls x 512 blocks x 4 KiB had been 128 MB per c3 step).
+constexpr int LNB_W = 8;
 template <int PF>
-__global__ __launch_bounds__(256) void ln_bwd512_kernel(const float* __restrict__ x, const bf16_t* __restrict__ dy,
+__global__ __launch_bounds__(64 * LNB_W) void ln_bwd512_kernel(const float* __restrict__ x, const bf16_t* __restrict__ dy,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ mean,
                                                         const float* __restrict__ rstd,
@@ -199,10 +202,10 @@ __global__ __launch_bounds__(256) void ln_bwd512_kernel(const float* __restrict_
                                                         uint64_t seed, float* __restrict__ part, int64_t rows) {
   seed = seed_eff(seed);
   constexpr int D = 512;
-  __shared__ float red[4][2 * D];
+  __shared__ float red[LNB_W][2 * D];
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t nw = (int64_t)gridDim.x * 4;
-  const int64_t gw = (int64_t)blockIdx.x * 4 + w;
+  const int64_t nw = (int64_t)gridDim.x * LNB_W;
+  const int64_t gw = (int64_t)blockIdx.x * LNB_W + w;
   float pg[8], pb[8], ga[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) { pg[i] = 0.f; pb[i] = 0.f; }
@@ -257,8 +260,12 @@ __global__ __launch_bounds__(256) void ln_bwd512_kernel(const float* __restrict_
     red[w][D + 8 * l + i] = pb[i];
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < 2 * D; c += 256)
-    part[(int64_t)blockIdx.x * 2 * D + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+  for (int c = threadIdx.x; c < 2 * D; c += 64 * LNB_W) {
+    float t = red[0][c];
+#pragma unroll
+    for (int i = 1; i < LNB_W; ++i) t += red[i][c];
+    part[(int64_t)blockIdx.x * 2 * D + c] = t;
+  }
 }
 
 // LN variant selection (asrx_set_tuning ASRX_TUNE_LN_PF: rows in flight per wave of the d = 512 kernels, default 2
@@ -526,7 +533,7 @@ extern "C" int asrx_layernorm_bwd(int32_t x_dtype, const void* x, int32_t dy_dty
       ((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx_out | (uintptr_t)dres | (uintptr_t)dx_drop) % 16 == 0) {
     const uint32_t thr = drop_threshold(dropout_p);
     const float sc = (dropout_p > 0.f && dropout_p < 1.f) ? 1.f / (1.f - dropout_p) : 1.f;
-#define ASRX_LNB(PF) hipLaunchKernelGGL((ln_bwd512_kernel<PF>), dim3(nblocks), dim3(256), 0, st, (const float*)x, \
+#define ASRX_LNB(PF) hipLaunchKernelGGL((ln_bwd512_kernel<PF>), dim3(nblocks), dim3(64 * LNB_W), 0, st, (const float*)x, \
                                         (const bf16_t*)dy, gamma, mean, rstd, dres, dx_out, (bf16_t*)dx_drop, thr, \
                                         sc, seed, part, rows)
     if (pf == 1) ASRX_LNB(1);
