@@ -192,8 +192,8 @@ __global__ __launch_bounds__(256) void ln_fwd512_kernel(const float* __restrict_
 // (round 6; were 4): the same waves per CU with half the blocks, so half the dgamma|dbeta partials written here and
 // read back by the step's grouped reduce (61 calls x 512 blocks x 4 KiB had been 128 MB per c3 step).
 constexpr int LNB_W = 8;
-template <int PF>
-__global__ __launch_bounds__(64 * LNB_W) void ln_bwd512_kernel(const float* __restrict__ x, const bf16_t* __restrict__ dy,
+template <int PF, bool DYF = false>   // DYF: dy fp32 (the encoder's final LayerNorm: the cross K/V data gradient)
+__global__ __launch_bounds__(64 * LNB_W) void ln_bwd512_kernel(const float* __restrict__ x, const void* __restrict__ dy,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ mean,
                                                         const float* __restrict__ rstd,
@@ -212,7 +212,8 @@ __global__ __launch_bounds__(64 * LNB_W) void ln_bwd512_kernel(const float* __re
   float xv[PF][8], dv[PF][8], rv[PF][8], mu[PF], rsv[PF];
   auto load = [&](int p, int64_t r) {
     ld8f(x + r * D + 8 * l, xv[p]);
-    ld8b(dy + r * D + 8 * l, dv[p]);
+    if constexpr (DYF) ld8f((const float*)dy + r * D + 8 * l, dv[p]);
+    else ld8b((const bf16_t*)dy + r * D + 8 * l, dv[p]);
     if (dres) ld8f(dres + r * D + 8 * l, rv[p]);
     mu[p] = mean[r];
     rsv[p] = rstd[r];
@@ -529,16 +530,18 @@ extern "C" int asrx_layernorm_bwd(int32_t x_dtype, const void* x, int32_t dy_dty
   if (!x || !dy || !gamma || !mean || !rstd || !dx_out || !part || nblocks <= 0 || rows < 0) return ASRX_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
   const int pf = ln_pf();
-  if (d == 512 && x_dtype == ASRX_F32 && dy_dtype == ASRX_BF16 && pf > 0 && (!dx_drop || drop_dtype == ASRX_BF16) &&
+  if (d == 512 && x_dtype == ASRX_F32 && (dy_dtype == ASRX_BF16 || dy_dtype == ASRX_F32) && pf > 0 &&
+      (!dx_drop || drop_dtype == ASRX_BF16) &&
       ((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx_out | (uintptr_t)dres | (uintptr_t)dx_drop) % 16 == 0) {
     const uint32_t thr = drop_threshold(dropout_p);
     const float sc = (dropout_p > 0.f && dropout_p < 1.f) ? 1.f / (1.f - dropout_p) : 1.f;
-#define ASRX_LNB(PF) hipLaunchKernelGGL((ln_bwd512_kernel<PF>), dim3(nblocks), dim3(64 * LNB_W), 0, st, (const float*)x, \
-                                        (const bf16_t*)dy, gamma, mean, rstd, dres, dx_out, (bf16_t*)dx_drop, thr, \
-                                        sc, seed, part, rows)
-    if (pf == 1) ASRX_LNB(1);
-    else if (pf == 4) ASRX_LNB(4);
-    else ASRX_LNB(2);
+#define ASRX_LNB(PF, DYF) hipLaunchKernelGGL((ln_bwd512_kernel<PF, DYF>), dim3(nblocks), dim3(64 * LNB_W), 0, st, \
+                                             (const float*)x, dy, gamma, mean, rstd, dres, dx_out, (bf16_t*)dx_drop, \
+                                             thr, sc, seed, part, rows)
+    if (dy_dtype == ASRX_F32) ASRX_LNB(2, true);
+    else if (pf == 1) ASRX_LNB(1, false);
+    else if (pf == 4) ASRX_LNB(4, false);
+    else ASRX_LNB(2, false);
 #undef ASRX_LNB
     ASRX_CHECK_LAUNCH();
     return ASRX_OK;
