@@ -903,6 +903,10 @@ void attn_fwd_kq_kernel(AttnArgs a, const uint32_t* qmaj) {
   const int qw0 = qg * 32;
   const bf16_t* Kb = a.k + b * a.kb + h * 64;
   const bf16_t* Vb = a.v + b * a.vb + h * 64;
+  __shared__ uint64_t sdbg[16];   // (diagnostic builds: phase timestamps, as in attn_fwd_res_kernel)
+  if (kStamps && a.dbg && threadIdx.x < 16) sdbg[threadIdx.x] = 0;
+  FWD_RT(12);
+  FWD_TS(0);
   // loads: Q fragments (4), keep words of this wave's two key tiles (2), then the K/V pieces
   s8_t qf[2][2];
   uint32_t dw[2][2];
@@ -938,6 +942,7 @@ void attn_fwd_kq_kernel(AttnArgs a, const uint32_t* qmaj) {
     smask[n] = make_uint2(((n & 1) ? 0xffffu : 0u) | ((n & 2) ? 0xffff0000u : 0u),
                           ((n & 4) ? 0xffffu : 0u) | ((n & 8) ? 0xffff0000u : 0u));
   }
+  FWD_TS(1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
   for (int qs = 0; qs < 2; ++qs) {
@@ -948,6 +953,8 @@ void attn_fwd_kq_kernel(AttnArgs a, const uint32_t* qmaj) {
     if (!DROP) dw[qs][0] = dw[qs][1] = 0xffffffffu;
   }
   lds_barrier();
+  FWD_TS(2);
+  FWD_RT(13);
 
   const float sc2 = a.scale2;
   f4_t o[4][2];
@@ -1021,9 +1028,11 @@ void attn_fwd_kq_kernel(AttnArgs a, const uint32_t* qmaj) {
 #pragma unroll
       for (int qs = 0; qs < 2; ++qs) o[u][qs] = mfma32(vt, cat8(pf[0][qs], pf[1][qs]), o[u][qs]);
     }
+    FWD_TS(3 + j);
   }
   // ---- partials: (m, l) per query in sml, O_j (fp32, this lane's 32 values) in the dead K/V image
   __syncthreads();   // every wave is done with the K/V image
+  FWD_TS(5);
   float* spo = (float*)sk;   // [wave][32 values][64 lanes]: 8 KiB per wave, 64 KiB in all (sk + sv)
   if (g == 0) {
 #pragma unroll
@@ -1041,6 +1050,15 @@ void attn_fwd_kq_kernel(AttnArgs a, const uint32_t* qmaj) {
         for (int r = 0; r < 4; ++r) spo[(w * 32 + (u * 2 + qs) * 4 + r) * 64 + l] = o[u][qs][r];
   }
   __syncthreads();
+  FWD_TS(6);
+  if (kStamps && a.dbg && threadIdx.x == 0) {   // (wave 0 stores last: its end stamp follows its own output stores)
+    // per-block start / staged stamps now, the end stamp after wave 0's stores below
+    if (bh < 1024) {
+      g_attn_dbg[128 + 4 * bh] = sdbg[12];
+      g_attn_dbg[129 + 4 * bh] = sdbg[13];
+      g_attn_dbg[131 + 4 * bh] = __smid();
+    }
+  }
   if (kq != 0 || qw0 >= a.Lq) return;
   const float dsc = DROP ? a.dscale : 1.f;
 #pragma unroll
@@ -1077,6 +1095,12 @@ void attn_fwd_kq_kernel(AttnArgs a, const uint32_t* qmaj) {
       store_o4(a.o + oo + 16 * u, a.o_lo ? a.o_lo + oo + 16 * u : nullptr, oc[u][0] * inv, oc[u][1] * inv,
                oc[u][2] * inv, oc[u][3] * inv);
     if (g == 0 && a.lse) a.lse[(int64_t)bh * a.Lq + q] = live ? Mu + log2f(L) : INFINITY;
+  }
+  FWD_TS(11);
+  if (kStamps && a.dbg && threadIdx.x == 0) {
+    if (blockIdx.y == 0)
+      for (int i = 0; i < 12; ++i) g_attn_dbg[44 + i] = sdbg[i];
+    if (bh < 1024) g_attn_dbg[130 + 4 * bh] = __builtin_amdgcn_s_memrealtime();
   }
 }
 
