@@ -1395,7 +1395,9 @@ extern "C" int asrx_adam(float* p, const float* g, float* m, float* v, void* p_b
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16) return ASRX_ERR_ARG;
   if (p_bf16 && (uintptr_t)p_bf16 % 8) return ASRX_ERR_ARG;
   if (n == 0) return ASRX_OK;
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1)), dim3(256), 0, (hipStream_t)stream, p, g, m, v,
+  // up to 16 K workgroups (64 per CU): tools/adam_bench.py, 44.5 M parameters, 226 -> 202 us (5.9 -> 6.6 TB/s of
+  // the 30 B per parameter) against the 8 K cap of the elementwise launches; 2 K / 4 K 253 / 241 us (round 6)
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1, 16384)), dim3(256), 0, (hipStream_t)stream, p, g, m, v,
                      (bf16_t*)p_bf16, n, lr, beta1, beta2, eps, weight_decay, bias_corr1, 1.f / sqrtf(bias_corr2),
                      grad_scale, decoupled, hyp);
   ASRX_CHECK_LAUNCH();
